@@ -1,0 +1,54 @@
+/*
+ * rocjpeg_amd.h -- extensions of the MI355X-native rocJPEG drop-in.  Nothing here is needed
+ * to use the reference API; these entry points exist for measurement and data staging.
+ */
+#ifndef ROC_JPEG_AMD_H
+#define ROC_JPEG_AMD_H
+
+#include "rocjpeg.h"
+
+#if defined(__cplusplus)
+extern "C" {
+#endif
+
+/* Parse-only image info that needs no decoder handle (rocJpegGetImageInfo requires one). */
+RocJpegStatus rocJpegAmdStreamGetInfo(RocJpegStreamHandle stream, uint8_t *num_components,
+                                      RocJpegChromaSubsampling *subsampling, uint32_t *widths, uint32_t *heights,
+                                      uint32_t *num_restart_intervals);
+
+/* Stage the entropy-coded bytes and restart-interval tables of parsed streams in the HBM of
+ * the handle's device.  A later rocJpegDecode[Batched] on the same handle then reads them
+ * from HBM instead of copying from host memory.  The copy is dropped when the stream is
+ * re-parsed or destroyed. */
+RocJpegStatus rocJpegAmdStreamsToDevice(RocJpegHandle handle, RocJpegStreamHandle *streams, int count);
+
+/* Per-stage device time of the most recent decode call, measured with HIP events on the
+ * handle's internal stream (enable with rocJpegAmdSetProfiling first). */
+typedef struct {
+  float h2d_ms;       /* staging of non-resident bitstreams + descriptors */
+  float destuff_ms;   /* K0 */
+  float huffman_ms;   /* K1 */
+  float idct_ms;      /* K2a (general path) or fused K2 (fast path) */
+  float output_ms;    /* K2b (general path; 0 on the fused path) */
+  float total_ms;
+  uint64_t ecs_bytes;     /* entropy-coded bytes consumed */
+  uint64_t coef_bytes;    /* int16 coefficient bytes written by K1 */
+  uint64_t output_bytes;  /* bytes written to the caller's buffers */
+  uint32_t images, intervals, fused_images;
+} RocJpegAmdTimings;
+
+RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);
+RocJpegStatus rocJpegAmdGetLastTimings(RocJpegHandle handle, RocJpegAmdTimings *timings);
+
+/* Select the output path: 0 = automatic (fused kernel where the output window allows it),
+ * 1 = always the general two-stage path (IDCT to planes, then format conversion). */
+RocJpegStatus rocJpegAmdSetPathPolicy(RocJpegHandle handle, int policy);
+
+/* The handle's HIP stream (as void*), e.g. for external event timing. */
+RocJpegStatus rocJpegAmdGetStream(RocJpegHandle handle, void **hip_stream);
+
+#if defined(__cplusplus)
+}
+#endif
+
+#endif /* ROC_JPEG_AMD_H */

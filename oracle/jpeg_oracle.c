@@ -212,6 +212,9 @@ static int build_htab(const uint8_t bits[16], const uint8_t *vals, int nvals_max
   if (k > nvals_max) return 0;
   memset(t->vals, 0, sizeof(t->vals));
   memcpy(t->vals, vals, (size_t)k);
+  if (nvals_max == 12) /* DC table: libjpeg rejects categories > 15 (jdhuff.c) */
+    for (int i = 0; i < k; i++)
+      if (vals[i] > 15) return 0;
   return 1;
 }
 

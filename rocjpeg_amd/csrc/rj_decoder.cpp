@@ -1,0 +1,395 @@
+// rj_decoder.cpp -- batch planner + launch sequence (see rj_decoder.h).
+#include "rj_decoder.h"
+
+#include <algorithm>
+#include <cstring>
+
+#include "rj_common.h"
+#include "rj_kernels.h"
+
+namespace rj {
+
+namespace {
+
+inline uint64_t AlignUp(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace
+
+int DeviceBuffer::Ensure(size_t bytes) {
+  if (bytes <= cap_) return kOk;
+  Release();
+  const size_t want = std::max<size_t>(AlignUp(bytes + bytes / 4, 1 << 20), 1 << 20);
+  if (hipMalloc(&ptr_, want) != hipSuccess) {
+    ptr_ = nullptr;
+    (void)hipGetLastError();
+    return kOutOfMemory;
+  }
+  cap_ = want;
+  return kOk;
+}
+
+void DeviceBuffer::Release() {
+  if (ptr_) (void)hipFree(ptr_);
+  ptr_ = nullptr;
+  cap_ = 0;
+}
+
+int PinnedBuffer::Ensure(size_t bytes) {
+  if (bytes <= cap_) return kOk;
+  Release();
+  const size_t want = std::max<size_t>(AlignUp(bytes + bytes / 4, 1 << 20), 1 << 20);
+  if (hipHostMalloc(&ptr_, want, hipHostMallocDefault) != hipSuccess) {
+    ptr_ = nullptr;
+    (void)hipGetLastError();
+    return kOutOfMemory;
+  }
+  cap_ = want;
+  return kOk;
+}
+
+void PinnedBuffer::Release() {
+  if (ptr_) (void)hipHostFree(ptr_);
+  ptr_ = nullptr;
+  cap_ = 0;
+}
+
+Decoder::~Decoder() {
+  if (stream_) {
+    (void)hipSetDevice(device_);
+    (void)hipStreamSynchronize(stream_);
+    for (auto &e : ev_)
+      if (e) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(stream_);
+  }
+}
+
+int Decoder::Initialize() {
+  // InitHIP (rocjpeg_decoder.cpp:46-61)
+  int count = 0;
+  RJ_HIP(hipGetDeviceCount(&count));
+  if (count < 1) {
+    RJ_ERR("no GPU found");
+    return kNotInitialized;
+  }
+  if (device_ >= count) {
+    RJ_ERR("device %d not found (%d devices)", device_, count);
+    return kInvalidParameter;
+  }
+  RJ_HIP(hipSetDevice(device_));
+  hipDeviceProp_t prop;
+  RJ_HIP(hipGetDeviceProperties(&prop, device_));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    RJ_ERR("device %d is %s; this build carries gfx950 (MI355X) kernels only", device_, prop.gcnArchName);
+    return -7;  // ROCJPEG_STATUS_ARCH_MISMATCH
+  }
+  RJ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  for (auto &e : ev_) RJ_HIP(hipEventCreate(&e));
+  (void)backend_;  // HARDWARE and HYBRID both run the HIP decoder
+  return kOk;
+}
+
+int Decoder::GetImageInfo(Stream *s, uint8_t *nc, RocJpegChromaSubsampling *css, uint32_t *w, uint32_t *h) {
+  std::lock_guard<std::mutex> lock(mu_);
+  if (s == nullptr || nc == nullptr || css == nullptr || w == nullptr || h == nullptr) return kInvalidParameter;
+  int c = -1;
+  const int st = ImageInfo(s->info(), nc, &c, w, h);
+  *css = RocJpegChromaSubsampling(c);
+  return st;
+}
+
+int Decoder::StreamsToDevice(Stream *const *streams, int n) {
+  std::lock_guard<std::mutex> lock(mu_);
+  if (streams == nullptr || n < 0) return kInvalidParameter;
+  RJ_HIP(hipSetDevice(device_));
+  for (int i = 0; i < n; i++) {
+    Stream *s = streams[i];
+    if (s == nullptr) return kInvalidParameter;
+    std::lock_guard<std::mutex> sl(s->mutex());
+    if (s->resident.device == device_ && s->resident.generation == s->generation()) continue;
+    s->ReleaseResident();
+    const StreamInfo &in = s->info();
+    const DecodePlan &p = s->plan();
+    if (p.status != 0) continue;
+    Stream::Resident r;
+    r.device = device_;
+    r.generation = s->generation();
+    RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.ecs), std::max<size_t>(in.ecs_size, 16)));
+    RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.segs), std::max<size_t>(p.segs.size() * sizeof(RjSegDev), 16)));
+    RJ_HIP(hipMemcpy(r.ecs, in.ecs, in.ecs_size, hipMemcpyHostToDevice));
+    RJ_HIP(hipMemcpy(r.segs, p.segs.data(), p.segs.size() * sizeof(RjSegDev), hipMemcpyHostToDevice));
+    s->resident = r;
+  }
+  return kOk;
+}
+
+int Decoder::Decode(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
+  std::lock_guard<std::mutex> lock(mu_);
+  if (streams == nullptr || params == nullptr || dst == nullptr || n < 0) return kInvalidParameter;
+  for (int i = 0; i < n; i++)
+    if (streams[i] == nullptr) return kInvalidParameter;
+  // Hold every stream's lock for the call: a concurrent re-parse must not move its bytes.
+  std::vector<std::unique_lock<std::mutex>> locks;
+  std::vector<Stream *> uniq(streams, streams + n);
+  std::sort(uniq.begin(), uniq.end());
+  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  locks.reserve(uniq.size());
+  for (Stream *s : uniq) locks.emplace_back(s->mutex());
+  return DecodeLocked(streams, n, params, dst);
+}
+
+int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
+  RJ_HIP(hipSetDevice(device_));
+  timings_ = RocJpegAmdTimings();
+  if (n == 0) return kOk;
+  const int fmt = int(params->output_format);
+
+  // ---- per-image validation (SubmitDecode checks, destination checks) ----
+  for (int i = 0; i < n; i++) {
+    const DecodePlan &p = streams[i]->plan();
+    if (p.status != 0) return p.status;
+  }
+
+  // ---- table de-duplication ----
+  std::vector<uint32_t> tab_of(n);
+  std::vector<const RjTableSet *> tabs;
+  {
+    std::unordered_map<uint64_t, std::vector<uint32_t>> seen;
+    for (int i = 0; i < n; i++) {
+      const DecodePlan &p = streams[i]->plan();
+      uint32_t idx = UINT32_MAX;
+      auto &cands = seen[p.table_hash];
+      for (uint32_t c : cands)
+        if (std::memcmp(tabs[c], &p.tables, sizeof(RjTableSet)) == 0) { idx = c; break; }
+      if (idx == UINT32_MAX) {
+        idx = uint32_t(tabs.size());
+        tabs.push_back(&p.tables);
+        cands.push_back(idx);
+      }
+      tab_of[i] = idx;
+    }
+  }
+
+  // ---- layout ----
+  std::vector<RjImageDev> imgs(n);
+  std::vector<RjJobDev> jobs;
+  uint64_t destuff_total = 0, coef_blocks = 0, plane_bytes = 0, stage_bytes = 0;
+  uint32_t seg_total = 0, blk_total = 0, rows_total = 0;
+  uint64_t ecs_bytes = 0, out_bytes = 0;
+  std::vector<uint64_t> stage_off(n, UINT64_MAX);
+  for (int i = 0; i < n; i++) {
+    Stream *s = streams[i];
+    const StreamInfo &in = s->info();
+    const DecodePlan &p = s->plan();
+    RjImageDev &d = imgs[i];
+    std::memset(&d, 0, sizeof(d));
+    d.width = in.width;
+    d.height = in.height;
+    d.mcux = p.mcux;
+    d.mcuy = p.mcuy;
+    d.ncomp = in.ncomp;
+    d.nblk_mcu = p.nblk_mcu;
+    d.interleaved = p.interleaved;
+    d.css = uint8_t(in.css);
+    d.hmax = p.hmax;
+    d.vmax = p.vmax;
+    d.fmt = uint8_t(fmt);
+    for (int c = 0; c < 4; c++) {
+      d.comp_h[c] = in.comp[c].h;
+      d.comp_v[c] = in.comp[c].v;
+      d.comp_td[c] = in.scomp[c].td;
+      d.comp_ta[c] = in.scomp[c].ta;
+      d.comp_tq[c] = in.comp[c].tq;
+      d.comp_blk0[c] = p.comp_blk0[c];
+    }
+    std::memcpy(d.blk_comp, p.blk_comp, RJ_MAX_BLK_MCU);
+    std::memcpy(d.blk_dx, p.blk_dx, RJ_MAX_BLK_MCU);
+    std::memcpy(d.blk_dy, p.blk_dy, RJ_MAX_BLK_MCU);
+    d.tabset = tab_of[i];
+    d.nseg = uint32_t(p.segs.size());
+    d.seg_prefix = seg_total;
+    seg_total += d.nseg;
+    d.destuff_off = destuff_total;
+    destuff_total += AlignUp(p.destuff_bytes, 256);
+    d.coef_off = coef_blocks;
+    coef_blocks += uint64_t(p.mcux) * p.mcuy * p.nblk_mcu;
+    d.blk_prefix = blk_total;
+    for (int c = 0; c < in.ncomp; c++) {
+      d.plane_pitch[c] = p.wblk[c] * 8;
+      d.plane_rows[c] = p.hblk[c] * 8;
+      d.plane_off[c] = plane_bytes;
+      plane_bytes += AlignUp(uint64_t(d.plane_pitch[c]) * d.plane_rows[c], 256);
+      blk_total += p.wblk[c] * p.hblk[c];
+    }
+    ecs_bytes += in.ecs_size;
+    if (!(s->resident.device == device_ && s->resident.generation == s->generation())) {
+      stage_off[i] = stage_bytes;
+      stage_bytes += AlignUp(p.segs.size() * sizeof(RjSegDev), 256) + AlignUp(in.ecs_size + 16, 256);
+    }
+
+    // output window: ROI semantics of rocjpeg_decoder.cpp:124-141 (no ROI decode on gfx950)
+    const uint32_t roi_w = uint32_t(int(params->crop_rectangle.right) - int(params->crop_rectangle.left));
+    const uint32_t roi_h = uint32_t(int(params->crop_rectangle.bottom) - int(params->crop_rectangle.top));
+    const bool roi = roi_w > 0 && roi_h > 0 && roi_w <= in.width && roi_h <= in.height;
+    d.roi = roi;
+    d.out_w = roi ? int32_t(roi_w) : in.width;
+    d.out_h = roi ? int32_t(roi_h) : in.height;
+    d.top = roi ? params->crop_rectangle.top : 0;
+    d.left = roi ? params->crop_rectangle.left : 0;
+    const RocJpegImage &o = dst[i];
+    for (int c = 0; c < 4; c++) {
+      d.dst[c] = o.channel[c];
+      d.dst_pitch[c] = o.pitch[c];
+    }
+
+    // ---- output jobs (general path): rocjpeg_decoder.cpp:143-180 ----
+    const int css = in.css;
+    const int32_t pw = d.out_w, ph = d.out_h, top = d.top, left = d.left;
+    auto need = [&](int c) { return o.channel[c] != nullptr; };
+    auto job = [&](uint32_t kind, uint32_t sel, int dc, int32_t rows, uint32_t bytes, uint32_t pitch, int32_t r0,
+                   int32_t b0) {
+      if (rows <= 0 || bytes == 0) return;
+      RjJobDev j;
+      std::memset(&j, 0, sizeof(j));
+      j.image = uint32_t(i);
+      j.kind = kind;
+      j.chan_sel = sel;
+      j.rows = uint32_t(rows);
+      j.row_bytes = bytes;
+      j.dst_pitch = pitch;
+      j.dst = o.channel[dc];
+      j.src_row0 = r0;
+      j.src_byte0 = b0;
+      j.row_prefix = rows_total;
+      rows_total += j.rows;
+      out_bytes += uint64_t(rows) * bytes;
+      jobs.push_back(j);
+    };
+    auto copy = [&](int sp, int chan, int dc, int32_t rows, int32_t r0, int32_t b0) {  // CopyChannel
+      if (o.channel[dc] != nullptr && o.pitch[dc] != 0)
+        job(RJ_JOB_COPY, uint32_t(sp | (chan << 4)), dc, rows, o.pitch[dc], o.pitch[dc], r0, b0);
+    };
+    const auto sel = [](int sp, int chan, int stride) { return uint32_t(sp | (chan << 4) | (stride << 8)); };
+    switch (fmt) {
+      case ROCJPEG_OUTPUT_NATIVE:
+        if (css == kCss422) {
+          copy(0, 0, 0, ph, top, 2 * left);
+        } else {
+          copy(0, 0, 0, ph, top, left);
+          if (css == kCss420) copy(1, 1, 1, ph >> 1, top >> 1, left);
+          if (css == kCss444) { copy(1, 1, 1, ph, top, left); copy(1, 2, 2, ph, top, left); }
+          if (css == kCss440) { copy(1, 1, 1, ph >> 1, top >> 1, left); copy(1, 2, 2, ph >> 1, top >> 1, left); }
+        }
+        break;
+      case ROCJPEG_OUTPUT_YUV_PLANAR:
+        if (css == kCss422) {
+          if (!need(0) || !need(1) || !need(2)) return kInvalidParameter;
+          job(RJ_JOB_Y, 0, 0, ph, uint32_t(pw), o.pitch[0], top, left);
+          job(RJ_JOB_CHROMA, sel(0, 0, 4), 1, ph, uint32_t(pw >> 1), o.pitch[1], top, 2 * left + 1);
+          job(RJ_JOB_CHROMA, sel(0, 0, 4), 2, ph, uint32_t(pw >> 1), o.pitch[1], top, 2 * left + 3);
+        } else {
+          if (!need(0)) return kInvalidParameter;
+          copy(0, 0, 0, ph, top, left);
+          if (css == kCss420) {
+            if (!need(1) || !need(2)) return kInvalidParameter;
+            job(RJ_JOB_CHROMA, sel(1, 1, 2), 1, ph >> 1, uint32_t(pw >> 1), o.pitch[1], top >> 1, left);
+            job(RJ_JOB_CHROMA, sel(1, 1, 2), 2, ph >> 1, uint32_t(pw >> 1), o.pitch[1], top >> 1, left + 1);
+          } else if (css == kCss444) {
+            if (!need(1) || !need(2)) return kInvalidParameter;
+            copy(1, 1, 1, ph, top, left);
+            copy(1, 2, 2, ph, top, left);
+          } else if (css == kCss440) {
+            if (!need(1) || !need(2)) return kInvalidParameter;
+            copy(1, 1, 1, ph >> 1, top >> 1, left);
+            copy(1, 2, 2, ph >> 1, top >> 1, left);
+          }
+        }
+        break;
+      case ROCJPEG_OUTPUT_Y:
+        if (!need(0)) return kInvalidParameter;
+        if (css == kCss422) job(RJ_JOB_Y, 0, 0, ph, uint32_t(pw), o.pitch[0], top, left);
+        else copy(0, 0, 0, ph, top, left);
+        break;
+      case ROCJPEG_OUTPUT_RGB:
+        if (!need(0)) return kInvalidParameter;
+        job(RJ_JOB_RGB, 0, 0, ph, uint32_t(3 * pw), o.pitch[0], 0, 0);
+        break;
+      case ROCJPEG_OUTPUT_RGB_PLANAR:
+        if (!need(0) || !need(1) || !need(2)) return kInvalidParameter;
+        for (int k = 0; k < 3; k++) job(RJ_JOB_RGB_PLANE, uint32_t(k << 4), k, ph, uint32_t(pw), o.pitch[0], 0, 0);
+        break;
+      default:
+        break;  // reference: unknown format writes nothing and succeeds
+    }
+  }
+
+  // ---- one host->device upload: descriptors + non-resident bitstreams ----
+  const uint64_t off_imgs = 0;
+  const uint64_t off_tabs = AlignUp(off_imgs + n * sizeof(RjImageDev), 256);
+  const uint64_t off_jobs = AlignUp(off_tabs + tabs.size() * sizeof(RjTableSet), 256);
+  const uint64_t off_stage = AlignUp(off_jobs + std::max<size_t>(jobs.size(), 1) * sizeof(RjJobDev), 256);
+  const uint64_t blob = off_stage + stage_bytes;
+  RJ_CHECK(h_stage_.Ensure(blob));
+  RJ_CHECK(d_desc_.Ensure(blob));
+  RJ_CHECK(d_destuff_.Ensure(std::max<uint64_t>(destuff_total, 256)));
+  RJ_CHECK(d_seglen_.Ensure(std::max<uint64_t>(uint64_t(seg_total) * 4, 256)));
+  RJ_CHECK(d_coefs_.Ensure(std::max<uint64_t>(coef_blocks * 128, 256)));
+  RJ_CHECK(d_planes_.Ensure(std::max<uint64_t>(plane_bytes, 256)));
+  uint8_t *h = h_stage_.data();
+  uint8_t *dbase = d_desc_.as<uint8_t>();
+  for (int i = 0; i < n; i++) {
+    Stream *s = streams[i];
+    RjImageDev &d = imgs[i];
+    if (stage_off[i] == UINT64_MAX) {
+      d.ecs = s->resident.ecs;
+      d.segs = s->resident.segs;
+    } else {
+      const DecodePlan &p = s->plan();
+      const uint64_t so = off_stage + stage_off[i];
+      const uint64_t eo = so + AlignUp(p.segs.size() * sizeof(RjSegDev), 256);
+      std::memcpy(h + so, p.segs.data(), p.segs.size() * sizeof(RjSegDev));
+      std::memcpy(h + eo, s->info().ecs, s->info().ecs_size);
+      d.segs = reinterpret_cast<const RjSegDev *>(dbase + so);
+      d.ecs = dbase + eo;
+    }
+  }
+  std::memcpy(h + off_imgs, imgs.data(), n * sizeof(RjImageDev));
+  for (size_t t = 0; t < tabs.size(); t++) std::memcpy(h + off_tabs + t * sizeof(RjTableSet), tabs[t], sizeof(RjTableSet));
+  if (!jobs.empty()) std::memcpy(h + off_jobs, jobs.data(), jobs.size() * sizeof(RjJobDev));
+
+  const RjImageDev *d_imgs = reinterpret_cast<const RjImageDev *>(dbase + off_imgs);
+  const RjTableSet *d_tabs = reinterpret_cast<const RjTableSet *>(dbase + off_tabs);
+  const RjJobDev *d_jobs = reinterpret_cast<const RjJobDev *>(dbase + off_jobs);
+
+  if (profiling_) RJ_HIP(hipEventRecord(ev_[0], stream_));
+  RJ_HIP(hipMemcpyAsync(dbase, h, blob, hipMemcpyHostToDevice, stream_));
+  if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
+  RJ_HIP(LaunchDestuff(stream_, d_imgs, n, seg_total, d_destuff_.as<uint8_t>(), d_seglen_.as<uint32_t>()));
+  if (profiling_) RJ_HIP(hipEventRecord(ev_[2], stream_));
+  RJ_HIP(LaunchHuffman(stream_, d_imgs, n, seg_total, d_destuff_.as<uint8_t>(), d_seglen_.as<uint32_t>(), d_tabs,
+                       d_coefs_.as<int16_t>()));
+  if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
+  RJ_HIP(LaunchIdctPlanes(stream_, d_imgs, n, blk_total, d_coefs_.as<int16_t>(), d_tabs, d_planes_.as<uint8_t>()));
+  if (profiling_) RJ_HIP(hipEventRecord(ev_[4], stream_));
+  RJ_HIP(LaunchOutputJobs(stream_, d_imgs, d_jobs, int(jobs.size()), rows_total, d_planes_.as<uint8_t>()));
+  if (profiling_) RJ_HIP(hipEventRecord(ev_[5], stream_));
+  RJ_HIP(hipStreamSynchronize(stream_));
+
+  timings_.images = uint32_t(n);
+  timings_.intervals = seg_total;
+  timings_.ecs_bytes = ecs_bytes;
+  timings_.coef_bytes = coef_blocks * 128;
+  timings_.output_bytes = out_bytes;
+  if (profiling_) {
+    float ms[5];
+    for (int k = 0; k < 5; k++) RJ_HIP(hipEventElapsedTime(&ms[k], ev_[k], ev_[k + 1]));
+    timings_.h2d_ms = ms[0];
+    timings_.destuff_ms = ms[1];
+    timings_.huffman_ms = ms[2];
+    timings_.idct_ms = ms[3];
+    timings_.output_ms = ms[4];
+    RJ_HIP(hipEventElapsedTime(&timings_.total_ms, ev_[0], ev_[5]));
+  }
+  return kOk;
+}
+
+}  // namespace rj

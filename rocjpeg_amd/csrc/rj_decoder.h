@@ -1,0 +1,76 @@
+// rj_decoder.h -- decode orchestration behind rocJpegDecode / rocJpegDecodeBatched.
+//
+// Role of the reference's RocJpegDecoder (src/rocjpeg_decoder.{h,cpp}): one HIP device and
+// one private stream per handle (rocjpeg_decoder.cpp:46-61), calls serialised by a
+// per-handle mutex (rocjpeg_decoder.h:174), synchronous return (:183, :290).  Instead of a
+// VA submit per image it plans the whole batch at once: one descriptor upload, then
+// K0 destuff -> K1 Huffman -> K2 (fused) or K2a+K2b (general) over every image together.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/rocjpeg.h"
+#include "../../include/rocjpeg_amd.h"
+#include "rj_device.h"
+#include "rj_stream.h"
+
+namespace rj {
+
+class DeviceBuffer {
+ public:
+  ~DeviceBuffer() { Release(); }
+  int Ensure(size_t bytes);  // grow-only
+  void Release();
+  template <typename T> T *as() const { return static_cast<T *>(ptr_); }
+  size_t capacity() const { return cap_; }
+
+ private:
+  void *ptr_ = nullptr;
+  size_t cap_ = 0;
+};
+
+class PinnedBuffer {
+ public:
+  ~PinnedBuffer() { Release(); }
+  int Ensure(size_t bytes);
+  void Release();
+  uint8_t *data() const { return static_cast<uint8_t *>(ptr_); }
+
+ private:
+  void *ptr_ = nullptr;
+  size_t cap_ = 0;
+};
+
+class Decoder {
+ public:
+  Decoder(RocJpegBackend backend, int device_id) : backend_(backend), device_(device_id) {}
+  ~Decoder();
+  int Initialize();
+  int GetImageInfo(Stream *s, uint8_t *nc, RocJpegChromaSubsampling *css, uint32_t *w, uint32_t *h);
+  int Decode(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
+  int StreamsToDevice(Stream *const *streams, int n);
+  void SetProfiling(bool on) { profiling_ = on; }
+  void SetPathPolicy(int p) { path_policy_ = p; }
+  RocJpegAmdTimings last_timings() const { return timings_; }
+  hipStream_t stream() const { return stream_; }
+
+ private:
+  int DecodeLocked(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
+
+  RocJpegBackend backend_;
+  int device_;
+  hipStream_t stream_ = nullptr;
+  std::mutex mu_;
+  bool profiling_ = false;
+  int path_policy_ = 0;
+  RocJpegAmdTimings timings_ = {};
+  hipEvent_t ev_[8] = {};
+
+  DeviceBuffer d_desc_, d_stage_, d_destuff_, d_seglen_, d_coefs_, d_planes_, d_strips_;
+  PinnedBuffer h_stage_;
+};
+
+}  // namespace rj

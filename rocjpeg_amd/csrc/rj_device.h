@@ -1,0 +1,90 @@
+// rj_device.h -- descriptors shared by the host planner (rj_decoder.cpp) and the HIP kernels
+// (rj_kernels.hip).  Plain PODs; every pointer is a device pointer on the handle's GPU.
+//
+// HBM layout of one batch (all regions carved from the handle's arena, rj_decoder.cpp):
+//   images[]   RjImageDev          one per image in the batch
+//   tabsets[]  RjTableSet          de-duplicated Huffman LUTs + natural-order quant tables
+//   segs       RjSegDev per image  restart intervals (resident with the stream's ECS bytes)
+//   destuffed  u8                  byte-unstuffed entropy data, each interval 16-B aligned
+//   coefs      int16[64] blocks    MCU-major: block (image.coef_off + mcu*nblk_mcu + b)
+//   planes     u8                  per component, padded to the MCU grid (general path only)
+#pragma once
+#include <stdint.h>
+
+#define RJ_LUT_BITS 9
+#define RJ_MAX_BLK_MCU 10
+
+// One restart interval of one image (host parser rj_stream.cpp builds these).
+struct RjSegDev {
+  uint32_t src_off;    // raw ECS byte offset of the interval's first data byte
+  uint32_t src_len;    // raw bytes (RST markers and trailing fill FFs excluded)
+  uint32_t dst_off;    // destuffed byte offset (16-B aligned), relative to image.destuff_off
+  uint32_t mcu_first;  // first MCU of the interval
+  uint32_t mcu_count;  // MCUs in the interval
+  uint32_t flags;      // RJ_SEG_MISSING: marker not found -> interval decodes to zero blocks
+};
+#define RJ_SEG_MISSING 1u
+
+// Canonical Huffman decoder for one table (T.81 Annex C), laid out for the GPU.
+struct RjHuffDev {
+  uint16_t fast[1 << RJ_LUT_BITS];  // (code_len << 8) | symbol for codes <= RJ_LUT_BITS, else 0
+  uint32_t maxcode16[18];           // exclusive upper bound of length-l codes, left-justified to 16 bits
+  int32_t valoff[18];               // symbol index = (code >> (16 - l)) + valoff[l]
+  uint8_t vals[256];
+};
+
+struct RjTableSet {
+  RjHuffDev dc[2];
+  RjHuffDev ac[2];
+  uint16_t q[4][64];  // natural order (DQT is zigzag order: rocjpeg_parser.cpp:239)
+};
+
+// Output jobs of the general (two-stage) path: one per written channel.
+enum RjJobKind : uint32_t {
+  RJ_JOB_COPY = 0,      // CopyChannel: surface plane bytes, dst pitch bytes per row
+  RJ_JOB_RGB = 1,       // interleaved RGB
+  RJ_JOB_RGB_PLANE = 2, // one of R/G/B planes (chan_sel)
+  RJ_JOB_Y = 3,         // luma samples (also YUYV luma extraction)
+  RJ_JOB_CHROMA = 4,    // planar U or V extracted from the surface model
+};
+
+struct RjJobDev {
+  uint32_t image;
+  uint32_t kind;
+  uint32_t chan_sel;     // which surface plane / which RGB component / U(1) or V(2)
+  uint32_t rows;         // rows written
+  uint32_t row_bytes;    // bytes written per row
+  uint32_t dst_pitch;
+  uint8_t *dst;
+  int32_t src_row0;      // surface row of output row 0
+  int32_t src_byte0;     // surface byte (or pixel) column of output byte 0
+  uint32_t row_prefix;   // exclusive prefix of rows over jobs (grid mapping)
+  uint32_t pad;
+};
+
+struct RjImageDev {
+  uint32_t width, height;
+  uint32_t mcux, mcuy;
+  uint8_t ncomp, nblk_mcu, interleaved, css;
+  uint8_t hmax, vmax, fmt, roi;
+  uint8_t comp_h[4], comp_v[4];
+  uint8_t comp_td[4], comp_ta[4], comp_tq[4];
+  uint8_t blk_comp[RJ_MAX_BLK_MCU], blk_dx[RJ_MAX_BLK_MCU], blk_dy[RJ_MAX_BLK_MCU];
+  uint8_t comp_blk0[4];  // first block of each component inside an MCU
+  uint32_t tabset;
+  // inputs
+  const uint8_t *ecs;
+  const RjSegDev *segs;
+  uint32_t nseg;
+  uint32_t seg_prefix;   // exclusive prefix of segments over the batch
+  uint64_t destuff_off;  // into the destuffed buffer
+  uint64_t coef_off;     // in blocks
+  // component planes (general path)
+  uint64_t plane_off[4];
+  uint32_t plane_pitch[4], plane_rows[4];
+  uint32_t blk_prefix;   // exclusive prefix of blocks over the batch (IDCT grid)
+  // output window (ROI semantics of rocjpeg_decoder.cpp:124-141)
+  int32_t out_w, out_h, top, left;
+  uint8_t *dst[4];
+  uint32_t dst_pitch[4];
+};

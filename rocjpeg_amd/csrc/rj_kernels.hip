@@ -1,0 +1,437 @@
+// rj_kernels.hip -- the JPEG decode hot path for MI355X (gfx950, wave64).
+//
+// Replaces the VCN fixed-function decode of the reference (src/rocjpeg_vaapi_decoder.cpp:
+// 574-692) and rewrites its post-processing kernels (src/rocjpeg_hip_kernels.cpp).
+//
+//   K0 k_destuff      one wavefront per restart interval: coalesced byte loads, FF00/fill
+//                     removal by per-lane keep masks + wave prefix sum, compacted stores.
+//   K1 k_huffman      one lane per restart interval: 64-bit MSB-first bit buffer refilled by
+//                     aligned dword loads, 9-bit LUT + canonical slow path, flattened
+//                     symbol loop (lanes never wait for each other at block boundaries),
+//                     per-lane 128-B coefficient block staged in LDS.
+//   K2a k_idct_planes thread per 8x8 block: dequant + libjpeg ISLOW IDCT in registers,
+//                     8-byte row stores into MCU-padded component planes.
+//   K2b k_output      every output format / ROI semantic of rocjpeg_decoder.cpp:143-180,
+//                     colour conversion identical to rocjpeg_hip_kernels.cpp:1431-1443.
+//   K2  k_fused       (rj_fused.hip) dequant + IDCT + upsample + CSC without the planes.
+#include <hip/hip_runtime.h>
+
+#include "rj_device.h"
+#include "rj_kernels.h"
+#include "rj_math.h"
+
+namespace rj {
+
+// ---------------------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------------------
+// index of the last entry with prefix <= key (prefix[0] == 0, monotone)
+template <typename F>
+__device__ __forceinline__ int upper_index(int n, uint32_t key, F prefix_of) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (prefix_of(mid) <= key) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v, uint32_t lane, uint32_t &total) {
+  uint32_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= uint32_t(off)) x += y;
+  }
+  total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+// ---------------------------------------------------------------------------------------
+// K0: destuff.  Within an interval's raw range the host guarantees only data bytes,
+// FF 00 pairs and FF fill runs in front of an FF 00 occur.  Byte i is dropped when
+// (b[i] == 00 && b[i-1] == FF) or (b[i] == FF && b[i+1] == FF).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ imgs, int nimg,
+                                                uint8_t *__restrict__ destuffed, uint32_t *__restrict__ seg_len) {
+  const uint32_t g = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  const int i = upper_index(nimg, g, [&](int k) { return imgs[k].seg_prefix; });
+  const RjImageDev &im = imgs[i];
+  const RjSegDev sg = im.segs[g - im.seg_prefix];
+  const uint8_t *src = im.ecs + sg.src_off;
+  uint8_t *dst = destuffed + im.destuff_off + sg.dst_off;
+  const uint32_t len = sg.src_len;
+  uint32_t out = 0;
+  uint32_t prev_byte = 0;  // byte before the current 256-B chunk
+  for (uint32_t base = 0; base < len; base += 256) {
+    const uint32_t p = base + 4 * lane;
+    uint32_t b[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) b[k] = (p + k < len) ? src[p + k] : 0x100u;  // 0x100 = past the end
+    const uint32_t nb_next = (base + 256 < len) ? src[base + 256] : 0x100u;
+    uint32_t prev = __shfl_up(b[3], 1, 64);
+    if (lane == 0) prev = prev_byte;
+    uint32_t next = __shfl_down(b[0], 1, 64);
+    if (lane == 63) next = nb_next;
+    uint32_t keep = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t pv = k == 0 ? prev : b[k - 1];
+      const uint32_t nx = k == 3 ? next : b[k + 1];
+      const bool drop = b[k] == 0x100u || (b[k] == 0x00u && pv == 0xFFu) || (b[k] == 0xFFu && nx == 0xFFu);
+      keep |= (drop ? 0u : 1u) << k;
+    }
+    uint32_t total;
+    uint32_t o = wave_exclusive_scan(__popc(keep), lane, total) + out;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (keep & (1u << k)) dst[o++] = uint8_t(b[k]);
+    out += total;
+    prev_byte = __shfl(b[3], 63, 64);
+  }
+  if (lane == 0) seg_len[g] = out;
+}
+
+hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nseg, uint8_t *destuffed,
+                         uint32_t *seg_len) {
+  if (nseg == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_destuff, dim3(nseg), dim3(64), 0, st, imgs, nimg, destuffed, seg_len);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// K1: Huffman decode, one lane per restart interval.
+// ---------------------------------------------------------------------------------------
+struct BitReader {
+  const uint32_t *w;  // 16-B aligned destuffed words (big-endian bytes)
+  uint32_t nbytes;
+  uint32_t wi;        // next word
+  int nb;             // valid bits in acc (left-justified)
+  uint64_t acc;
+
+  __device__ __forceinline__ void refill() {
+    if (nb <= 32) {
+      uint32_t v = 0;
+      const uint32_t byte = wi * 4u;
+      if (byte < nbytes) {
+        v = __builtin_bswap32(w[wi]);
+        const uint32_t valid = nbytes - byte;
+        if (valid < 4) v &= ~0u << (32 - 8 * valid);
+      }
+      acc |= uint64_t(v) << (32 - nb);
+      nb += 32;
+      wi++;
+    }
+  }
+  __device__ __forceinline__ uint32_t bits(int n) {  // 1 <= n <= 16
+    const uint32_t v = uint32_t(acc >> (64 - n));
+    acc <<= n;
+    nb -= n;
+    return v;
+  }
+  __device__ __forceinline__ bool overrun() const { return uint64_t(wi) * 32u - uint64_t(nb) > uint64_t(nbytes) * 8u; }
+};
+
+__device__ __forceinline__ int huff_decode(const RjHuffDev *__restrict__ t, BitReader &br) {
+  const uint32_t peek = uint32_t(br.acc >> 48);
+  const uint32_t e = t->fast[peek >> (16 - RJ_LUT_BITS)];
+  int len, sym;
+  if (e != 0) {
+    len = int(e >> 8);
+    sym = int(e & 255);
+  } else {  // codes longer than RJ_LUT_BITS: canonical search (libjpeg jpeg_huff_decode)
+    len = 17;
+    sym = 0;  // corrupt code: libjpeg consumes 17 bits and returns 0
+    for (int l = RJ_LUT_BITS + 1; l <= 16; l++) {
+      if (peek < t->maxcode16[l]) {
+        len = l;
+        sym = t->vals[((peek >> (16 - l)) + t->valoff[l]) & 255];
+        break;
+      }
+    }
+  }
+  br.acc <<= len;
+  br.nb -= len;
+  return sym;
+}
+
+__device__ __forceinline__ int huff_extend(uint32_t v, int s) {
+  return (v < (1u << (s - 1))) ? int(v) - (1 << s) + 1 : int(v);
+}
+
+__constant__ uint8_t c_zigzag[80] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33,
+    40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36,
+    29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
+    47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+
+__global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ imgs, int nimg, uint32_t nseg,
+                                                const uint8_t *__restrict__ destuffed,
+                                                const uint32_t *__restrict__ seg_len,
+                                                const RjTableSet *__restrict__ tabsets, int16_t *__restrict__ coefs) {
+  __shared__ __attribute__((aligned(16))) int16_t s_blk[64][64];
+  __shared__ uint8_t s_zz[80];
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t k = lane; k < 80; k += 64) s_zz[k] = c_zigzag[k];
+  __syncthreads();
+  const uint32_t g = blockIdx.x * 64u + lane;
+  if (g >= nseg) return;
+  const int i = upper_index(nimg, g, [&](int k) { return imgs[k].seg_prefix; });
+  const RjImageDev &im = imgs[i];
+  const RjSegDev sg = im.segs[g - im.seg_prefix];
+  const RjTableSet *ts = tabsets + im.tabset;
+  const uint32_t nblk = im.nblk_mcu;
+  // per-block component packed 2 bits per block-in-MCU (no dynamic register indexing)
+  uint32_t comp_bits = 0;
+  for (uint32_t b = 0; b < nblk; b++) comp_bits |= uint32_t(im.blk_comp[b]) << (2 * b);
+  const RjHuffDev *dc0 = &ts->dc[im.comp_td[0] & 1], *dc1 = &ts->dc[im.comp_td[1] & 1], *dc2 = &ts->dc[im.comp_td[2] & 1];
+  const RjHuffDev *ac0 = &ts->ac[im.comp_ta[0] & 1], *ac1 = &ts->ac[im.comp_ta[1] & 1], *ac2 = &ts->ac[im.comp_ta[2] & 1];
+
+  BitReader br;
+  br.w = reinterpret_cast<const uint32_t *>(destuffed + im.destuff_off + sg.dst_off);
+  br.nbytes = seg_len[g];
+  br.wi = 0;
+  br.nb = 0;
+  br.acc = 0;
+
+  int16_t *out = coefs + (im.coef_off + uint64_t(sg.mcu_first) * nblk) * 64u;
+  int16_t *blk = s_blk[lane];
+  uint4 *blk4 = reinterpret_cast<uint4 *>(blk);
+  const uint4 zero4 = make_uint4(0, 0, 0, 0);
+
+  int pred0 = 0, pred1 = 0, pred2 = 0;
+  bool skip = (sg.flags & RJ_SEG_MISSING) != 0;
+  uint32_t m = 0, b = 0;
+  int k = 0;
+  const uint32_t nmcu = sg.mcu_count;
+  while (m < nmcu) {
+    const uint32_t c = (comp_bits >> (2 * b)) & 3u;
+    if (k == 0) {
+#pragma unroll
+      for (int q = 0; q < 8; q++) blk4[q] = zero4;
+    }
+    if (skip) {
+      k = 64;
+    } else {
+      br.refill();
+      if (k == 0) {
+        const RjHuffDev *t = c == 0 ? dc0 : (c == 1 ? dc1 : dc2);
+        const int s = huff_decode(t, br) & 15;
+        const int diff = s ? huff_extend(br.bits(s), s) : 0;
+        int p = (c == 0 ? pred0 : (c == 1 ? pred1 : pred2)) + diff;
+        if (c == 0) pred0 = p;
+        else if (c == 1) pred1 = p;
+        else pred2 = p;
+        blk[0] = int16_t(p);
+        k = 1;
+      } else {
+        const RjHuffDev *t = c == 0 ? ac0 : (c == 1 ? ac1 : ac2);
+        const int rs = huff_decode(t, br);
+        const int r = rs >> 4, s = rs & 15;
+        if (s) {
+          k += r;
+          const int v = huff_extend(br.bits(s), s);
+          blk[s_zz[k < 79 ? k : 79]] = int16_t(v);
+          k++;
+        } else if (r == 15) {
+          k += 16;
+        } else {
+          k = 64;
+        }
+      }
+    }
+    if (k >= 64) {  // block complete: 128 B out, next block
+      uint4 *o = reinterpret_cast<uint4 *>(out + (uint64_t(m) * nblk + b) * 64u);
+#pragma unroll
+      for (int q = 0; q < 8; q++) o[q] = blk4[q];
+      k = 0;
+      if (++b == nblk) {
+        b = 0;
+        m++;
+        if (br.overrun()) skip = true;  // libjpeg: rest of the interval stays zero
+      }
+    }
+  }
+}
+
+hipError_t LaunchHuffman(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nseg, const uint8_t *destuffed,
+                         const uint32_t *seg_len, const RjTableSet *tabsets, int16_t *coefs) {
+  if (nseg == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_huffman, dim3((nseg + 63) / 64), dim3(64), 0, st, imgs, nimg, nseg, destuffed, seg_len, tabsets,
+                     coefs);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// K2a: IDCT into component planes (general path).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_idct_planes(const RjImageDev *__restrict__ imgs, int nimg, uint64_t nblocks,
+                                                     const int16_t *__restrict__ coefs,
+                                                     const RjTableSet *__restrict__ tabsets,
+                                                     uint8_t *__restrict__ planes) {
+  const uint64_t gb = uint64_t(blockIdx.x) * 256u + threadIdx.x;
+  if (gb >= nblocks) return;
+  const int i = upper_index(nimg, uint32_t(gb), [&](int k) { return imgs[k].blk_prefix; });
+  const RjImageDev &im = imgs[i];
+  uint32_t local = uint32_t(gb) - im.blk_prefix;
+  int c = 0;
+  uint32_t wb = im.plane_pitch[0] >> 3, hb = im.plane_rows[0] >> 3;
+  while (c + 1 < im.ncomp && local >= wb * hb) {
+    local -= wb * hb;
+    c++;
+    wb = im.plane_pitch[c] >> 3;
+    hb = im.plane_rows[c] >> 3;
+  }
+  const uint32_t by = local / wb, bx = local - by * wb;
+  uint64_t cb;
+  if (im.interleaved) {
+    const uint32_t hc = im.comp_h[c], vc = im.comp_v[c];
+    const uint32_t mx = bx / hc, my = by / vc;
+    const uint32_t b = im.comp_blk0[c] + (by - my * vc) * hc + (bx - mx * hc);
+    cb = im.coef_off + (uint64_t(my) * im.mcux + mx) * im.nblk_mcu + b;
+  } else {
+    cb = im.coef_off + local;
+  }
+  const uint4 *src = reinterpret_cast<const uint4 *>(coefs + cb * 64u);
+  const uint4 *q4 = reinterpret_cast<const uint4 *>(tabsets[im.tabset].q[im.comp_tq[c] & 3]);
+  int32_t v[64];
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const uint4 a = src[r];   // coefficients r*8 .. r*8+7
+    const uint4 qa = q4[r];   // quant entries r*8 .. r*8+7
+    const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
+    const uint32_t qw[4] = {qa.x, qa.y, qa.z, qa.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      v[r * 8 + 2 * j] = int32_t(int16_t(aw[j] & 0xFFFF)) * int32_t(qw[j] & 0xFFFF);
+      v[r * 8 + 2 * j + 1] = int32_t(int16_t(aw[j] >> 16)) * int32_t(qw[j] >> 16);
+    }
+  }
+  uint8_t o[64];
+  idct_islow_block(v, o);
+  uint8_t *dst = planes + im.plane_off[c] + uint64_t(by) * 8u * im.plane_pitch[c] + bx * 8u;
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    uint2 w;
+    w.x = uint32_t(o[r * 8 + 0]) | (uint32_t(o[r * 8 + 1]) << 8) | (uint32_t(o[r * 8 + 2]) << 16) | (uint32_t(o[r * 8 + 3]) << 24);
+    w.y = uint32_t(o[r * 8 + 4]) | (uint32_t(o[r * 8 + 5]) << 8) | (uint32_t(o[r * 8 + 6]) << 16) | (uint32_t(o[r * 8 + 7]) << 24);
+    *reinterpret_cast<uint2 *>(dst + uint64_t(r) * im.plane_pitch[c]) = w;
+  }
+}
+
+hipError_t LaunchIdctPlanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint64_t nblocks, const int16_t *coefs,
+                            const RjTableSet *tabsets, uint8_t *planes) {
+  if (nblocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_idct_planes, dim3(uint32_t((nblocks + 255) / 256)), dim3(256), 0, st, imgs, nimg, nblocks, coefs,
+                     tabsets, planes);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// K2b: general output stage over the VCN-surface model (see oracle oj_decode).
+// ---------------------------------------------------------------------------------------
+struct PlaneView {
+  const uint8_t *base;
+  const RjImageDev *im;
+  __device__ __forceinline__ uint8_t px(int c, int64_t r, int64_t x) const {
+    const int64_t rows = im->plane_rows[c], pitch = im->plane_pitch[c];
+    r = r < 0 ? 0 : (r >= rows ? rows - 1 : r);
+    x = x < 0 ? 0 : (x >= pitch ? pitch - 1 : x);
+    return base[im->plane_off[c] + uint64_t(r) * uint64_t(pitch) + uint64_t(x)];
+  }
+  // byte b of row r of surface plane sp (0 = luma / packed YUYV, 1 = chroma) for channel chan
+  __device__ __forceinline__ uint8_t surf(int sp, int chan, int64_t r, int64_t b) const {
+    if (im->css == 2 && sp == 0) {  // YUYV
+      const int64_t q = b >> 2;
+      switch (b & 3) {
+        case 0: return px(0, r, 2 * q);
+        case 1: return px(1, r, q);
+        case 2: return px(0, r, 2 * q + 1);
+        default: return px(2, r, q);
+      }
+    }
+    if (im->css == 3 && sp == 1) return (b & 1) ? px(2, r, b >> 1) : px(1, r, b >> 1);  // NV12 UV
+    return px(chan, r, b);
+  }
+  __device__ __forceinline__ void rgb(int64_t y, int64_t x, uint8_t out[3]) const {
+    const int64_t top = im->top, left = im->left;
+    const uint8_t Y = px(0, top + y, left + x);
+    uint8_t U = 128, V = 128;
+    switch (im->css) {
+      case 0:  // 4:4:4 -- luma ROI offset applied twice (rocjpeg_decoder.cpp:464-467)
+        U = px(1, 2 * top + y, 2 * left + x);
+        V = px(2, 2 * top + y, 2 * left + x);
+        break;
+      case 1:  // 4:4:0 -- chroma ROI offset commented out (rocjpeg_decoder.cpp:470)
+        U = px(1, top + (y >> 1), left + x);
+        V = px(2, top + (y >> 1), left + x);
+        break;
+      case 2: {  // YUYV read from byte 2*left
+        const int64_t b = 2 * left + 4 * (x >> 1);
+        U = surf(0, 0, top + y, b + 1);
+        V = surf(0, 0, top + y, b + 3);
+        break;
+      }
+      case 3: {  // NV12: UV + (top>>1)*pitch + left
+        const int64_t b = left + 2 * (x >> 1);
+        U = surf(1, 1, (top >> 1) + (y >> 1), b);
+        V = surf(1, 1, (top >> 1) + (y >> 1), b + 1);
+        break;
+      }
+      default:
+        out[0] = out[1] = out[2] = Y;
+        return;
+    }
+    csc_pixel(Y, U, V, out);
+  }
+};
+
+__global__ __launch_bounds__(256) void k_output(const RjImageDev *__restrict__ imgs, const RjJobDev *__restrict__ jobs,
+                                                int njobs, const uint8_t *__restrict__ planes) {
+  const uint32_t row_g = blockIdx.x;
+  const int j = upper_index(njobs, row_g, [&](int k) { return jobs[k].row_prefix; });
+  const RjJobDev jb = jobs[j];
+  const uint32_t row = row_g - jb.row_prefix;
+  PlaneView pv{planes, &imgs[jb.image]};
+  uint8_t *dst = jb.dst + uint64_t(row) * jb.dst_pitch;
+  const int64_t sr = int64_t(jb.src_row0) + row;
+  const int sp = jb.chan_sel & 15, chan = (jb.chan_sel >> 4) & 15, stride = jb.chan_sel >> 8;
+  for (uint32_t x = threadIdx.x; x < jb.row_bytes; x += 256) {
+    uint8_t v;
+    switch (jb.kind) {
+      case RJ_JOB_COPY:
+        v = pv.surf(sp, chan, sr, int64_t(jb.src_byte0) + x);
+        break;
+      case RJ_JOB_CHROMA:
+        v = pv.surf(sp, chan, sr, int64_t(jb.src_byte0) + int64_t(stride) * x);
+        break;
+      case RJ_JOB_Y:
+        v = pv.px(0, sr, int64_t(jb.src_byte0) + x);
+        break;
+      case RJ_JOB_RGB: {
+        uint8_t p[3];
+        pv.rgb(row, x / 3, p);
+        v = p[x % 3];
+        break;
+      }
+      default: {  // RJ_JOB_RGB_PLANE
+        uint8_t p[3];
+        pv.rgb(row, x, p);
+        v = p[chan];
+        break;
+      }
+    }
+    dst[x] = v;
+  }
+}
+
+hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobDev *jobs, int njobs, uint32_t total_rows,
+                            const uint8_t *planes) {
+  if (total_rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_output, dim3(total_rows), dim3(256), 0, st, imgs, jobs, njobs, planes);
+  return hipGetLastError();
+}
+
+}  // namespace rj

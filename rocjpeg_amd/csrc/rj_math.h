@@ -1,0 +1,98 @@
+// rj_math.h -- per-element arithmetic of the decode path, shared by the general and the
+// fused kernels so both produce identical bytes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rj {
+
+// libjpeg ISLOW constants (jidctint.c: CONST_BITS 13, PASS1_BITS 2).  Computed in int32:
+// exact for every stream whose dequantised coefficients stay in the range a real 8-bit DCT
+// produces (libjpeg-turbo's SIMD ISLOW kernels make the same assumption).
+#define RJ_FIX_0_298631336 2446
+#define RJ_FIX_0_390180644 3196
+#define RJ_FIX_0_541196100 4433
+#define RJ_FIX_0_765366865 6270
+#define RJ_FIX_0_899976223 7373
+#define RJ_FIX_1_175875602 9633
+#define RJ_FIX_1_501321110 12299
+#define RJ_FIX_1_847759065 15137
+#define RJ_FIX_1_961570560 16069
+#define RJ_FIX_2_053119869 16819
+#define RJ_FIX_2_562915447 20995
+#define RJ_FIX_3_072711026 25172
+
+// One 8-point ISLOW butterfly on x0..x7 (already dequantised / pass-1 outputs).  Writes the
+// eight pre-descale sums to t[0..7] in output order 0..7.
+__device__ __forceinline__ void islow_1d(int32_t x0, int32_t x1, int32_t x2, int32_t x3, int32_t x4, int32_t x5,
+                                         int32_t x6, int32_t x7, int32_t t[8]) {
+  int32_t z1 = (x2 + x6) * RJ_FIX_0_541196100;
+  const int32_t tmp2 = z1 - x6 * RJ_FIX_1_847759065;
+  const int32_t tmp3 = z1 + x2 * RJ_FIX_0_765366865;
+  const int32_t e0 = (x0 + x4) * 8192, e1 = (x0 - x4) * 8192;
+  const int32_t t10 = e0 + tmp3, t13 = e0 - tmp3, t11 = e1 + tmp2, t12 = e1 - tmp2;
+  int32_t o0 = x7, o1 = x5, o2 = x3, o3 = x1;
+  z1 = o0 + o3;
+  int32_t z2 = o1 + o2, z3 = o0 + o2, z4 = o1 + o3;
+  const int32_t z5 = (z3 + z4) * RJ_FIX_1_175875602;
+  o0 *= RJ_FIX_0_298631336;
+  o1 *= RJ_FIX_2_053119869;
+  o2 *= RJ_FIX_3_072711026;
+  o3 *= RJ_FIX_1_501321110;
+  z1 *= -RJ_FIX_0_899976223;
+  z2 *= -RJ_FIX_2_562915447;
+  z3 *= -RJ_FIX_1_961570560;
+  z4 *= -RJ_FIX_0_390180644;
+  z3 += z5;
+  z4 += z5;
+  o0 += z1 + z3;
+  o1 += z2 + z4;
+  o2 += z2 + z3;
+  o3 += z1 + z4;
+  t[0] = t10 + o3;
+  t[7] = t10 - o3;
+  t[1] = t11 + o2;
+  t[6] = t11 - o2;
+  t[2] = t12 + o1;
+  t[5] = t12 - o1;
+  t[3] = t13 + o0;
+  t[4] = t13 - o0;
+}
+
+// libjpeg range_limit[(x) & RANGE_MASK] after the final descale: wrap mod 1024, +128, clamp.
+__device__ __forceinline__ uint32_t islow_range_limit(int32_t v) {
+  const int32_t w = ((v + 512) & 1023) - 384;
+  return uint32_t(w < 0 ? 0 : (w > 255 ? 255 : w));
+}
+
+// pass 1 (columns) on v in place, then pass 2 (rows) into o.
+__device__ __forceinline__ void idct_islow_block(int32_t (&v)[64], uint8_t (&o)[64]) {
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    int32_t t[8];
+    islow_1d(v[c], v[8 + c], v[16 + c], v[24 + c], v[32 + c], v[40 + c], v[48 + c], v[56 + c], t);
+#pragma unroll
+    for (int r = 0; r < 8; r++) v[r * 8 + c] = (t[r] + 1024) >> 11;  // DESCALE(, CONST_BITS-PASS1_BITS)
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    int32_t t[8];
+    islow_1d(v[r * 8], v[r * 8 + 1], v[r * 8 + 2], v[r * 8 + 3], v[r * 8 + 4], v[r * 8 + 5], v[r * 8 + 6],
+             v[r * 8 + 7], t);
+#pragma unroll
+    for (int x = 0; x < 8; x++) o[r * 8 + x] = uint8_t(islow_range_limit((t[x] + (1 << 17)) >> 18));
+  }
+}
+
+// Colour conversion of the reference (src/rocjpeg_hip_kernels.cpp:1431-1443, same in every
+// CSC kernel): BT.709-style constants, fmaf order as written there, u8 by v_cvt_pk_u8_f32.
+__device__ __forceinline__ uint32_t cvt_u8(float f) { return __builtin_amdgcn_cvt_pk_u8_f32(f, 0, 0u) & 0xFFu; }
+
+__device__ __forceinline__ void csc_pixel(uint32_t y, uint32_t u, uint32_t v, uint8_t out[3]) {
+  const float fy = float(y), fu = float(u) - 128.0f, fv = float(v) - 128.0f;
+  out[0] = uint8_t(cvt_u8(fmaf(1.5748f, fv, fy)));
+  out[1] = uint8_t(cvt_u8(fmaf(-0.4681f, fv, fmaf(-0.1873f, fu, fy))));
+  out[2] = uint8_t(cvt_u8(fmaf(1.8556f, fu, fy)));
+}
+
+}  // namespace rj

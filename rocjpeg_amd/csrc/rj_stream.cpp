@@ -1,0 +1,363 @@
+// rj_stream.cpp -- host parser (see rj_stream.h).
+#include "rj_stream.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "rj_common.h"
+
+namespace rj {
+
+namespace {
+
+inline uint32_t Be16(const uint8_t *p) { return (uint32_t(p[0]) << 8) | p[1]; }
+
+// rocjpeg_parser.cpp:432-470.  comp[1]/comp[2] are zero for grayscale.
+int ClassifyCss(const StreamInfo &s) {
+  const int h1 = s.comp[0].h, h2 = s.comp[1].h, h3 = s.comp[2].h;
+  const int v1 = s.comp[0].v, v2 = s.comp[1].v, v3 = s.comp[2].v;
+  auto is = [&](int a, int b, int c, int d, int e, int f) {
+    return h1 == a && h2 == b && h3 == c && v1 == d && v2 == e && v3 == f;
+  };
+  if (is(1, 1, 1, 1, 1, 1) || is(2, 2, 2, 2, 2, 2) || is(4, 4, 4, 4, 4, 4)) return kCss444;
+  if (is(1, 1, 1, 2, 1, 1)) return kCss440;
+  if (is(2, 1, 1, 1, 1, 1) || is(2, 1, 1, 2, 2, 2) || is(2, 2, 2, 2, 1, 1)) return kCss422;
+  if (is(2, 1, 1, 2, 1, 1)) return kCss420;
+  if (is(4, 1, 1, 1, 1, 1)) return kCss411;
+  if (is(1, 0, 0, 1, 0, 0) || is(4, 0, 0, 4, 0, 0)) return kCss400;
+  return kCssUnknown;
+}
+
+const uint8_t kZigzagToNatural[64] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+    41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+uint64_t Fnv1a(uint64_t h, const void *p, size_t n) {
+  const uint8_t *b = static_cast<const uint8_t *>(p);
+  for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+  return h;
+}
+
+}  // namespace
+
+bool BuildHuffman(const uint8_t bits[16], const uint8_t *vals, bool is_dc, RjHuffDev *t) {
+  std::memset(t, 0, sizeof(*t));
+  int k = 0, code = 0;
+  for (int l = 1; l <= 16; l++) {
+    const int nb = bits[l - 1];
+    if (nb) {
+      t->valoff[l] = k - code;
+      for (int i = 0; i < nb; i++, k++, code++) {
+        if (l <= RJ_LUT_BITS) {
+          const int shift = RJ_LUT_BITS - l;
+          for (int f = 0; f < (1 << shift); f++)
+            t->fast[(code << shift) | f] = uint16_t((l << 8) | vals[k]);
+        }
+      }
+      t->maxcode16[l] = uint32_t(code) << (16 - l);  // exclusive bound, left-justified
+    } else {
+      t->maxcode16[l] = 0;
+    }
+    if (code > (1 << l)) return false;  // over-subscribed (libjpeg JERR_BAD_HUFF_TABLE)
+    code <<= 1;
+  }
+  if (k > 256) return false;
+  std::memcpy(t->vals, vals, size_t(k));
+  if (is_dc)
+    for (int i = 0; i < k; i++)
+      if (vals[i] > 15) return false;  // libjpeg rejects DC categories > 15
+  return true;
+}
+
+bool Stream::Parse(const uint8_t *d, uint32_t n) {
+  std::lock_guard<std::mutex> lock(mu_);  // rocjpeg_parser.cpp:44
+  ReleaseResident();
+  generation_++;
+  info_ = StreamInfo();
+  plan_ = DecodePlan();
+  plan_.status = -3;
+  StreamInfo &s = info_;
+  if (d == nullptr || n < 4) return false;
+  if (d[0] != 0xFF || d[1] != 0xD8) return false;  // :64-67
+  size_t pos = 2;
+  bool sos = false, dht = false, dqt = false;
+  while (!sos && pos < n) {  // marker walk :74-109, bounds-checked
+    while (pos < n && d[pos] == 0xFF) pos++;
+    if (pos + 3 > n) return false;
+    const uint32_t marker = d[pos++];
+    const size_t seg = pos;
+    const size_t len = Be16(d + seg);
+    const size_t next = seg + len;
+    if (len < 2 || next > n) return false;
+    switch (marker) {
+      case 0xC0: {  // SOF0 :160-207
+        if (len < 8) return false;
+        s.precision = d[seg + 2];
+        s.height = uint16_t(Be16(d + seg + 3));
+        s.width = uint16_t(Be16(d + seg + 5));
+        s.ncomp = d[seg + 7];
+        if (s.ncomp > 3) return false;
+        if (len < 8 + 3u * s.ncomp) return false;
+        for (int i = 0; i < s.ncomp; i++) {
+          const uint8_t *c = d + seg + 8 + 3 * i;
+          s.comp[i].id = c[0];
+          if (c[2] >= 4) return false;
+          s.comp[i].h = c[1] >> 4;
+          s.comp[i].v = c[1] & 15;
+          s.comp[i].tq = c[2];
+        }
+        const uint32_t hf = s.comp[0].h, vf = s.comp[0].v;
+        if (hf && vf) s.num_mcus = ((s.width + hf * 8 - 1) / (hf * 8)) * ((s.height + vf * 8 - 1) / (vf * 8));
+        s.css = ClassifyCss(s);
+        s.sof_seen = true;
+        break;
+      }
+      case 0xC4: {  // DHT :256-313
+        long left = long(len) - 2;
+        size_t p = seg + 2;
+        while (left > 0) {
+          if (p + 17 > next) return false;
+          const uint32_t idx = d[p++];
+          const uint32_t id = idx & 15;
+          const bool ac = (idx & 0xF0) != 0;
+          if (id >= 2) return false;
+          uint32_t cnt = 0;
+          for (int i = 0; i < 16; i++) cnt += d[p + i];
+          std::memcpy(ac ? s.ht[id].ac_bits : s.ht[id].dc_bits, d + p, 16);
+          p += 16;
+          if (p + cnt > next) return false;
+          if (cnt > (ac ? 162u : 12u)) return false;
+          std::memcpy(ac ? s.ht[id].ac_vals : s.ht[id].dc_vals, d + p, cnt);
+          s.ht_loaded[id] = 1;
+          left -= 17 + long(cnt);
+          p += cnt;
+        }
+        dht = true;
+        break;
+      }
+      case 0xDB: {  // DQT :217-246 (8-bit tables only)
+        size_t p = seg + 2;
+        while (p < next) {
+          const uint32_t idx = d[p++];
+          if (idx >> 4) return false;
+          if (idx >= 4) return false;
+          if (p + 64 > n) return false;
+          std::memcpy(s.qt_zz[idx], d + p, 64);
+          s.qt_loaded[idx] = 1;
+          p += 64;
+        }
+        dqt = true;
+        break;
+      }
+      case 0xDD:  // DRI :374-390
+        if (len != 4) return false;
+        s.restart_interval = uint16_t(Be16(d + seg + 2));
+        break;
+      case 0xDA: {  // SOS :324-363
+        const uint32_t ns = d[seg + 2];
+        if (ns > 3) return false;
+        if (len < 6 + 2 * ns) return false;
+        s.scan_ncomp = uint8_t(ns);
+        for (uint32_t i = 0; i < ns; i++) {
+          const uint32_t cs = d[seg + 3 + 2 * i], t = d[seg + 4 + 2 * i];
+          s.scomp[i].cs = uint8_t(cs);
+          s.scomp[i].td = uint8_t(t >> 4);
+          s.scomp[i].ta = uint8_t(t & 15);
+          if ((t & 15) >= 4 || (t >> 4) >= 4) return false;
+          if (cs != s.comp[i].id) return false;
+        }
+        sos = true;
+        break;
+      }
+      default:
+        break;
+    }
+    pos = next;
+  }
+  if (!dht || !dqt) return false;  // :111-118
+  // ParseEOI (:400-416): the entropy-coded segment runs to the first FF D9.
+  size_t end = n;
+  if (sos) {
+    const uint8_t *p = d + pos;
+    while (true) {
+      p = static_cast<const uint8_t *>(std::memchr(p, 0xFF, size_t(d + n - p)));
+      if (p == nullptr || p + 1 >= d + n) break;
+      if (p[1] == 0xD9) { end = size_t(p - d); break; }
+      p++;
+    }
+  }
+  s.ecs = d + (sos ? pos : n);
+  s.ecs_size = sos ? uint32_t(end - pos) : 0;
+  BuildPlan();
+  return true;
+}
+
+void Stream::BuildPlan() {
+  const StreamInfo &s = info_;
+  DecodePlan &p = plan_;
+  p.status = 0;
+  // what the reference's SubmitDecode rejects (rocjpeg_vaapi_decoder.cpp:586-592, 612-636),
+  // plus streams this baseline decoder cannot reconstruct.
+  if (!s.sof_seen || s.ncomp == 0 || s.width < 64 || s.height < 64 || s.width > 16384 || s.height > 16384) {
+    p.status = -4;  // JPEG_NOT_SUPPORTED
+    return;
+  }
+  if (!(s.css == kCss444 || s.css == kCss440 || s.css == kCss422 || s.css == kCss420 || s.css == kCss400)) {
+    p.status = -4;
+    return;
+  }
+  if (s.precision != 8 || s.scan_ncomp != s.ncomp) {
+    p.status = -4;
+    return;
+  }
+  const int nc = s.ncomp;
+  p.hmax = p.vmax = 1;
+  for (int c = 0; c < nc; c++) {
+    if (s.comp[c].h < 1 || s.comp[c].h > 4 || s.comp[c].v < 1 || s.comp[c].v > 4) { p.status = -3; return; }
+    p.hmax = std::max(p.hmax, s.comp[c].h);
+    p.vmax = std::max(p.vmax, s.comp[c].v);
+  }
+  p.interleaved = nc > 1;
+  if (p.interleaved) {
+    p.mcux = (s.width + 8u * p.hmax - 1) / (8u * p.hmax);
+    p.mcuy = (s.height + 8u * p.vmax - 1) / (8u * p.vmax);
+    int b = 0;
+    for (int c = 0; c < nc; c++) {
+      p.comp_blk0[c] = uint8_t(b);
+      p.wblk[c] = p.mcux * s.comp[c].h;
+      p.hblk[c] = p.mcuy * s.comp[c].v;
+      for (int y = 0; y < s.comp[c].v; y++)
+        for (int x = 0; x < s.comp[c].h; x++) {
+          if (b >= RJ_MAX_BLK_MCU) { p.status = -3; return; }
+          p.blk_comp[b] = uint8_t(c);
+          p.blk_dx[b] = uint8_t(x);
+          p.blk_dy[b] = uint8_t(y);
+          b++;
+        }
+    }
+    p.nblk_mcu = uint8_t(b);
+  } else {
+    const uint32_t cw = (s.width * s.comp[0].h + p.hmax - 1) / p.hmax;
+    const uint32_t ch = (s.height * s.comp[0].v + p.vmax - 1) / p.vmax;
+    p.wblk[0] = (cw + 7) / 8;
+    p.hblk[0] = (ch + 7) / 8;
+    p.mcux = p.wblk[0];
+    p.mcuy = p.hblk[0];
+    p.nblk_mcu = 1;
+  }
+  // tables
+  uint64_t h = 1469598103934665603ull;
+  for (int c = 0; c < nc; c++) {
+    const int td = s.scomp[c].td, ta = s.scomp[c].ta, tq = s.comp[c].tq;
+    if (td >= 2 || ta >= 2 || !s.ht_loaded[td] || !s.ht_loaded[ta] || !s.qt_loaded[tq]) { p.status = -3; return; }
+  }
+  for (int t = 0; t < 2; t++) {
+    if (!s.ht_loaded[t]) continue;
+    if (!BuildHuffman(s.ht[t].dc_bits, s.ht[t].dc_vals, true, &p.tables.dc[t]) ||
+        !BuildHuffman(s.ht[t].ac_bits, s.ht[t].ac_vals, false, &p.tables.ac[t])) {
+      // only fatal when the scan actually uses this table
+      for (int c = 0; c < nc; c++)
+        if (s.scomp[c].td == t || s.scomp[c].ta == t) { p.status = -3; return; }
+    }
+  }
+  for (int q = 0; q < 4; q++)
+    for (int k = 0; k < 64; k++) p.tables.q[q][kZigzagToNatural[k]] = s.qt_zz[q][k];
+  h = Fnv1a(h, &p.tables, sizeof(p.tables));
+  p.table_hash = h;
+
+  // Restart-interval table: split the ECS at RSTn markers (FF D0..D7).  Fill FFs in front
+  // of a marker are excluded; FF 00 stays (the destuff kernel removes the 00).
+  const uint32_t total_mcus = p.mcux * p.mcuy;
+  const uint32_t ri = s.restart_interval;
+  const uint32_t expected = ri ? (total_mcus + ri - 1) / ri : 1;
+  p.segs.reserve(expected);
+  const uint8_t *e = s.ecs;
+  const uint32_t n = s.ecs_size;
+  uint32_t start = 0, i = 0;
+  uint64_t dst = 0;
+  auto emit = [&](uint32_t b, uint32_t stop) {
+    while (stop > b && e[stop - 1] == 0xFF) stop--;  // trailing fill
+    if (p.segs.size() >= expected) return;
+    RjSegDev sg;
+    sg.src_off = b;
+    sg.src_len = stop - b;
+    sg.dst_off = uint32_t(dst);
+    sg.mcu_first = uint32_t(p.segs.size()) * (ri ? ri : total_mcus);
+    sg.mcu_count = ri ? std::min(ri, total_mcus - sg.mcu_first) : total_mcus;
+    sg.flags = 0;
+    dst += (uint64_t(sg.src_len) + 16 + 15) & ~uint64_t(15);  // >= 16 B of slack after each interval
+    p.segs.push_back(sg);
+  };
+  // Any other marker inside an interval ends its data (a decoder reads zero bits past a
+  // marker, libjpeg jdhuff.c fill_bit_buffer); the interval itself still ends at the next RST.
+  uint32_t cut = UINT32_MAX;
+  while (i + 1 < n) {
+    const uint8_t *f = static_cast<const uint8_t *>(std::memchr(e + i, 0xFF, n - i));
+    if (f == nullptr) break;
+    i = uint32_t(f - e);
+    if (i + 1 >= n) break;
+    const uint8_t m = e[i + 1];
+    if (m == 0x00) {
+      i += 2;
+    } else if (m == 0xFF) {
+      i += 1;
+    } else if (ri && m >= 0xD0 && m <= 0xD7) {
+      emit(start, std::min(i, cut));
+      start = i + 2;
+      cut = UINT32_MAX;
+      i += 2;
+    } else {
+      if (cut == UINT32_MAX) cut = i;
+      i += 2;
+    }
+  }
+  emit(start, std::min(n, cut));
+  while (p.segs.size() < expected) {  // intervals whose RST marker never came: zero blocks
+    RjSegDev sg;
+    sg.src_off = n;
+    sg.src_len = 0;
+    sg.dst_off = uint32_t(dst);
+    sg.mcu_first = uint32_t(p.segs.size()) * ri;
+    sg.mcu_count = std::min(ri, total_mcus - sg.mcu_first);
+    sg.flags = RJ_SEG_MISSING;
+    dst += 16;
+    p.segs.push_back(sg);
+  }
+  p.destuff_bytes = dst;
+}
+
+void Stream::ReleaseResident() {
+  if (resident.device >= 0) {
+    int cur = 0;
+    if (hipGetDevice(&cur) == hipSuccess) {
+      (void)hipSetDevice(resident.device);
+      (void)hipFree(resident.ecs);
+      (void)hipFree(resident.segs);
+      (void)hipSetDevice(cur);
+    }
+  }
+  resident = Resident();
+}
+
+int ImageInfo(const StreamInfo &s, uint8_t *nc, int *css, uint32_t *w, uint32_t *h) {
+  if (!nc || !css || !w || !h) return -2;
+  *nc = s.ncomp;
+  w[0] = s.width;
+  h[0] = s.height;
+  w[3] = h[3] = 0;
+  switch (s.css) {
+    case kCss444: *css = 0; w[2] = w[1] = w[0]; h[2] = h[1] = h[0]; break;
+    case kCss440: *css = 1; w[2] = w[1] = w[0]; h[2] = h[1] = h[0] >> 1; break;
+    case kCss422: *css = 2; w[2] = w[1] = w[0] >> 1; h[2] = h[1] = h[0]; break;
+    case kCss420: *css = 3; w[2] = w[1] = w[0] >> 1; h[2] = h[1] = h[0] >> 1; break;
+    case kCss400: *css = 5; w[3] = w[2] = w[1] = 0; h[3] = h[2] = h[1] = 0; break;
+    case kCss411: *css = 4; w[2] = w[1] = w[0] >> 2; h[2] = h[1] = h[0]; break;
+    default: *css = -1; break;
+  }
+  return 0;
+}
+
+}  // namespace rj

@@ -1,0 +1,88 @@
+// rj_stream.h -- host JPEG bitstream parser behind rocJpegStreamParse.
+//
+// Replaces RocJpegStreamParser (reference src/rocjpeg_parser.{h,cpp}): same acceptance
+// rules and the same fields (so GetImageInfo and every error path behave identically),
+// plus what the GPU decoder needs and the VCN path never built on the host:
+//   * the restart-interval table (RST scan folded into the FFD9 scan the reference already
+//     does in ParseEOI, rocjpeg_parser.cpp:400-416),
+//   * MCU geometry, canonical Huffman LUTs and natural-order quant tables (RjTableSet).
+#pragma once
+#include <stdint.h>
+
+#include <mutex>
+#include <vector>
+
+#include "rj_device.h"
+
+namespace rj {
+
+// ChromaSubsampling of the reference parser (src/rocjpeg_parser.h:148-156).
+enum Css { kCss444 = 0, kCss440 = 1, kCss422 = 2, kCss420 = 3, kCss411 = 4, kCss400 = 5, kCssUnknown = -1 };
+
+struct StreamInfo {
+  // --- fields the reference parser fills (src/rocjpeg_parser.h:62-172) ---
+  uint16_t width = 0, height = 0;
+  uint8_t precision = 0, ncomp = 0;
+  struct { uint8_t id, h, v, tq; } comp[4] = {};
+  uint8_t qt_loaded[4] = {};
+  uint8_t qt_zz[4][64] = {};
+  uint8_t ht_loaded[2] = {};
+  struct { uint8_t dc_bits[16], dc_vals[12], ac_bits[16], ac_vals[162]; } ht[2] = {};
+  uint8_t scan_ncomp = 0;
+  struct { uint8_t cs, td, ta; } scomp[4] = {};
+  uint16_t restart_interval = 0;
+  uint32_t num_mcus = 0;
+  const uint8_t *ecs = nullptr;   // borrowed from the caller (rocjpeg_parser.cpp:413)
+  uint32_t ecs_size = 0;
+  int css = kCssUnknown;
+  bool sof_seen = false;
+};
+
+// Everything the batch planner needs to decode this stream on the GPU.
+struct DecodePlan {
+  int status = 0;  // RocJpegStatus the decode call returns for this stream (0 = decodable)
+  uint32_t mcux = 0, mcuy = 0;
+  uint8_t hmax = 1, vmax = 1, nblk_mcu = 0, interleaved = 0;
+  uint8_t blk_comp[RJ_MAX_BLK_MCU] = {}, blk_dx[RJ_MAX_BLK_MCU] = {}, blk_dy[RJ_MAX_BLK_MCU] = {};
+  uint8_t comp_blk0[4] = {};
+  uint32_t wblk[4] = {}, hblk[4] = {};
+  std::vector<RjSegDev> segs;      // one per restart interval
+  uint64_t destuff_bytes = 0;      // destuffed buffer size incl. per-interval alignment
+  RjTableSet tables;               // derived tables
+  uint64_t table_hash = 0;         // de-duplication key for tables
+};
+
+class Stream {
+ public:
+  // RocJpegStreamParser::ParseJpegStream semantics; true = parsed (else BAD_JPEG).
+  bool Parse(const uint8_t *data, uint32_t size);
+  const StreamInfo &info() const { return info_; }
+  const DecodePlan &plan() const { return plan_; }
+  uint64_t generation() const { return generation_; }
+  std::mutex &mutex() { return mu_; }
+
+  // Device-resident copy of the ECS bytes + interval table (rocJpegAmdStreamsToDevice).
+  struct Resident {
+    int device = -1;
+    uint64_t generation = 0;
+    uint8_t *ecs = nullptr;
+    RjSegDev *segs = nullptr;
+  } resident;
+  void ReleaseResident();
+  ~Stream() { ReleaseResident(); }
+
+ private:
+  void BuildPlan();
+  StreamInfo info_;
+  DecodePlan plan_;
+  uint64_t generation_ = 0;
+  std::mutex mu_;
+};
+
+// GetImageInfo restatement (rocjpeg_decoder.cpp:307-358); returns RocJpegStatus.
+int ImageInfo(const StreamInfo &s, uint8_t *num_components, int *subsampling, uint32_t *widths, uint32_t *heights);
+
+// Canonical Huffman table -> RjHuffDev; false for an invalid table.
+bool BuildHuffman(const uint8_t bits[16], const uint8_t *vals, bool is_dc, RjHuffDev *out);
+
+}  // namespace rj

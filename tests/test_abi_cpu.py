@@ -1,0 +1,96 @@
+"""C-ABI checks that need no GPU: the library loads, exports exactly what include/*.h
+declares, and the host parser behind rocJpegStreamParse agrees with the reference parser
+(src/rocjpeg_parser.cpp, recorded per fixture in tests/golden/manifest.json)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import rocjpeg_amd as R
+from tests import oracle_lib as O
+
+INCLUDE = os.path.join(O.ROOT, "include")
+
+
+def declared_functions():
+    names = set()
+    for h in ("rocjpeg.h", "rocjpeg_amd.h"):
+        src = open(os.path.join(INCLUDE, h)).read()
+        names |= set(re.findall(r"\b(rocJpeg\w+)\s*\(", src))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    L = R.lib()
+    declared = declared_functions()
+    assert set(R.API_SYMBOLS) <= declared
+    for name in declared:
+        assert hasattr(L, name), name
+
+
+def test_error_names_match_reference_strings():
+    # rocjpeg_api.cpp:246-277
+    for st in R.Status:
+        assert R.error_name(st) == "ROCJPEG_STATUS_" + st.name
+    assert R.error_name(-99) == "UNKNOWN_ERROR"
+
+
+def test_null_arguments_are_invalid_parameter():
+    L = R.lib()
+    assert L.rocJpegStreamCreate(None) == R.Status.INVALID_PARAMETER
+    assert L.rocJpegStreamParse(None, 0, None) == R.Status.INVALID_PARAMETER
+    assert L.rocJpegStreamDestroy(None) == R.Status.INVALID_PARAMETER
+    assert L.rocJpegCreate(0, 0, None) == R.Status.INVALID_PARAMETER
+    assert L.rocJpegDestroy(None) == R.Status.INVALID_PARAMETER
+    assert L.rocJpegDecode(None, None, None, None) == R.Status.INVALID_PARAMETER
+    assert L.rocJpegDecodeBatched(None, None, 0, None, None) == R.Status.INVALID_PARAMETER
+    assert L.rocJpegGetImageInfo(None, None, None, None, None, None) == R.Status.INVALID_PARAMETER
+
+
+@pytest.mark.parametrize("ent", O.manifest(), ids=[f["name"] for f in O.manifest()])
+def test_stream_parse_matches_reference_parser(ent):
+    data = O.fixture_bytes(ent)
+    s = R.JpegStream()
+    st = s.try_parse(data)
+    ref = ent["ref_parse"]
+    assert (st == R.Status.SUCCESS) == bool(ref["ok"])
+    if st != R.Status.SUCCESS:
+        assert st == R.Status.BAD_JPEG
+        return
+    info = s.info()
+    assert info["num_components"] == ref["ncomp"]
+    assert info["subsampling"] == ref["css"]
+    w, h = ref["width"], ref["height"]
+    assert info["widths"][0] == w and info["heights"][0] == h
+    css = ref["css"]
+    expect_w1 = {0: w, 1: w, 2: w >> 1, 3: w >> 1, 4: w >> 2, 5: 0}.get(css, None)
+    expect_h1 = {0: h, 1: h >> 1, 2: h, 3: h >> 1, 4: h, 5: 0}.get(css, None)
+    if expect_w1 is not None:  # GetImageInfo, rocjpeg_decoder.cpp:321-355
+        assert info["widths"][1:3] == [expect_w1] * 2 and info["heights"][1:3] == [expect_h1] * 2
+    ri = ref["restart_interval"]
+    if ri and "libjpeg_coef_sha256" in ent:
+        assert info["restart_intervals"] == -(-ref["num_mcus"] // ri)
+
+
+def test_truncated_and_garbage_streams():
+    s = R.JpegStream()
+    assert s.try_parse(b"\xff\xd8") == R.Status.BAD_JPEG
+    assert s.try_parse(b"\x00" * 64) == R.Status.BAD_JPEG
+    good = O.fixture_bytes(O.manifest()[0])
+    for cut in (3, 20, 100, 400):
+        assert s.try_parse(good[:cut]) in (R.Status.BAD_JPEG, R.Status.SUCCESS)
+
+
+def test_create_without_gpu_fails_cleanly():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except ImportError:
+        pass
+    h = ctypes.c_void_p()
+    st = R.lib().rocJpegCreate(0, 0, ctypes.byref(h))
+    assert st in (R.Status.EXECUTION_FAILED, R.Status.NOT_INITIALIZED)
+    if h:
+        R.lib().rocJpegDestroy(h)
