@@ -582,6 +582,10 @@ uint8_t oj_cvt_u8(float f) {
   return (uint8_t)r;
 }
 
+void oj_csc_bulk(const uint8_t *y, const uint8_t *u, const uint8_t *v, size_t n, uint8_t *rgb) {
+  for (size_t i = 0; i < n; i++) oj_csc_pixel(y[i], u[i], v[i], rgb + 3 * i);
+}
+
 void oj_csc_pixel(uint8_t y, uint8_t u, uint8_t v, uint8_t rgb[3]) {
   float fy = (float)y, fu = (float)u - 128.0f, fv = (float)v - 128.0f;
   rgb[0] = oj_cvt_u8(fmaf(1.5748f, fv, fy));

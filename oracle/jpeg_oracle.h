@@ -72,6 +72,7 @@ int oj_decode(const uint8_t *data, size_t len, int output_format,
 
 /* One pixel of the reference colour conversion (rocjpeg_hip_kernels.cpp:1431-1443). */
 void oj_csc_pixel(uint8_t y, uint8_t u, uint8_t v, uint8_t rgb[3]);
+void oj_csc_bulk(const uint8_t *y, const uint8_t *u, const uint8_t *v, size_t n, uint8_t *rgb);
 /* v_cvt_pk_u8_f32 semantics restated: RNE, saturate to [0,255] (NaN -> 0). */
 uint8_t oj_cvt_u8(float f);
 
