@@ -13,6 +13,40 @@ namespace {
 
 inline uint64_t AlignUp(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
+// Can the fused kernel (rj_fused.hip) produce exactly what the reference semantics ask for?
+// It handles the whole-image output window of RGB / RGB_PLANAR / Y / YUV_PLANAR for the
+// canonical sampling geometry of each subsampling class.  ROI crops (with the reference's
+// offset quirks), NATIVE layouts and "pitch > width" copies go to the general path.
+bool FusedEligible(const StreamInfo &in, const DecodePlan &p, int fmt, bool roi, const RocJpegImage &o) {
+  if (roi) return false;
+  if (!(fmt == ROCJPEG_OUTPUT_RGB || fmt == ROCJPEG_OUTPUT_RGB_PLANAR || fmt == ROCJPEG_OUTPUT_Y ||
+        fmt == ROCJPEG_OUTPUT_YUV_PLANAR))
+    return false;
+  const int css = in.css;
+  if (in.ncomp == 1) {
+    if (css != kCss400) return false;
+  } else {
+    if (in.ncomp != 3) return false;
+    if (in.comp[0].h != p.hmax || in.comp[0].v != p.vmax) return false;
+    if (in.comp[1].h != in.comp[2].h || in.comp[1].v != in.comp[2].v) return false;
+    const int rh = p.hmax / in.comp[1].h, rv = p.vmax / in.comp[1].v;
+    if (p.hmax % in.comp[1].h || p.vmax % in.comp[1].v || rh > 2 || rv > 2) return false;
+    const bool ok = (css == kCss444 && rh == 1 && rv == 1) || (css == kCss440 && rh == 1 && rv == 2) ||
+                    (css == kCss422 && rh == 2 && rv == 1) || (css == kCss420 && rh == 2 && rv == 2);
+    if (!ok) return false;
+  }
+  const uint32_t W = in.width;
+  if (8u * p.hmax > 256) return false;
+  // copy-type channels write `pitch` bytes per row in the reference: only pitch == width is fused
+  if ((fmt == ROCJPEG_OUTPUT_Y || fmt == ROCJPEG_OUTPUT_YUV_PLANAR) && css != kCss422 && o.pitch[0] != W) return false;
+  if (fmt == ROCJPEG_OUTPUT_YUV_PLANAR && in.ncomp == 3) {
+    if (css == kCss444 || css == kCss440) {
+      if (o.pitch[1] != W || o.pitch[2] != W) return false;
+    }
+  }
+  return true;
+}
+
 }  // namespace
 
 int DeviceBuffer::Ensure(size_t bytes) {
@@ -176,6 +210,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   uint32_t seg_total = 0, blk_total = 0, rows_total = 0;
   uint64_t ecs_bytes = 0, out_bytes = 0;
   std::vector<uint64_t> stage_off(n, UINT64_MAX);
+  std::vector<uint32_t> strip_prefix(n);
+  uint32_t strip_total = 0, fused_images = 0;
   for (int i = 0; i < n; i++) {
     Stream *s = streams[i];
     const StreamInfo &in = s->info();
@@ -216,9 +252,6 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     for (int c = 0; c < in.ncomp; c++) {
       d.plane_pitch[c] = p.wblk[c] * 8;
       d.plane_rows[c] = p.hblk[c] * 8;
-      d.plane_off[c] = plane_bytes;
-      plane_bytes += AlignUp(uint64_t(d.plane_pitch[c]) * d.plane_rows[c], 256);
-      blk_total += p.wblk[c] * p.hblk[c];
     }
     ecs_bytes += in.ecs_size;
     if (!(s->resident.device == device_ && s->resident.generation == s->generation())) {
@@ -240,8 +273,11 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       d.dst[c] = o.channel[c];
       d.dst_pitch[c] = o.pitch[c];
     }
+    strip_prefix[i] = strip_total;
 
     // ---- output jobs (general path): rocjpeg_decoder.cpp:143-180 ----
+    const size_t jobs_before = jobs.size();
+    const uint32_t jobs_rows_before = rows_total;
     const int css = in.css;
     const int32_t pw = d.out_w, ph = d.out_h, top = d.top, left = d.left;
     auto need = [&](int c) { return o.channel[c] != nullptr; };
@@ -320,13 +356,28 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       default:
         break;  // reference: unknown format writes nothing and succeeds
     }
+    // fast path: drop the general jobs again and count fused strips instead
+    if (path_policy_ == 0 && FusedEligible(in, p, fmt, roi, o)) {
+      rows_total -= jobs_rows_before;
+      jobs.resize(jobs_before);
+      const uint32_t S = 256 / (8u * p.hmax);
+      strip_total += ((p.mcux + S - 1) / S) * p.mcuy;
+      fused_images++;
+    } else {
+      for (int c = 0; c < in.ncomp; c++) {
+        d.plane_off[c] = plane_bytes;
+        plane_bytes += AlignUp(uint64_t(d.plane_pitch[c]) * d.plane_rows[c], 256);
+        blk_total += p.wblk[c] * p.hblk[c];
+      }
+    }
   }
 
   // ---- one host->device upload: descriptors + non-resident bitstreams ----
   const uint64_t off_imgs = 0;
   const uint64_t off_tabs = AlignUp(off_imgs + n * sizeof(RjImageDev), 256);
   const uint64_t off_jobs = AlignUp(off_tabs + tabs.size() * sizeof(RjTableSet), 256);
-  const uint64_t off_stage = AlignUp(off_jobs + std::max<size_t>(jobs.size(), 1) * sizeof(RjJobDev), 256);
+  const uint64_t off_strips = AlignUp(off_jobs + std::max<size_t>(jobs.size(), 1) * sizeof(RjJobDev), 256);
+  const uint64_t off_stage = AlignUp(off_strips + n * sizeof(uint32_t), 256);
   const uint64_t blob = off_stage + stage_bytes;
   RJ_CHECK(h_stage_.Ensure(blob));
   RJ_CHECK(d_desc_.Ensure(blob));
@@ -355,6 +406,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   std::memcpy(h + off_imgs, imgs.data(), n * sizeof(RjImageDev));
   for (size_t t = 0; t < tabs.size(); t++) std::memcpy(h + off_tabs + t * sizeof(RjTableSet), tabs[t], sizeof(RjTableSet));
   if (!jobs.empty()) std::memcpy(h + off_jobs, jobs.data(), jobs.size() * sizeof(RjJobDev));
+  std::memcpy(h + off_strips, strip_prefix.data(), n * sizeof(uint32_t));
+  const uint32_t *d_strips = reinterpret_cast<const uint32_t *>(dbase + off_strips);
 
   const RjImageDev *d_imgs = reinterpret_cast<const RjImageDev *>(dbase + off_imgs);
   const RjTableSet *d_tabs = reinterpret_cast<const RjTableSet *>(dbase + off_tabs);
@@ -368,6 +421,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   RJ_HIP(LaunchHuffman(stream_, d_imgs, n, seg_total, d_destuff_.as<uint8_t>(), d_seglen_.as<uint32_t>(), d_tabs,
                        d_coefs_.as<int16_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
+  RJ_HIP(LaunchFusedOutput(stream_, d_imgs, n, d_strips, strip_total, d_coefs_.as<int16_t>(), d_tabs));
   RJ_HIP(LaunchIdctPlanes(stream_, d_imgs, n, blk_total, d_coefs_.as<int16_t>(), d_tabs, d_planes_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[4], stream_));
   RJ_HIP(LaunchOutputJobs(stream_, d_imgs, d_jobs, int(jobs.size()), rows_total, d_planes_.as<uint8_t>()));
@@ -379,6 +433,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   timings_.ecs_bytes = ecs_bytes;
   timings_.coef_bytes = coef_blocks * 128;
   timings_.output_bytes = out_bytes;
+  timings_.fused_images = fused_images;
   if (profiling_) {
     float ms[5];
     for (int k = 0; k < 5; k++) RJ_HIP(hipEventElapsedTime(&ms[k], ev_[k], ev_[k + 1]));

@@ -88,11 +88,20 @@ __device__ __forceinline__ void idct_islow_block(int32_t (&v)[64], uint8_t (&o)[
 // CSC kernel): BT.709-style constants, fmaf order as written there, u8 by v_cvt_pk_u8_f32.
 __device__ __forceinline__ uint32_t cvt_u8(float f) { return __builtin_amdgcn_cvt_pk_u8_f32(f, 0, 0u) & 0xFFu; }
 
-__device__ __forceinline__ void csc_pixel(uint32_t y, uint32_t u, uint32_t v, uint8_t out[3]) {
+// R | G << 8 | B << 16, packed by v_cvt_pk_u8_f32 exactly as the reference's hipPack does.
+__device__ __forceinline__ uint32_t csc_pixel_packed(uint32_t y, uint32_t u, uint32_t v) {
   const float fy = float(y), fu = float(u) - 128.0f, fv = float(v) - 128.0f;
-  out[0] = uint8_t(cvt_u8(fmaf(1.5748f, fv, fy)));
-  out[1] = uint8_t(cvt_u8(fmaf(-0.4681f, fv, fmaf(-0.1873f, fu, fy))));
-  out[2] = uint8_t(cvt_u8(fmaf(1.8556f, fu, fy)));
+  const float r = fmaf(1.5748f, fv, fy);
+  const float g = fmaf(-0.4681f, fv, fmaf(-0.1873f, fu, fy));
+  const float b = fmaf(1.8556f, fu, fy);
+  return __builtin_amdgcn_cvt_pk_u8_f32(b, 2, __builtin_amdgcn_cvt_pk_u8_f32(g, 1, __builtin_amdgcn_cvt_pk_u8_f32(r, 0, 0u)));
+}
+
+__device__ __forceinline__ void csc_pixel(uint32_t y, uint32_t u, uint32_t v, uint8_t out[3]) {
+  const uint32_t p = csc_pixel_packed(y, u, v);
+  out[0] = uint8_t(p);
+  out[1] = uint8_t(p >> 8);
+  out[2] = uint8_t(p >> 16);
 }
 
 }  // namespace rj

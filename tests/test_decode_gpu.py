@@ -14,11 +14,13 @@ SMALL = [f for f in DECODABLE if f["bytes"] < 100_000]
 FORMATS = list(R.OutputFormat)
 
 
-@pytest.fixture(scope="module")
-def dec():
+@pytest.fixture(scope="module", params=[0, 1], ids=["auto_path", "general_path"])
+def dec(request):
+    """policy 0: fused K2 wherever the output window allows it; 1: always the general path."""
     from tests import gpu_util as G
     G.torch()
     d = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    d.set_path_policy(request.param)
     yield d
     d.close()
 
