@@ -36,7 +36,7 @@ bool FusedEligible(const StreamInfo &in, const DecodePlan &p, int fmt, bool roi,
     if (!ok) return false;
   }
   const uint32_t W = in.width;
-  if (8u * p.hmax > 256) return false;
+  if (8u * p.hmax > 512 || (512u / (8u * p.hmax)) * p.nblk_mcu > 256) return false;  // strip limits of k_fused
   // copy-type channels write `pitch` bytes per row in the reference: only pitch == width is fused
   if ((fmt == ROCJPEG_OUTPUT_Y || fmt == ROCJPEG_OUTPUT_YUV_PLANAR) && css != kCss422 && o.pitch[0] != W) return false;
   if (fmt == ROCJPEG_OUTPUT_YUV_PLANAR && in.ncomp == 3) {
@@ -358,9 +358,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
     // fast path: drop the general jobs again and count fused strips instead
     if (path_policy_ == 0 && FusedEligible(in, p, fmt, roi, o)) {
-      rows_total -= jobs_rows_before;
+      rows_total = jobs_rows_before;
       jobs.resize(jobs_before);
-      const uint32_t S = 256 / (8u * p.hmax);
+      const uint32_t S = 512 / (8u * p.hmax);  // MCUs per k_fused strip (RJ_STRIP_PX)
       strip_total += ((p.mcux + S - 1) / S) * p.mcuy;
       fused_images++;
     } else {

@@ -1,15 +1,21 @@
 // rj_fused.hip -- K2 fused output kernel: dequant + ISLOW IDCT + nearest chroma upsample +
 // YUV->RGB (or planar layouts) straight from the coefficient blocks to the caller's buffers.
 //
-// One workgroup (256 threads = 4 waves) per strip: one MCU row x 256 pixels (16 MCUs at
-// 4:2:0).  HBM traffic per strip = its coefficient blocks (read once, contiguous: the MCU-major
-// layout K1 writes) + its output bytes (written once, whole 16-B chunks per lane).
-// LDS per workgroup (4:2:0): 12 KB coefficients aliased by the sample tiles + 24 KB pass-1
-// workspace + quant tables ~= 37 KB -> 4 workgroups per CU.
+// One workgroup (256 threads = 4 waves) per strip = one MCU row x 512 pixels (32 MCUs,
+// 192 blocks at 4:2:0; never more than 256 blocks).
+//   A  coalesced copy of the strip's coefficient blocks (contiguous in K1's MCU-major layout)
+//      into LDS, 16 B per lane, block stride padded to 144 B so that the per-thread
+//      ds_read_b128 of phase B is bank-conflict free (36*l mod 64 distinct for 16 lanes).
+//   B  thread b: block b's 64 coefficients into VGPRs, dequant, full 2-D ISLOW IDCT in
+//      registers, 8 x 8-byte rows into the strip's component sample tiles (aliasing A).
+//   C  lane = 4 consecutive pixels: one ds_read_b32 of luma, one ds_read_u16 (4:2:0/4:2:2)
+//      or b32 (4:4:4) per chroma plane, 4 x (4 fma + 3 v_cvt_pk_u8_f32) packed straight
+//      into 3 dwords -> one 12-B store per lane, 768 contiguous bytes per wave instruction.
+// HBM traffic per strip = its coefficient bytes read once + its output bytes written once.
 //
-// Same integer IDCT (rj_math.h islow_1d) and the same CSC (rj_math.h csc_pixel) as the general
-// path, so both paths are bit-identical; eligibility (no ROI, canonical sampling geometry,
-// copy channels with pitch == width) is decided on the host (rj_decoder.cpp).
+// Same integer IDCT (rj_math.h) and CSC arithmetic as the general path, so both paths are
+// bit-identical; eligibility (no ROI, canonical sampling geometry, copy channels with
+// pitch == width) is decided on the host (rj_decoder.cpp FusedEligible).
 #include <hip/hip_runtime.h>
 
 #include "rj_device.h"
@@ -18,199 +24,240 @@
 
 namespace rj {
 
-#define RJ_STRIP_PX 256
-#define RJ_MAX_STRIP_BLK 128
+#define RJ_STRIP_PX 512
+#define RJ_MAX_STRIP_BLK 256
+#define RJ_BLK_STRIDE 144  // bytes per staged block in LDS (128 + 16 pad)
+
+// byte b of w as float: the backend selects v_cvt_f32_ubyte{0..3} for this pattern
+__device__ __forceinline__ float u8f(uint32_t w, int b) { return float((w >> (8 * b)) & 255u); }
+
+// 4 pixels -> 12 bytes RGB.  y4: 4 luma bytes; u/v: per-pixel chroma as float minus 128.
+// Arithmetic and packing order exactly as rocjpeg_hip_kernels.cpp:1431-1443 / :25-30.
+__device__ __forceinline__ void csc4(uint32_t y4, const float (&u)[4], const float (&v)[4], uint32_t &d0, uint32_t &d1,
+                                     uint32_t &d2) {
+  float r[4], g[4], b[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const float fy = u8f(y4, j);
+    r[j] = fmaf(1.5748f, v[j], fy);
+    g[j] = fmaf(-0.4681f, v[j], fmaf(-0.1873f, u[j], fy));
+    b[j] = fmaf(1.8556f, u[j], fy);
+  }
+  d0 = __builtin_amdgcn_cvt_pk_u8_f32(r[1], 3, __builtin_amdgcn_cvt_pk_u8_f32(b[0], 2,
+       __builtin_amdgcn_cvt_pk_u8_f32(g[0], 1, __builtin_amdgcn_cvt_pk_u8_f32(r[0], 0, 0u))));
+  d1 = __builtin_amdgcn_cvt_pk_u8_f32(g[2], 3, __builtin_amdgcn_cvt_pk_u8_f32(r[2], 2,
+       __builtin_amdgcn_cvt_pk_u8_f32(b[1], 1, __builtin_amdgcn_cvt_pk_u8_f32(g[1], 0, 0u))));
+  d2 = __builtin_amdgcn_cvt_pk_u8_f32(b[3], 3, __builtin_amdgcn_cvt_pk_u8_f32(g[3], 2,
+       __builtin_amdgcn_cvt_pk_u8_f32(r[3], 1, __builtin_amdgcn_cvt_pk_u8_f32(b[2], 0, 0u))));
+}
+
+__device__ __forceinline__ void store_bytes(uint8_t *d, uint32_t n, const uint32_t *w) {
+#pragma unroll
+  for (int j = 0; j < 12; j++)
+    if (uint32_t(j) < n) d[j] = uint8_t(w[j >> 2] >> (8 * (j & 3)));
+}
 
 __global__ __launch_bounds__(256) void k_fused(const RjImageDev *__restrict__ imgs, int nimg,
                                                const uint32_t *__restrict__ strip_prefix,
                                                const int16_t *__restrict__ coefs,
                                                const RjTableSet *__restrict__ tabsets) {
-  __shared__ __attribute__((aligned(16))) int16_t s_coef[RJ_MAX_STRIP_BLK * 64];  // later: sample tiles
-  __shared__ __attribute__((aligned(16))) int32_t s_ws[RJ_MAX_STRIP_BLK * 64];
-  __shared__ int32_t s_q[3][64];
-  __shared__ uint32_t s_tile_off[3], s_tile_w[3];
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_MAX_STRIP_BLK * RJ_BLK_STRIDE];  // A/B, then tiles
+  __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
 
   const uint32_t tid = threadIdx.x;
   const uint32_t sg = blockIdx.x;
-  const int i = [&] {
+  int i;
+  {
     int lo = 0, hi = nimg - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
       if (strip_prefix[mid] <= sg) lo = mid;
       else hi = mid - 1;
     }
-    return lo;
-  }();
+    i = lo;
+  }
   const RjImageDev &im = imgs[i];
   const uint32_t hmax = im.hmax, vmax = im.vmax;
   const uint32_t mcu_w = 8 * hmax, mcu_h = 8 * vmax;
-  const uint32_t S = RJ_STRIP_PX / mcu_w;               // MCUs per strip
+  const uint32_t S = RJ_STRIP_PX / mcu_w;  // MCUs per strip
   const uint32_t strips_x = (im.mcux + S - 1) / S;
   const uint32_t local = sg - strip_prefix[i];
   const uint32_t my = local / strips_x;
   const uint32_t mx0 = (local - my * strips_x) * S;
-  const uint32_t nm = min(S, im.mcux - mx0);           // MCUs in this strip
+  const uint32_t nm = min(S, im.mcux - mx0);
   const uint32_t nblk = im.nblk_mcu;
-  const uint32_t nb = nm * nblk;                        // blocks in this strip
-  const uint32_t ncomp = im.interleaved ? im.ncomp : 1;
+  const uint32_t nb = nm * nblk;
+  const bool inter = im.interleaved != 0;
+  const uint32_t ncomp = inter ? im.ncomp : 1;
 
-  // ---- quant tables + tile geometry ----
-  const RjTableSet *ts = tabsets + im.tabset;
-  for (uint32_t k = tid; k < ncomp * 64; k += 256) s_q[k >> 6][k & 63] = ts->q[im.comp_tq[k >> 6] & 3][k & 63];
-  if (tid == 0) {
+  // tile geometry (component c: width S*hc*8, height vc*8), all offsets multiples of 8
+  uint32_t tw[3], toff[3];
+  {
     uint32_t off = 0;
-    for (uint32_t c = 0; c < ncomp; c++) {
-      const uint32_t hc = im.interleaved ? im.comp_h[c] : 1, vc = im.interleaved ? im.comp_v[c] : 1;
-      s_tile_w[c] = S * hc * 8;
-      s_tile_off[c] = off;
-      off += S * hc * 8 * vc * 8;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      const bool has = c < int(ncomp);
+      const uint32_t hc = (inter && has) ? im.comp_h[c] : 1, vc = (inter && has) ? im.comp_v[c] : 1;
+      tw[c] = S * hc * 8;
+      toff[c] = off;
+      off += has ? tw[c] * vc * 8 : 0;
     }
   }
-  // ---- phase A: coefficient blocks -> LDS (contiguous, 16 B per lane) ----
+
+  // ---- A: quant tables + coefficient blocks -> LDS ----
+  const RjTableSet *ts = tabsets + im.tabset;
+  for (uint32_t k = tid; k < ncomp * 64; k += 256) s_q[k >> 6][k & 63] = ts->q[im.comp_tq[k >> 6] & 3][k & 63];
   {
     const uint4 *src = reinterpret_cast<const uint4 *>(coefs + (im.coef_off + (uint64_t(my) * im.mcux + mx0) * nblk) * 64u);
-    uint4 *dst = reinterpret_cast<uint4 *>(s_coef);
     const uint32_t n16 = nb * 8;
-    for (uint32_t k = tid; k < n16; k += 256) dst[k] = src[k];
-  }
-  __syncthreads();
-  // ---- phase B1: column pass (block, column) -> s_ws ----
-  for (uint32_t t = tid; t < nb * 8; t += 256) {
-    const uint32_t blk = t >> 3, col = t & 7;
-    const uint32_t c = im.interleaved ? im.blk_comp[blk % nblk] : 0;
-    const int16_t *in = s_coef + blk * 64 + col;
-    const int32_t *q = s_q[c] + col;
-    int32_t o[8];
-    islow_1d(in[0] * q[0], in[8] * q[8], in[16] * q[16], in[24] * q[24], in[32] * q[32], in[40] * q[40],
-             in[48] * q[48], in[56] * q[56], o);
-    int32_t *w = s_ws + blk * 64 + col;
-#pragma unroll
-    for (int r = 0; r < 8; r++) w[r * 8] = (o[r] + 1024) >> 11;
-  }
-  __syncthreads();
-  // ---- phase B2: row pass (block, row) -> sample tiles (aliasing s_coef) ----
-  uint8_t *tiles = reinterpret_cast<uint8_t *>(s_coef);
-  for (uint32_t t = tid; t < nb * 8; t += 256) {
-    const uint32_t blk = t >> 3, row = t & 7;
-    const uint32_t mcu = blk / nblk, b = blk - mcu * nblk;
-    const uint32_t c = im.interleaved ? im.blk_comp[b] : 0;
-    const uint32_t hc = im.interleaved ? im.comp_h[c] : 1;
-    const uint32_t dx = im.interleaved ? im.blk_dx[b] : 0, dy = im.interleaved ? im.blk_dy[b] : 0;
-    const int32_t *w = s_ws + blk * 64 + row * 8;
-    int32_t o[8];
-    islow_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
-    uint2 pk;
-    pk.x = islow_range_limit((o[0] + (1 << 17)) >> 18) | (islow_range_limit((o[1] + (1 << 17)) >> 18) << 8) |
-           (islow_range_limit((o[2] + (1 << 17)) >> 18) << 16) | (islow_range_limit((o[3] + (1 << 17)) >> 18) << 24);
-    pk.y = islow_range_limit((o[4] + (1 << 17)) >> 18) | (islow_range_limit((o[5] + (1 << 17)) >> 18) << 8) |
-           (islow_range_limit((o[6] + (1 << 17)) >> 18) << 16) | (islow_range_limit((o[7] + (1 << 17)) >> 18) << 24);
-    const uint32_t tx = (mcu * hc + dx) * 8, ty = dy * 8 + row;
-    *reinterpret_cast<uint2 *>(tiles + s_tile_off[c] + ty * s_tile_w[c] + tx) = pk;
+    for (uint32_t k = tid; k < n16; k += 256)
+      *reinterpret_cast<uint4 *>(s_buf + (k >> 3) * RJ_BLK_STRIDE + (k & 7) * 16) = src[k];
   }
   __syncthreads();
 
-  // ---- phase C: output ----
-  const uint32_t strip_w = nm * mcu_w;                  // pixels in this strip
+  // ---- B: thread-per-block IDCT in registers ----
+  int32_t v[64];
+  uint32_t c_b = 0, tx = 0, ty = 0;
+  const bool has_blk = tid < nb;
+  if (has_blk) {
+    const uint32_t mcu = tid / nblk, b = tid - mcu * nblk;
+    c_b = inter ? im.blk_comp[b] : 0;
+    const uint32_t hc = inter ? im.comp_h[c_b] : 1;
+    tx = (mcu * hc + (inter ? im.blk_dx[b] : 0)) * 8;
+    ty = (inter ? im.blk_dy[b] : 0) * 8;
+    const uint4 *blk = reinterpret_cast<const uint4 *>(s_buf + tid * RJ_BLK_STRIDE);
+    const uint4 *q4 = reinterpret_cast<const uint4 *>(s_q[c_b]);
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      const uint4 a = blk[r], qa = q4[r];
+      const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, qw[4] = {qa.x, qa.y, qa.z, qa.w};
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        v[r * 8 + 2 * j] = int32_t(int16_t(aw[j] & 0xFFFF)) * int32_t(qw[j] & 0xFFFF);
+        v[r * 8 + 2 * j + 1] = int32_t(int16_t(aw[j] >> 16)) * int32_t(qw[j] >> 16);
+      }
+    }
+  }
+  __syncthreads();  // every block is in registers: the staging area becomes the sample tiles
+  if (has_blk) {
+    uint8_t o[64];
+    idct_islow_block(v, o);
+    const uint32_t twc = c_b == 0 ? tw[0] : (c_b == 1 ? tw[1] : tw[2]);
+    const uint32_t toc = c_b == 0 ? toff[0] : (c_b == 1 ? toff[1] : toff[2]);
+    uint8_t *dst = s_buf + toc + ty * twc + tx;
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      uint2 w;
+      w.x = uint32_t(o[r * 8 + 0]) | (uint32_t(o[r * 8 + 1]) << 8) | (uint32_t(o[r * 8 + 2]) << 16) |
+            (uint32_t(o[r * 8 + 3]) << 24);
+      w.y = uint32_t(o[r * 8 + 4]) | (uint32_t(o[r * 8 + 5]) << 8) | (uint32_t(o[r * 8 + 6]) << 16) |
+            (uint32_t(o[r * 8 + 7]) << 24);
+      *reinterpret_cast<uint2 *>(dst + r * twc) = w;
+    }
+  }
+  __syncthreads();
+
+  // ---- C: output, lane = 4 consecutive pixels ----
+  const uint32_t strip_w = nm * mcu_w;
   const uint32_t px0 = mx0 * mcu_w, py0 = my * mcu_h;
   const uint32_t W = im.width, H = im.height;
   const uint32_t fmt = im.fmt;
-  const uint8_t *ty0 = tiles + s_tile_off[0];
-  const uint32_t tw0 = s_tile_w[0];
-  // chroma sampling ratios (canonical geometries only: power-of-two ratios)
-  const uint32_t hs1 = (im.ncomp == 3) ? (hmax / im.comp_h[1] == 2 ? 1u : 0u) : 0u;
-  const uint32_t vs1 = (im.ncomp == 3) ? (vmax / im.comp_v[1] == 2 ? 1u : 0u) : 0u;
+  const uint32_t hs1 = (ncomp == 3) ? (hmax / im.comp_h[1] == 2 ? 1u : 0u) : 0u;
+  const uint32_t vs1 = (ncomp == 3) ? (vmax / im.comp_v[1] == 2 ? 1u : 0u) : 0u;
+  const uint32_t quads_x = strip_w >> 2;  // strip_w is a multiple of 8
+  const uint32_t wmax = min(strip_w, W > px0 ? W - px0 : 0u);
+  const uint32_t rows = min(mcu_h, H > py0 ? H - py0 : 0u);
 
   if (fmt >= 1 && fmt <= 4) {
-    // luma-resolution pass: 16-pixel chunks
-    const uint32_t chunks_x = (strip_w + 15) / 16;
-    const uint32_t nchunks = chunks_x * mcu_h;
-    for (uint32_t k = tid; k < nchunks; k += 256) {
-      const uint32_t y = k / chunks_x, xc = (k - y * chunks_x) * 16;
-      const uint32_t py = py0 + y;
-      if (py >= H) continue;
-      const uint32_t px = px0 + xc;
-      if (px >= W) continue;
-      const uint32_t n = min(16u, min(strip_w - xc, W - px));
-      const uint8_t *yrow = ty0 + y * tw0 + xc;
+    const bool a4 = ((reinterpret_cast<uintptr_t>(im.dst[0]) | im.dst_pitch[0]) & 3) == 0;
+    for (uint32_t k = tid; k < quads_x * rows; k += 256) {
+      const uint32_t y = k / quads_x, x = (k - y * quads_x) * 4;
+      if (x >= wmax) continue;
+      const uint32_t n = min(4u, wmax - x);
+      const uint32_t y4 = *reinterpret_cast<const uint32_t *>(s_buf + toff[0] + y * tw[0] + x);
+      const uint32_t py = py0 + y, px = px0 + x;
       if (fmt == 3 || fmt == 4) {
-        uint32_t w[12];  // 16 RGB pixels packed little-endian, constant-indexed (stays in VGPRs)
-#pragma unroll
-        for (int q = 0; q < 12; q++) w[q] = 0;
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-          uint32_t p3;
-          if (im.ncomp == 3) {
-            const uint32_t cx = (xc + j) >> hs1;
-            p3 = csc_pixel_packed(yrow[j], tiles[s_tile_off[1] + (y >> vs1) * s_tile_w[1] + cx],
-                                  tiles[s_tile_off[2] + (y >> vs1) * s_tile_w[2] + cx]);
+        uint32_t w[3];
+        if (ncomp == 3) {
+          float u[4], vv[4];
+          const uint8_t *ur = s_buf + toff[1] + (y >> vs1) * tw[1];
+          const uint8_t *vr = s_buf + toff[2] + (y >> vs1) * tw[2];
+          if (hs1) {
+            const uint32_t u2 = *reinterpret_cast<const uint16_t *>(ur + (x >> 1));
+            const uint32_t v2 = *reinterpret_cast<const uint16_t *>(vr + (x >> 1));
+            u[0] = u[1] = u8f(u2, 0) - 128.0f;
+            u[2] = u[3] = u8f(u2, 1) - 128.0f;
+            vv[0] = vv[1] = u8f(v2, 0) - 128.0f;
+            vv[2] = vv[3] = u8f(v2, 1) - 128.0f;
           } else {
-            p3 = uint32_t(yrow[j]) * 0x010101u;
-          }
+            const uint32_t u4 = *reinterpret_cast<const uint32_t *>(ur + x);
+            const uint32_t v4 = *reinterpret_cast<const uint32_t *>(vr + x);
 #pragma unroll
-          for (int e = 0; e < 3; e++) w[(3 * j + e) >> 2] |= ((p3 >> (8 * e)) & 255u) << (8 * ((3 * j + e) & 3));
+            for (int j = 0; j < 4; j++) {
+              u[j] = u8f(u4, j) - 128.0f;
+              vv[j] = u8f(v4, j) - 128.0f;
+            }
+          }
+          csc4(y4, u, vv, w[0], w[1], w[2]);
+        } else {  // 4:0:0 -> R = G = B = Y (rocjpeg_hip_kernels.cpp:1874-1932)
+          const uint32_t b0 = y4 & 255, b1 = (y4 >> 8) & 255, b2 = (y4 >> 16) & 255, b3 = y4 >> 24;
+          w[0] = b0 | (b0 << 8) | (b0 << 16) | (b1 << 24);
+          w[1] = b1 | (b1 << 8) | (b2 << 16) | (b2 << 24);
+          w[2] = b2 | (b3 << 8) | (b3 << 16) | (b3 << 24);
         }
         if (fmt == 3) {
           uint8_t *d = im.dst[0] + uint64_t(py) * im.dst_pitch[0] + uint64_t(px) * 3;
-          if (n == 16 && ((reinterpret_cast<uintptr_t>(d) & 15) == 0)) {
-            uint4 *d4 = reinterpret_cast<uint4 *>(d);
-            d4[0] = make_uint4(w[0], w[1], w[2], w[3]);
-            d4[1] = make_uint4(w[4], w[5], w[6], w[7]);
-            d4[2] = make_uint4(w[8], w[9], w[10], w[11]);
+          if (n == 4 && a4) {
+            uint32_t *d32 = reinterpret_cast<uint32_t *>(d);
+            d32[0] = w[0];
+            d32[1] = w[1];
+            d32[2] = w[2];
           } else {
-#pragma unroll
-            for (int j = 0; j < 48; j++)
-              if (uint32_t(j) < 3 * n) d[j] = uint8_t(w[j >> 2] >> (8 * (j & 3)));
+            store_bytes(d, 3 * n, w);
           }
-        } else {
+        } else {  // RGB planar: R, G, B planes, all with pitch[0] (rocjpeg_decoder.cpp:525-544)
+          // byte k of w = pixel k/3, channel k%3
+          const uint32_t R = (w[0] & 0xFFu) | ((w[0] >> 16) & 0xFF00u) | (w[1] & 0xFF0000u) | ((w[2] << 16) & 0xFF000000u);
+          const uint32_t G = ((w[0] >> 8) & 0xFFu) | ((w[1] << 8) & 0xFF00u) | ((w[1] >> 8) & 0xFF0000u) |
+                             ((w[2] << 8) & 0xFF000000u);
+          const uint32_t B = ((w[0] >> 16) & 0xFFu) | (w[1] & 0xFF00u) | ((w[2] << 16) & 0xFF0000u) | (w[2] & 0xFF000000u);
+          const uint32_t pl[3] = {R, G, B};
+          const bool ap = ((reinterpret_cast<uintptr_t>(im.dst[0]) | reinterpret_cast<uintptr_t>(im.dst[1]) |
+                            reinterpret_cast<uintptr_t>(im.dst[2]) | im.dst_pitch[0]) & 3) == 0;
 #pragma unroll
           for (int p = 0; p < 3; p++) {
-            uint32_t pl[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-              const int b = 3 * j + p;
-              pl[j >> 2] |= ((w[b >> 2] >> (8 * (b & 3))) & 255u) << (8 * (j & 3));
-            }
             uint8_t *d = im.dst[p] + uint64_t(py) * im.dst_pitch[0] + px;
-            if (n == 16 && ((reinterpret_cast<uintptr_t>(d) & 15) == 0)) {
-              *reinterpret_cast<uint4 *>(d) = make_uint4(pl[0], pl[1], pl[2], pl[3]);
-            } else {
-#pragma unroll
-              for (int j = 0; j < 16; j++)
-                if (uint32_t(j) < n) d[j] = uint8_t(pl[j >> 2] >> (8 * (j & 3)));
-            }
+            if (n == 4 && ap) *reinterpret_cast<uint32_t *>(d) = pl[p];
+            else store_bytes(d, n, &pl[p]);
           }
         }
-      } else {  // Y plane (OUTPUT_Y and the luma of YUV_PLANAR)
+      } else {  // Y plane (OUTPUT_Y, and the luma of YUV_PLANAR)
         uint8_t *d = im.dst[0] + uint64_t(py) * im.dst_pitch[0] + px;
-        if (n == 16 && ((reinterpret_cast<uintptr_t>(d) & 15) == 0) && ((reinterpret_cast<uintptr_t>(yrow) & 15) == 0)) {
-          *reinterpret_cast<uint4 *>(d) = *reinterpret_cast<const uint4 *>(yrow);
-        } else {
-          for (uint32_t j = 0; j < n; j++) d[j] = yrow[j];
-        }
+        if (n == 4 && a4) *reinterpret_cast<uint32_t *>(d) = y4;
+        else store_bytes(d, n, &y4);
       }
     }
   }
-  if (fmt == 1 && im.ncomp == 3) {  // chroma planes of YUV_PLANAR at native resolution
-#pragma unroll
-    for (int c = 1; c < 3; c++) {
-      const uint32_t hc = im.comp_h[c], vc = im.comp_v[c];
-      const uint32_t cw = nm * hc * 8, ch = vc * 8;
-      const uint32_t cx0 = mx0 * hc * 8, cy0 = my * vc * 8;
-      const uint32_t cW = (hs1 ? (W >> 1) : W), cH = (vs1 ? (H >> 1) : H);
-      const uint32_t chunks_x = (cw + 15) / 16;
-      for (uint32_t k = tid; k < chunks_x * ch; k += 256) {
-        const uint32_t y = k / chunks_x, xc = (k - y * chunks_x) * 16;
-        const uint32_t py = cy0 + y, px = cx0 + xc;
-        if (py >= cH || px >= cW) continue;
-        const uint32_t n = min(16u, min(cw - xc, cW - px));
-        const uint8_t *srow = tiles + s_tile_off[c] + y * s_tile_w[c] + xc;
-        uint8_t *d = im.dst[c] + uint64_t(py) * im.dst_pitch[1] + px;  // U and V share pitch[1] (host-checked)
-        if (n == 16 && ((reinterpret_cast<uintptr_t>(d) & 15) == 0)) {
-          *reinterpret_cast<uint4 *>(d) = *reinterpret_cast<const uint4 *>(srow);
-        } else {
-          for (uint32_t j = 0; j < n; j++) d[j] = srow[j];
-        }
-      }
+  if (fmt == 1 && ncomp == 3) {  // YUV_PLANAR chroma planes at native resolution; U and V share pitch[1]
+    const bool a4 = ((reinterpret_cast<uintptr_t>(im.dst[1]) | reinterpret_cast<uintptr_t>(im.dst[2]) |
+                      im.dst_pitch[1]) & 3) == 0;
+    const uint32_t cW = hs1 ? (W >> 1) : W, cH = vs1 ? (H >> 1) : H;
+    const uint32_t cw = strip_w >> hs1, ch = mcu_h >> vs1;
+    const uint32_t cx0 = px0 >> hs1, cy0 = py0 >> vs1;
+    const uint32_t cq = cw >> 2;
+    const uint32_t cwmax = min(cw, cW > cx0 ? cW - cx0 : 0u);
+    const uint32_t crows = min(ch, cH > cy0 ? cH - cy0 : 0u);
+    for (uint32_t k = tid; k < 2 * cq * crows; k += 256) {
+      const uint32_t second = k >= cq * crows ? 1u : 0u;
+      const uint32_t kk = k - second * cq * crows;
+      const uint32_t y = kk / cq, x = (kk - y * cq) * 4;
+      if (x >= cwmax) continue;
+      const uint32_t n = min(4u, cwmax - x);
+      const uint32_t s4 = *reinterpret_cast<const uint32_t *>(s_buf + (second ? toff[2] : toff[1]) +
+                                                              y * (second ? tw[2] : tw[1]) + x);
+      uint8_t *d = (second ? im.dst[2] : im.dst[1]) + uint64_t(cy0 + y) * im.dst_pitch[1] + cx0 + x;
+      if (n == 4 && a4) *reinterpret_cast<uint32_t *>(d) = s4;
+      else store_bytes(d, n, &s4);
     }
   }
 }

@@ -429,7 +429,7 @@ __global__ __launch_bounds__(256) void k_output(const RjImageDev *__restrict__ i
 
 hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobDev *jobs, int njobs, uint32_t total_rows,
                             const uint8_t *planes) {
-  if (total_rows == 0) return hipSuccess;
+  if (total_rows == 0 || njobs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_output, dim3(total_rows), dim3(256), 0, st, imgs, jobs, njobs, planes);
   return hipGetLastError();
 }
