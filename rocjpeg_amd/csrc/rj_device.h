@@ -11,7 +11,6 @@
 #pragma once
 #include <stdint.h>
 
-#define RJ_LUT_BITS 9
 #define RJ_MAX_BLK_MCU 10
 
 // One restart interval of one image (host parser rj_stream.cpp builds these).
@@ -26,10 +25,20 @@ struct RjSegDev {
 #define RJ_SEG_MISSING 1u
 
 // Canonical Huffman decoder for one table (T.81 Annex C), laid out for the GPU.
+//   lut[0..511]      first level, indexed by the next 9 bits:
+//                      (code_len << 8) | symbol      for codes of <= 9 bits
+//                      0x8000 | sub                  longer codes: second level `sub`
+//                      0xFFFF                        second-level pool exhausted: canonical search
+//                      0x1100 (len 17, symbol 0)     no code: libjpeg's "bad code" result
+//   lut[512 + sub*128 + next 7 bits]  second level for codes of 10..16 bits (same encoding)
+#define RJ_LUT_L1 512
+#define RJ_L2_SUBTABLES 8
+#define RJ_LUT_ENTRIES (RJ_LUT_L1 + RJ_L2_SUBTABLES * 128)
+#define RJ_LUT_BAD 0x1100u
 struct RjHuffDev {
-  uint16_t fast[1 << RJ_LUT_BITS];  // (code_len << 8) | symbol for codes <= RJ_LUT_BITS, else 0
-  uint32_t maxcode16[18];           // exclusive upper bound of length-l codes, left-justified to 16 bits
-  int32_t valoff[18];               // symbol index = (code >> (16 - l)) + valoff[l]
+  uint16_t lut[RJ_LUT_ENTRIES];
+  uint32_t maxcode16[18];  // exclusive upper bound of length-l codes, left-justified to 16 bits
+  int32_t valoff[18];      // symbol index = (code >> (16 - l)) + valoff[l]
   uint8_t vals[256];
 };
 

@@ -91,6 +91,10 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
     out += total;
     prev_byte = __shfl(b[3], 63, 64);
   }
+  // zero the slack after the data (>= 16 B, see rj_stream.cpp BuildPlan): K1 reads whole 16-B
+  // chunks and must see zero bits past the end, as libjpeg inserts after a marker
+  const uint32_t pad_end = (len + 16u + 15u) & ~15u;
+  for (uint32_t b = out + lane; b < pad_end; b += 64) dst[b] = 0;
   if (lane == 0) seg_len[g] = out;
 }
 
@@ -103,62 +107,62 @@ hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint3
 
 // ---------------------------------------------------------------------------------------
 // K1: Huffman decode, one lane per restart interval.
+//
+// Per lane: a 64-bit MSB-first bit buffer fed 32 bits at a time from a 16-B register double
+// buffer (cur/nxt): the next 16-B chunk is loaded ~4 refills (~25 symbols) before it is
+// needed, so the HBM/L2 latency hides behind decode work.  Huffman lookups hit a per-wave LDS
+// copy of the image's tables (9-bit first level + 7-bit second level, rj_device.h), so the
+// dependent chain per symbol is one ds_read (two for codes > 9 bits) plus ~20 ALU ops; the
+// extra bits are cut from the same 32-bit peek (no second read).  The flattened symbol loop
+// lets every lane run at its own pace across block boundaries; a finished block (zeroed LDS
+// staging + scattered coefficients) leaves as 8 x 16-B stores.
 // ---------------------------------------------------------------------------------------
 struct BitReader {
-  const uint32_t *w;  // 16-B aligned destuffed words (big-endian bytes)
+  const uint4 *src;   // 16-B aligned destuffed bytes, zero-padded after nbytes
   uint32_t nbytes;
-  uint32_t wi;        // next word
+  uint32_t qi;        // next 16-B chunk to load
+  uint32_t wsel;      // next word of cur (0..4)
+  uint32_t words;     // 32-bit words shifted into acc so far
   int nb;             // valid bits in acc (left-justified)
   uint64_t acc;
+  uint4 cur, nxt;
 
+  __device__ __forceinline__ uint4 load(uint32_t q) const {
+    return (q * 16u < nbytes) ? src[q] : make_uint4(0, 0, 0, 0);
+  }
+  __device__ __forceinline__ void init(const uint4 *s, uint32_t n) {
+    src = s;
+    nbytes = n;
+    cur = load(0);
+    nxt = load(1);
+    qi = 2;
+    wsel = 0;
+    words = 0;
+    nb = 0;
+    acc = 0;
+  }
   __device__ __forceinline__ void refill() {
     if (nb <= 32) {
-      uint32_t v = 0;
-      const uint32_t byte = wi * 4u;
-      if (byte < nbytes) {
-        v = __builtin_bswap32(w[wi]);
-        const uint32_t valid = nbytes - byte;
-        if (valid < 4) v &= ~0u << (32 - 8 * valid);
+      if (wsel == 4) {
+        cur = nxt;
+        nxt = load(qi++);
+        wsel = 0;
       }
-      acc |= uint64_t(v) << (32 - nb);
+      const uint32_t w = wsel == 0 ? cur.x : (wsel == 1 ? cur.y : (wsel == 2 ? cur.z : cur.w));
+      wsel++;
+      acc |= uint64_t(__builtin_bswap32(w)) << (32 - nb);
       nb += 32;
-      wi++;
+      words++;
     }
   }
-  __device__ __forceinline__ uint32_t bits(int n) {  // 1 <= n <= 16
-    const uint32_t v = uint32_t(acc >> (64 - n));
-    acc <<= n;
-    nb -= n;
-    return v;
-  }
-  __device__ __forceinline__ bool overrun() const { return uint64_t(wi) * 32u - uint64_t(nb) > uint64_t(nbytes) * 8u; }
+  __device__ __forceinline__ bool overrun() const { return uint64_t(words) * 32u - uint64_t(nb) > uint64_t(nbytes) * 8u; }
 };
 
-__device__ __forceinline__ int huff_decode(const RjHuffDev *__restrict__ t, BitReader &br) {
-  const uint32_t peek = uint32_t(br.acc >> 48);
-  const uint32_t e = t->fast[peek >> (16 - RJ_LUT_BITS)];
-  int len, sym;
-  if (e != 0) {
-    len = int(e >> 8);
-    sym = int(e & 255);
-  } else {  // codes longer than RJ_LUT_BITS: canonical search (libjpeg jpeg_huff_decode)
-    len = 17;
-    sym = 0;  // corrupt code: libjpeg consumes 17 bits and returns 0
-    for (int l = RJ_LUT_BITS + 1; l <= 16; l++) {
-      if (peek < t->maxcode16[l]) {
-        len = l;
-        sym = t->vals[((peek >> (16 - l)) + t->valoff[l]) & 255];
-        break;
-      }
-    }
-  }
-  br.acc <<= len;
-  br.nb -= len;
-  return sym;
-}
-
-__device__ __forceinline__ int huff_extend(uint32_t v, int s) {
-  return (v < (1u << (s - 1))) ? int(v) - (1 << s) + 1 : int(v);
+// canonical search (second-level pool exhausted): libjpeg jpeg_huff_decode from the global copy
+__device__ __noinline__ uint32_t huff_slow(const RjHuffDev *__restrict__ t, uint32_t peek16) {
+  for (int l = 10; l <= 16; l++)
+    if (peek16 < t->maxcode16[l]) return uint32_t(l << 8) | t->vals[((peek16 >> (16 - l)) + t->valoff[l]) & 255];
+  return RJ_LUT_BAD;
 }
 
 __constant__ uint8_t c_zigzag[80] = {
@@ -172,85 +176,115 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
                                                 const uint32_t *__restrict__ seg_len,
                                                 const RjTableSet *__restrict__ tabsets, int16_t *__restrict__ coefs) {
   __shared__ __attribute__((aligned(16))) int16_t s_blk[64][64];
+  __shared__ __attribute__((aligned(16))) uint16_t s_lut[4][RJ_LUT_ENTRIES];  // dc0, dc1, ac0, ac1
   __shared__ uint8_t s_zz[80];
   const uint32_t lane = threadIdx.x;
   for (uint32_t k = lane; k < 80; k += 64) s_zz[k] = c_zigzag[k];
-  __syncthreads();
   const uint32_t g = blockIdx.x * 64u + lane;
-  if (g >= nseg) return;
-  const int i = upper_index(nimg, g, [&](int k) { return imgs[k].seg_prefix; });
+  const bool valid = g < nseg;
+  const int i = valid ? upper_index(nimg, g, [&](int k) { return imgs[k].seg_prefix; }) : 0;
   const RjImageDev &im = imgs[i];
-  const RjSegDev sg = im.segs[g - im.seg_prefix];
-  const RjTableSet *ts = tabsets + im.tabset;
-  const uint32_t nblk = im.nblk_mcu;
-  // per-block component packed 2 bits per block-in-MCU (no dynamic register indexing)
-  uint32_t comp_bits = 0;
-  for (uint32_t b = 0; b < nblk; b++) comp_bits |= uint32_t(im.blk_comp[b]) << (2 * b);
-  const RjHuffDev *dc0 = &ts->dc[im.comp_td[0] & 1], *dc1 = &ts->dc[im.comp_td[1] & 1], *dc2 = &ts->dc[im.comp_td[2] & 1];
-  const RjHuffDev *ac0 = &ts->ac[im.comp_ta[0] & 1], *ac1 = &ts->ac[im.comp_ta[1] & 1], *ac2 = &ts->ac[im.comp_ta[2] & 1];
-
-  BitReader br;
-  br.w = reinterpret_cast<const uint32_t *>(destuffed + im.destuff_off + sg.dst_off);
-  br.nbytes = seg_len[g];
-  br.wi = 0;
-  br.nb = 0;
-  br.acc = 0;
-
-  int16_t *out = coefs + (im.coef_off + uint64_t(sg.mcu_first) * nblk) * 64u;
-  int16_t *blk = s_blk[lane];
-  uint4 *blk4 = reinterpret_cast<uint4 *>(blk);
-  const uint4 zero4 = make_uint4(0, 0, 0, 0);
-
-  int pred0 = 0, pred1 = 0, pred2 = 0;
-  bool skip = (sg.flags & RJ_SEG_MISSING) != 0;
-  uint32_t m = 0, b = 0;
-  int k = 0;
-  const uint32_t nmcu = sg.mcu_count;
-  while (m < nmcu) {
-    const uint32_t c = (comp_bits >> (2 * b)) & 3u;
-    if (k == 0) {
+  const uint32_t my_ts = im.tabset;
+  bool pending = valid;
+  // one pass per distinct table set among the wave's lanes (normally exactly one)
+  while (true) {
+    const uint64_t m = __ballot(pending);
+    if (m == 0) break;
+    const uint32_t T = __shfl(my_ts, __ffsll((long long)m) - 1, 64);
+    __syncthreads();
+    {
+      const RjTableSet *tsT = tabsets + T;
+      const RjHuffDev *src[4] = {&tsT->dc[0], &tsT->dc[1], &tsT->ac[0], &tsT->ac[1]};
 #pragma unroll
-      for (int q = 0; q < 8; q++) blk4[q] = zero4;
-    }
-    if (skip) {
-      k = 64;
-    } else {
-      br.refill();
-      if (k == 0) {
-        const RjHuffDev *t = c == 0 ? dc0 : (c == 1 ? dc1 : dc2);
-        const int s = huff_decode(t, br) & 15;
-        const int diff = s ? huff_extend(br.bits(s), s) : 0;
-        int p = (c == 0 ? pred0 : (c == 1 ? pred1 : pred2)) + diff;
-        if (c == 0) pred0 = p;
-        else if (c == 1) pred1 = p;
-        else pred2 = p;
-        blk[0] = int16_t(p);
-        k = 1;
-      } else {
-        const RjHuffDev *t = c == 0 ? ac0 : (c == 1 ? ac1 : ac2);
-        const int rs = huff_decode(t, br);
-        const int r = rs >> 4, s = rs & 15;
-        if (s) {
-          k += r;
-          const int v = huff_extend(br.bits(s), s);
-          blk[s_zz[k < 79 ? k : 79]] = int16_t(v);
-          k++;
-        } else if (r == 15) {
-          k += 16;
-        } else {
-          k = 64;
-        }
+      for (int t = 0; t < 4; t++) {
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(src[t]->lut);
+        uint4 *d4 = reinterpret_cast<uint4 *>(s_lut[t]);
+        for (uint32_t k = lane; k < RJ_LUT_ENTRIES / 8; k += 64) d4[k] = s4[k];
       }
     }
-    if (k >= 64) {  // block complete: 128 B out, next block
-      uint4 *o = reinterpret_cast<uint4 *>(out + (uint64_t(m) * nblk + b) * 64u);
+    __syncthreads();
+    if (pending && my_ts == T) {
+      pending = false;
+      const RjSegDev sg = im.segs[g - im.seg_prefix];
+      const RjTableSet *ts = tabsets + T;
+      const uint32_t nblk = im.nblk_mcu;
+      uint32_t comp_bits = 0;  // 2 bits per block-in-MCU: its component
+      for (uint32_t b = 0; b < nblk; b++) comp_bits |= uint32_t(im.blk_comp[b]) << (2 * b);
+      const uint32_t dco0 = (im.comp_td[0] & 1) * RJ_LUT_ENTRIES, aco0 = (2 + (im.comp_ta[0] & 1)) * RJ_LUT_ENTRIES;
+      const uint32_t dco1 = (im.comp_td[1] & 1) * RJ_LUT_ENTRIES, aco1 = (2 + (im.comp_ta[1] & 1)) * RJ_LUT_ENTRIES;
+      const uint32_t dco2 = (im.comp_td[2] & 1) * RJ_LUT_ENTRIES, aco2 = (2 + (im.comp_ta[2] & 1)) * RJ_LUT_ENTRIES;
+      const uint16_t *lut = &s_lut[0][0];
+
+      BitReader br;
+      br.init(reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off), seg_len[g]);
+
+      int16_t *out = coefs + (im.coef_off + uint64_t(sg.mcu_first) * nblk) * 64u;
+      int16_t *blk = s_blk[lane];
+      uint4 *blk4 = reinterpret_cast<uint4 *>(blk);
+      const uint4 zero4 = make_uint4(0, 0, 0, 0);
 #pragma unroll
-      for (int q = 0; q < 8; q++) o[q] = blk4[q];
-      k = 0;
-      if (++b == nblk) {
-        b = 0;
-        m++;
-        if (br.overrun()) skip = true;  // libjpeg: rest of the interval stays zero
+      for (int q = 0; q < 8; q++) blk4[q] = zero4;
+
+      int pred0 = 0, pred1 = 0, pred2 = 0;
+      bool skip = (sg.flags & RJ_SEG_MISSING) != 0;
+      uint32_t m_i = 0, b = 0;
+      int k = 0;
+      const uint32_t nmcu = sg.mcu_count;
+      while (m_i < nmcu) {
+        const uint32_t c = (comp_bits >> (2 * b)) & 3u;
+        if (skip) {
+          k = 64;
+        } else {
+          br.refill();
+          const uint32_t peek32 = uint32_t(br.acc >> 32);
+          const uint32_t toff = k == 0 ? (c == 0 ? dco0 : (c == 1 ? dco1 : dco2)) : (c == 0 ? aco0 : (c == 1 ? aco1 : aco2));
+          uint32_t e = lut[toff + (peek32 >> 23)];
+          if (e & 0x8000u) {
+            if (e != 0xFFFFu) {
+              e = lut[toff + RJ_LUT_L1 + (e & 0x7Fu) * 128u + ((peek32 >> 16) & 127u)];
+            } else {
+              const RjHuffDev *gt = k == 0 ? &ts->dc[(c == 0 ? dco0 : (c == 1 ? dco1 : dco2)) / RJ_LUT_ENTRIES]
+                                           : &ts->ac[(c == 0 ? aco0 : (c == 1 ? aco1 : aco2)) / RJ_LUT_ENTRIES - 2];
+              e = huff_slow(gt, peek32 >> 16);
+            }
+          }
+          const uint32_t len = e >> 8, sym = e & 255u;
+          const uint32_t s = sym & 15u, r = sym >> 4;
+          // extra bits follow the code inside the same peek (len + s <= 32 < bits available)
+          const uint32_t t = peek32 << len;
+          const uint32_t raw = s ? (t >> (32u - s)) : 0u;
+          const int val = (s && raw < (1u << (s - 1))) ? int(raw) - (1 << s) + 1 : int(raw);
+          br.acc <<= (len + s);
+          br.nb -= int(len + s);
+          if (k == 0) {  // DC: predictor per component (F.2.1.3)
+            const int p = (c == 0 ? pred0 : (c == 1 ? pred1 : pred2)) + val;
+            if (c == 0) pred0 = p;
+            else if (c == 1) pred1 = p;
+            else pred2 = p;
+            blk[0] = int16_t(p);
+            k = 1;
+          } else if (s) {
+            k += int(r);
+            blk[s_zz[k < 79 ? k : 79]] = int16_t(val);
+            k++;
+          } else {
+            k = (r == 15) ? k + 16 : 64;  // ZRL / EOB
+          }
+        }
+        if (k >= 64) {  // block complete: 128 B out, LDS staging cleared for the next one
+          uint4 *o = reinterpret_cast<uint4 *>(out + (uint64_t(m_i) * nblk + b) * 64u);
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            o[q] = blk4[q];
+            blk4[q] = zero4;
+          }
+          k = 0;
+          if (++b == nblk) {
+            b = 0;
+            m_i++;
+            if (br.overrun()) skip = true;  // libjpeg: rest of the interval stays zero
+          }
+        }
       }
     }
   }

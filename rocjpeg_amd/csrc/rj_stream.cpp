@@ -45,16 +45,39 @@ uint64_t Fnv1a(uint64_t h, const void *p, size_t n) {
 
 bool BuildHuffman(const uint8_t bits[16], const uint8_t *vals, bool is_dc, RjHuffDev *t) {
   std::memset(t, 0, sizeof(*t));
+  for (int e = 0; e < RJ_LUT_ENTRIES; e++) t->lut[e] = uint16_t(RJ_LUT_BAD);
+  int nsub = 0;
+  int sub_of_prefix[RJ_LUT_L1];
+  for (int e = 0; e < RJ_LUT_L1; e++) sub_of_prefix[e] = -1;
   int k = 0, code = 0;
   for (int l = 1; l <= 16; l++) {
     const int nb = bits[l - 1];
     if (nb) {
       t->valoff[l] = k - code;
       for (int i = 0; i < nb; i++, k++, code++) {
-        if (l <= RJ_LUT_BITS) {
-          const int shift = RJ_LUT_BITS - l;
-          for (int f = 0; f < (1 << shift); f++)
-            t->fast[(code << shift) | f] = uint16_t((l << 8) | vals[k]);
+        const uint16_t ent = uint16_t((l << 8) | vals[k]);
+        if (l <= 9) {
+          const int shift = 9 - l;
+          for (int f = 0; f < (1 << shift); f++) t->lut[(code << shift) | f] = ent;
+        } else {
+          const int prefix = code >> (l - 9);
+          if (sub_of_prefix[prefix] < 0) {
+            if (nsub < RJ_L2_SUBTABLES) {
+              sub_of_prefix[prefix] = nsub;
+              t->lut[prefix] = uint16_t(0x8000 | nsub);
+              nsub++;
+            } else {
+              t->lut[prefix] = 0xFFFF;  // canonical search for this prefix
+              sub_of_prefix[prefix] = RJ_L2_SUBTABLES;
+            }
+          }
+          const int sub = sub_of_prefix[prefix];
+          if (sub < RJ_L2_SUBTABLES) {
+            const int rest = code & ((1 << (l - 9)) - 1);
+            const int shift = 16 - l;
+            for (int f = 0; f < (1 << shift); f++)
+              t->lut[RJ_LUT_L1 + sub * 128 + ((rest << shift) | f)] = ent;
+          }
         }
       }
       t->maxcode16[l] = uint32_t(code) << (16 - l);  // exclusive bound, left-justified
