@@ -117,52 +117,85 @@ hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint3
 // lets every lane run at its own pace across block boundaries; a finished block (zeroed LDS
 // staging + scattered coefficients) leaves as 8 x 16-B stores.
 // ---------------------------------------------------------------------------------------
+// Bit reader over a per-lane LDS ring of the interval's destuffed bytes.  The ring is
+// refilled at wave-uniform phase boundaries (every RJ_PHASE symbols): the two 16-B chunks
+// loaded at boundary p are committed to LDS at boundary p+1, so their latency hides behind a
+// whole phase of decoding and the symbol loop itself issues no global load (a conditional
+// load inside the loop costs a full vmcnt(0) round trip per symbol on CDNA: the PHI copy of
+// its destination register waits for it).
+#define RJ_RING_CHUNKS 16  // 16-B chunks per lane (256 B)
+#define RJ_PHASE 16        // symbols per refill phase: <= 16 words consumed (<= 32 bits/symbol)
+#define RJ_PREFETCH 4      // chunks (16 words) fetched per phase >= worst-case consumption
+// Invariant: at every phase boundary the ring holds >= 17 unread words (or all that remain),
+// so a refill never has to fall back to a global read inside the symbol loop.
 struct BitReader {
   const uint4 *src;   // 16-B aligned destuffed bytes, zero-padded after nbytes
+  uint4 *ring;        // this lane's LDS ring
+  uint32_t nchunks;   // 16-B chunks holding data
+  uint32_t rd;        // words consumed from the ring (monotonic)
+  uint32_t cm;        // chunks committed to the ring (monotonic)
+  uint32_t pq;        // first chunk of the pending prefetch
+  uint32_t pn;        // chunks in the pending prefetch (0..RJ_PREFETCH)
+  uint4 pf[RJ_PREFETCH];
   uint32_t nbytes;
-  uint32_t qi;        // next 16-B chunk to load
-  uint32_t wsel;      // next word of cur (0..4)
-  uint32_t words;     // 32-bit words shifted into acc so far
   int nb;             // valid bits in acc (left-justified)
   uint64_t acc;
-  uint4 cur, nxt;
 
-  __device__ __forceinline__ uint4 load(uint32_t q) const {
-    return (q * 16u < nbytes) ? src[q] : make_uint4(0, 0, 0, 0);
-  }
-  __device__ __forceinline__ void init(const uint4 *s, uint32_t n) {
+  __device__ __forceinline__ void init(const uint4 *s, uint4 *r, uint32_t n) {
     src = s;
+    ring = r;
     nbytes = n;
-    cur = load(0);
-    nxt = load(1);
-    qi = 2;
-    wsel = 0;
-    words = 0;
+    nchunks = (n + 15) / 16;
+    const uint32_t first = nchunks < RJ_RING_CHUNKS ? nchunks : RJ_RING_CHUNKS;
+    for (uint32_t q = 0; q < first; q++) ring[q] = src[q];
+    cm = first;
+    rd = 0;
+    pq = cm;
+    pn = 0;
+#pragma unroll
+    for (int q = 0; q < RJ_PREFETCH; q++) pf[q] = make_uint4(0, 0, 0, 0);
     nb = 0;
     acc = 0;
   }
+  // phase boundary: commit the previous prefetch, issue the next one (loads unconditional:
+  // a conditional load would again force an immediate wait at the control-flow join)
+  __device__ __forceinline__ void phase() {
+#pragma unroll
+    for (int q = 0; q < RJ_PREFETCH; q++)
+      if (uint32_t(q) < pn) ring[(pq + q) & (RJ_RING_CHUNKS - 1)] = pf[q];
+    cm += pn;
+    const uint32_t used = cm - (rd >> 2);             // chunks not fully consumed
+    const uint32_t room = RJ_RING_CHUNKS - 1 - used;  // never overwrite the chunk being read
+    uint32_t want = nchunks > cm ? nchunks - cm : 0u;
+    want = want < room ? want : room;
+    pn = want < RJ_PREFETCH ? want : RJ_PREFETCH;
+    pq = cm;
+    const uint32_t last = nchunks ? nchunks - 1 : 0;
+#pragma unroll
+    for (int q = 0; q < RJ_PREFETCH; q++) pf[q] = src[pq + q < last ? pq + q : last];
+  }
   __device__ __forceinline__ void refill() {
     if (nb <= 32) {
-      if (wsel == 4) {
-        cur = nxt;
-        nxt = load(qi++);
-        wsel = 0;
-      }
-      const uint32_t w = wsel == 0 ? cur.x : (wsel == 1 ? cur.y : (wsel == 2 ? cur.z : cur.w));
-      wsel++;
+      // past the committed chunks only when past the data: zero bits (libjpeg inserts zeros)
+      const uint32_t w = ((rd >> 2) < cm) ? reinterpret_cast<const uint32_t *>(ring)[rd & (RJ_RING_CHUNKS * 4 - 1)] : 0u;
+      rd++;
       acc |= uint64_t(__builtin_bswap32(w)) << (32 - nb);
       nb += 32;
-      words++;
     }
   }
-  __device__ __forceinline__ bool overrun() const { return uint64_t(words) * 32u - uint64_t(nb) > uint64_t(nbytes) * 8u; }
+  __device__ __forceinline__ bool overrun() const { return uint64_t(rd) * 32u - uint64_t(nb) > uint64_t(nbytes) * 8u; }
 };
 
-// canonical search (second-level pool exhausted): libjpeg jpeg_huff_decode from the global copy
-__device__ __noinline__ uint32_t huff_slow(const RjHuffDev *__restrict__ t, uint32_t peek16) {
+// canonical search when the second-level pool is exhausted (libjpeg jpeg_huff_decode), on
+// the LDS copy of the table
+__device__ __forceinline__ uint32_t huff_slow(const RjHuffDev *t, uint32_t peek16) {
+  uint32_t e = RJ_LUT_BAD;
   for (int l = 10; l <= 16; l++)
-    if (peek16 < t->maxcode16[l]) return uint32_t(l << 8) | t->vals[((peek16 >> (16 - l)) + t->valoff[l]) & 255];
-  return RJ_LUT_BAD;
+    if (peek16 < t->maxcode16[l]) {
+      e = uint32_t(l << 8) | t->vals[((peek16 >> (16 - l)) + t->valoff[l]) & 255];
+      break;
+    }
+  return e;
 }
 
 __constant__ uint8_t c_zigzag[80] = {
@@ -176,7 +209,8 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
                                                 const uint32_t *__restrict__ seg_len,
                                                 const RjTableSet *__restrict__ tabsets, int16_t *__restrict__ coefs) {
   __shared__ __attribute__((aligned(16))) int16_t s_blk[64][64];
-  __shared__ __attribute__((aligned(16))) uint16_t s_lut[4][RJ_LUT_ENTRIES];  // dc0, dc1, ac0, ac1
+  __shared__ __attribute__((aligned(16))) uint4 s_ring[64][RJ_RING_CHUNKS];
+  __shared__ __attribute__((aligned(16))) RjHuffDev s_tab[4];  // dc0, dc1, ac0, ac1
   __shared__ uint8_t s_zz[80];
   const uint32_t lane = threadIdx.x;
   for (uint32_t k = lane; k < 80; k += 64) s_zz[k] = c_zigzag[k];
@@ -194,29 +228,25 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
     __syncthreads();
     {
       const RjTableSet *tsT = tabsets + T;
-      const RjHuffDev *src[4] = {&tsT->dc[0], &tsT->dc[1], &tsT->ac[0], &tsT->ac[1]};
-#pragma unroll
-      for (int t = 0; t < 4; t++) {
-        const uint4 *s4 = reinterpret_cast<const uint4 *>(src[t]->lut);
-        uint4 *d4 = reinterpret_cast<uint4 *>(s_lut[t]);
-        for (uint32_t k = lane; k < RJ_LUT_ENTRIES / 8; k += 64) d4[k] = s4[k];
-      }
+      static_assert(sizeof(RjHuffDev) % 16 == 0, "RjHuffDev must be 16-B multiple");
+      const uint4 *s4 = reinterpret_cast<const uint4 *>(&tsT->dc[0]);  // dc[0], dc[1], ac[0], ac[1] contiguous
+      uint4 *d4 = reinterpret_cast<uint4 *>(s_tab);
+      for (uint32_t k = lane; k < 4 * sizeof(RjHuffDev) / 16; k += 64) d4[k] = s4[k];
     }
     __syncthreads();
     if (pending && my_ts == T) {
       pending = false;
       const RjSegDev sg = im.segs[g - im.seg_prefix];
-      const RjTableSet *ts = tabsets + T;
       const uint32_t nblk = im.nblk_mcu;
       uint32_t comp_bits = 0;  // 2 bits per block-in-MCU: its component
       for (uint32_t b = 0; b < nblk; b++) comp_bits |= uint32_t(im.blk_comp[b]) << (2 * b);
-      const uint32_t dco0 = (im.comp_td[0] & 1) * RJ_LUT_ENTRIES, aco0 = (2 + (im.comp_ta[0] & 1)) * RJ_LUT_ENTRIES;
-      const uint32_t dco1 = (im.comp_td[1] & 1) * RJ_LUT_ENTRIES, aco1 = (2 + (im.comp_ta[1] & 1)) * RJ_LUT_ENTRIES;
-      const uint32_t dco2 = (im.comp_td[2] & 1) * RJ_LUT_ENTRIES, aco2 = (2 + (im.comp_ta[2] & 1)) * RJ_LUT_ENTRIES;
-      const uint16_t *lut = &s_lut[0][0];
+      // table index per component: dc tables 0/1, ac tables 2/3 of s_tab
+      const uint32_t dc0 = im.comp_td[0] & 1, ac0 = 2 + (im.comp_ta[0] & 1);
+      const uint32_t dc1 = im.comp_td[1] & 1, ac1 = 2 + (im.comp_ta[1] & 1);
+      const uint32_t dc2 = im.comp_td[2] & 1, ac2 = 2 + (im.comp_ta[2] & 1);
 
       BitReader br;
-      br.init(reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off), seg_len[g]);
+      br.init(reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off), s_ring[lane], seg_len[g]);
 
       int16_t *out = coefs + (im.coef_off + uint64_t(sg.mcu_first) * nblk) * 64u;
       int16_t *blk = s_blk[lane];
@@ -230,23 +260,21 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
       uint32_t m_i = 0, b = 0;
       int k = 0;
       const uint32_t nmcu = sg.mcu_count;
+      uint32_t iter = 0;
       while (m_i < nmcu) {
+        if ((iter++ & (RJ_PHASE - 1)) == 0) br.phase();  // same count in every active lane
         const uint32_t c = (comp_bits >> (2 * b)) & 3u;
         if (skip) {
           k = 64;
         } else {
           br.refill();
           const uint32_t peek32 = uint32_t(br.acc >> 32);
-          const uint32_t toff = k == 0 ? (c == 0 ? dco0 : (c == 1 ? dco1 : dco2)) : (c == 0 ? aco0 : (c == 1 ? aco1 : aco2));
-          uint32_t e = lut[toff + (peek32 >> 23)];
+          const uint32_t tix = k == 0 ? (c == 0 ? dc0 : (c == 1 ? dc1 : dc2)) : (c == 0 ? ac0 : (c == 1 ? ac1 : ac2));
+          const RjHuffDev *tab = &s_tab[tix];
+          uint32_t e = tab->lut[peek32 >> 23];
           if (e & 0x8000u) {
-            if (e != 0xFFFFu) {
-              e = lut[toff + RJ_LUT_L1 + (e & 0x7Fu) * 128u + ((peek32 >> 16) & 127u)];
-            } else {
-              const RjHuffDev *gt = k == 0 ? &ts->dc[(c == 0 ? dco0 : (c == 1 ? dco1 : dco2)) / RJ_LUT_ENTRIES]
-                                           : &ts->ac[(c == 0 ? aco0 : (c == 1 ? aco1 : aco2)) / RJ_LUT_ENTRIES - 2];
-              e = huff_slow(gt, peek32 >> 16);
-            }
+            if (e != 0xFFFFu) e = tab->lut[RJ_LUT_L1 + (e & 0x7Fu) * 128u + ((peek32 >> 16) & 127u)];
+            else e = huff_slow(tab, peek32 >> 16);
           }
           const uint32_t len = e >> 8, sym = e & 255u;
           const uint32_t s = sym & 15u, r = sym >> 4;
