@@ -164,8 +164,11 @@ struct BitReader {
     for (int q = 0; q < RJ_PREFETCH; q++)
       if (uint32_t(q) < pn) ring[(pq + q) & (RJ_RING_CHUNKS - 1)] = pf[q];
     cm += pn;
-    const uint32_t used = cm - (rd >> 2);             // chunks not fully consumed
-    const uint32_t room = RJ_RING_CHUNKS - 1 - used;  // never overwrite the chunk being read
+    // chunks (rd>>2) .. cm-1 are live in the ring (incl. the one being read); new chunks may
+    // only take the remaining slots -- a prefetch is committed one phase later, when at least
+    // as many slots are free again
+    const uint32_t used = cm - (rd >> 2);
+    const uint32_t room = RJ_RING_CHUNKS - used;
     uint32_t want = nchunks > cm ? nchunks - cm : 0u;
     want = want < room ? want : room;
     pn = want < RJ_PREFETCH ? want : RJ_PREFETCH;
