@@ -211,8 +211,10 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
                                                 const uint8_t *__restrict__ destuffed,
                                                 const uint32_t *__restrict__ seg_len,
                                                 const RjTableSet *__restrict__ tabsets, int16_t *__restrict__ coefs) {
-  __shared__ __attribute__((aligned(16))) int16_t s_blk[64][64];
-  __shared__ __attribute__((aligned(16))) uint4 s_ring[64][RJ_RING_CHUNKS];
+  // per-lane LDS areas padded to 144 B / 272 B so that the 8/16-lane groups of ds_*_b128
+  // hit distinct banks (unpadded 128/256-B strides put a whole group on one bank set)
+  __shared__ __attribute__((aligned(16))) uint4 s_blk[64][9];
+  __shared__ __attribute__((aligned(16))) uint4 s_ring[64][RJ_RING_CHUNKS + 1];
   __shared__ __attribute__((aligned(16))) RjHuffDev s_tab[4];  // dc0, dc1, ac0, ac1
   __shared__ uint8_t s_zz[80];
   const uint32_t lane = threadIdx.x;
@@ -252,8 +254,8 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
       br.init(reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off), s_ring[lane], seg_len[g]);
 
       int16_t *out = coefs + (im.coef_off + uint64_t(sg.mcu_first) * nblk) * 64u;
-      int16_t *blk = s_blk[lane];
-      uint4 *blk4 = reinterpret_cast<uint4 *>(blk);
+      uint4 *blk4 = s_blk[lane];
+      int16_t *blk = reinterpret_cast<int16_t *>(blk4);
       const uint4 zero4 = make_uint4(0, 0, 0, 0);
 #pragma unroll
       for (int q = 0; q < 8; q++) blk4[q] = zero4;
