@@ -6,7 +6,8 @@
 //   tabsets[]  RjTableSet          de-duplicated Huffman LUTs + natural-order quant tables
 //   segs       RjSegDev per image  restart intervals (resident with the stream's ECS bytes)
 //   destuffed  u8                  byte-unstuffed entropy data, each interval 16-B aligned
-//   coefs      int16[64] blocks    MCU-major: block (image.coef_off + mcu*nblk_mcu + b)
+//   coefs      int16[64] blocks    MCU-major: block (image.coef_off + mcu*nblk_mcu + b), each
+//                                  block in zigzag order (K1's decode order)
 //   planes     u8                  per component, padded to the MCU grid (general path only)
 #pragma once
 #include <stdint.h>
@@ -45,7 +46,7 @@ struct RjHuffDev {
 struct RjTableSet {
   RjHuffDev dc[2];
   RjHuffDev ac[2];
-  uint16_t q[4][64];  // natural order (DQT is zigzag order: rocjpeg_parser.cpp:239)
+  uint16_t qz[4][64];  // zigzag (DQT) order, as stored by the parser (rocjpeg_parser.cpp:239)
 };
 
 // Output jobs of the general (two-stage) path: one per written channel.

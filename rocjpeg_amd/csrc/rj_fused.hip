@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void k_fused(const RjImageDev *__restrict__ im
 
   // ---- A: quant tables + coefficient blocks -> LDS ----
   const RjTableSet *ts = tabsets + im.tabset;
-  for (uint32_t k = tid; k < ncomp * 64; k += 256) s_q[k >> 6][k & 63] = ts->q[im.comp_tq[k >> 6] & 3][k & 63];
+  for (uint32_t k = tid; k < ncomp * 64; k += 256) s_q[k >> 6][k & 63] = ts->qz[im.comp_tq[k >> 6] & 3][k & 63];
   {
     const uint4 *src = reinterpret_cast<const uint4 *>(coefs + (im.coef_off + (uint64_t(my) * im.mcux + mx0) * nblk) * 64u);
     const uint32_t n16 = nb * 8;
@@ -125,18 +125,8 @@ __global__ __launch_bounds__(256) void k_fused(const RjImageDev *__restrict__ im
     const uint32_t hc = inter ? im.comp_h[c_b] : 1;
     tx = (mcu * hc + (inter ? im.blk_dx[b] : 0)) * 8;
     ty = (inter ? im.blk_dy[b] : 0) * 8;
-    const uint4 *blk = reinterpret_cast<const uint4 *>(s_buf + tid * RJ_BLK_STRIDE);
-    const uint4 *q4 = reinterpret_cast<const uint4 *>(s_q[c_b]);
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-      const uint4 a = blk[r], qa = q4[r];
-      const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, qw[4] = {qa.x, qa.y, qa.z, qa.w};
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        v[r * 8 + 2 * j] = int32_t(int16_t(aw[j] & 0xFFFF)) * int32_t(qw[j] & 0xFFFF);
-        v[r * 8 + 2 * j + 1] = int32_t(int16_t(aw[j] >> 16)) * int32_t(qw[j] >> 16);
-      }
-    }
+    dezigzag_dequant(reinterpret_cast<const uint4 *>(s_buf + tid * RJ_BLK_STRIDE),
+                     reinterpret_cast<const uint4 *>(s_q[c_b]), v);
   }
   __syncthreads();  // every block is in registers: the staging area becomes the sample tiles
   if (has_blk) {

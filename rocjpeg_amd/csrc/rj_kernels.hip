@@ -201,24 +201,14 @@ __device__ __forceinline__ uint32_t huff_slow(const RjHuffDev *t, uint32_t peek1
   return e;
 }
 
-__constant__ uint8_t c_zigzag[80] = {
-    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33,
-    40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36,
-    29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
-    47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
-
 __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ imgs, int nimg, uint32_t nseg,
                                                 const uint8_t *__restrict__ destuffed,
                                                 const uint32_t *__restrict__ seg_len,
                                                 const RjTableSet *__restrict__ tabsets, int16_t *__restrict__ coefs) {
-  // per-lane LDS areas padded to 144 B / 272 B so that the 8/16-lane groups of ds_*_b128
-  // hit distinct banks (unpadded 128/256-B strides put a whole group on one bank set)
-  __shared__ __attribute__((aligned(16))) uint4 s_blk[64][9];
+  // per-lane ring padded to 272 B so the 8-lane groups of its ds_write_b128 hit distinct banks
   __shared__ __attribute__((aligned(16))) uint4 s_ring[64][RJ_RING_CHUNKS + 1];
   __shared__ __attribute__((aligned(16))) RjHuffDev s_tab[4];  // dc0, dc1, ac0, ac1
-  __shared__ uint8_t s_zz[80];
   const uint32_t lane = threadIdx.x;
-  for (uint32_t k = lane; k < 80; k += 64) s_zz[k] = c_zigzag[k];
   const uint32_t g = blockIdx.x * 64u + lane;
   const bool valid = g < nseg;
   const int i = valid ? upper_index(nimg, g, [&](int k) { return imgs[k].seg_prefix; }) : 0;
@@ -232,9 +222,8 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
     const uint32_t T = __shfl(my_ts, __ffsll((long long)m) - 1, 64);
     __syncthreads();
     {
-      const RjTableSet *tsT = tabsets + T;
       static_assert(sizeof(RjHuffDev) % 16 == 0, "RjHuffDev must be 16-B multiple");
-      const uint4 *s4 = reinterpret_cast<const uint4 *>(&tsT->dc[0]);  // dc[0], dc[1], ac[0], ac[1] contiguous
+      const uint4 *s4 = reinterpret_cast<const uint4 *>(&tabsets[T].dc[0]);  // dc0, dc1, ac0, ac1 contiguous
       uint4 *d4 = reinterpret_cast<uint4 *>(s_tab);
       for (uint32_t k = lane; k < 4 * sizeof(RjHuffDev) / 16; k += 64) d4[k] = s4[k];
     }
@@ -245,34 +234,34 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
       const uint32_t nblk = im.nblk_mcu;
       uint32_t comp_bits = 0;  // 2 bits per block-in-MCU: its component
       for (uint32_t b = 0; b < nblk; b++) comp_bits |= uint32_t(im.blk_comp[b]) << (2 * b);
-      // table index per component: dc tables 0/1, ac tables 2/3 of s_tab
+      // s_tab index per component: dc tables 0/1, ac tables 2/3
       const uint32_t dc0 = im.comp_td[0] & 1, ac0 = 2 + (im.comp_ta[0] & 1);
       const uint32_t dc1 = im.comp_td[1] & 1, ac1 = 2 + (im.comp_ta[1] & 1);
       const uint32_t dc2 = im.comp_td[2] & 1, ac2 = 2 + (im.comp_ta[2] & 1);
 
       BitReader br;
       br.init(reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off), s_ring[lane], seg_len[g]);
-
-      int16_t *out = coefs + (im.coef_off + uint64_t(sg.mcu_first) * nblk) * 64u;
-      uint4 *blk4 = s_blk[lane];
-      int16_t *blk = reinterpret_cast<int16_t *>(blk4);
+      int16_t *blk = coefs + (im.coef_off + uint64_t(sg.mcu_first) * nblk) * 64u;  // current block (zigzag order)
+      int16_t *const blk_end = blk + uint64_t(sg.mcu_count) * nblk * 64u;
       const uint4 zero4 = make_uint4(0, 0, 0, 0);
-#pragma unroll
-      for (int q = 0; q < 8; q++) blk4[q] = zero4;
 
       int pred0 = 0, pred1 = 0, pred2 = 0;
       bool skip = (sg.flags & RJ_SEG_MISSING) != 0;
-      uint32_t m_i = 0, b = 0;
+      uint32_t b = 0;
       int k = 0;
-      const uint32_t nmcu = sg.mcu_count;
       uint32_t iter = 0;
-      while (m_i < nmcu) {
+      while (blk < blk_end) {
         if ((iter++ & (RJ_PHASE - 1)) == 0) br.phase();  // same count in every active lane
-        const uint32_t c = (comp_bits >> (2 * b)) & 3u;
+        if (k == 0) {  // new block: zero it in HBM first (same-lane stores stay ordered)
+          uint4 *o = reinterpret_cast<uint4 *>(blk);
+#pragma unroll
+          for (int q = 0; q < 8; q++) o[q] = zero4;
+        }
         if (skip) {
           k = 64;
         } else {
           br.refill();
+          const uint32_t c = (comp_bits >> (2 * b)) & 3u;
           const uint32_t peek32 = uint32_t(br.acc >> 32);
           const uint32_t tix = k == 0 ? (c == 0 ? dc0 : (c == 1 ? dc1 : dc2)) : (c == 0 ? ac0 : (c == 1 ? ac1 : ac2));
           const RjHuffDev *tab = &s_tab[tix];
@@ -283,38 +272,28 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
           }
           const uint32_t len = e >> 8, sym = e & 255u;
           const uint32_t s = sym & 15u, r = sym >> 4;
-          // extra bits follow the code inside the same peek (len + s <= 32 < bits available)
+          // the extra bits follow the code inside the same 32-bit peek (len + s <= 31)
           const uint32_t t = peek32 << len;
           const uint32_t raw = s ? (t >> (32u - s)) : 0u;
           const int val = (s && raw < (1u << (s - 1))) ? int(raw) - (1 << s) + 1 : int(raw);
           br.acc <<= (len + s);
           br.nb -= int(len + s);
-          if (k == 0) {  // DC: predictor per component (F.2.1.3)
-            const int p = (c == 0 ? pred0 : (c == 1 ? pred1 : pred2)) + val;
-            if (c == 0) pred0 = p;
-            else if (c == 1) pred1 = p;
-            else pred2 = p;
-            blk[0] = int16_t(p);
-            k = 1;
-          } else if (s) {
-            k += int(r);
-            blk[s_zz[k < 79 ? k : 79]] = int16_t(val);
-            k++;
-          } else {
-            k = (r == 15) ? k + 16 : 64;  // ZRL / EOB
-          }
+          // DC (k == 0): predictor per component (F.2.1.3); AC: run/size (F.2.2.2)
+          const bool isdc = k == 0;
+          const int pc = c == 0 ? pred0 : (c == 1 ? pred1 : pred2);
+          const int p = pc + val;
+          pred0 = (isdc && c == 0) ? p : pred0;
+          pred1 = (isdc && c == 1) ? p : pred1;
+          pred2 = (isdc && c == 2) ? p : pred2;
+          const int kk = isdc ? 0 : k + int(r);  // zigzag position of this coefficient
+          if (isdc || s) blk[kk < 63 ? kk : 63] = int16_t(isdc ? p : val);
+          k = isdc ? 1 : (s ? kk + 1 : (r == 15 ? k + 16 : 64));  // ZRL / EOB
         }
-        if (k >= 64) {  // block complete: 128 B out, LDS staging cleared for the next one
-          uint4 *o = reinterpret_cast<uint4 *>(out + (uint64_t(m_i) * nblk + b) * 64u);
-#pragma unroll
-          for (int q = 0; q < 8; q++) {
-            o[q] = blk4[q];
-            blk4[q] = zero4;
-          }
+        if (k >= 64) {  // block complete
+          blk += 64;
           k = 0;
           if (++b == nblk) {
             b = 0;
-            m_i++;
             if (br.overrun()) skip = true;  // libjpeg: rest of the interval stays zero
           }
         }
@@ -362,20 +341,9 @@ __global__ __launch_bounds__(256) void k_idct_planes(const RjImageDev *__restric
     cb = im.coef_off + local;
   }
   const uint4 *src = reinterpret_cast<const uint4 *>(coefs + cb * 64u);
-  const uint4 *q4 = reinterpret_cast<const uint4 *>(tabsets[im.tabset].q[im.comp_tq[c] & 3]);
+  const uint4 *q4 = reinterpret_cast<const uint4 *>(tabsets[im.tabset].qz[im.comp_tq[c] & 3]);
   int32_t v[64];
-#pragma unroll
-  for (int r = 0; r < 8; r++) {
-    const uint4 a = src[r];   // coefficients r*8 .. r*8+7
-    const uint4 qa = q4[r];   // quant entries r*8 .. r*8+7
-    const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
-    const uint32_t qw[4] = {qa.x, qa.y, qa.z, qa.w};
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      v[r * 8 + 2 * j] = int32_t(int16_t(aw[j] & 0xFFFF)) * int32_t(qw[j] & 0xFFFF);
-      v[r * 8 + 2 * j + 1] = int32_t(int16_t(aw[j] >> 16)) * int32_t(qw[j] >> 16);
-    }
-  }
+  dezigzag_dequant(src, q4, v);
   uint8_t o[64];
   idct_islow_block(v, o);
   uint8_t *dst = planes + im.plane_off[c] + uint64_t(by) * 8u * im.plane_pitch[c] + bx * 8u;

@@ -59,6 +59,26 @@ __device__ __forceinline__ void islow_1d(int32_t x0, int32_t x1, int32_t x2, int
   t[4] = t13 - o0;
 }
 
+// K1 stores each block in zigzag order (its decode order); the quant tables are also kept in
+// zigzag (DQT) order, so dequantisation is element-wise and the permutation to natural order
+// happens in registers with compile-time indices.
+__device__ __forceinline__ void dezigzag_dequant(const uint4 *coef_zz, const uint4 *q_zz, int32_t (&v)[64]) {
+  constexpr uint8_t kNat[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const uint4 a = coef_zz[r], qa = q_zz[r];
+    const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, qw[4] = {qa.x, qa.y, qa.z, qa.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      v[kNat[r * 8 + 2 * j]] = int32_t(int16_t(aw[j] & 0xFFFF)) * int32_t(qw[j] & 0xFFFF);
+      v[kNat[r * 8 + 2 * j + 1]] = int32_t(int16_t(aw[j] >> 16)) * int32_t(qw[j] >> 16);
+    }
+  }
+}
+
 // libjpeg range_limit[(x) & RANGE_MASK] after the final descale: wrap mod 1024, +128, clamp.
 __device__ __forceinline__ uint32_t islow_range_limit(int32_t v) {
   const int32_t w = ((v + 512) & 1023) - 384;

@@ -30,10 +30,6 @@ int ClassifyCss(const StreamInfo &s) {
   return kCssUnknown;
 }
 
-const uint8_t kZigzagToNatural[64] = {
-    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
-    41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
-    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
 uint64_t Fnv1a(uint64_t h, const void *p, size_t n) {
   const uint8_t *b = static_cast<const uint8_t *>(p);
@@ -287,7 +283,7 @@ void Stream::BuildPlan() {
     }
   }
   for (int q = 0; q < 4; q++)
-    for (int k = 0; k < 64; k++) p.tables.q[q][kZigzagToNatural[k]] = s.qt_zz[q][k];
+    for (int k = 0; k < 64; k++) p.tables.qz[q][k] = s.qt_zz[q][k];
   h = Fnv1a(h, &p.tables, sizeof(p.tables));
   p.table_hash = h;
 
