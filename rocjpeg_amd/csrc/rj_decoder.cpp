@@ -206,7 +206,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // ---- layout ----
   std::vector<RjImageDev> imgs(n);
   std::vector<RjJobDev> jobs;
-  uint64_t destuff_total = 0, coef_blocks = 0, plane_bytes = 0, stage_bytes = 0;
+  uint64_t destuff_total = 0, coef_blocks = 0, ent_total = 0, plane_bytes = 0, stage_bytes = 0;
   uint32_t seg_total = 0, blk_total = 0, rows_total = 0;
   uint64_t ecs_bytes = 0, out_bytes = 0;
   std::vector<uint64_t> stage_off(n, UINT64_MAX);
@@ -248,6 +248,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     destuff_total += AlignUp(p.destuff_bytes, 256);
     d.coef_off = coef_blocks;
     coef_blocks += uint64_t(p.mcux) * p.mcuy * p.nblk_mcu;
+    d.ent_off = ent_total;
+    ent_total += AlignUp(p.entries, 4);
     d.blk_prefix = blk_total;
     for (int c = 0; c < in.ncomp; c++) {
       d.plane_pitch[c] = p.wblk[c] * 8;
@@ -383,7 +385,11 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   RJ_CHECK(d_desc_.Ensure(blob));
   RJ_CHECK(d_destuff_.Ensure(std::max<uint64_t>(destuff_total, 256)));
   RJ_CHECK(d_seglen_.Ensure(std::max<uint64_t>(uint64_t(seg_total) * 4, 256)));
-  RJ_CHECK(d_coefs_.Ensure(std::max<uint64_t>(coef_blocks * 128, 256)));
+  RJ_CHECK(d_coefs_.Ensure(std::max<uint64_t>(coef_blocks * sizeof(uint2), 256)));
+  RJ_CHECK(d_entries_.Ensure(std::max<uint64_t>(ent_total * 4, 256)));
+  RjCoefBuf cbuf;
+  cbuf.blk = d_coefs_.as<uint2>();
+  cbuf.ent = d_entries_.as<uint32_t>();
   RJ_CHECK(d_planes_.Ensure(std::max<uint64_t>(plane_bytes, 256)));
   uint8_t *h = h_stage_.data();
   uint8_t *dbase = d_desc_.as<uint8_t>();
@@ -419,10 +425,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   RJ_HIP(LaunchDestuff(stream_, d_imgs, n, seg_total, d_destuff_.as<uint8_t>(), d_seglen_.as<uint32_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[2], stream_));
   RJ_HIP(LaunchHuffman(stream_, d_imgs, n, seg_total, d_destuff_.as<uint8_t>(), d_seglen_.as<uint32_t>(), d_tabs,
-                       d_coefs_.as<int16_t>()));
+                       cbuf));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
-  RJ_HIP(LaunchFusedOutput(stream_, d_imgs, n, d_strips, strip_total, d_coefs_.as<int16_t>(), d_tabs));
-  RJ_HIP(LaunchIdctPlanes(stream_, d_imgs, n, blk_total, d_coefs_.as<int16_t>(), d_tabs, d_planes_.as<uint8_t>()));
+  RJ_HIP(LaunchFusedOutput(stream_, d_imgs, n, d_strips, strip_total, cbuf, d_tabs));
+  RJ_HIP(LaunchIdctPlanes(stream_, d_imgs, n, blk_total, cbuf, d_tabs, d_planes_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[4], stream_));
   RJ_HIP(LaunchOutputJobs(stream_, d_imgs, d_jobs, int(jobs.size()), rows_total, d_planes_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[5], stream_));
@@ -431,7 +437,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   timings_.images = uint32_t(n);
   timings_.intervals = seg_total;
   timings_.ecs_bytes = ecs_bytes;
-  timings_.coef_bytes = coef_blocks * 128;
+  timings_.coef_bytes = coef_blocks * 128;  // dense-equivalent; the sparse bytes are data-dependent
   timings_.output_bytes = out_bytes;
   timings_.fused_images = fused_images;
   if (profiling_) {

@@ -6,13 +6,24 @@
 //   tabsets[]  RjTableSet          de-duplicated Huffman LUTs + natural-order quant tables
 //   segs       RjSegDev per image  restart intervals (resident with the stream's ECS bytes)
 //   destuffed  u8                  byte-unstuffed entropy data, each interval 16-B aligned
-//   coefs      int16[64] blocks    MCU-major: block (image.coef_off + mcu*nblk_mcu + b), each
-//                                  block in zigzag order (K1's decode order)
+//   coef index uint2 per block     MCU-major: block (image.coef_off + mcu*nblk_mcu + b) ->
+//                                  {first entry (image-relative), entry count}
+//   coef entries uint32            sparse coefficients: int16 value | zigzag position << 16;
+//                                  each block's list 16-B aligned, each interval's region sized
+//                                  for the worst case (64 entries per block)
 //   planes     u8                  per component, padded to the MCU grid (general path only)
 #pragma once
+#include <hip/hip_runtime.h>  // uint2/uint4 vector types (all users are built with hipcc)
 #include <stdint.h>
 
 #define RJ_MAX_BLK_MCU 10
+
+// Sparse coefficient storage written by K1 and read by the IDCT kernels.
+struct RjCoefBuf {
+  uint2 *blk;     // per block: {first entry relative to image.ent_off, entry count}
+  uint32_t *ent;  // entries: uint16 value | zigzag position << 16
+};
+#define RJ_ENT_PER_BLOCK 64  // worst case: DC + 63 AC (each position written at most once)
 
 // One restart interval of one image (host parser rj_stream.cpp builds these).
 struct RjSegDev {
@@ -22,6 +33,8 @@ struct RjSegDev {
   uint32_t mcu_first;  // first MCU of the interval
   uint32_t mcu_count;  // MCUs in the interval
   uint32_t flags;      // RJ_SEG_MISSING: marker not found -> interval decodes to zero blocks
+  uint32_t ent_off;    // first sparse-coefficient entry of the interval, relative to image.ent_off
+  uint32_t pad;
 };
 #define RJ_SEG_MISSING 1u
 
@@ -88,7 +101,8 @@ struct RjImageDev {
   uint32_t nseg;
   uint32_t seg_prefix;   // exclusive prefix of segments over the batch
   uint64_t destuff_off;  // into the destuffed buffer
-  uint64_t coef_off;     // in blocks
+  uint64_t coef_off;     // in blocks (coefficient index)
+  uint64_t ent_off;      // in entries (sparse coefficients)
   // component planes (general path)
   uint64_t plane_off[4];
   uint32_t plane_pitch[4], plane_rows[4];

@@ -3,15 +3,16 @@
 //
 // One workgroup (256 threads = 4 waves) per strip = one MCU row x 512 pixels (32 MCUs,
 // 192 blocks at 4:2:0; never more than 256 blocks).
-//   A  coalesced copy of the strip's coefficient blocks (contiguous in K1's MCU-major layout)
-//      into LDS, 16 B per lane, block stride padded to 144 B so that the per-thread
-//      ds_read_b128 of phase B is bank-conflict free (36*l mod 64 distinct for 16 lanes).
+//   A  zero the strip's LDS blocks, then thread b expands block b's sparse coefficient list
+//      (K1's {start,count} index + 16-B aligned entries) into its block; block stride padded
+//      to 144 B so that the per-thread ds_read_b128 of phase B is bank-conflict free.
 //   B  thread b: block b's 64 coefficients into VGPRs, dequant, full 2-D ISLOW IDCT in
 //      registers, 8 x 8-byte rows into the strip's component sample tiles (aliasing A).
 //   C  lane = 4 consecutive pixels: one ds_read_b32 of luma, one ds_read_u16 (4:2:0/4:2:2)
 //      or b32 (4:4:4) per chroma plane, 4 x (4 fma + 3 v_cvt_pk_u8_f32) packed straight
 //      into 3 dwords -> one 12-B store per lane, 768 contiguous bytes per wave instruction.
-// HBM traffic per strip = its coefficient bytes read once + its output bytes written once.
+// HBM traffic per strip = its sparse coefficients (~4 B per nonzero + 8 B per block) read once +
+// its output bytes written once.
 //
 // Same integer IDCT (rj_math.h) and CSC arithmetic as the general path, so both paths are
 // bit-identical; eligibility (no ROI, canonical sampling geometry, copy channels with
@@ -59,7 +60,7 @@ __device__ __forceinline__ void store_bytes(uint8_t *d, uint32_t n, const uint32
 
 __global__ __launch_bounds__(256) void k_fused(const RjImageDev *__restrict__ imgs, int nimg,
                                                const uint32_t *__restrict__ strip_prefix,
-                                               const int16_t *__restrict__ coefs,
+                                               RjCoefBuf coefs,
                                                const RjTableSet *__restrict__ tabsets) {
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_MAX_STRIP_BLK * RJ_BLK_STRIDE];  // A/B, then tiles
   __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
@@ -107,11 +108,13 @@ __global__ __launch_bounds__(256) void k_fused(const RjImageDev *__restrict__ im
   // ---- A: quant tables + coefficient blocks -> LDS ----
   const RjTableSet *ts = tabsets + im.tabset;
   for (uint32_t k = tid; k < ncomp * 64; k += 256) s_q[k >> 6][k & 63] = ts->qz[im.comp_tq[k >> 6] & 3][k & 63];
-  {
-    const uint4 *src = reinterpret_cast<const uint4 *>(coefs + (im.coef_off + (uint64_t(my) * im.mcux + mx0) * nblk) * 64u);
-    const uint32_t n16 = nb * 8;
-    for (uint32_t k = tid; k < n16; k += 256)
-      *reinterpret_cast<uint4 *>(s_buf + (k >> 3) * RJ_BLK_STRIDE + (k & 7) * 16) = src[k];
+  for (uint32_t k = tid; k < nb * 8; k += 256)
+    *reinterpret_cast<uint4 *>(s_buf + (k >> 3) * RJ_BLK_STRIDE + (k & 7) * 16) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  if (tid < nb) {  // thread t expands block t's sparse entries (zigzag order) into LDS
+    const uint2 bi = coefs.blk[im.coef_off + (uint64_t(my) * im.mcux + mx0) * nblk + tid];
+    scatter_block(reinterpret_cast<const uint4 *>(coefs.ent + im.ent_off + bi.x), bi.y,
+                  reinterpret_cast<int16_t *>(s_buf + tid * RJ_BLK_STRIDE));
   }
   __syncthreads();
 
@@ -253,7 +256,7 @@ __global__ __launch_bounds__(256) void k_fused(const RjImageDev *__restrict__ im
 }
 
 hipError_t LaunchFusedOutput(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *strip_prefix,
-                             uint32_t nstrips, const int16_t *coefs, const RjTableSet *tabsets) {
+                             uint32_t nstrips, RjCoefBuf coefs, const RjTableSet *tabsets) {
   if (nstrips == 0) return hipSuccess;
   hipLaunchKernelGGL(k_fused, dim3(nstrips), dim3(256), 0, st, imgs, nimg, strip_prefix, coefs, tabsets);
   return hipGetLastError();

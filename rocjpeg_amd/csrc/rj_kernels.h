@@ -11,12 +11,12 @@ namespace rj {
 hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nseg, uint8_t *destuffed,
                          uint32_t *seg_len);
 
-// K1: Huffman entropy decode, one lane per restart interval -> int16 coefficient blocks.
+// K1: Huffman entropy decode, one lane per restart interval -> sparse coefficients.
 hipError_t LaunchHuffman(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nseg, const uint8_t *destuffed,
-                         const uint32_t *seg_len, const RjTableSet *tabsets, int16_t *coefs);
+                         const uint32_t *seg_len, const RjTableSet *tabsets, RjCoefBuf coefs);
 
 // K2a (general path): dequantise + ISLOW IDCT of every block into MCU-padded component planes.
-hipError_t LaunchIdctPlanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint64_t nblocks, const int16_t *coefs,
+hipError_t LaunchIdctPlanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint64_t nblocks, RjCoefBuf coefs,
                             const RjTableSet *tabsets, uint8_t *planes);
 
 // K2b (general path): every output format / ROI of rocjpeg_decoder.cpp:143-180 from the planes.
@@ -27,6 +27,6 @@ hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobD
 // coefficients to the caller's buffers, one workgroup per MCU-row strip.  Only for images whose
 // output window is tile-local (no ROI quirks); see rj_decoder.cpp::FusedEligible.
 hipError_t LaunchFusedOutput(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *strip_prefix,
-                             uint32_t nstrips, const int16_t *coefs, const RjTableSet *tabsets);
+                             uint32_t nstrips, RjCoefBuf coefs, const RjTableSet *tabsets);
 
 }  // namespace rj

@@ -204,7 +204,7 @@ __device__ __forceinline__ uint32_t huff_slow(const RjHuffDev *t, uint32_t peek1
 __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ imgs, int nimg, uint32_t nseg,
                                                 const uint8_t *__restrict__ destuffed,
                                                 const uint32_t *__restrict__ seg_len,
-                                                const RjTableSet *__restrict__ tabsets, int16_t *__restrict__ coefs) {
+                                                const RjTableSet *__restrict__ tabsets, RjCoefBuf coefs) {
   // per-lane ring padded to 272 B so the 8-lane groups of its ds_write_b128 hit distinct banks
   __shared__ __attribute__((aligned(16))) uint4 s_ring[64][RJ_RING_CHUNKS + 1];
   __shared__ __attribute__((aligned(16))) RjHuffDev s_tab[4];  // dc0, dc1, ac0, ac1
@@ -241,22 +241,18 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
 
       BitReader br;
       br.init(reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off), s_ring[lane], seg_len[g]);
-      int16_t *blk = coefs + (im.coef_off + uint64_t(sg.mcu_first) * nblk) * 64u;  // current block (zigzag order)
-      int16_t *const blk_end = blk + uint64_t(sg.mcu_count) * nblk * 64u;
-      const uint4 zero4 = make_uint4(0, 0, 0, 0);
+      uint2 *bidx = coefs.blk + im.coef_off + uint64_t(sg.mcu_first) * nblk;  // current block's index slot
+      uint2 *const bidx_end = bidx + uint64_t(sg.mcu_count) * nblk;
+      uint32_t *const ent = coefs.ent + im.ent_off + sg.ent_off;  // this interval's entry region
+      uint32_t ne = 0, bstart = 0;
 
       int pred0 = 0, pred1 = 0, pred2 = 0;
       bool skip = (sg.flags & RJ_SEG_MISSING) != 0;
       uint32_t b = 0;
       int k = 0;
       uint32_t iter = 0;
-      while (blk < blk_end) {
+      while (bidx < bidx_end) {
         if ((iter++ & (RJ_PHASE - 1)) == 0) br.phase();  // same count in every active lane
-        if (k == 0) {  // new block: zero it in HBM first (same-lane stores stay ordered)
-          uint4 *o = reinterpret_cast<uint4 *>(blk);
-#pragma unroll
-          for (int q = 0; q < 8; q++) o[q] = zero4;
-        }
         if (skip) {
           k = 64;
         } else {
@@ -286,11 +282,13 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
           pred1 = (isdc && c == 1) ? p : pred1;
           pred2 = (isdc && c == 2) ? p : pred2;
           const int kk = isdc ? 0 : k + int(r);  // zigzag position of this coefficient
-          if (isdc || s) blk[kk < 63 ? kk : 63] = int16_t(isdc ? p : val);
+          if (isdc || s) ent[ne++] = (uint32_t(isdc ? p : val) & 0xFFFFu) | (uint32_t(kk < 63 ? kk : 63) << 16);
           k = isdc ? 1 : (s ? kk + 1 : (r == 15 ? k + 16 : 64));  // ZRL / EOB
         }
-        if (k >= 64) {  // block complete
-          blk += 64;
+        if (k >= 64) {  // block complete: its index entry; next list starts 16-B aligned
+          *bidx++ = make_uint2(sg.ent_off + bstart, ne - bstart);
+          ne = (ne + 3u) & ~3u;
+          bstart = ne;
           k = 0;
           if (++b == nblk) {
             b = 0;
@@ -303,7 +301,7 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
 }
 
 hipError_t LaunchHuffman(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nseg, const uint8_t *destuffed,
-                         const uint32_t *seg_len, const RjTableSet *tabsets, int16_t *coefs) {
+                         const uint32_t *seg_len, const RjTableSet *tabsets, RjCoefBuf coefs) {
   if (nseg == 0) return hipSuccess;
   hipLaunchKernelGGL(k_huffman, dim3((nseg + 63) / 64), dim3(64), 0, st, imgs, nimg, nseg, destuffed, seg_len, tabsets,
                      coefs);
@@ -314,36 +312,46 @@ hipError_t LaunchHuffman(hipStream_t st, const RjImageDev *imgs, int nimg, uint3
 // K2a: IDCT into component planes (general path).
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_idct_planes(const RjImageDev *__restrict__ imgs, int nimg, uint64_t nblocks,
-                                                     const int16_t *__restrict__ coefs,
-                                                     const RjTableSet *__restrict__ tabsets,
+                                                     RjCoefBuf coefs, const RjTableSet *__restrict__ tabsets,
                                                      uint8_t *__restrict__ planes) {
+  __shared__ __attribute__((aligned(16))) uint4 s_blk[256][9];  // 144-B stride: conflict-free b128
   const uint64_t gb = uint64_t(blockIdx.x) * 256u + threadIdx.x;
-  if (gb >= nblocks) return;
-  const int i = upper_index(nimg, uint32_t(gb), [&](int k) { return imgs[k].blk_prefix; });
+  const bool active = gb < nblocks;
+#pragma unroll
+  for (int q = 0; q < 8; q++) s_blk[threadIdx.x][q] = make_uint4(0, 0, 0, 0);
+  int i = 0, c = 0;
+  uint32_t bx = 0, by = 0;
+  if (active) {
+    i = upper_index(nimg, uint32_t(gb), [&](int k) { return imgs[k].blk_prefix; });
+    const RjImageDev &im = imgs[i];
+    uint32_t local = uint32_t(gb) - im.blk_prefix;
+    uint32_t wb = im.plane_pitch[0] >> 3, hb = im.plane_rows[0] >> 3;
+    while (c + 1 < im.ncomp && local >= wb * hb) {
+      local -= wb * hb;
+      c++;
+      wb = im.plane_pitch[c] >> 3;
+      hb = im.plane_rows[c] >> 3;
+    }
+    by = local / wb;
+    bx = local - by * wb;
+    uint64_t cb;
+    if (im.interleaved) {
+      const uint32_t hc = im.comp_h[c], vc = im.comp_v[c];
+      const uint32_t mx = bx / hc, my = by / vc;
+      const uint32_t b = im.comp_blk0[c] + (by - my * vc) * hc + (bx - mx * hc);
+      cb = im.coef_off + (uint64_t(my) * im.mcux + mx) * im.nblk_mcu + b;
+    } else {
+      cb = im.coef_off + local;
+    }
+    const uint2 bi = coefs.blk[cb];
+    scatter_block(reinterpret_cast<const uint4 *>(coefs.ent + im.ent_off + bi.x), bi.y,
+                  reinterpret_cast<int16_t *>(s_blk[threadIdx.x]));
+  }
+  if (!active) return;  // each thread only touches its own LDS block: no barrier needed
   const RjImageDev &im = imgs[i];
-  uint32_t local = uint32_t(gb) - im.blk_prefix;
-  int c = 0;
-  uint32_t wb = im.plane_pitch[0] >> 3, hb = im.plane_rows[0] >> 3;
-  while (c + 1 < im.ncomp && local >= wb * hb) {
-    local -= wb * hb;
-    c++;
-    wb = im.plane_pitch[c] >> 3;
-    hb = im.plane_rows[c] >> 3;
-  }
-  const uint32_t by = local / wb, bx = local - by * wb;
-  uint64_t cb;
-  if (im.interleaved) {
-    const uint32_t hc = im.comp_h[c], vc = im.comp_v[c];
-    const uint32_t mx = bx / hc, my = by / vc;
-    const uint32_t b = im.comp_blk0[c] + (by - my * vc) * hc + (bx - mx * hc);
-    cb = im.coef_off + (uint64_t(my) * im.mcux + mx) * im.nblk_mcu + b;
-  } else {
-    cb = im.coef_off + local;
-  }
-  const uint4 *src = reinterpret_cast<const uint4 *>(coefs + cb * 64u);
   const uint4 *q4 = reinterpret_cast<const uint4 *>(tabsets[im.tabset].qz[im.comp_tq[c] & 3]);
   int32_t v[64];
-  dezigzag_dequant(src, q4, v);
+  dezigzag_dequant(s_blk[threadIdx.x], q4, v);
   uint8_t o[64];
   idct_islow_block(v, o);
   uint8_t *dst = planes + im.plane_off[c] + uint64_t(by) * 8u * im.plane_pitch[c] + bx * 8u;
@@ -356,7 +364,7 @@ __global__ __launch_bounds__(256) void k_idct_planes(const RjImageDev *__restric
   }
 }
 
-hipError_t LaunchIdctPlanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint64_t nblocks, const int16_t *coefs,
+hipError_t LaunchIdctPlanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint64_t nblocks, RjCoefBuf coefs,
                             const RjTableSet *tabsets, uint8_t *planes) {
   if (nblocks == 0) return hipSuccess;
   hipLaunchKernelGGL(k_idct_planes, dim3(uint32_t((nblocks + 255) / 256)), dim3(256), 0, st, imgs, nimg, nblocks, coefs,

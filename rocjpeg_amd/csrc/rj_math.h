@@ -59,6 +59,20 @@ __device__ __forceinline__ void islow_1d(int32_t x0, int32_t x1, int32_t x2, int
   t[4] = t13 - o0;
 }
 
+// Expand one block's sparse entries (16-B aligned list, `cnt` valid) into a zeroed 128-B LDS
+// block in zigzag order.  Two 16-B loads in flight per step.
+__device__ __forceinline__ void scatter_block(const uint4 *src, uint32_t cnt, int16_t *dst_zz) {
+  const uint32_t nq = (cnt + 3) >> 2;
+  for (uint32_t q = 0; q < nq; q += 2) {
+    const uint4 a = src[q];
+    const uint4 b = (q + 1 < nq) ? src[q + 1] : make_uint4(0, 0, 0, 0);
+    const uint32_t e[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if (4 * q + j < cnt) dst_zz[(e[j] >> 16) & 63] = int16_t(e[j] & 0xFFFF);
+  }
+}
+
 // K1 stores each block in zigzag order (its decode order); the quant tables are also kept in
 // zigzag (DQT) order, so dequantisation is element-wise and the permutation to natural order
 // happens in registers with compile-time indices.

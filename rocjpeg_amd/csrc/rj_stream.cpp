@@ -296,7 +296,7 @@ void Stream::BuildPlan() {
   const uint8_t *e = s.ecs;
   const uint32_t n = s.ecs_size;
   uint32_t start = 0, i = 0;
-  uint64_t dst = 0;
+  uint64_t dst = 0, ent = 0;
   auto emit = [&](uint32_t b, uint32_t stop) {
     while (stop > b && e[stop - 1] == 0xFF) stop--;  // trailing fill
     if (p.segs.size() >= expected) return;
@@ -307,6 +307,9 @@ void Stream::BuildPlan() {
     sg.mcu_first = uint32_t(p.segs.size()) * (ri ? ri : total_mcus);
     sg.mcu_count = ri ? std::min(ri, total_mcus - sg.mcu_first) : total_mcus;
     sg.flags = 0;
+    sg.ent_off = uint32_t(ent);
+    sg.pad = 0;
+    ent += uint64_t(sg.mcu_count) * p.nblk_mcu * RJ_ENT_PER_BLOCK;
     dst += (uint64_t(sg.src_len) + 16 + 15) & ~uint64_t(15);  // >= 16 B of slack after each interval
     p.segs.push_back(sg);
   };
@@ -342,10 +345,14 @@ void Stream::BuildPlan() {
     sg.mcu_first = uint32_t(p.segs.size()) * ri;
     sg.mcu_count = std::min(ri, total_mcus - sg.mcu_first);
     sg.flags = RJ_SEG_MISSING;
+    sg.ent_off = uint32_t(ent);
+    sg.pad = 0;
+    ent += uint64_t(sg.mcu_count) * p.nblk_mcu * RJ_ENT_PER_BLOCK;
     dst += 16;
     p.segs.push_back(sg);
   }
   p.destuff_bytes = dst;
+  p.entries = ent;
 }
 
 void Stream::ReleaseResident() {

@@ -48,6 +48,7 @@ struct DecodePlan {
   uint32_t wblk[4] = {}, hblk[4] = {};
   std::vector<RjSegDev> segs;      // one per restart interval
   uint64_t destuff_bytes = 0;      // destuffed buffer size incl. per-interval alignment
+  uint64_t entries = 0;            // sparse-coefficient entries reserved (worst case)
   RjTableSet tables;               // derived tables
   uint64_t table_hash = 0;         // de-duplication key for tables
 };
