@@ -36,7 +36,9 @@ bool FusedEligible(const StreamInfo &in, const DecodePlan &p, int fmt, bool roi,
     if (!ok) return false;
   }
   const uint32_t W = in.width;
-  if (8u * p.hmax > 512 || (512u / (8u * p.hmax)) * p.nblk_mcu > 256) return false;  // strip limits of k_fused
+  for (int c = 0; c < 4; c++)  // k_fused addresses the destination with 32-bit offsets
+    if (o.pitch[c] >= (1u << 24) || uint64_t(o.pitch[c]) * (p.mcuy * 8u * p.vmax) >= (1ull << 31)) return false;
+  if (p.nblk_mcu == 0 || rj_fused_strip_mcus(p.hmax, p.nblk_mcu) == 0) return false;  // strip limits of k_fused
   // copy-type channels write `pitch` bytes per row in the reference: only pitch == width is fused
   if ((fmt == ROCJPEG_OUTPUT_Y || fmt == ROCJPEG_OUTPUT_YUV_PLANAR) && css != kCss422 && o.pitch[0] != W) return false;
   if (fmt == ROCJPEG_OUTPUT_YUV_PLANAR && in.ncomp == 3) {
@@ -210,8 +212,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   uint32_t seg_total = 0, blk_total = 0, rows_total = 0;
   uint64_t ecs_bytes = 0, out_bytes = 0;
   std::vector<uint64_t> stage_off(n, UINT64_MAX);
-  std::vector<uint32_t> strip_prefix(n);
-  uint32_t strip_total = 0, fused_images = 0;
+  std::vector<uint32_t> row_prefix(n);
+  uint32_t fused_rows = 0, fused_images = 0;
   for (int i = 0; i < n; i++) {
     Stream *s = streams[i];
     const StreamInfo &in = s->info();
@@ -275,7 +277,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       d.dst[c] = o.channel[c];
       d.dst_pitch[c] = o.pitch[c];
     }
-    strip_prefix[i] = strip_total;
+    row_prefix[i] = fused_rows;
 
     // ---- output jobs (general path): rocjpeg_decoder.cpp:143-180 ----
     const size_t jobs_before = jobs.size();
@@ -362,8 +364,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (path_policy_ == 0 && FusedEligible(in, p, fmt, roi, o)) {
       rows_total = jobs_rows_before;
       jobs.resize(jobs_before);
-      const uint32_t S = 512 / (8u * p.hmax);  // MCUs per k_fused strip (RJ_STRIP_PX)
-      strip_total += ((p.mcux + S - 1) / S) * p.mcuy;
+      fused_rows += p.mcuy;  // k_fused: one workgroup per MCU row
       fused_images++;
     } else {
       for (int c = 0; c < in.ncomp; c++) {
@@ -378,8 +379,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t off_imgs = 0;
   const uint64_t off_tabs = AlignUp(off_imgs + n * sizeof(RjImageDev), 256);
   const uint64_t off_jobs = AlignUp(off_tabs + tabs.size() * sizeof(RjTableSet), 256);
-  const uint64_t off_strips = AlignUp(off_jobs + std::max<size_t>(jobs.size(), 1) * sizeof(RjJobDev), 256);
-  const uint64_t off_stage = AlignUp(off_strips + n * sizeof(uint32_t), 256);
+  const uint64_t off_rows = AlignUp(off_jobs + std::max<size_t>(jobs.size(), 1) * sizeof(RjJobDev), 256);
+  const uint64_t off_stage = AlignUp(off_rows + n * sizeof(uint32_t), 256);
   const uint64_t blob = off_stage + stage_bytes;
   RJ_CHECK(h_stage_.Ensure(blob));
   RJ_CHECK(d_desc_.Ensure(blob));
@@ -412,8 +413,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   std::memcpy(h + off_imgs, imgs.data(), n * sizeof(RjImageDev));
   for (size_t t = 0; t < tabs.size(); t++) std::memcpy(h + off_tabs + t * sizeof(RjTableSet), tabs[t], sizeof(RjTableSet));
   if (!jobs.empty()) std::memcpy(h + off_jobs, jobs.data(), jobs.size() * sizeof(RjJobDev));
-  std::memcpy(h + off_strips, strip_prefix.data(), n * sizeof(uint32_t));
-  const uint32_t *d_strips = reinterpret_cast<const uint32_t *>(dbase + off_strips);
+  std::memcpy(h + off_rows, row_prefix.data(), n * sizeof(uint32_t));
+  const uint32_t *d_rows = reinterpret_cast<const uint32_t *>(dbase + off_rows);
 
   const RjImageDev *d_imgs = reinterpret_cast<const RjImageDev *>(dbase + off_imgs);
   const RjTableSet *d_tabs = reinterpret_cast<const RjTableSet *>(dbase + off_tabs);
@@ -427,7 +428,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   RJ_HIP(LaunchHuffman(stream_, d_imgs, n, seg_total, d_destuff_.as<uint8_t>(), d_seglen_.as<uint32_t>(), d_tabs,
                        cbuf));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
-  RJ_HIP(LaunchFusedOutput(stream_, d_imgs, n, d_strips, strip_total, cbuf, d_tabs));
+  RJ_HIP(LaunchFusedOutput(stream_, d_imgs, n, d_rows, fused_rows, cbuf, d_tabs));
   RJ_HIP(LaunchIdctPlanes(stream_, d_imgs, n, blk_total, cbuf, d_tabs, d_planes_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[4], stream_));
   RJ_HIP(LaunchOutputJobs(stream_, d_imgs, d_jobs, int(jobs.size()), rows_total, d_planes_.as<uint8_t>()));

@@ -18,6 +18,15 @@
 
 #define RJ_MAX_BLK_MCU 10
 
+// k_fused strips: one 64-lane workgroup per strip of S MCUs of one MCU row, at most one block
+// per lane and at most RJ_FUSED_MAX_PX pixels wide (4:2:0 -> 10 MCUs = 160 px, 60 blocks).
+#define RJ_FUSED_MAX_BLK 64
+#define RJ_FUSED_MAX_PX 512
+__host__ __device__ inline uint32_t rj_fused_strip_mcus(uint32_t hmax, uint32_t nblk_mcu) {
+  const uint32_t a = RJ_FUSED_MAX_PX / (8u * hmax), b = RJ_FUSED_MAX_BLK / nblk_mcu;
+  return a < b ? a : b;
+}
+
 // Sparse coefficient storage written by K1 and read by the IDCT kernels.
 struct RjCoefBuf {
   uint2 *blk;     // per block: {first entry relative to image.ent_off, entry count}

@@ -1,16 +1,18 @@
 // rj_fused.hip -- K2 fused output kernel: dequant + ISLOW IDCT + nearest chroma upsample +
 // YUV->RGB (or planar layouts) straight from the coefficient blocks to the caller's buffers.
 //
-// One workgroup (256 threads = 4 waves) per strip = one MCU row x 512 pixels (32 MCUs,
-// 192 blocks at 4:2:0; never more than 256 blocks).
-//   A  zero the strip's LDS blocks, then thread b expands block b's sparse coefficient list
+// One workgroup = ONE wavefront (64 lanes) per strip of S MCUs of one MCU row, at most one
+// block per lane (rj_fused_strip_mcus: 4:2:0 -> 10 MCUs = 160 x 16 px, 60 blocks).  Single-wave
+// workgroups need no cross-wave barriers, so the ~17 strips resident per CU run out of phase
+// and one strip's coefficient fetch (A) hides behind the others' IDCT / colour work (B, C).
+//   A  zero the strip's LDS blocks, then lane b expands block b's sparse coefficient list
 //      (K1's {start,count} index + 16-B aligned entries) into its block; block stride padded
-//      to 144 B so that the per-thread ds_read_b128 of phase B is bank-conflict free.
-//   B  thread b: block b's 64 coefficients into VGPRs, dequant, full 2-D ISLOW IDCT in
+//      to 144 B so that the per-lane ds_read_b128 of phase B is bank-conflict free.
+//   B  lane b: block b's 64 coefficients into VGPRs, dequant, full 2-D ISLOW IDCT in
 //      registers, 8 x 8-byte rows into the strip's component sample tiles (aliasing A).
 //   C  lane = 4 consecutive pixels: one ds_read_b32 of luma, one ds_read_u16 (4:2:0/4:2:2)
 //      or b32 (4:4:4) per chroma plane, 4 x (4 fma + 3 v_cvt_pk_u8_f32) packed straight
-//      into 3 dwords -> one 12-B store per lane, 768 contiguous bytes per wave instruction.
+//      into 3 dwords -> one 12-B store per lane.
 // HBM traffic per strip = its sparse coefficients (~4 B per nonzero + 8 B per block) read once +
 // its output bytes written once.
 //
@@ -25,8 +27,6 @@
 
 namespace rj {
 
-#define RJ_STRIP_PX 512
-#define RJ_MAX_STRIP_BLK 256
 #define RJ_BLK_STRIDE 144  // bytes per staged block in LDS (128 + 16 pad)
 
 // byte b of w as float: the backend selects v_cvt_f32_ubyte{0..3} for this pattern
@@ -52,44 +52,43 @@ __device__ __forceinline__ void csc4(uint32_t y4, const float (&u)[4], const flo
        __builtin_amdgcn_cvt_pk_u8_f32(r[3], 1, __builtin_amdgcn_cvt_pk_u8_f32(b[2], 0, 0u))));
 }
 
+// wave-uniform value: keeps it in an SGPR (the byte-sized descriptor fields arrive through
+// vector loads, which would otherwise pin a VGPR copy per uniform value across the strip loop)
+__device__ __forceinline__ uint32_t U(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
 __device__ __forceinline__ void store_bytes(uint8_t *d, uint32_t n, const uint32_t *w) {
 #pragma unroll
   for (int j = 0; j < 12; j++)
     if (uint32_t(j) < n) d[j] = uint8_t(w[j >> 2] >> (8 * (j & 3)));
 }
 
-__global__ __launch_bounds__(256) void k_fused(const RjImageDev *__restrict__ imgs, int nimg,
-                                               const uint32_t *__restrict__ strip_prefix,
-                                               RjCoefBuf coefs,
-                                               const RjTableSet *__restrict__ tabsets) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_MAX_STRIP_BLK * RJ_BLK_STRIDE];  // A/B, then tiles
+__global__ __launch_bounds__(64) void k_fused(const RjImageDev *__restrict__ imgs, int nimg,
+                                              const uint32_t *__restrict__ row_prefix,
+                                              RjCoefBuf coefs,
+                                              const RjTableSet *__restrict__ tabsets) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];  // A/B, then tiles
   __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
 
   const uint32_t tid = threadIdx.x;
-  const uint32_t sg = blockIdx.x;
+  const uint32_t row = blockIdx.x;
   int i;
   {
     int lo = 0, hi = nimg - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (strip_prefix[mid] <= sg) lo = mid;
+      if (row_prefix[mid] <= row) lo = mid;
       else hi = mid - 1;
     }
-    i = lo;
+    i = __builtin_amdgcn_readfirstlane(lo);  // wave-uniform: image fields become scalar loads
   }
   const RjImageDev &im = imgs[i];
-  const uint32_t hmax = im.hmax, vmax = im.vmax;
+  const uint32_t hmax = U(im.hmax), vmax = U(im.vmax);
   const uint32_t mcu_w = 8 * hmax, mcu_h = 8 * vmax;
-  const uint32_t S = RJ_STRIP_PX / mcu_w;  // MCUs per strip
-  const uint32_t strips_x = (im.mcux + S - 1) / S;
-  const uint32_t local = sg - strip_prefix[i];
-  const uint32_t my = local / strips_x;
-  const uint32_t mx0 = (local - my * strips_x) * S;
-  const uint32_t nm = min(S, im.mcux - mx0);
-  const uint32_t nblk = im.nblk_mcu;
-  const uint32_t nb = nm * nblk;
-  const bool inter = im.interleaved != 0;
-  const uint32_t ncomp = inter ? im.ncomp : 1;
+  const uint32_t nblk = U(im.nblk_mcu);
+  const uint32_t S = U(rj_fused_strip_mcus(hmax, nblk));  // MCUs per strip
+  const uint32_t my = row - row_prefix[i];
+  const bool inter = U(im.interleaved) != 0;
+  const uint32_t ncomp = inter ? U(im.ncomp) : 1;
 
   // tile geometry (component c: width S*hc*8, height vc*8), all offsets multiples of 8
   uint32_t tw[3], toff[3];
@@ -99,82 +98,102 @@ __global__ __launch_bounds__(256) void k_fused(const RjImageDev *__restrict__ im
     for (int c = 0; c < 3; c++) {
       const bool has = c < int(ncomp);
       const uint32_t hc = (inter && has) ? im.comp_h[c] : 1, vc = (inter && has) ? im.comp_v[c] : 1;
-      tw[c] = S * hc * 8;
-      toff[c] = off;
+      tw[c] = U(S * hc * 8);
+      toff[c] = U(off);
       off += has ? tw[c] * vc * 8 : 0;
     }
   }
+  // this lane's block inside an MCU and its tile position (constant over the row's strips),
+  // packed into one VGPR: tile byte offset | component << 16
+  uint32_t lane_tile;
+  {
+    const uint32_t mcu_l = tid / nblk, b_l = tid - mcu_l * nblk;
+    const uint32_t c = inter ? im.blk_comp[b_l] : 0;
+    const uint32_t tx = (mcu_l * (inter ? im.comp_h[c] : 1) + (inter ? im.blk_dx[b_l] : 0)) * 8;
+    const uint32_t ty = (inter ? im.blk_dy[b_l] : 0) * 8;
+    const uint32_t twc = c == 0 ? tw[0] : (c == 1 ? tw[1] : tw[2]);
+    lane_tile = ((c == 0 ? toff[0] : (c == 1 ? toff[1] : toff[2])) + ty * twc + tx) | (c << 16);
+  }
 
-  // ---- A: quant tables + coefficient blocks -> LDS ----
   const RjTableSet *ts = tabsets + im.tabset;
-  for (uint32_t k = tid; k < ncomp * 64; k += 256) s_q[k >> 6][k & 63] = ts->qz[im.comp_tq[k >> 6] & 3][k & 63];
-  for (uint32_t k = tid; k < nb * 8; k += 256)
-    *reinterpret_cast<uint4 *>(s_buf + (k >> 3) * RJ_BLK_STRIDE + (k & 7) * 16) = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-  if (tid < nb) {  // thread t expands block t's sparse entries (zigzag order) into LDS
-    const uint2 bi = coefs.blk[im.coef_off + (uint64_t(my) * im.mcux + mx0) * nblk + tid];
-    scatter_block(reinterpret_cast<const uint4 *>(coefs.ent + im.ent_off + bi.x), bi.y,
-                  reinterpret_cast<int16_t *>(s_buf + tid * RJ_BLK_STRIDE));
-  }
-  __syncthreads();
+  for (uint32_t k = tid; k < ncomp * 64; k += 64) s_q[k >> 6][k & 63] = ts->qz[im.comp_tq[k >> 6] & 3][k & 63];
 
-  // ---- B: thread-per-block IDCT in registers ----
-  int32_t v[64];
-  uint32_t c_b = 0, tx = 0, ty = 0;
-  const bool has_blk = tid < nb;
-  if (has_blk) {
-    const uint32_t mcu = tid / nblk, b = tid - mcu * nblk;
-    c_b = inter ? im.blk_comp[b] : 0;
-    const uint32_t hc = inter ? im.comp_h[c_b] : 1;
-    tx = (mcu * hc + (inter ? im.blk_dx[b] : 0)) * 8;
-    ty = (inter ? im.blk_dy[b] : 0) * 8;
-    dezigzag_dequant(reinterpret_cast<const uint4 *>(s_buf + tid * RJ_BLK_STRIDE),
-                     reinterpret_cast<const uint4 *>(s_q[c_b]), v);
-  }
-  __syncthreads();  // every block is in registers: the staging area becomes the sample tiles
-  if (has_blk) {
-    uint8_t o[64];
-    idct_islow_block(v, o);
-    const uint32_t twc = c_b == 0 ? tw[0] : (c_b == 1 ? tw[1] : tw[2]);
-    const uint32_t toc = c_b == 0 ? toff[0] : (c_b == 1 ? toff[1] : toff[2]);
-    uint8_t *dst = s_buf + toc + ty * twc + tx;
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-      uint2 w;
-      w.x = uint32_t(o[r * 8 + 0]) | (uint32_t(o[r * 8 + 1]) << 8) | (uint32_t(o[r * 8 + 2]) << 16) |
-            (uint32_t(o[r * 8 + 3]) << 24);
-      w.y = uint32_t(o[r * 8 + 4]) | (uint32_t(o[r * 8 + 5]) << 8) | (uint32_t(o[r * 8 + 6]) << 16) |
-            (uint32_t(o[r * 8 + 7]) << 24);
-      *reinterpret_cast<uint2 *>(dst + r * twc) = w;
+  const uint32_t mcux = U(im.mcux);
+  const uint32_t strips_x = (mcux + S - 1) / S;
+  const uint2 *blk_row = coefs.blk + im.coef_off + uint64_t(my) * mcux * nblk;
+  const uint32_t *ent = coefs.ent + im.ent_off;
+  uint32_t nb = min(S, mcux) * nblk;
+  uint2 bi = tid < nb ? blk_row[tid] : make_uint2(0, 0);
+
+  for (uint32_t sx = 0; sx < strips_x; sx++) {
+    const uint32_t mx0 = sx * S;
+    const uint32_t nm = min(S, mcux - mx0);
+    nb = nm * nblk;
+    const bool has_blk = tid < nb;
+
+    // ---- A: clear the strip's LDS blocks, expand this lane's sparse list into its block ----
+    __syncthreads();  // previous strip's tiles fully read
+    for (uint32_t k = tid; k < nb * 8; k += 64)
+      *reinterpret_cast<uint4 *>(s_buf + (k >> 3) * RJ_BLK_STRIDE + (k & 7) * 16) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    if (has_blk)
+      scatter_block(reinterpret_cast<const uint4 *>(ent + bi.x), bi.y,
+                    reinterpret_cast<int16_t *>(s_buf + tid * RJ_BLK_STRIDE));
+    // next strip's block index: in flight during this strip's IDCT and output
+    if (sx + 1 < strips_x) {
+      const uint32_t nb1 = min(S, mcux - mx0 - S) * nblk;
+      bi = tid < nb1 ? blk_row[(mx0 + S) * nblk + tid] : make_uint2(0, 0);
     }
-  }
-  __syncthreads();
+    __syncthreads();
+
+    // ---- B: lane-per-block IDCT in registers ----
+    int32_t v[64];
+    if (has_blk)
+      dezigzag_dequant(reinterpret_cast<const uint4 *>(s_buf + tid * RJ_BLK_STRIDE),
+                       reinterpret_cast<const uint4 *>(s_q[lane_tile >> 16]), v);
+    __syncthreads();  // every block is in registers: the staging area becomes the sample tiles
+    if (has_blk) {
+      uint32_t o[16];
+      idct_islow_block(v, o);
+      const uint32_t c = lane_tile >> 16;
+      const uint32_t twc = c == 0 ? tw[0] : (c == 1 ? tw[1] : tw[2]);
+      uint8_t *dst = s_buf + (lane_tile & 0xFFFF);
+#pragma unroll
+      for (int r = 0; r < 8; r++) *reinterpret_cast<uint2 *>(dst + r * twc) = make_uint2(o[2 * r], o[2 * r + 1]);
+    }
+    __syncthreads();
 
   // ---- C: output, lane = 4 consecutive pixels ----
   const uint32_t strip_w = nm * mcu_w;
   const uint32_t px0 = mx0 * mcu_w, py0 = my * mcu_h;
-  const uint32_t W = im.width, H = im.height;
-  const uint32_t fmt = im.fmt;
-  const uint32_t hs1 = (ncomp == 3) ? (hmax / im.comp_h[1] == 2 ? 1u : 0u) : 0u;
-  const uint32_t vs1 = (ncomp == 3) ? (vmax / im.comp_v[1] == 2 ? 1u : 0u) : 0u;
+  const uint32_t W = U(im.width), H = U(im.height);
+  const uint32_t fmt = U(im.fmt);
+  const uint32_t hs1 = U((ncomp == 3) ? (hmax / im.comp_h[1] == 2 ? 1u : 0u) : 0u);
+  const uint32_t vs1 = U((ncomp == 3) ? (vmax / im.comp_v[1] == 2 ? 1u : 0u) : 0u);
   const uint32_t quads_x = strip_w >> 2;  // strip_w is a multiple of 8
   const uint32_t wmax = min(strip_w, W > px0 ? W - px0 : 0u);
   const uint32_t rows = min(mcu_h, H > py0 ? H - py0 : 0u);
 
+  // destination offsets are 32-bit (the host only fuses when pitch * height < 2^31, pitch < 2^24)
   if (fmt >= 1 && fmt <= 4) {
-    const bool a4 = ((reinterpret_cast<uintptr_t>(im.dst[0]) | im.dst_pitch[0]) & 3) == 0;
-    for (uint32_t k = tid; k < quads_x * rows; k += 256) {
-      const uint32_t y = k / quads_x, x = (k - y * quads_x) * 4;
+    const uint32_t pitch = U(im.dst_pitch[0]);
+    const bool a4 = ((reinterpret_cast<uintptr_t>(im.dst[0]) | pitch) & 3) == 0;
+    // lane walks quads tid, tid+64, ... of the strip (row-major) with an incremental (x, y)
+    const uint32_t qsy = 64 / quads_x, qsx = 64 - qsy * quads_x;
+    uint32_t qy = tid / quads_x, qx = tid - qy * quads_x;
+    for (; qy < rows; qx += qsx, qy += qsy) {
+      if (qx >= quads_x) { qx -= quads_x; qy++; if (qy >= rows) break; }
+      const uint32_t y = qy, x = qx * 4;
       if (x >= wmax) continue;
       const uint32_t n = min(4u, wmax - x);
-      const uint32_t y4 = *reinterpret_cast<const uint32_t *>(s_buf + toff[0] + y * tw[0] + x);
+      const uint32_t y4 = *reinterpret_cast<const uint32_t *>(s_buf + toff[0] + __umul24(y, tw[0]) + x);
       const uint32_t py = py0 + y, px = px0 + x;
       if (fmt == 3 || fmt == 4) {
         uint32_t w[3];
         if (ncomp == 3) {
           float u[4], vv[4];
-          const uint8_t *ur = s_buf + toff[1] + (y >> vs1) * tw[1];
-          const uint8_t *vr = s_buf + toff[2] + (y >> vs1) * tw[2];
+          const uint8_t *ur = s_buf + toff[1] + __umul24(y >> vs1, tw[1]);
+          const uint8_t *vr = s_buf + toff[2] + __umul24(y >> vs1, tw[2]);
           if (hs1) {
             const uint32_t u2 = *reinterpret_cast<const uint16_t *>(ur + (x >> 1));
             const uint32_t v2 = *reinterpret_cast<const uint16_t *>(vr + (x >> 1));
@@ -199,7 +218,7 @@ __global__ __launch_bounds__(256) void k_fused(const RjImageDev *__restrict__ im
           w[2] = b2 | (b3 << 8) | (b3 << 16) | (b3 << 24);
         }
         if (fmt == 3) {
-          uint8_t *d = im.dst[0] + uint64_t(py) * im.dst_pitch[0] + uint64_t(px) * 3;
+          uint8_t *d = im.dst[0] + (__umul24(py, pitch) + px * 3);
           if (n == 4 && a4) {
             uint32_t *d32 = reinterpret_cast<uint32_t *>(d);
             d32[0] = w[0];
@@ -216,16 +235,17 @@ __global__ __launch_bounds__(256) void k_fused(const RjImageDev *__restrict__ im
           const uint32_t B = ((w[0] >> 16) & 0xFFu) | (w[1] & 0xFF00u) | ((w[2] << 16) & 0xFF0000u) | (w[2] & 0xFF000000u);
           const uint32_t pl[3] = {R, G, B};
           const bool ap = ((reinterpret_cast<uintptr_t>(im.dst[0]) | reinterpret_cast<uintptr_t>(im.dst[1]) |
-                            reinterpret_cast<uintptr_t>(im.dst[2]) | im.dst_pitch[0]) & 3) == 0;
+                            reinterpret_cast<uintptr_t>(im.dst[2]) | pitch) & 3) == 0;
+          const uint32_t off = __umul24(py, pitch) + px;
 #pragma unroll
           for (int p = 0; p < 3; p++) {
-            uint8_t *d = im.dst[p] + uint64_t(py) * im.dst_pitch[0] + px;
+            uint8_t *d = im.dst[p] + off;
             if (n == 4 && ap) *reinterpret_cast<uint32_t *>(d) = pl[p];
             else store_bytes(d, n, &pl[p]);
           }
         }
       } else {  // Y plane (OUTPUT_Y, and the luma of YUV_PLANAR)
-        uint8_t *d = im.dst[0] + uint64_t(py) * im.dst_pitch[0] + px;
+        uint8_t *d = im.dst[0] + (__umul24(py, pitch) + px);
         if (n == 4 && a4) *reinterpret_cast<uint32_t *>(d) = y4;
         else store_bytes(d, n, &y4);
       }
@@ -240,25 +260,26 @@ __global__ __launch_bounds__(256) void k_fused(const RjImageDev *__restrict__ im
     const uint32_t cq = cw >> 2;
     const uint32_t cwmax = min(cw, cW > cx0 ? cW - cx0 : 0u);
     const uint32_t crows = min(ch, cH > cy0 ? cH - cy0 : 0u);
-    for (uint32_t k = tid; k < 2 * cq * crows; k += 256) {
+    for (uint32_t k = tid; k < 2 * cq * crows; k += 64) {
       const uint32_t second = k >= cq * crows ? 1u : 0u;
       const uint32_t kk = k - second * cq * crows;
       const uint32_t y = kk / cq, x = (kk - y * cq) * 4;
       if (x >= cwmax) continue;
       const uint32_t n = min(4u, cwmax - x);
       const uint32_t s4 = *reinterpret_cast<const uint32_t *>(s_buf + (second ? toff[2] : toff[1]) +
-                                                              y * (second ? tw[2] : tw[1]) + x);
-      uint8_t *d = (second ? im.dst[2] : im.dst[1]) + uint64_t(cy0 + y) * im.dst_pitch[1] + cx0 + x;
+                                                              __umul24(y, second ? tw[2] : tw[1]) + x);
+      uint8_t *d = (second ? im.dst[2] : im.dst[1]) + (__umul24(cy0 + y, im.dst_pitch[1]) + cx0 + x);
       if (n == 4 && a4) *reinterpret_cast<uint32_t *>(d) = s4;
       else store_bytes(d, n, &s4);
     }
   }
+  }  // strips
 }
 
-hipError_t LaunchFusedOutput(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *strip_prefix,
-                             uint32_t nstrips, RjCoefBuf coefs, const RjTableSet *tabsets) {
-  if (nstrips == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fused, dim3(nstrips), dim3(256), 0, st, imgs, nimg, strip_prefix, coefs, tabsets);
+hipError_t LaunchFusedOutput(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
+                             uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets) {
+  if (nrows == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fused, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, coefs, tabsets);
   return hipGetLastError();
 }
 

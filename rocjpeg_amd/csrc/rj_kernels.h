@@ -24,9 +24,10 @@ hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobD
                             const uint8_t *planes);
 
 // K2 (fused fast path): dequant + IDCT + nearest upsample + YUV->RGB / layout straight from the
-// coefficients to the caller's buffers, one workgroup per MCU-row strip.  Only for images whose
+// coefficients to the caller's buffers, one single-wave workgroup per MCU row (looping over the
+// row's strips); row_prefix[i] = first row of image i (fused images only).  Only for images whose
 // output window is tile-local (no ROI quirks); see rj_decoder.cpp::FusedEligible.
-hipError_t LaunchFusedOutput(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *strip_prefix,
-                             uint32_t nstrips, RjCoefBuf coefs, const RjTableSet *tabsets);
+hipError_t LaunchFusedOutput(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
+                             uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets);
 
 }  // namespace rj

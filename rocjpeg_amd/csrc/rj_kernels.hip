@@ -352,16 +352,12 @@ __global__ __launch_bounds__(256) void k_idct_planes(const RjImageDev *__restric
   const uint4 *q4 = reinterpret_cast<const uint4 *>(tabsets[im.tabset].qz[im.comp_tq[c] & 3]);
   int32_t v[64];
   dezigzag_dequant(s_blk[threadIdx.x], q4, v);
-  uint8_t o[64];
+  uint32_t o[16];
   idct_islow_block(v, o);
   uint8_t *dst = planes + im.plane_off[c] + uint64_t(by) * 8u * im.plane_pitch[c] + bx * 8u;
 #pragma unroll
-  for (int r = 0; r < 8; r++) {
-    uint2 w;
-    w.x = uint32_t(o[r * 8 + 0]) | (uint32_t(o[r * 8 + 1]) << 8) | (uint32_t(o[r * 8 + 2]) << 16) | (uint32_t(o[r * 8 + 3]) << 24);
-    w.y = uint32_t(o[r * 8 + 4]) | (uint32_t(o[r * 8 + 5]) << 8) | (uint32_t(o[r * 8 + 6]) << 16) | (uint32_t(o[r * 8 + 7]) << 24);
-    *reinterpret_cast<uint2 *>(dst + uint64_t(r) * im.plane_pitch[c]) = w;
-  }
+  for (int r = 0; r < 8; r++)
+    *reinterpret_cast<uint2 *>(dst + uint64_t(r) * im.plane_pitch[c]) = make_uint2(o[2 * r], o[2 * r + 1]);
 }
 
 hipError_t LaunchIdctPlanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint64_t nblocks, RjCoefBuf coefs,

@@ -6,9 +6,12 @@
 
 namespace rj {
 
-// libjpeg ISLOW constants (jidctint.c: CONST_BITS 13, PASS1_BITS 2).  Computed in int32:
-// exact for every stream whose dequantised coefficients stay in the range a real 8-bit DCT
-// produces (libjpeg-turbo's SIMD ISLOW kernels make the same assumption).
+// libjpeg ISLOW constants (jidctint.c: CONST_BITS 13, PASS1_BITS 2).  Computed in int32
+// with 24-bit multiplies (v_mul_i32_i24, full rate; v_mul_lo_u32 is quarter rate): exact --
+// i.e. equal to libjpeg's wide arithmetic -- whenever every dequantised coefficient has
+// |x| < 2^14, which every stream produced from an 8-bit DCT satisfies (|x| <= ~2^11 * 8);
+// then every multiplicand is < 2^17 and every product and sum fits int32.  libjpeg-turbo's
+// SIMD ISLOW kernels make the same (in fact a 16-bit) assumption.
 #define RJ_FIX_0_298631336 2446
 #define RJ_FIX_0_390180644 3196
 #define RJ_FIX_0_541196100 4433
@@ -22,29 +25,30 @@ namespace rj {
 #define RJ_FIX_2_562915447 20995
 #define RJ_FIX_3_072711026 25172
 
-// One 8-point ISLOW butterfly on x0..x7 (already dequantised / pass-1 outputs).  Writes the
-// eight pre-descale sums to t[0..7] in output order 0..7.
+__device__ __forceinline__ int32_t m24(int32_t a, int32_t k) { return __mul24(a, k); }
+
+// One 8-point ISLOW butterfly on x0..x7 (dequantised coefficients or pass-1 outputs).  `rnd`
+// is added to the even part, so it reaches all eight outputs: callers fold the descale
+// rounding (and the range-limit offset) into it.  Writes the pre-shift sums t[0..7].
 __device__ __forceinline__ void islow_1d(int32_t x0, int32_t x1, int32_t x2, int32_t x3, int32_t x4, int32_t x5,
-                                         int32_t x6, int32_t x7, int32_t t[8]) {
-  int32_t z1 = (x2 + x6) * RJ_FIX_0_541196100;
-  const int32_t tmp2 = z1 - x6 * RJ_FIX_1_847759065;
-  const int32_t tmp3 = z1 + x2 * RJ_FIX_0_765366865;
-  const int32_t e0 = (x0 + x4) * 8192, e1 = (x0 - x4) * 8192;
+                                         int32_t x6, int32_t x7, int32_t rnd, int32_t t[8]) {
+  int32_t z1 = m24(x2 + x6, RJ_FIX_0_541196100);
+  const int32_t tmp2 = z1 - m24(x6, RJ_FIX_1_847759065);
+  const int32_t tmp3 = z1 + m24(x2, RJ_FIX_0_765366865);
+  const int32_t e0 = ((x0 + x4) << 13) + rnd, e1 = ((x0 - x4) << 13) + rnd;
   const int32_t t10 = e0 + tmp3, t13 = e0 - tmp3, t11 = e1 + tmp2, t12 = e1 - tmp2;
   int32_t o0 = x7, o1 = x5, o2 = x3, o3 = x1;
   z1 = o0 + o3;
   int32_t z2 = o1 + o2, z3 = o0 + o2, z4 = o1 + o3;
-  const int32_t z5 = (z3 + z4) * RJ_FIX_1_175875602;
-  o0 *= RJ_FIX_0_298631336;
-  o1 *= RJ_FIX_2_053119869;
-  o2 *= RJ_FIX_3_072711026;
-  o3 *= RJ_FIX_1_501321110;
-  z1 *= -RJ_FIX_0_899976223;
-  z2 *= -RJ_FIX_2_562915447;
-  z3 *= -RJ_FIX_1_961570560;
-  z4 *= -RJ_FIX_0_390180644;
-  z3 += z5;
-  z4 += z5;
+  const int32_t z5 = m24(z3 + z4, RJ_FIX_1_175875602);
+  o0 = m24(o0, RJ_FIX_0_298631336);
+  o1 = m24(o1, RJ_FIX_2_053119869);
+  o2 = m24(o2, RJ_FIX_3_072711026);
+  o3 = m24(o3, RJ_FIX_1_501321110);
+  z1 = m24(z1, -RJ_FIX_0_899976223);
+  z2 = m24(z2, -RJ_FIX_2_562915447);
+  z3 = m24(z3, -RJ_FIX_1_961570560) + z5;
+  z4 = m24(z4, -RJ_FIX_0_390180644) + z5;
   o0 += z1 + z3;
   o1 += z2 + z4;
   o2 += z2 + z3;
@@ -93,28 +97,40 @@ __device__ __forceinline__ void dezigzag_dequant(const uint4 *coef_zz, const uin
   }
 }
 
-// libjpeg range_limit[(x) & RANGE_MASK] after the final descale: wrap mod 1024, +128, clamp.
-__device__ __forceinline__ uint32_t islow_range_limit(int32_t v) {
-  const int32_t w = ((v + 512) & 1023) - 384;
-  return uint32_t(w < 0 ? 0 : (w > 255 ? 255 : w));
+// libjpeg range_limit[DESCALE(t, 18) & RANGE_MASK] (+CENTERJSAMPLE folded in) for a pass-2
+// sum t that already carries RJ_PASS2_RND: bits 18..27 are ((DESCALE(t) + 512) & 1023) = w,
+// the sample is clamp(w - 384, 0, 255).  Returned as med3(w, 384, 639), whose low byte XOR
+// 0x80 is that sample (384 = 0x180): four of them pack with v_perm + one XOR.
+#define RJ_PASS1_RND (1 << 10)
+#define RJ_PASS2_RND ((1 << 17) + (512 << 18))
+__device__ __forceinline__ uint32_t islow_limit_biased(int32_t t) {
+  const uint32_t w = __builtin_amdgcn_ubfe(uint32_t(t), 18, 10);
+  return min(max(w, 384u), 639u);  // v_med3_u32
 }
-
-// pass 1 (columns) on v in place, then pass 2 (rows) into o.
-__device__ __forceinline__ void idct_islow_block(int32_t (&v)[64], uint8_t (&o)[64]) {
+__device__ __forceinline__ uint32_t islow_pack4(uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3) {
+  const uint32_t p01 = __builtin_amdgcn_perm(m1, m0, 0x0c0c0400u);
+  const uint32_t p23 = __builtin_amdgcn_perm(m3, m2, 0x0c0c0400u);
+  return __builtin_amdgcn_perm(p23, p01, 0x05040100u) ^ 0x80808080u;
+}
+// pass 1 (columns) on v in place, then pass 2 (rows): row r of samples -> o[2r] (x 0..3),
+// o[2r+1] (x 4..7), little-endian bytes.
+__device__ __forceinline__ void idct_islow_block(int32_t (&v)[64], uint32_t (&o)[16]) {
 #pragma unroll
   for (int c = 0; c < 8; c++) {
     int32_t t[8];
-    islow_1d(v[c], v[8 + c], v[16 + c], v[24 + c], v[32 + c], v[40 + c], v[48 + c], v[56 + c], t);
+    islow_1d(v[c], v[8 + c], v[16 + c], v[24 + c], v[32 + c], v[40 + c], v[48 + c], v[56 + c], RJ_PASS1_RND, t);
 #pragma unroll
-    for (int r = 0; r < 8; r++) v[r * 8 + c] = (t[r] + 1024) >> 11;  // DESCALE(, CONST_BITS-PASS1_BITS)
+    for (int r = 0; r < 8; r++) v[r * 8 + c] = t[r] >> 11;  // DESCALE(, CONST_BITS-PASS1_BITS)
   }
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     int32_t t[8];
     islow_1d(v[r * 8], v[r * 8 + 1], v[r * 8 + 2], v[r * 8 + 3], v[r * 8 + 4], v[r * 8 + 5], v[r * 8 + 6],
-             v[r * 8 + 7], t);
-#pragma unroll
-    for (int x = 0; x < 8; x++) o[r * 8 + x] = uint8_t(islow_range_limit((t[x] + (1 << 17)) >> 18));
+             v[r * 8 + 7], RJ_PASS2_RND, t);
+    o[2 * r] = islow_pack4(islow_limit_biased(t[0]), islow_limit_biased(t[1]), islow_limit_biased(t[2]),
+                           islow_limit_biased(t[3]));
+    o[2 * r + 1] = islow_pack4(islow_limit_biased(t[4]), islow_limit_biased(t[5]), islow_limit_biased(t[6]),
+                               islow_limit_biased(t[7]));
   }
 }
 
