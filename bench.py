@@ -101,6 +101,34 @@ def turbo_baseline(data_list, procs):
             "lib": "Pillow bundled libjpeg-turbo (BT.601 + fancy upsampling: throughput context only)"}
 
 
+def pmc_traffic(kernel, batch):
+    """HBM bytes per launch of `kernel` from the committed PMC profile (tools/gpu_pmc.sh +
+    tools/pmc_traffic.py on this workload): FETCH_SIZE x 2 (gfx950 correction, MI355X_MICROARCH.md
+    HBM section) + WRITE_SIZE, per image, scaled to this launch's batch.  None if absent."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            prof = json.load(f)
+        k = prof["kernels"][kernel]
+        return int(k["hbm_bytes_per_image"] * batch)
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def work_table(rank, world, batch, device):
+    """Rank 0 builds the work table (one image seed per slot, `batch` images per rank) and one
+    broadcast (RCCL on GPUs, gloo in the CPU tests) hands every rank the whole table; each rank
+    keeps its own row.  Returns this rank's seeds."""
+    import torch
+    import torch.distributed as dist
+    table = torch.empty((world, batch), dtype=torch.int64, device=device)
+    if rank == 0:
+        table.copy_(torch.arange(world * batch, dtype=torch.int64).view(world, batch) + 1234)
+    if world > 1:
+        dist.broadcast(table, src=0)
+    return table[rank].cpu().tolist()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -121,13 +149,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    # work table: rank 0 picks the seeds, one RCCL broadcast hands every rank its shard
-    table = torch.empty((world, args.batch), dtype=torch.int64, device=dev)
-    if rank == 0:
-        table.copy_(torch.arange(world * args.batch, dtype=torch.int64).view(world, args.batch) + 1234)
-    if world > 1:
-        dist.broadcast(table, src=0)
-    seeds = table[rank].cpu().tolist()
+    seeds = work_table(rank, world, args.batch, dev)
     procs = max(1, min(16, (os.cpu_count() or 16)))
     t_gen = time.perf_counter()
     data = make_dataset(seeds, procs=procs)
@@ -177,6 +199,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # PCIe-inclusive rate: the same batch from host memory (fresh stream objects, so
+    # every call stages the bitstreams through pinned memory + H2D); reported, never `value`
+    host_streams = [R.JpegStream(b) for b in data]
+    hs2 = (ctypes.c_void_p * n)(*[s.handle for s in host_streams])
+    st = L.rocJpegDecodeBatched(dec.handle, hs2, n, ctypes.byref(params), arr)  # warm-up
+    torch.cuda.synchronize()
+    t_h = time.perf_counter()
+    host_steps = 3
+    for _ in range(host_steps):
+        st |= L.rocJpegDecodeBatched(dec.handle, hs2, n, ctypes.byref(params), arr)
+    torch.cuda.synchronize()
+    host_rate = host_steps * n / (time.perf_counter() - t_h) if st == 0 else None
+    del host_streams
+
     # parity spot-check of this run's output (first image vs the CPU oracle), outside timing
     from tests import oracle_lib as O
     ost, want = O.oracle_decode(data[0], 3, [(H, 3 * W)])
@@ -197,8 +233,9 @@ def main():
             algo["idct_ms"] = coef + outb
         dom = max(("huffman_ms", "idct_ms", "output_ms", "destuff_ms"), key=lambda k: per[k])
         ach = algo[dom] / (per[dom] * 1e-3) / 1e9 if per[dom] > 0 else 0.0
-        names = {"destuff_ms": "k_destuff", "huffman_ms": "k_huffman", "idct_ms": "k_idct_planes/k_fused",
-                 "output_ms": "k_output"}
+        names = {"destuff_ms": "k_destuff", "huffman_ms": "k_huffman",
+                 "idct_ms": "k_fused" if last.get("fused_images", 0) else "k_idct_planes", "output_ms": "k_output"}
+        traffic = pmc_traffic(names[dom], args.batch)
         res = {
             "metric": "images/s (1080p 4:2:0 batch) at 1/2/4/8 MI355X + achieved HBM GB/s",
             "value": round(value, 2),
@@ -216,10 +253,11 @@ def main():
                        "batch_per_gpu": args.batch, "output_format": "RGB", "parallelism": f"images sharded, {world} rank(s)",
                        "ecs_bytes_per_image": round(ecs / args.batch)},
             "roofline": {"bound": "hbm", "kernel": names[dom], "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "algorithmic_bytes_per_launch": int(algo[dom]), "avg_launch_ms": round(per[dom], 4)},
             "stages_ms_per_step": {k: round(v, 4) for k, v in per.items()},
             "end_to_end_algorithmic_GBps": round((ecs + outb) / (elapsed / K) / 1e9, 2),
+            "host_input_images_per_s_per_gpu": round(host_rate, 1) if host_rate else None,
             "parity_first_image": parity_ok,
             "dataset_gen_s": round(t_gen, 1),
         }
