@@ -209,11 +209,11 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   std::vector<RjImageDev> imgs(n);
   std::vector<RjJobDev> jobs;
   uint64_t destuff_total = 0, coef_blocks = 0, ent_total = 0, plane_bytes = 0, stage_bytes = 0;
-  uint32_t seg_total = 0, blk_total = 0, rows_total = 0;
+  uint32_t seg_total = 0, rows_total = 0, mcu_rows = 0;
   uint64_t ecs_bytes = 0, out_bytes = 0;
   std::vector<uint64_t> stage_off(n, UINT64_MAX);
-  std::vector<uint32_t> row_prefix(n);
-  uint32_t fused_rows = 0, fused_images = 0;
+  std::vector<uint32_t> row_prefix(n), grow_prefix(n);  // K2 rows: fused images / general images
+  uint32_t fused_rows = 0, general_rows = 0, fused_images = 0;
   for (int i = 0; i < n; i++) {
     Stream *s = streams[i];
     const StreamInfo &in = s->info();
@@ -248,11 +248,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     seg_total += d.nseg;
     d.destuff_off = destuff_total;
     destuff_total += AlignUp(p.destuff_bytes, 256);
-    d.coef_off = coef_blocks;
     coef_blocks += uint64_t(p.mcux) * p.mcuy * p.nblk_mcu;
     d.ent_off = ent_total;
-    ent_total += AlignUp(p.entries, 4);
-    d.blk_prefix = blk_total;
+    ent_total += AlignUp(p.entries, RJ_ENT_GROUP);
+    d.ri_mcus = in.restart_interval;
+    d.row_off = mcu_rows;
+    mcu_rows += p.mcuy;
     for (int c = 0; c < in.ncomp; c++) {
       d.plane_pitch[c] = p.wblk[c] * 8;
       d.plane_rows[c] = p.hblk[c] * 8;
@@ -278,6 +279,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       d.dst_pitch[c] = o.pitch[c];
     }
     row_prefix[i] = fused_rows;
+    grow_prefix[i] = general_rows;
 
     // ---- output jobs (general path): rocjpeg_decoder.cpp:143-180 ----
     const size_t jobs_before = jobs.size();
@@ -370,8 +372,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       for (int c = 0; c < in.ncomp; c++) {
         d.plane_off[c] = plane_bytes;
         plane_bytes += AlignUp(uint64_t(d.plane_pitch[c]) * d.plane_rows[c], 256);
-        blk_total += p.wblk[c] * p.hblk[c];
       }
+      general_rows += p.mcuy;
     }
   }
 
@@ -380,17 +382,18 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t off_tabs = AlignUp(off_imgs + n * sizeof(RjImageDev), 256);
   const uint64_t off_jobs = AlignUp(off_tabs + tabs.size() * sizeof(RjTableSet), 256);
   const uint64_t off_rows = AlignUp(off_jobs + std::max<size_t>(jobs.size(), 1) * sizeof(RjJobDev), 256);
-  const uint64_t off_stage = AlignUp(off_rows + n * sizeof(uint32_t), 256);
+  const uint64_t off_grows = AlignUp(off_rows + n * sizeof(uint32_t), 256);
+  const uint64_t off_stage = AlignUp(off_grows + n * sizeof(uint32_t), 256);
   const uint64_t blob = off_stage + stage_bytes;
   RJ_CHECK(h_stage_.Ensure(blob));
   RJ_CHECK(d_desc_.Ensure(blob));
   RJ_CHECK(d_destuff_.Ensure(std::max<uint64_t>(destuff_total, 256)));
   RJ_CHECK(d_seglen_.Ensure(std::max<uint64_t>(uint64_t(seg_total) * 4, 256)));
-  RJ_CHECK(d_coefs_.Ensure(std::max<uint64_t>(coef_blocks * sizeof(uint2), 256)));
-  RJ_CHECK(d_entries_.Ensure(std::max<uint64_t>(ent_total * 4, 256)));
+  RJ_CHECK(d_rowidx_.Ensure(std::max<uint64_t>(uint64_t(mcu_rows) * 4, 256)));
+  RJ_CHECK(d_entries_.Ensure((ent_total + RJ_ENT_SLACK) * 4));
   RjCoefBuf cbuf;
-  cbuf.blk = d_coefs_.as<uint2>();
   cbuf.ent = d_entries_.as<uint32_t>();
+  cbuf.row = d_rowidx_.as<uint32_t>();
   RJ_CHECK(d_planes_.Ensure(std::max<uint64_t>(plane_bytes, 256)));
   uint8_t *h = h_stage_.data();
   uint8_t *dbase = d_desc_.as<uint8_t>();
@@ -414,7 +417,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   for (size_t t = 0; t < tabs.size(); t++) std::memcpy(h + off_tabs + t * sizeof(RjTableSet), tabs[t], sizeof(RjTableSet));
   if (!jobs.empty()) std::memcpy(h + off_jobs, jobs.data(), jobs.size() * sizeof(RjJobDev));
   std::memcpy(h + off_rows, row_prefix.data(), n * sizeof(uint32_t));
+  std::memcpy(h + off_grows, grow_prefix.data(), n * sizeof(uint32_t));
   const uint32_t *d_rows = reinterpret_cast<const uint32_t *>(dbase + off_rows);
+  const uint32_t *d_grows = reinterpret_cast<const uint32_t *>(dbase + off_grows);
 
   const RjImageDev *d_imgs = reinterpret_cast<const RjImageDev *>(dbase + off_imgs);
   const RjTableSet *d_tabs = reinterpret_cast<const RjTableSet *>(dbase + off_tabs);
@@ -428,8 +433,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   RJ_HIP(LaunchHuffman(stream_, d_imgs, n, seg_total, d_destuff_.as<uint8_t>(), d_seglen_.as<uint32_t>(), d_tabs,
                        cbuf));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
-  RJ_HIP(LaunchFusedOutput(stream_, d_imgs, n, d_rows, fused_rows, cbuf, d_tabs));
-  RJ_HIP(LaunchIdctPlanes(stream_, d_imgs, n, blk_total, cbuf, d_tabs, d_planes_.as<uint8_t>()));
+  RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, fused_rows, cbuf, d_tabs, nullptr));
+  RJ_HIP(LaunchRows(stream_, true, d_imgs, n, d_grows, general_rows, cbuf, d_tabs, d_planes_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[4], stream_));
   RJ_HIP(LaunchOutputJobs(stream_, d_imgs, d_jobs, int(jobs.size()), rows_total, d_planes_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[5], stream_));

@@ -69,7 +69,7 @@ class Decoder {
   RocJpegAmdTimings timings_ = {};
   hipEvent_t ev_[8] = {};
 
-  DeviceBuffer d_desc_, d_stage_, d_destuff_, d_seglen_, d_coefs_, d_entries_, d_planes_, d_strips_;
+  DeviceBuffer d_desc_, d_stage_, d_destuff_, d_seglen_, d_rowidx_, d_entries_, d_planes_;
   PinnedBuffer h_stage_;
 };
 

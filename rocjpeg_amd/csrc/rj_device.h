@@ -6,11 +6,12 @@
 //   tabsets[]  RjTableSet          de-duplicated Huffman LUTs + natural-order quant tables
 //   segs       RjSegDev per image  restart intervals (resident with the stream's ECS bytes)
 //   destuffed  u8                  byte-unstuffed entropy data, each interval 16-B aligned
-//   coef index uint2 per block     MCU-major: block (image.coef_off + mcu*nblk_mcu + b) ->
-//                                  {first entry (image-relative), entry count}
-//   coef entries uint32            sparse coefficients: int16 value | zigzag position << 16;
-//                                  each block's list 16-B aligned, each interval's region sized
-//                                  for the worst case (64 entries per block)
+//   entries    uint32              sparse coefficients (K1 -> K2): per restart interval one
+//                                  stream, per block its DC entry (zigzag pos 0, absolute value)
+//                                  then its nonzero AC entries; a terminator (pos 127) after the
+//                                  interval's last block.  Region per interval sized for the
+//                                  worst case (64 entries per block), 64-B aligned.
+//   row index  uint32 per MCU row  entry index (image-relative) of the row's first block
 //   planes     u8                  per component, padded to the MCU grid (general path only)
 #pragma once
 #include <hip/hip_runtime.h>  // uint2/uint4 vector types (all users are built with hipcc)
@@ -27,12 +28,20 @@ __host__ __device__ inline uint32_t rj_fused_strip_mcus(uint32_t hmax, uint32_t 
   return a < b ? a : b;
 }
 
-// Sparse coefficient storage written by K1 and read by the IDCT kernels.
+// Sparse coefficient storage written by K1 and read by K2 (rj_fused.hip).
+//   entry = uint16 value | zigzag position << 16 (positions 0..63; RJ_ENT_TERM ends an interval)
 struct RjCoefBuf {
-  uint2 *blk;     // per block: {first entry relative to image.ent_off, entry count}
-  uint32_t *ent;  // entries: uint16 value | zigzag position << 16
+  uint32_t *ent;  // entry streams, one region per interval (image.ent_off + seg.ent_off)
+  uint32_t *row;  // per MCU row (image.row_off + my): first entry of the row, image-relative
 };
-#define RJ_ENT_PER_BLOCK 64  // worst case: DC + 63 AC (each position written at most once)
+#define RJ_ENT_PER_BLOCK 64       // worst case: DC + 63 AC (each position written at most once)
+#define RJ_ENT_GROUP 16           // K1 writes entries in 64-B groups; regions are group-aligned
+#define RJ_ENT_TERM (127u << 16)  // end-of-interval marker
+#define RJ_ENT_SLACK 1024         // entries of read slack after the last region (K2 reads 512-entry windows)
+// entries reserved for an interval of `blocks` blocks: worst case + terminator, group-aligned
+__host__ __device__ inline uint64_t rj_interval_entries(uint64_t blocks) {
+  return (blocks * RJ_ENT_PER_BLOCK + 1 + RJ_ENT_GROUP - 1) / RJ_ENT_GROUP * RJ_ENT_GROUP;
+}
 
 // One restart interval of one image (host parser rj_stream.cpp builds these).
 struct RjSegDev {
@@ -110,12 +119,12 @@ struct RjImageDev {
   uint32_t nseg;
   uint32_t seg_prefix;   // exclusive prefix of segments over the batch
   uint64_t destuff_off;  // into the destuffed buffer
-  uint64_t coef_off;     // in blocks (coefficient index)
-  uint64_t ent_off;      // in entries (sparse coefficients)
+  uint64_t ent_off;      // in entries (sparse coefficients), group-aligned
+  uint32_t ri_mcus;      // MCUs per restart interval (0: one interval)
+  uint32_t row_off;      // first MCU row of this image in the batch's row index
   // component planes (general path)
   uint64_t plane_off[4];
   uint32_t plane_pitch[4], plane_rows[4];
-  uint32_t blk_prefix;   // exclusive prefix of blocks over the batch (IDCT grid)
   // output window (ROI semantics of rocjpeg_decoder.cpp:124-141)
   int32_t out_w, out_h, top, left;
   uint8_t *dst[4];

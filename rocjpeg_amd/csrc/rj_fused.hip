@@ -62,10 +62,79 @@ __device__ __forceinline__ void store_bytes(uint8_t *d, uint32_t n, const uint32
     if (uint32_t(j) < n) d[j] = uint8_t(w[j >> 2] >> (8 * (j & 3)));
 }
 
-__global__ __launch_bounds__(64) void k_fused(const RjImageDev *__restrict__ imgs, int nimg,
-                                              const uint32_t *__restrict__ row_prefix,
-                                              RjCoefBuf coefs,
-                                              const RjTableSet *__restrict__ tabsets) {
+// Entry-stream window of one wave: w[r] = ent[base + r * 64 + lane] (coalesced rows).  The
+// loads of the next strip's window are issued as soon as its start is known (end of phase A)
+// and complete behind the IDCT and output phases.
+#define RJ_WIN_ROWS 8
+struct EntWin {
+  uint32_t w[RJ_WIN_ROWS];
+  uint32_t base;
+  __device__ __forceinline__ void load(const uint32_t *__restrict__ ent, uint32_t at, uint32_t lane) {
+    base = at;
+#pragma unroll
+    for (int r = 0; r < RJ_WIN_ROWS; r++) w[r] = ent[at + r * 64u + lane];
+  }
+};
+
+// Expand the next `nb` blocks of the image's entry stream into the zeroed LDS blocks [0, nb)
+// (block j at s_buf + j * RJ_BLK_STRIDE, int16 in zigzag order).  A block starts at its DC
+// entry (pos 0); the terminator (pos 127) closes an interval; a block has <= 64 entries.
+// Entries are consumed row by row from the window; the ordinal of an entry's block is the
+// number of block starts at or before it, so rows need no alignment to block starts.
+//   cur    image-relative entry index of the next block's DC entry (== win.base on entry)
+//   bleft  blocks left in the current restart interval; at 0 the cursor moves to the next one
+//   gblk   image-relative index of the next block (locates the next interval)
+__device__ __forceinline__ void parse_blocks(const RjImageDev &im, const uint32_t *__restrict__ ent, uint32_t lane,
+                                             uint32_t nb, uint32_t nblk, EntWin &win, uint32_t &cur,
+                                             uint32_t &bleft, uint32_t &gblk, uint8_t *s_buf) {
+  uint32_t done = 0;
+  while (done < nb) {
+    if (bleft == 0) {  // the next block opens a new restart interval (rare: synchronous reload)
+      const uint32_t ri = im.ri_mcus;
+      const RjSegDev sg = im.segs[ri ? gblk / nblk / ri : 0];
+      cur = U(sg.ent_off);
+      bleft = U(sg.mcu_count * nblk);
+      win.load(ent, cur, lane);
+    }
+    const uint32_t piece = min(nb - done, bleft);  // blocks taken from this interval
+    uint32_t seen = 0;                              // block starts before the current row
+    bool found = false;
+    for (int guard = 0; !found && guard < 64; guard++) {  // <= 64 entries per block: bounded
+#pragma unroll
+      for (int r = 0; r < RJ_WIN_ROWS; r++) {
+        const uint32_t e = win.w[r];
+        const uint32_t p = (e >> 16) & 127u;
+        const bool st = p == 0 || p == 127;
+        const uint64_t m = __ballot(st);
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+        const uint32_t ord = seen + below + (st ? 1u : 0u) - 1u;
+        if (ord < piece && p < 64u)
+          *reinterpret_cast<int16_t *>(s_buf + (done + ord) * RJ_BLK_STRIDE + p * 2) = int16_t(e & 0xFFFFu);
+        const uint64_t hit = __ballot(st && ord == piece);  // start of the first block past the piece
+        seen += __popcll(m);
+        if (hit) {
+          cur = win.base + uint32_t(r) * 64u + uint32_t(__ffsll((long long)hit) - 1);
+          found = true;
+          break;
+        }
+      }
+      if (!found) win.load(ent, win.base + RJ_WIN_ROWS * 64u, lane);  // block longer than the window
+    }
+    done += piece;
+    bleft -= piece;
+    gblk += piece;
+  }
+}
+
+// K2: one wavefront per MCU row of one image, looping over the row's strips of S MCUs.
+//   kPlanes = false: fused output (rj_decoder.cpp FusedEligible images)
+//   kPlanes = true : general path, blocks into the MCU-padded component planes (K2b reads them)
+template <bool kPlanes>
+__global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ imgs, int nimg,
+                                             const uint32_t *__restrict__ row_prefix,
+                                             RjCoefBuf coefs,
+                                             const RjTableSet *__restrict__ tabsets,
+                                             uint8_t *__restrict__ planes) {
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];  // A/B, then tiles
   __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
 
@@ -103,16 +172,15 @@ __global__ __launch_bounds__(64) void k_fused(const RjImageDev *__restrict__ img
       off += has ? tw[c] * vc * 8 : 0;
     }
   }
-  // this lane's block inside an MCU and its tile position (constant over the row's strips),
-  // packed into one VGPR: tile byte offset | component << 16
-  uint32_t lane_tile;
+  // this lane's block inside the strip: component, block column (relative to the strip's first
+  // block column of that component) and block row; constant over the row's strips
+  uint32_t lane_blk;  // bx | by << 8 | c << 12
   {
     const uint32_t mcu_l = tid / nblk, b_l = tid - mcu_l * nblk;
     const uint32_t c = inter ? im.blk_comp[b_l] : 0;
-    const uint32_t tx = (mcu_l * (inter ? im.comp_h[c] : 1) + (inter ? im.blk_dx[b_l] : 0)) * 8;
-    const uint32_t ty = (inter ? im.blk_dy[b_l] : 0) * 8;
-    const uint32_t twc = c == 0 ? tw[0] : (c == 1 ? tw[1] : tw[2]);
-    lane_tile = ((c == 0 ? toff[0] : (c == 1 ? toff[1] : toff[2])) + ty * twc + tx) | (c << 16);
+    const uint32_t bx = mcu_l * (inter ? im.comp_h[c] : 1) + (inter ? im.blk_dx[b_l] : 0);
+    const uint32_t by = inter ? im.blk_dy[b_l] : 0;
+    lane_blk = (bx & 255u) | (by << 8) | (c << 12);
   }
 
   const RjTableSet *ts = tabsets + im.tabset;
@@ -120,44 +188,60 @@ __global__ __launch_bounds__(64) void k_fused(const RjImageDev *__restrict__ img
 
   const uint32_t mcux = U(im.mcux);
   const uint32_t strips_x = (mcux + S - 1) / S;
-  const uint2 *blk_row = coefs.blk + im.coef_off + uint64_t(my) * mcux * nblk;
   const uint32_t *ent = coefs.ent + im.ent_off;
-  uint32_t nb = min(S, mcux) * nblk;
-  uint2 bi = tid < nb ? blk_row[tid] : make_uint2(0, 0);
+  // entry cursor at the row's first block, blocks left in its restart interval
+  uint32_t cur = U(coefs.row[im.row_off + my]);
+  uint32_t gblk = my * mcux * nblk;
+  uint32_t bleft;
+  {
+    const uint32_t ri = U(im.ri_mcus);
+    const RjSegDev sg = im.segs[ri ? (my * mcux) / ri : 0];
+    bleft = U((sg.mcu_first + sg.mcu_count - my * mcux) * nblk);
+  }
+  EntWin win;
+  win.load(ent, cur, tid);
 
   for (uint32_t sx = 0; sx < strips_x; sx++) {
     const uint32_t mx0 = sx * S;
     const uint32_t nm = min(S, mcux - mx0);
-    nb = nm * nblk;
+    const uint32_t nb = nm * nblk;
     const bool has_blk = tid < nb;
 
-    // ---- A: clear the strip's LDS blocks, expand this lane's sparse list into its block ----
+    // ---- A: clear the strip's LDS blocks, expand the entry stream into them ----
     __syncthreads();  // previous strip's tiles fully read
     for (uint32_t k = tid; k < nb * 8; k += 64)
       *reinterpret_cast<uint4 *>(s_buf + (k >> 3) * RJ_BLK_STRIDE + (k & 7) * 16) = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    if (has_blk)
-      scatter_block(reinterpret_cast<const uint4 *>(ent + bi.x), bi.y,
-                    reinterpret_cast<int16_t *>(s_buf + tid * RJ_BLK_STRIDE));
-    // next strip's block index: in flight during this strip's IDCT and output
-    if (sx + 1 < strips_x) {
-      const uint32_t nb1 = min(S, mcux - mx0 - S) * nblk;
-      bi = tid < nb1 ? blk_row[(mx0 + S) * nblk + tid] : make_uint2(0, 0);
-    }
+    parse_blocks(im, ent, tid, nb, nblk, win, cur, bleft, gblk, s_buf);
+    if (sx + 1 < strips_x) win.load(ent, cur, tid);  // next strip's window: lands behind B and C
     __syncthreads();
 
     // ---- B: lane-per-block IDCT in registers ----
+    const uint32_t c_b = lane_blk >> 12;
     int32_t v[64];
     if (has_blk)
       dezigzag_dequant(reinterpret_cast<const uint4 *>(s_buf + tid * RJ_BLK_STRIDE),
-                       reinterpret_cast<const uint4 *>(s_q[lane_tile >> 16]), v);
+                       reinterpret_cast<const uint4 *>(s_q[c_b]), v);
+    if constexpr (kPlanes) {
+      if (has_blk) {
+        uint32_t o[16];
+        idct_islow_block(v, o);
+        const uint32_t hc = inter ? im.comp_h[c_b] : 1, vc = inter ? im.comp_v[c_b] : 1;
+        const uint32_t bx = mx0 * hc + (lane_blk & 255u), by = my * vc + ((lane_blk >> 8) & 15u);
+        const uint32_t pitch = im.plane_pitch[c_b];
+        uint8_t *dst = planes + im.plane_off[c_b] + uint64_t(by) * 8u * pitch + bx * 8u;
+#pragma unroll
+        for (int r = 0; r < 8; r++) *reinterpret_cast<uint2 *>(dst + uint64_t(r) * pitch) = make_uint2(o[2 * r], o[2 * r + 1]);
+      }
+      continue;
+    }
     __syncthreads();  // every block is in registers: the staging area becomes the sample tiles
     if (has_blk) {
       uint32_t o[16];
       idct_islow_block(v, o);
-      const uint32_t c = lane_tile >> 16;
-      const uint32_t twc = c == 0 ? tw[0] : (c == 1 ? tw[1] : tw[2]);
-      uint8_t *dst = s_buf + (lane_tile & 0xFFFF);
+      const uint32_t twc = c_b == 0 ? tw[0] : (c_b == 1 ? tw[1] : tw[2]);
+      const uint32_t toc = c_b == 0 ? toff[0] : (c_b == 1 ? toff[1] : toff[2]);
+      uint8_t *dst = s_buf + toc + ((lane_blk >> 8) & 15u) * 8u * twc + (lane_blk & 255u) * 8u;
 #pragma unroll
       for (int r = 0; r < 8; r++) *reinterpret_cast<uint2 *>(dst + r * twc) = make_uint2(o[2 * r], o[2 * r + 1]);
     }
@@ -276,10 +360,13 @@ __global__ __launch_bounds__(64) void k_fused(const RjImageDev *__restrict__ img
   }  // strips
 }
 
-hipError_t LaunchFusedOutput(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
-                             uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets) {
+hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
+                      uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets, uint8_t *planes) {
   if (nrows == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fused, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, coefs, tabsets);
+  if (to_planes)
+    hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, coefs, tabsets, planes);
+  else
+    hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, coefs, tabsets, planes);
   return hipGetLastError();
 }
 

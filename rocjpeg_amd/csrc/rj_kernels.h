@@ -15,19 +15,15 @@ hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint3
 hipError_t LaunchHuffman(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nseg, const uint8_t *destuffed,
                          const uint32_t *seg_len, const RjTableSet *tabsets, RjCoefBuf coefs);
 
-// K2a (general path): dequantise + ISLOW IDCT of every block into MCU-padded component planes.
-hipError_t LaunchIdctPlanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint64_t nblocks, RjCoefBuf coefs,
-                            const RjTableSet *tabsets, uint8_t *planes);
-
 // K2b (general path): every output format / ROI of rocjpeg_decoder.cpp:143-180 from the planes.
 hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobDev *jobs, int njobs, uint32_t total_rows,
                             const uint8_t *planes);
 
-// K2 (fused fast path): dequant + IDCT + nearest upsample + YUV->RGB / layout straight from the
-// coefficients to the caller's buffers, one single-wave workgroup per MCU row (looping over the
-// row's strips); row_prefix[i] = first row of image i (fused images only).  Only for images whose
-// output window is tile-local (no ROI quirks); see rj_decoder.cpp::FusedEligible.
-hipError_t LaunchFusedOutput(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
-                             uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets);
+// K2: one wavefront per MCU row (row_prefix[i] = first row of image i in this launch; images
+// with no rows in it have equal consecutive prefixes).  Sparse entries -> dequant + ISLOW IDCT
+// -> either the fused output (upsample + CSC / layout straight into the caller's buffers, only
+// for rj_decoder.cpp::FusedEligible images) or the MCU-padded component planes (to_planes).
+hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
+                      uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets, uint8_t *planes);
 
 }  // namespace rj

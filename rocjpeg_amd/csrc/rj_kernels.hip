@@ -5,15 +5,14 @@
 //
 //   K0 k_destuff      one wavefront per restart interval: coalesced byte loads, FF00/fill
 //                     removal by per-lane keep masks + wave prefix sum, compacted stores.
-//   K1 k_huffman      one lane per restart interval: 64-bit MSB-first bit buffer refilled by
-//                     aligned dword loads, 9-bit LUT + canonical slow path, flattened
-//                     symbol loop (lanes never wait for each other at block boundaries),
-//                     per-lane 128-B coefficient block staged in LDS.
-//   K2a k_idct_planes thread per 8x8 block: dequant + libjpeg ISLOW IDCT in registers,
-//                     8-byte row stores into MCU-padded component planes.
+//   K1 k_huffman      one lane per restart interval: LDS bit ring + two-level LDS LUT,
+//                     flattened symbol loop (lanes never wait for each other at block
+//                     boundaries), sparse entry stream staged in LDS, 64-B group stores.
+//   K2 k_rows         (rj_fused.hip) one wave per MCU row: entry stream -> LDS blocks ->
+//                     dequant + ISLOW IDCT -> fused output (upsample + CSC / layout) or
+//                     MCU-padded component planes (general path).
 //   K2b k_output      every output format / ROI semantic of rocjpeg_decoder.cpp:143-180,
 //                     colour conversion identical to rocjpeg_hip_kernels.cpp:1431-1443.
-//   K2  k_fused       (rj_fused.hip) dequant + IDCT + upsample + CSC without the planes.
 #include <hip/hip_runtime.h>
 
 #include "rj_device.h"
@@ -106,68 +105,63 @@ hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint3
 }
 
 // ---------------------------------------------------------------------------------------
-// K1: Huffman decode, one lane per restart interval.
+// K1: Huffman decode, one lane per restart interval (T.81 F.2.2, libjpeg jdhuff.c semantics).
 //
-// Per lane: a 64-bit MSB-first bit buffer fed 32 bits at a time from a 16-B register double
-// buffer (cur/nxt): the next 16-B chunk is loaded ~4 refills (~25 symbols) before it is
-// needed, so the HBM/L2 latency hides behind decode work.  Huffman lookups hit a per-wave LDS
-// copy of the image's tables (9-bit first level + 7-bit second level, rj_device.h), so the
-// dependent chain per symbol is one ds_read (two for codes > 9 bits) plus ~20 ALU ops; the
-// extra bits are cut from the same 32-bit peek (no second read).  The flattened symbol loop
-// lets every lane run at its own pace across block boundaries; a finished block (zeroed LDS
-// staging + scattered coefficients) leaves as 8 x 16-B stores.
+// Per lane everything on the per-symbol dependency chain stays on-chip:
+//   * bits: a 64-bit MSB-first buffer refilled 32 bits at a time from a per-lane LDS ring of
+//     the interval's destuffed bytes; the next ring word is read one symbol ahead, so the only
+//     LDS round trip left on the chain is the Huffman lookup itself.  The ring is topped up
+//     from HBM at wave-uniform phase boundaries (every RJ_PHASE symbols) with loads issued one
+//     phase before they are committed, so their latency hides behind a whole phase of decoding
+//     (a conditional global load inside the loop would cost a full vmcnt(0) round trip).
+//   * lookup: two-level LUT in LDS (9-bit first level + 7-bit second level, rj_device.h); the
+//     extra bits come from the same 32-bit peek (v_bfe_u32), HUFF_EXTEND branch-free.
+//   * output: entries are staged in a per-lane LDS ring and leave in 64-B groups at phase
+//     boundaries (4 x 16-B stores) -- no per-symbol global store, no per-block index.
+// The flattened symbol loop lets every lane run at its own pace across block boundaries.
 // ---------------------------------------------------------------------------------------
-// Bit reader over a per-lane LDS ring of the interval's destuffed bytes.  The ring is
-// refilled at wave-uniform phase boundaries (every RJ_PHASE symbols): the two 16-B chunks
-// loaded at boundary p are committed to LDS at boundary p+1, so their latency hides behind a
-// whole phase of decoding and the symbol loop itself issues no global load (a conditional
-// load inside the loop costs a full vmcnt(0) round trip per symbol on CDNA: the PHI copy of
-// its destination register waits for it).
-#define RJ_RING_CHUNKS 16  // 16-B chunks per lane (256 B)
-#define RJ_PHASE 16        // symbols per refill phase: <= 16 words consumed (<= 32 bits/symbol)
-#define RJ_PREFETCH 4      // chunks (16 words) fetched per phase >= worst-case consumption
-// Invariant: at every phase boundary the ring holds >= 17 unread words (or all that remain),
-// so a refill never has to fall back to a global read inside the symbol loop.
+#define RJ_RING_CHUNKS 8   // 16-B chunks per lane in the bit ring (128 B)
+#define RJ_RING_WORDS (RJ_RING_CHUNKS * 4)
+#define RJ_PHASE 16        // symbols per phase
+#define RJ_PREFETCH 4      // chunks fetched per phase at most
+#define RJ_STAGE 32        // staged entries per lane (two 64-B groups)
+
 struct BitReader {
   const uint4 *src;   // 16-B aligned destuffed bytes, zero-padded after nbytes
-  uint4 *ring;        // this lane's LDS ring
+  uint32_t *ring;     // this lane's LDS ring (RJ_RING_WORDS words)
   uint32_t nchunks;   // 16-B chunks holding data
-  uint32_t rd;        // words consumed from the ring (monotonic)
+  uint32_t rd;        // next word to move into the bit buffer (monotonic)
   uint32_t cm;        // chunks committed to the ring (monotonic)
-  uint32_t pq;        // first chunk of the pending prefetch
-  uint32_t pn;        // chunks in the pending prefetch (0..RJ_PREFETCH)
+  uint32_t pq, pn;    // pending prefetch: first chunk, count
   uint4 pf[RJ_PREFETCH];
-  uint32_t nbytes;
+  uint32_t nw;        // ring word rd, read ahead
   int nb;             // valid bits in acc (left-justified)
   uint64_t acc;
 
-  __device__ __forceinline__ void init(const uint4 *s, uint4 *r, uint32_t n) {
+  __device__ __forceinline__ void init(const uint4 *s, uint32_t *r, uint32_t nbytes) {
     src = s;
     ring = r;
-    nbytes = n;
-    nchunks = (n + 15) / 16;
+    nchunks = (nbytes + 15) / 16;
     const uint32_t first = nchunks < RJ_RING_CHUNKS ? nchunks : RJ_RING_CHUNKS;
-    for (uint32_t q = 0; q < first; q++) ring[q] = src[q];
+    for (uint32_t q = 0; q < first; q++) reinterpret_cast<uint4 *>(ring)[q] = src[q];
     cm = first;
     rd = 0;
     pq = cm;
     pn = 0;
 #pragma unroll
     for (int q = 0; q < RJ_PREFETCH; q++) pf[q] = make_uint4(0, 0, 0, 0);
+    nw = ring[0];
     nb = 0;
     acc = 0;
   }
-  // phase boundary: commit the previous prefetch, issue the next one (loads unconditional:
-  // a conditional load would again force an immediate wait at the control-flow join)
+  // phase boundary: commit the previous prefetch into free slots, issue the next one (loads
+  // unconditional: a conditional load would force an immediate wait at the join)
   __device__ __forceinline__ void phase() {
 #pragma unroll
     for (int q = 0; q < RJ_PREFETCH; q++)
-      if (uint32_t(q) < pn) ring[(pq + q) & (RJ_RING_CHUNKS - 1)] = pf[q];
+      if (uint32_t(q) < pn) reinterpret_cast<uint4 *>(ring)[(pq + q) & (RJ_RING_CHUNKS - 1)] = pf[q];
     cm += pn;
-    // chunks (rd>>2) .. cm-1 are live in the ring (incl. the one being read); new chunks may
-    // only take the remaining slots -- a prefetch is committed one phase later, when at least
-    // as many slots are free again
-    const uint32_t used = cm - (rd >> 2);
+    const uint32_t used = cm - (rd >> 2);  // live chunks, incl. the one being read
     const uint32_t room = RJ_RING_CHUNKS - used;
     uint32_t want = nchunks > cm ? nchunks - cm : 0u;
     want = want < room ? want : room;
@@ -176,22 +170,32 @@ struct BitReader {
     const uint32_t last = nchunks ? nchunks - 1 : 0;
 #pragma unroll
     for (int q = 0; q < RJ_PREFETCH; q++) pf[q] = src[pq + q < last ? pq + q : last];
+    nw = ring[rd & (RJ_RING_WORDS - 1)];  // the commit may have landed the read-ahead word
   }
   __device__ __forceinline__ void refill() {
     if (nb <= 32) {
-      // past the committed chunks only when past the data: zero bits (libjpeg inserts zeros)
-      const uint32_t w = ((rd >> 2) < cm) ? reinterpret_cast<const uint32_t *>(ring)[rd & (RJ_RING_CHUNKS * 4 - 1)] : 0u;
-      rd++;
+      uint32_t w;
+      if ((rd >> 2) < cm) {
+        w = nw;
+      } else if ((rd >> 2) < nchunks) {  // ring ran dry (pathological bit rates): read HBM
+        w = reinterpret_cast<const uint32_t *>(src)[rd];
+      } else {
+        w = 0;  // past the data: zero bits, as libjpeg inserts
+      }
       acc |= uint64_t(__builtin_bswap32(w)) << (32 - nb);
       nb += 32;
+      rd++;
     }
+    nw = ring[rd & (RJ_RING_WORDS - 1)];
   }
-  __device__ __forceinline__ bool overrun() const { return uint64_t(rd) * 32u - uint64_t(nb) > uint64_t(nbytes) * 8u; }
+  __device__ __forceinline__ bool overrun(uint32_t nbytes) const {
+    return uint64_t(rd) * 32u - uint64_t(nb) > uint64_t(nbytes) * 8u;
+  }
 };
 
-// canonical search when the second-level pool is exhausted (libjpeg jpeg_huff_decode), on
-// the LDS copy of the table
-__device__ __forceinline__ uint32_t huff_slow(const RjHuffDev *t, uint32_t peek16) {
+// canonical search when the second-level pool is exhausted (libjpeg jpeg_huff_decode); the
+// pathological tables that need it are read from HBM
+__device__ __noinline__ uint32_t huff_slow(const RjHuffDev *t, uint32_t peek16) {
   uint32_t e = RJ_LUT_BAD;
   for (int l = 10; l <= 16; l++)
     if (peek16 < t->maxcode16[l]) {
@@ -205,9 +209,10 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
                                                 const uint8_t *__restrict__ destuffed,
                                                 const uint32_t *__restrict__ seg_len,
                                                 const RjTableSet *__restrict__ tabsets, RjCoefBuf coefs) {
-  // per-lane ring padded to 272 B so the 8-lane groups of its ds_write_b128 hit distinct banks
-  __shared__ __attribute__((aligned(16))) uint4 s_ring[64][RJ_RING_CHUNKS + 1];
-  __shared__ __attribute__((aligned(16))) RjHuffDev s_tab[4];  // dc0, dc1, ac0, ac1
+  // strides padded by 16 B so the 8-lane groups of ds_*_b128 hit distinct banks
+  __shared__ __attribute__((aligned(16))) uint32_t s_ring[64][RJ_RING_WORDS + 4];
+  __shared__ __attribute__((aligned(16))) uint32_t s_stage[64][RJ_STAGE + 4];
+  __shared__ __attribute__((aligned(16))) uint16_t s_lut[4][RJ_LUT_ENTRIES];  // dc0, dc1, ac0, ac1
   const uint32_t lane = threadIdx.x;
   const uint32_t g = blockIdx.x * 64u + lane;
   const bool valid = g < nseg;
@@ -221,80 +226,115 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
     if (m == 0) break;
     const uint32_t T = __shfl(my_ts, __ffsll((long long)m) - 1, 64);
     __syncthreads();
-    {
-      static_assert(sizeof(RjHuffDev) % 16 == 0, "RjHuffDev must be 16-B multiple");
-      const uint4 *s4 = reinterpret_cast<const uint4 *>(&tabsets[T].dc[0]);  // dc0, dc1, ac0, ac1 contiguous
-      uint4 *d4 = reinterpret_cast<uint4 *>(s_tab);
-      for (uint32_t k = lane; k < 4 * sizeof(RjHuffDev) / 16; k += 64) d4[k] = s4[k];
+    for (uint32_t t = 0; t < 4; t++) {
+      const RjHuffDev *h = t < 2 ? &tabsets[T].dc[t] : &tabsets[T].ac[t - 2];
+      const uint4 *s4 = reinterpret_cast<const uint4 *>(h->lut);
+      uint4 *d4 = reinterpret_cast<uint4 *>(s_lut[t]);
+      for (uint32_t k = lane; k < RJ_LUT_ENTRIES * 2 / 16; k += 64) d4[k] = s4[k];
     }
     __syncthreads();
     if (pending && my_ts == T) {
       pending = false;
       const RjSegDev sg = im.segs[g - im.seg_prefix];
-      const uint32_t nblk = im.nblk_mcu;
-      uint32_t comp_bits = 0;  // 2 bits per block-in-MCU: its component
-      for (uint32_t b = 0; b < nblk; b++) comp_bits |= uint32_t(im.blk_comp[b]) << (2 * b);
-      // s_tab index per component: dc tables 0/1, ac tables 2/3
-      const uint32_t dc0 = im.comp_td[0] & 1, ac0 = 2 + (im.comp_ta[0] & 1);
-      const uint32_t dc1 = im.comp_td[1] & 1, ac1 = 2 + (im.comp_ta[1] & 1);
-      const uint32_t dc2 = im.comp_td[2] & 1, ac2 = 2 + (im.comp_ta[2] & 1);
-
+      const uint32_t nblk = im.nblk_mcu, mcux = im.mcux;
+      // per block-in-MCU b: component (2 bits) | dc table (1) | ac table (1), 4 bits each
+      uint64_t binfo = 0;
+      for (uint32_t b = 0; b < nblk; b++) {
+        const uint32_t c = im.blk_comp[b] & 3;
+        binfo |= uint64_t(c | ((im.comp_td[c] & 1) << 2) | ((im.comp_ta[c] & 1) << 3)) << (4 * b);
+      }
+      const uint32_t nbytes = seg_len[g];
       BitReader br;
-      br.init(reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off), s_ring[lane], seg_len[g]);
-      uint2 *bidx = coefs.blk + im.coef_off + uint64_t(sg.mcu_first) * nblk;  // current block's index slot
-      uint2 *const bidx_end = bidx + uint64_t(sg.mcu_count) * nblk;
-      uint32_t *const ent = coefs.ent + im.ent_off + sg.ent_off;  // this interval's entry region
-      uint32_t ne = 0, bstart = 0;
+      br.init(reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off), s_ring[lane], nbytes);
+      uint32_t *const ent = coefs.ent + im.ent_off + sg.ent_off;  // group-aligned region
+      uint32_t *const stage = s_stage[lane];
+      uint32_t ne = 0, fl = 0;  // entries produced / flushed (fl multiple of RJ_ENT_GROUP)
+
+      // MCU row checkpoints for K2
+      const uint32_t row0 = im.row_off;
+      uint32_t mrow = sg.mcu_first / mcux;
+      uint32_t to_row = mcux - (sg.mcu_first - mrow * mcux);  // MCUs until the next row starts
+      if (to_row == mcux) coefs.row[row0 + mrow] = sg.ent_off;
 
       int pred0 = 0, pred1 = 0, pred2 = 0;
       bool skip = (sg.flags & RJ_SEG_MISSING) != 0;
+      uint32_t blocks_left = sg.mcu_count * nblk;
       uint32_t b = 0;
+      uint32_t info = uint32_t(binfo) & 15u;
       int k = 0;
       uint32_t iter = 0;
-      while (bidx < bidx_end) {
-        if ((iter++ & (RJ_PHASE - 1)) == 0) br.phase();  // same count in every active lane
-        if (skip) {
+      while (blocks_left > 0) {
+        if ((iter++ & (RJ_PHASE - 1)) == 0) {  // same count in every active lane
+          br.phase();
+          if (ne - fl >= RJ_ENT_GROUP) {  // one full 64-B group leaves the stage
+            const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
+            uint4 *d4 = reinterpret_cast<uint4 *>(ent + fl);
+#pragma unroll
+            for (int q = 0; q < RJ_ENT_GROUP / 4; q++) d4[q] = s4[q];
+            fl += RJ_ENT_GROUP;
+          }
+        }
+        uint32_t entry;
+        bool emit;
+        if (skip) {  // libjpeg: the rest of the interval decodes to zero blocks
+          entry = 0;
+          emit = true;
           k = 64;
         } else {
           br.refill();
-          const uint32_t c = (comp_bits >> (2 * b)) & 3u;
+          const uint32_t c = info & 3u;
           const uint32_t peek32 = uint32_t(br.acc >> 32);
-          const uint32_t tix = k == 0 ? (c == 0 ? dc0 : (c == 1 ? dc1 : dc2)) : (c == 0 ? ac0 : (c == 1 ? ac1 : ac2));
-          const RjHuffDev *tab = &s_tab[tix];
-          uint32_t e = tab->lut[peek32 >> 23];
+          const uint32_t tix = k == 0 ? ((info >> 2) & 1u) : 2u + ((info >> 3) & 1u);
+          uint32_t e = s_lut[tix][peek32 >> 23];
           if (e & 0x8000u) {
-            if (e != 0xFFFFu) e = tab->lut[RJ_LUT_L1 + (e & 0x7Fu) * 128u + ((peek32 >> 16) & 127u)];
-            else e = huff_slow(tab, peek32 >> 16);
+            if (e != 0xFFFFu) e = s_lut[tix][RJ_LUT_L1 + (e & 0x7Fu) * 128u + ((peek32 >> 16) & 127u)];
+            else e = huff_slow(tix < 2 ? &tabsets[T].dc[tix] : &tabsets[T].ac[tix - 2], peek32 >> 16);
           }
           const uint32_t len = e >> 8, sym = e & 255u;
           const uint32_t s = sym & 15u, r = sym >> 4;
-          // the extra bits follow the code inside the same 32-bit peek (len + s <= 31)
-          const uint32_t t = peek32 << len;
-          const uint32_t raw = s ? (t >> (32u - s)) : 0u;
-          const int val = (s && raw < (1u << (s - 1))) ? int(raw) - (1 << s) + 1 : int(raw);
+          // extra bits follow the code inside the same peek (len + s <= 31); width 0 -> 0
+          const uint32_t raw = __builtin_amdgcn_ubfe(peek32, 32u - len - s, s);
+          // HUFF_EXTEND (jdhuff.h): negative when the top extra bit is 0; s == 0 gives 0
+          const int val = int(raw) + (int32_t(raw - (1u << ((s - 1) & 31))) >> 31 & int32_t(1u - (1u << s)));
           br.acc <<= (len + s);
           br.nb -= int(len + s);
           // DC (k == 0): predictor per component (F.2.1.3); AC: run/size (F.2.2.2)
           const bool isdc = k == 0;
-          const int pc = c == 0 ? pred0 : (c == 1 ? pred1 : pred2);
-          const int p = pc + val;
+          const int p = (c == 0 ? pred0 : (c == 1 ? pred1 : pred2)) + val;
           pred0 = (isdc && c == 0) ? p : pred0;
           pred1 = (isdc && c == 1) ? p : pred1;
           pred2 = (isdc && c == 2) ? p : pred2;
           const int kk = isdc ? 0 : k + int(r);  // zigzag position of this coefficient
-          if (isdc || s) ent[ne++] = (uint32_t(isdc ? p : val) & 0xFFFFu) | (uint32_t(kk < 63 ? kk : 63) << 16);
+          entry = (uint32_t(isdc ? p : val) & 0xFFFFu) | (uint32_t(kk < 63 ? kk : 63) << 16);
+          emit = isdc || s;
           k = isdc ? 1 : (s ? kk + 1 : (r == 15 ? k + 16 : 64));  // ZRL / EOB
         }
-        if (k >= 64) {  // block complete: its index entry; next list starts 16-B aligned
-          *bidx++ = make_uint2(sg.ent_off + bstart, ne - bstart);
-          ne = (ne + 3u) & ~3u;
-          bstart = ne;
+        stage[ne & (RJ_STAGE - 1)] = entry;  // a non-emitted write lands in the next free slot
+        ne += emit ? 1u : 0u;
+        if (k >= 64) {  // block complete
           k = 0;
+          blocks_left--;
           if (++b == nblk) {
             b = 0;
-            if (br.overrun()) skip = true;  // libjpeg: rest of the interval stays zero
+            if (!skip && br.overrun(nbytes)) skip = true;  // libjpeg: rest of the interval stays zero
+            if (--to_row == 0) {  // the next MCU starts a row
+              to_row = mcux;
+              mrow++;
+              if (blocks_left) coefs.row[row0 + mrow] = sg.ent_off + ne;
+            }
           }
+          info = uint32_t(binfo >> (4 * b)) & 15u;
         }
+      }
+      // terminator, then everything still staged (whole groups; the slack is reserved)
+      stage[ne & (RJ_STAGE - 1)] = RJ_ENT_TERM;
+      ne++;
+      while (fl < ne) {
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
+        uint4 *d4 = reinterpret_cast<uint4 *>(ent + fl);
+#pragma unroll
+        for (int q = 0; q < RJ_ENT_GROUP / 4; q++) d4[q] = s4[q];
+        fl += RJ_ENT_GROUP;
       }
     }
   }
@@ -305,66 +345,6 @@ hipError_t LaunchHuffman(hipStream_t st, const RjImageDev *imgs, int nimg, uint3
   if (nseg == 0) return hipSuccess;
   hipLaunchKernelGGL(k_huffman, dim3((nseg + 63) / 64), dim3(64), 0, st, imgs, nimg, nseg, destuffed, seg_len, tabsets,
                      coefs);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------
-// K2a: IDCT into component planes (general path).
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_idct_planes(const RjImageDev *__restrict__ imgs, int nimg, uint64_t nblocks,
-                                                     RjCoefBuf coefs, const RjTableSet *__restrict__ tabsets,
-                                                     uint8_t *__restrict__ planes) {
-  __shared__ __attribute__((aligned(16))) uint4 s_blk[256][9];  // 144-B stride: conflict-free b128
-  const uint64_t gb = uint64_t(blockIdx.x) * 256u + threadIdx.x;
-  const bool active = gb < nblocks;
-#pragma unroll
-  for (int q = 0; q < 8; q++) s_blk[threadIdx.x][q] = make_uint4(0, 0, 0, 0);
-  int i = 0, c = 0;
-  uint32_t bx = 0, by = 0;
-  if (active) {
-    i = upper_index(nimg, uint32_t(gb), [&](int k) { return imgs[k].blk_prefix; });
-    const RjImageDev &im = imgs[i];
-    uint32_t local = uint32_t(gb) - im.blk_prefix;
-    uint32_t wb = im.plane_pitch[0] >> 3, hb = im.plane_rows[0] >> 3;
-    while (c + 1 < im.ncomp && local >= wb * hb) {
-      local -= wb * hb;
-      c++;
-      wb = im.plane_pitch[c] >> 3;
-      hb = im.plane_rows[c] >> 3;
-    }
-    by = local / wb;
-    bx = local - by * wb;
-    uint64_t cb;
-    if (im.interleaved) {
-      const uint32_t hc = im.comp_h[c], vc = im.comp_v[c];
-      const uint32_t mx = bx / hc, my = by / vc;
-      const uint32_t b = im.comp_blk0[c] + (by - my * vc) * hc + (bx - mx * hc);
-      cb = im.coef_off + (uint64_t(my) * im.mcux + mx) * im.nblk_mcu + b;
-    } else {
-      cb = im.coef_off + local;
-    }
-    const uint2 bi = coefs.blk[cb];
-    scatter_block(reinterpret_cast<const uint4 *>(coefs.ent + im.ent_off + bi.x), bi.y,
-                  reinterpret_cast<int16_t *>(s_blk[threadIdx.x]));
-  }
-  if (!active) return;  // each thread only touches its own LDS block: no barrier needed
-  const RjImageDev &im = imgs[i];
-  const uint4 *q4 = reinterpret_cast<const uint4 *>(tabsets[im.tabset].qz[im.comp_tq[c] & 3]);
-  int32_t v[64];
-  dezigzag_dequant(s_blk[threadIdx.x], q4, v);
-  uint32_t o[16];
-  idct_islow_block(v, o);
-  uint8_t *dst = planes + im.plane_off[c] + uint64_t(by) * 8u * im.plane_pitch[c] + bx * 8u;
-#pragma unroll
-  for (int r = 0; r < 8; r++)
-    *reinterpret_cast<uint2 *>(dst + uint64_t(r) * im.plane_pitch[c]) = make_uint2(o[2 * r], o[2 * r + 1]);
-}
-
-hipError_t LaunchIdctPlanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint64_t nblocks, RjCoefBuf coefs,
-                            const RjTableSet *tabsets, uint8_t *planes) {
-  if (nblocks == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_idct_planes, dim3(uint32_t((nblocks + 255) / 256)), dim3(256), 0, st, imgs, nimg, nblocks, coefs,
-                     tabsets, planes);
   return hipGetLastError();
 }
 

@@ -309,7 +309,7 @@ void Stream::BuildPlan() {
     sg.flags = 0;
     sg.ent_off = uint32_t(ent);
     sg.pad = 0;
-    ent += uint64_t(sg.mcu_count) * p.nblk_mcu * RJ_ENT_PER_BLOCK;
+    ent += rj_interval_entries(uint64_t(sg.mcu_count) * p.nblk_mcu);
     dst += (uint64_t(sg.src_len) + 16 + 15) & ~uint64_t(15);  // >= 16 B of slack after each interval
     p.segs.push_back(sg);
   };
@@ -347,7 +347,7 @@ void Stream::BuildPlan() {
     sg.flags = RJ_SEG_MISSING;
     sg.ent_off = uint32_t(ent);
     sg.pad = 0;
-    ent += uint64_t(sg.mcu_count) * p.nblk_mcu * RJ_ENT_PER_BLOCK;
+    ent += rj_interval_entries(uint64_t(sg.mcu_count) * p.nblk_mcu);
     dst += 16;
     p.segs.push_back(sg);
   }
