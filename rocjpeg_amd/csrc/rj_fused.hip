@@ -59,7 +59,7 @@ __device__ __forceinline__ uint32_t U(uint32_t x) { return __builtin_amdgcn_read
 __device__ __forceinline__ void store_bytes(uint8_t *d, uint32_t n, const uint32_t *w) {
 #pragma unroll
   for (int j = 0; j < 12; j++)
-    if (uint32_t(j) < n) d[j] = uint8_t(w[j >> 2] >> (8 * (j & 3)));
+    if (uint32_t(j) < n) gp(d)[j] = uint8_t(w[j >> 2] >> (8 * (j & 3)));
 }
 
 // Entry-stream window of one wave: w[r] = ent[base + r * 64 + lane] (coalesced rows).  The
@@ -91,7 +91,7 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const uint32_
   while (done < nb) {
     if (bleft == 0) {  // the next block opens a new restart interval (rare: synchronous reload)
       const uint32_t ri = im.ri_mcus;
-      const RjSegDev sg = im.segs[ri ? gblk / nblk / ri : 0];
+      const RjSegDev sg = gp(im.segs)[ri ? gblk / nblk / ri : 0];
       cur = U(sg.ent_off);
       bleft = U(sg.mcu_count * nblk);
       win.load(ent, cur, lane);
@@ -195,11 +195,24 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
   uint32_t bleft;
   {
     const uint32_t ri = U(im.ri_mcus);
-    const RjSegDev sg = im.segs[ri ? (my * mcux) / ri : 0];
+    const RjSegDev sg = gp(im.segs)[ri ? (my * mcux) / ri : 0];
     bleft = U((sg.mcu_first + sg.mcu_count - my * mcux) * nblk);
   }
   EntWin win;
   win.load(ent, cur, tid);
+
+  // output descriptor, read once before the strip loop (the output stores could otherwise
+  // force re-reads of the descriptor inside the pixel loops)
+  uint8_t *const dst0 = im.dst[0], *const dst1 = im.dst[1], *const dst2 = im.dst[2];
+  const uint32_t pitch0 = U(im.dst_pitch[0]), pitch1 = U(im.dst_pitch[1]);
+  const uint32_t W = U(im.width), H = U(im.height);
+  const uint32_t fmt = U(im.fmt);
+  const uint32_t hs1 = U((ncomp == 3) ? (hmax / im.comp_h[1] == 2 ? 1u : 0u) : 0u);
+  const uint32_t vs1 = U((ncomp == 3) ? (vmax / im.comp_v[1] == 2 ? 1u : 0u) : 0u);
+  const bool al_y = ((reinterpret_cast<uintptr_t>(dst0) | pitch0) & 3) == 0;
+  const bool al_rgbp = ((reinterpret_cast<uintptr_t>(dst0) | reinterpret_cast<uintptr_t>(dst1) |
+                         reinterpret_cast<uintptr_t>(dst2) | pitch0) & 3) == 0;
+  const bool al_uv = ((reinterpret_cast<uintptr_t>(dst1) | reinterpret_cast<uintptr_t>(dst2) | pitch1) & 3) == 0;
 
   for (uint32_t sx = 0; sx < strips_x; sx++) {
     const uint32_t mx0 = sx * S;
@@ -231,7 +244,7 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
         const uint32_t pitch = im.plane_pitch[c_b];
         uint8_t *dst = planes + im.plane_off[c_b] + uint64_t(by) * 8u * pitch + bx * 8u;
 #pragma unroll
-        for (int r = 0; r < 8; r++) *reinterpret_cast<uint2 *>(dst + uint64_t(r) * pitch) = make_uint2(o[2 * r], o[2 * r + 1]);
+        for (int r = 0; r < 8; r++) *gp(reinterpret_cast<uint2 *>(dst + uint64_t(r) * pitch)) = make_uint2(o[2 * r], o[2 * r + 1]);
       }
       continue;
     }
@@ -250,18 +263,14 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
   // ---- C: output, lane = 4 consecutive pixels ----
   const uint32_t strip_w = nm * mcu_w;
   const uint32_t px0 = mx0 * mcu_w, py0 = my * mcu_h;
-  const uint32_t W = U(im.width), H = U(im.height);
-  const uint32_t fmt = U(im.fmt);
-  const uint32_t hs1 = U((ncomp == 3) ? (hmax / im.comp_h[1] == 2 ? 1u : 0u) : 0u);
-  const uint32_t vs1 = U((ncomp == 3) ? (vmax / im.comp_v[1] == 2 ? 1u : 0u) : 0u);
   const uint32_t quads_x = strip_w >> 2;  // strip_w is a multiple of 8
   const uint32_t wmax = min(strip_w, W > px0 ? W - px0 : 0u);
   const uint32_t rows = min(mcu_h, H > py0 ? H - py0 : 0u);
 
   // destination offsets are 32-bit (the host only fuses when pitch * height < 2^31, pitch < 2^24)
   if (fmt >= 1 && fmt <= 4) {
-    const uint32_t pitch = U(im.dst_pitch[0]);
-    const bool a4 = ((reinterpret_cast<uintptr_t>(im.dst[0]) | pitch) & 3) == 0;
+    const uint32_t pitch = pitch0;
+    const bool a4 = al_y;
     // lane walks quads tid, tid+64, ... of the strip (row-major) with an incremental (x, y)
     const uint32_t qsy = 64 / quads_x, qsx = 64 - qsy * quads_x;
     uint32_t qy = tid / quads_x, qx = tid - qy * quads_x;
@@ -302,12 +311,9 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
           w[2] = b2 | (b3 << 8) | (b3 << 16) | (b3 << 24);
         }
         if (fmt == 3) {
-          uint8_t *d = im.dst[0] + (__umul24(py, pitch) + px * 3);
+          uint8_t *d = dst0 + (__umul24(py, pitch) + px * 3);
           if (n == 4 && a4) {
-            uint32_t *d32 = reinterpret_cast<uint32_t *>(d);
-            d32[0] = w[0];
-            d32[1] = w[1];
-            d32[2] = w[2];
+            *gp(reinterpret_cast<uint3 *>(d)) = make_uint3(w[0], w[1], w[2]);
           } else {
             store_bytes(d, 3 * n, w);
           }
@@ -318,26 +324,24 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
                              ((w[2] << 8) & 0xFF000000u);
           const uint32_t B = ((w[0] >> 16) & 0xFFu) | (w[1] & 0xFF00u) | ((w[2] << 16) & 0xFF0000u) | (w[2] & 0xFF000000u);
           const uint32_t pl[3] = {R, G, B};
-          const bool ap = ((reinterpret_cast<uintptr_t>(im.dst[0]) | reinterpret_cast<uintptr_t>(im.dst[1]) |
-                            reinterpret_cast<uintptr_t>(im.dst[2]) | pitch) & 3) == 0;
+          const bool ap = al_rgbp;
           const uint32_t off = __umul24(py, pitch) + px;
 #pragma unroll
           for (int p = 0; p < 3; p++) {
-            uint8_t *d = im.dst[p] + off;
-            if (n == 4 && ap) *reinterpret_cast<uint32_t *>(d) = pl[p];
+            uint8_t *d = (p == 0 ? dst0 : (p == 1 ? dst1 : dst2)) + off;
+            if (n == 4 && ap) *gp(reinterpret_cast<uint32_t *>(d)) = pl[p];
             else store_bytes(d, n, &pl[p]);
           }
         }
       } else {  // Y plane (OUTPUT_Y, and the luma of YUV_PLANAR)
-        uint8_t *d = im.dst[0] + (__umul24(py, pitch) + px);
-        if (n == 4 && a4) *reinterpret_cast<uint32_t *>(d) = y4;
+        uint8_t *d = dst0 + (__umul24(py, pitch) + px);
+        if (n == 4 && a4) *gp(reinterpret_cast<uint32_t *>(d)) = y4;
         else store_bytes(d, n, &y4);
       }
     }
   }
   if (fmt == 1 && ncomp == 3) {  // YUV_PLANAR chroma planes at native resolution; U and V share pitch[1]
-    const bool a4 = ((reinterpret_cast<uintptr_t>(im.dst[1]) | reinterpret_cast<uintptr_t>(im.dst[2]) |
-                      im.dst_pitch[1]) & 3) == 0;
+    const bool a4 = al_uv;
     const uint32_t cW = hs1 ? (W >> 1) : W, cH = vs1 ? (H >> 1) : H;
     const uint32_t cw = strip_w >> hs1, ch = mcu_h >> vs1;
     const uint32_t cx0 = px0 >> hs1, cy0 = py0 >> vs1;
@@ -352,8 +356,8 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
       const uint32_t n = min(4u, cwmax - x);
       const uint32_t s4 = *reinterpret_cast<const uint32_t *>(s_buf + (second ? toff[2] : toff[1]) +
                                                               __umul24(y, second ? tw[2] : tw[1]) + x);
-      uint8_t *d = (second ? im.dst[2] : im.dst[1]) + (__umul24(cy0 + y, im.dst_pitch[1]) + cx0 + x);
-      if (n == 4 && a4) *reinterpret_cast<uint32_t *>(d) = s4;
+      uint8_t *d = (second ? dst2 : dst1) + (__umul24(cy0 + y, pitch1) + cx0 + x);
+      if (n == 4 && a4) *gp(reinterpret_cast<uint32_t *>(d)) = s4;
       else store_bytes(d, n, &s4);
     }
   }

@@ -58,8 +58,8 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
   const uint32_t lane = threadIdx.x;
   const int i = upper_index(nimg, g, [&](int k) { return imgs[k].seg_prefix; });
   const RjImageDev &im = imgs[i];
-  const RjSegDev sg = im.segs[g - im.seg_prefix];
-  const uint8_t *src = im.ecs + sg.src_off;
+  const RjSegDev sg = gp(im.segs)[g - im.seg_prefix];
+  const RJ_GLOBAL uint8_t *src = gp(im.ecs + sg.src_off);
   uint8_t *dst = destuffed + im.destuff_off + sg.dst_off;
   const uint32_t len = sg.src_len;
   uint32_t out = 0;
@@ -120,19 +120,24 @@ hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint3
 //     boundaries (4 x 16-B stores) -- no per-symbol global store, no per-block index.
 // The flattened symbol loop lets every lane run at its own pace across block boundaries.
 // ---------------------------------------------------------------------------------------
-#define RJ_RING_CHUNKS 8   // 16-B chunks per lane in the bit ring (128 B)
+#define RJ_RING_CHUNKS 12  // 16-B chunks per lane in the bit ring (192 B)
 #define RJ_RING_WORDS (RJ_RING_CHUNKS * 4)
-#define RJ_PHASE 16        // symbols per phase
-#define RJ_PREFETCH 4      // chunks fetched per phase at most
-#define RJ_STAGE 32        // staged entries per lane (two 64-B groups)
+#define RJ_PHASE 16         // symbols per phase: <= 16 ring words consumed (<= 32 bits/symbol)
+#define RJ_PREFETCH 4       // chunks fetched per phase at most
+#define RJ_STAGE 32         // staged entries per lane (two 64-B groups)
+// Ring invariant: after every phase commit the ring holds >= 17 unread words (or all that is
+// left).  With U unread words, a phase prefetches n = min(4, 12 - used) chunks and consumes at
+// most 16 words, so U' = U - 16 + 4n >= min(U, 28) -- the symbol loop never reads HBM.
 
 struct BitReader {
   const uint4 *src;   // 16-B aligned destuffed bytes, zero-padded after nbytes
   uint32_t *ring;     // this lane's LDS ring (RJ_RING_WORDS words)
   uint32_t nchunks;   // 16-B chunks holding data
-  uint32_t rd;        // next word to move into the bit buffer (monotonic)
+  uint32_t rd;        // words moved into the bit buffer (monotonic)
+  uint32_t rdw;       // rd mod RJ_RING_WORDS
   uint32_t cm;        // chunks committed to the ring (monotonic)
-  uint32_t pq, pn;    // pending prefetch: first chunk, count
+  uint32_t cms;       // cm mod RJ_RING_CHUNKS
+  uint32_t pn;        // chunks in the pending prefetch
   uint4 pf[RJ_PREFETCH];
   uint32_t nw;        // ring word rd, read ahead
   int nb;             // valid bits in acc (left-justified)
@@ -145,8 +150,9 @@ struct BitReader {
     const uint32_t first = nchunks < RJ_RING_CHUNKS ? nchunks : RJ_RING_CHUNKS;
     for (uint32_t q = 0; q < first; q++) reinterpret_cast<uint4 *>(ring)[q] = src[q];
     cm = first;
+    cms = first == RJ_RING_CHUNKS ? 0 : first;
     rd = 0;
-    pq = cm;
+    rdw = 0;
     pn = 0;
 #pragma unroll
     for (int q = 0; q < RJ_PREFETCH; q++) pf[q] = make_uint4(0, 0, 0, 0);
@@ -154,56 +160,56 @@ struct BitReader {
     nb = 0;
     acc = 0;
   }
-  // phase boundary: commit the previous prefetch into free slots, issue the next one (loads
-  // unconditional: a conditional load would force an immediate wait at the join)
+  // phase boundary: commit the previous prefetch (loaded one phase ago), issue the next one
+  // (loads unconditional, clamped: a conditional load would force an immediate wait)
   __device__ __forceinline__ void phase() {
 #pragma unroll
     for (int q = 0; q < RJ_PREFETCH; q++)
-      if (uint32_t(q) < pn) reinterpret_cast<uint4 *>(ring)[(pq + q) & (RJ_RING_CHUNKS - 1)] = pf[q];
+      if (uint32_t(q) < pn) {
+        reinterpret_cast<uint4 *>(ring)[cms] = pf[q];
+        cms = cms == RJ_RING_CHUNKS - 1 ? 0 : cms + 1;
+      }
     cm += pn;
     const uint32_t used = cm - (rd >> 2);  // live chunks, incl. the one being read
     const uint32_t room = RJ_RING_CHUNKS - used;
     uint32_t want = nchunks > cm ? nchunks - cm : 0u;
     want = want < room ? want : room;
     pn = want < RJ_PREFETCH ? want : RJ_PREFETCH;
-    pq = cm;
     const uint32_t last = nchunks ? nchunks - 1 : 0;
 #pragma unroll
-    for (int q = 0; q < RJ_PREFETCH; q++) pf[q] = src[pq + q < last ? pq + q : last];
-    nw = ring[rd & (RJ_RING_WORDS - 1)];  // the commit may have landed the read-ahead word
+    for (int q = 0; q < RJ_PREFETCH; q++) pf[q] = src[cm + q < last ? cm + q : last];
+    nw = ring[rdw];  // the commit may have landed the read-ahead word
   }
   __device__ __forceinline__ void refill() {
     if (nb <= 32) {
-      uint32_t w;
-      if ((rd >> 2) < cm) {
-        w = nw;
-      } else if ((rd >> 2) < nchunks) {  // ring ran dry (pathological bit rates): read HBM
-        w = reinterpret_cast<const uint32_t *>(src)[rd];
-      } else {
-        w = 0;  // past the data: zero bits, as libjpeg inserts
-      }
+      const uint32_t w = rd < 4 * cm ? nw : 0u;  // past the data: zero bits, as libjpeg inserts
       acc |= uint64_t(__builtin_bswap32(w)) << (32 - nb);
       nb += 32;
       rd++;
+      rdw = rdw == RJ_RING_WORDS - 1 ? 0 : rdw + 1;
     }
-    nw = ring[rd & (RJ_RING_WORDS - 1)];
+    nw = ring[rdw];
   }
   __device__ __forceinline__ bool overrun(uint32_t nbytes) const {
     return uint64_t(rd) * 32u - uint64_t(nb) > uint64_t(nbytes) * 8u;
   }
 };
 
-// canonical search when the second-level pool is exhausted (libjpeg jpeg_huff_decode); the
-// pathological tables that need it are read from HBM
-__device__ __noinline__ uint32_t huff_slow(const RjHuffDev *t, uint32_t peek16) {
+// canonical search for codes the LDS tables do not resolve (second-level pool exhausted, or a
+// DC code longer than 9 bits): libjpeg jpeg_huff_decode on the table in HBM
+__device__ __forceinline__ uint32_t huff_slow(const RjHuffDev *t, uint32_t peek16) {
   uint32_t e = RJ_LUT_BAD;
-  for (int l = 10; l <= 16; l++)
+  for (int l = 1; l <= 16; l++)
     if (peek16 < t->maxcode16[l]) {
       e = uint32_t(l << 8) | t->vals[((peek16 >> (16 - l)) + t->valoff[l]) & 255];
       break;
     }
   return e;
 }
+
+// LDS table image: DC tables first level only (512 entries each), AC tables both levels
+#define RJ_SLUT_AC0 (2 * RJ_LUT_L1)
+#define RJ_SLUT_ENTRIES (2 * RJ_LUT_L1 + 2 * RJ_LUT_ENTRIES)
 
 __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ imgs, int nimg, uint32_t nseg,
                                                 const uint8_t *__restrict__ destuffed,
@@ -212,7 +218,7 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
   // strides padded by 16 B so the 8-lane groups of ds_*_b128 hit distinct banks
   __shared__ __attribute__((aligned(16))) uint32_t s_ring[64][RJ_RING_WORDS + 4];
   __shared__ __attribute__((aligned(16))) uint32_t s_stage[64][RJ_STAGE + 4];
-  __shared__ __attribute__((aligned(16))) uint16_t s_lut[4][RJ_LUT_ENTRIES];  // dc0, dc1, ac0, ac1
+  __shared__ __attribute__((aligned(16))) uint16_t s_lut[RJ_SLUT_ENTRIES];
   const uint32_t lane = threadIdx.x;
   const uint32_t g = blockIdx.x * 64u + lane;
   const bool valid = g < nseg;
@@ -226,16 +232,23 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
     if (m == 0) break;
     const uint32_t T = __shfl(my_ts, __ffsll((long long)m) - 1, 64);
     __syncthreads();
-    for (uint32_t t = 0; t < 4; t++) {
-      const RjHuffDev *h = t < 2 ? &tabsets[T].dc[t] : &tabsets[T].ac[t - 2];
-      const uint4 *s4 = reinterpret_cast<const uint4 *>(h->lut);
-      uint4 *d4 = reinterpret_cast<uint4 *>(s_lut[t]);
-      for (uint32_t k = lane; k < RJ_LUT_ENTRIES * 2 / 16; k += 64) d4[k] = s4[k];
+    {
+      const RjTableSet &ts = tabsets[T];
+      uint4 *d4 = reinterpret_cast<uint4 *>(s_lut);
+      constexpr uint32_t L1Q = RJ_LUT_L1 * 2 / 16, FQ = RJ_LUT_ENTRIES * 2 / 16;
+      for (uint32_t k = lane; k < 2 * L1Q + 2 * FQ; k += 64) {
+        const uint4 *s4;
+        if (k < L1Q) s4 = reinterpret_cast<const uint4 *>(ts.dc[0].lut) + k;
+        else if (k < 2 * L1Q) s4 = reinterpret_cast<const uint4 *>(ts.dc[1].lut) + (k - L1Q);
+        else if (k < 2 * L1Q + FQ) s4 = reinterpret_cast<const uint4 *>(ts.ac[0].lut) + (k - 2 * L1Q);
+        else s4 = reinterpret_cast<const uint4 *>(ts.ac[1].lut) + (k - 2 * L1Q - FQ);
+        d4[k] = *s4;
+      }
     }
     __syncthreads();
     if (pending && my_ts == T) {
       pending = false;
-      const RjSegDev sg = im.segs[g - im.seg_prefix];
+      const RjSegDev sg = gp(im.segs)[g - im.seg_prefix];
       const uint32_t nblk = im.nblk_mcu, mcux = im.mcux;
       // per block-in-MCU b: component (2 bits) | dc table (1) | ac table (1), 4 bits each
       uint64_t binfo = 0;
@@ -262,68 +275,74 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
       uint32_t b = 0;
       uint32_t info = uint32_t(binfo) & 15u;
       int k = 0;
-      uint32_t iter = 0;
       while (blocks_left > 0) {
-        if ((iter++ & (RJ_PHASE - 1)) == 0) {  // same count in every active lane
-          br.phase();
-          if (ne - fl >= RJ_ENT_GROUP) {  // one full 64-B group leaves the stage
-            const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
-            uint4 *d4 = reinterpret_cast<uint4 *>(ent + fl);
+        // ---- phase boundary (same iteration count in every active lane) ----
+        br.phase();
+        if (ne - fl >= RJ_ENT_GROUP) {  // one full 64-B group leaves the stage
+          const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
+          uint4 *d4 = reinterpret_cast<uint4 *>(ent + fl);
 #pragma unroll
-            for (int q = 0; q < RJ_ENT_GROUP / 4; q++) d4[q] = s4[q];
-            fl += RJ_ENT_GROUP;
-          }
+          for (int q = 0; q < RJ_ENT_GROUP / 4; q++) d4[q] = s4[q];
+          fl += RJ_ENT_GROUP;
         }
-        uint32_t entry;
-        bool emit;
-        if (skip) {  // libjpeg: the rest of the interval decodes to zero blocks
-          entry = 0;
-          emit = true;
-          k = 64;
-        } else {
-          br.refill();
-          const uint32_t c = info & 3u;
-          const uint32_t peek32 = uint32_t(br.acc >> 32);
-          const uint32_t tix = k == 0 ? ((info >> 2) & 1u) : 2u + ((info >> 3) & 1u);
-          uint32_t e = s_lut[tix][peek32 >> 23];
-          if (e & 0x8000u) {
-            if (e != 0xFFFFu) e = s_lut[tix][RJ_LUT_L1 + (e & 0x7Fu) * 128u + ((peek32 >> 16) & 127u)];
-            else e = huff_slow(tix < 2 ? &tabsets[T].dc[tix] : &tabsets[T].ac[tix - 2], peek32 >> 16);
-          }
-          const uint32_t len = e >> 8, sym = e & 255u;
-          const uint32_t s = sym & 15u, r = sym >> 4;
-          // extra bits follow the code inside the same peek (len + s <= 31); width 0 -> 0
-          const uint32_t raw = __builtin_amdgcn_ubfe(peek32, 32u - len - s, s);
-          // HUFF_EXTEND (jdhuff.h): negative when the top extra bit is 0; s == 0 gives 0
-          const int val = int(raw) + (int32_t(raw - (1u << ((s - 1) & 31))) >> 31 & int32_t(1u - (1u << s)));
-          br.acc <<= (len + s);
-          br.nb -= int(len + s);
-          // DC (k == 0): predictor per component (F.2.1.3); AC: run/size (F.2.2.2)
-          const bool isdc = k == 0;
-          const int p = (c == 0 ? pred0 : (c == 1 ? pred1 : pred2)) + val;
-          pred0 = (isdc && c == 0) ? p : pred0;
-          pred1 = (isdc && c == 1) ? p : pred1;
-          pred2 = (isdc && c == 2) ? p : pred2;
-          const int kk = isdc ? 0 : k + int(r);  // zigzag position of this coefficient
-          entry = (uint32_t(isdc ? p : val) & 0xFFFFu) | (uint32_t(kk < 63 ? kk : 63) << 16);
-          emit = isdc || s;
-          k = isdc ? 1 : (s ? kk + 1 : (r == 15 ? k + 16 : 64));  // ZRL / EOB
-        }
-        stage[ne & (RJ_STAGE - 1)] = entry;  // a non-emitted write lands in the next free slot
-        ne += emit ? 1u : 0u;
-        if (k >= 64) {  // block complete
-          k = 0;
-          blocks_left--;
-          if (++b == nblk) {
-            b = 0;
-            if (!skip && br.overrun(nbytes)) skip = true;  // libjpeg: rest of the interval stays zero
-            if (--to_row == 0) {  // the next MCU starts a row
-              to_row = mcux;
-              mrow++;
-              if (blocks_left) coefs.row[row0 + mrow] = sg.ent_off + ne;
+        for (uint32_t j = 0; j < RJ_PHASE && blocks_left > 0; j++) {
+          uint32_t entry;
+          bool emit;
+          if (skip) {  // libjpeg: the rest of the interval decodes to zero blocks
+            entry = 0;
+            emit = true;
+            k = 64;
+          } else {
+            br.refill();
+            const uint32_t c = info & 3u;
+            const uint32_t peek32 = uint32_t(br.acc >> 32);
+            // LDS table base: DC tables (first level only) at 0 / 512, AC tables after them
+            const uint32_t tbase = k == 0 ? ((info >> 2) & 1u) * RJ_LUT_L1
+                                          : RJ_SLUT_AC0 + ((info >> 3) & 1u) * RJ_LUT_ENTRIES;
+            uint32_t e = s_lut[tbase + (peek32 >> 23)];
+            if (e & 0x8000u) {
+              if (e != 0xFFFFu && k != 0) {
+                e = s_lut[tbase + RJ_LUT_L1 + (e & 0x7Fu) * 128u + ((peek32 >> 16) & 127u)];
+              } else {
+                const RjHuffDev *t = k == 0 ? &tabsets[T].dc[(info >> 2) & 1u] : &tabsets[T].ac[(info >> 3) & 1u];
+                e = huff_slow(t, peek32 >> 16);
+              }
             }
+            const uint32_t len = e >> 8, sym = e & 255u;
+            const uint32_t s = sym & 15u, r = sym >> 4;
+            // extra bits follow the code inside the same peek (len + s <= 31); width 0 -> 0
+            const uint32_t raw = __builtin_amdgcn_ubfe(peek32, 32u - len - s, s);
+            // HUFF_EXTEND (jdhuff.h): negative when the top extra bit is 0; s == 0 gives 0
+            const int val = int(raw) + (int32_t(raw - (1u << ((s - 1) & 31))) >> 31 & int32_t(1u - (1u << s)));
+            br.acc <<= (len + s);
+            br.nb -= int(len + s);
+            // DC (k == 0): predictor per component (F.2.1.3); AC: run/size (F.2.2.2)
+            const bool isdc = k == 0;
+            const int p = (c == 0 ? pred0 : (c == 1 ? pred1 : pred2)) + val;
+            pred0 = (isdc && c == 0) ? p : pred0;
+            pred1 = (isdc && c == 1) ? p : pred1;
+            pred2 = (isdc && c == 2) ? p : pred2;
+            const int kk = isdc ? 0 : k + int(r);  // zigzag position of this coefficient
+            entry = (uint32_t(isdc ? p : val) & 0xFFFFu) | (uint32_t(kk < 63 ? kk : 63) << 16);
+            emit = isdc || s;
+            k = isdc ? 1 : (s ? kk + 1 : (r == 15 ? k + 16 : 64));  // ZRL / EOB
           }
-          info = uint32_t(binfo >> (4 * b)) & 15u;
+          stage[ne & (RJ_STAGE - 1)] = entry;  // a non-emitted write lands in the next free slot
+          ne += emit ? 1u : 0u;
+          if (k >= 64) {  // block complete
+            k = 0;
+            blocks_left--;
+            if (++b == nblk) {
+              b = 0;
+              if (!skip && br.overrun(nbytes)) skip = true;  // libjpeg: rest of the interval stays zero
+              if (--to_row == 0) {  // the next MCU starts a row
+                to_row = mcux;
+                mrow++;
+                if (blocks_left) coefs.row[row0 + mrow] = sg.ent_off + ne;
+              }
+            }
+            info = uint32_t(binfo >> (4 * b)) & 15u;
+          }
         }
       }
       // terminator, then everything still staged (whole groups; the slack is reserved)
@@ -442,7 +461,7 @@ __global__ __launch_bounds__(256) void k_output(const RjImageDev *__restrict__ i
         break;
       }
     }
-    dst[x] = v;
+    gp(dst)[x] = v;
   }
 }
 

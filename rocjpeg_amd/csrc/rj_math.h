@@ -6,6 +6,24 @@
 
 namespace rj {
 
+// Global-address-space views of generic pointers.  Pointers read from descriptors are generic,
+// and the backend then emits FLAT memory instructions, which count in lgkmcnt as well as
+// vmcnt: every later s_waitcnt on an LDS read would also wait for those stores to reach
+// memory.  Every global access in the kernels goes through these (global_* instructions).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RJ_GLOBAL __attribute__((address_space(1)))
+#else
+#define RJ_GLOBAL  // host pass of the single-source build: never executed
+#endif
+template <typename T>
+__device__ __forceinline__ RJ_GLOBAL T *gp(T *p) {
+  return (RJ_GLOBAL T *)p;
+}
+template <typename T>
+__device__ __forceinline__ const RJ_GLOBAL T *gp(const T *p) {
+  return (const RJ_GLOBAL T *)p;
+}
+
 // libjpeg ISLOW constants (jidctint.c: CONST_BITS 13, PASS1_BITS 2).  Computed in int32
 // with 24-bit multiplies (v_mul_i32_i24, full rate; v_mul_lo_u32 is quarter rate): exact --
 // i.e. equal to libjpeg's wide arithmetic -- whenever every dequantised coefficient has
