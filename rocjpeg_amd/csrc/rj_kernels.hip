@@ -267,7 +267,7 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
       const uint32_t row0 = im.row_off;
       uint32_t mrow = sg.mcu_first / mcux;
       uint32_t to_row = mcux - (sg.mcu_first - mrow * mcux);  // MCUs until the next row starts
-      if (to_row == mcux) coefs.row[row0 + mrow] = sg.ent_off;
+      if (to_row == mcux) gp(coefs.row)[row0 + mrow] = sg.ent_off;
 
       int pred0 = 0, pred1 = 0, pred2 = 0;
       bool skip = (sg.flags & RJ_SEG_MISSING) != 0;
@@ -275,17 +275,20 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
       uint32_t b = 0;
       uint32_t info = uint32_t(binfo) & 15u;
       int k = 0;
+      uint32_t dcbase = ((info >> 2) & 1u) * RJ_LUT_L1, acbase = RJ_SLUT_AC0 + ((info >> 3) & 1u) * RJ_LUT_ENTRIES;
+      uint32_t iter = 0;
       while (blocks_left > 0) {
-        // ---- phase boundary (same iteration count in every active lane) ----
-        br.phase();
-        if (ne - fl >= RJ_ENT_GROUP) {  // one full 64-B group leaves the stage
-          const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
-          uint4 *d4 = reinterpret_cast<uint4 *>(ent + fl);
+        if ((iter++ & (RJ_PHASE - 1)) == 0) {  // phase boundary: same count in every active lane
+          br.phase();
+          if (ne - fl >= RJ_ENT_GROUP) {  // one full 64-B group leaves the stage
+            const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
+            uint4 *d4 = reinterpret_cast<uint4 *>(ent + fl);
 #pragma unroll
-          for (int q = 0; q < RJ_ENT_GROUP / 4; q++) d4[q] = s4[q];
-          fl += RJ_ENT_GROUP;
+            for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = s4[q];
+            fl += RJ_ENT_GROUP;
+          }
         }
-        for (uint32_t j = 0; j < RJ_PHASE && blocks_left > 0; j++) {
+        {
           uint32_t entry;
           bool emit;
           if (skip) {  // libjpeg: the rest of the interval decodes to zero blocks
@@ -297,8 +300,7 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
             const uint32_t c = info & 3u;
             const uint32_t peek32 = uint32_t(br.acc >> 32);
             // LDS table base: DC tables (first level only) at 0 / 512, AC tables after them
-            const uint32_t tbase = k == 0 ? ((info >> 2) & 1u) * RJ_LUT_L1
-                                          : RJ_SLUT_AC0 + ((info >> 3) & 1u) * RJ_LUT_ENTRIES;
+            const uint32_t tbase = k == 0 ? dcbase : acbase;
             uint32_t e = s_lut[tbase + (peek32 >> 23)];
             if (e & 0x8000u) {
               if (e != 0xFFFFu && k != 0) {
@@ -338,10 +340,12 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
               if (--to_row == 0) {  // the next MCU starts a row
                 to_row = mcux;
                 mrow++;
-                if (blocks_left) coefs.row[row0 + mrow] = sg.ent_off + ne;
+                if (blocks_left) gp(coefs.row)[row0 + mrow] = sg.ent_off + ne;
               }
             }
             info = uint32_t(binfo >> (4 * b)) & 15u;
+            dcbase = ((info >> 2) & 1u) * RJ_LUT_L1;
+            acbase = RJ_SLUT_AC0 + ((info >> 3) & 1u) * RJ_LUT_ENTRIES;
           }
         }
       }
@@ -352,7 +356,7 @@ __global__ __launch_bounds__(64) void k_huffman(const RjImageDev *__restrict__ i
         const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
         uint4 *d4 = reinterpret_cast<uint4 *>(ent + fl);
 #pragma unroll
-        for (int q = 0; q < RJ_ENT_GROUP / 4; q++) d4[q] = s4[q];
+        for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = s4[q];
         fl += RJ_ENT_GROUP;
       }
     }
