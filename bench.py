@@ -178,7 +178,7 @@ def main():
     for _ in range(args.warmup):
         step()
     dec.set_profiling(True)
-    stage = {"destuff_ms": 0.0, "huffman_ms": 0.0, "idct_ms": 0.0, "output_ms": 0.0, "h2d_ms": 0.0}
+    stage = {"host_ms": 0.0, "h2d_ms": 0.0, "destuff_ms": 0.0, "huffman_ms": 0.0, "idct_ms": 0.0, "output_ms": 0.0}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -35,6 +35,7 @@ typedef struct {
   uint64_t coef_bytes;    /* int16 coefficient bytes written by K1 */
   uint64_t output_bytes;  /* bytes written to the caller's buffers */
   uint32_t images, intervals, fused_images;
+  float host_ms;          /* host planning of the call (validation, layout, descriptors), wall clock */
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);

@@ -82,7 +82,8 @@ class RocJpegAmdTimings(ctypes.Structure):
     _fields_ = [("h2d_ms", ctypes.c_float), ("destuff_ms", ctypes.c_float), ("huffman_ms", ctypes.c_float),
                 ("idct_ms", ctypes.c_float), ("output_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
                 ("ecs_bytes", ctypes.c_uint64), ("coef_bytes", ctypes.c_uint64), ("output_bytes", ctypes.c_uint64),
-                ("images", ctypes.c_uint32), ("intervals", ctypes.c_uint32), ("fused_images", ctypes.c_uint32)]
+                ("images", ctypes.c_uint32), ("intervals", ctypes.c_uint32), ("fused_images", ctypes.c_uint32),
+                ("host_ms", ctypes.c_float)]
 
 
 class RocJpegError(RuntimeError):

@@ -2,6 +2,7 @@
 #include "rj_decoder.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 
 #include "rj_common.h"
@@ -174,6 +175,7 @@ int Decoder::Decode(Stream *const *streams, int n, const RocJpegDecodeParams *pa
 }
 
 int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
+  const auto t_host0 = std::chrono::steady_clock::now();
   RJ_HIP(hipSetDevice(device_));
   timings_ = RocJpegAmdTimings();
   if (n == 0) return kOk;
@@ -189,19 +191,30 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   std::vector<uint32_t> tab_of(n);
   std::vector<const RjTableSet *> tabs;
   {
+    std::vector<const DecodePlan *> owner;  // plan whose derived tables tabs[idx] points at
     std::unordered_map<uint64_t, std::vector<uint32_t>> seen;
+    uint32_t last = UINT32_MAX;  // batches are usually one encoder's output: try the last hit first
     for (int i = 0; i < n; i++) {
       const DecodePlan &p = streams[i]->plan();
+      auto same = [&](uint32_t c) {
+        return owner[c] == &p || (owner[c]->table_hash == p.table_hash &&
+                                  std::memcmp(owner[c]->table_key, p.table_key, sizeof(p.table_key)) == 0);
+      };
       uint32_t idx = UINT32_MAX;
-      auto &cands = seen[p.table_hash];
-      for (uint32_t c : cands)
-        if (std::memcmp(tabs[c], &p.tables, sizeof(RjTableSet)) == 0) { idx = c; break; }
-      if (idx == UINT32_MAX) {
-        idx = uint32_t(tabs.size());
-        tabs.push_back(&p.tables);
-        cands.push_back(idx);
+      if (last != UINT32_MAX && same(last)) {
+        idx = last;
+      } else {
+        auto &cands = seen[p.table_hash];
+        for (uint32_t c : cands)
+          if (same(c)) { idx = c; break; }
+        if (idx == UINT32_MAX) {
+          idx = uint32_t(tabs.size());
+          tabs.push_back(&p.tables);
+          owner.push_back(&p);
+          cands.push_back(idx);
+        }
       }
-      tab_of[i] = idx;
+      tab_of[i] = last = idx;
     }
   }
 
@@ -425,6 +438,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const RjTableSet *d_tabs = reinterpret_cast<const RjTableSet *>(dbase + off_tabs);
   const RjJobDev *d_jobs = reinterpret_cast<const RjJobDev *>(dbase + off_jobs);
 
+  timings_.host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
   if (profiling_) RJ_HIP(hipEventRecord(ev_[0], stream_));
   RJ_HIP(hipMemcpyAsync(dbase, h, blob, hipMemcpyHostToDevice, stream_));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));

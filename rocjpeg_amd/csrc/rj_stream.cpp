@@ -284,7 +284,16 @@ void Stream::BuildPlan() {
   }
   for (int q = 0; q < 4; q++)
     for (int k = 0; k < 64; k++) p.tables.qz[q][k] = s.qt_zz[q][k];
-  h = Fnv1a(h, &p.tables, sizeof(p.tables));
+  {
+    static_assert(sizeof(s.ht) == 2 * (16 + 12 + 16 + 162), "raw DHT layout");
+    uint8_t *kp = p.table_key;
+    *kp++ = s.ht_loaded[0];
+    *kp++ = s.ht_loaded[1];
+    std::memcpy(kp, s.ht, sizeof(s.ht));
+    kp += sizeof(s.ht);
+    std::memcpy(kp, s.qt_zz, sizeof(s.qt_zz));
+  }
+  h = Fnv1a(h, p.table_key, sizeof(p.table_key));
   p.table_hash = h;
 
   // Restart-interval table: split the ECS at RSTn markers (FF D0..D7).  Fill FFs in front

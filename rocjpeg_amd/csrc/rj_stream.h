@@ -50,7 +50,11 @@ struct DecodePlan {
   uint64_t destuff_bytes = 0;      // destuffed buffer size incl. per-interval alignment
   uint64_t entries = 0;            // sparse-coefficient entries reserved (worst case)
   RjTableSet tables;               // derived tables
-  uint64_t table_hash = 0;         // de-duplication key for tables
+  // De-duplication key: the raw DHT/DQT content the derived tables are a function of (the
+  // batch planner compares these ~670 B instead of the 14.5 KB RjTableSet) and its hash.
+  static constexpr size_t kTableKeyBytes = 2 + 2 * (16 + 12 + 16 + 162) + 4 * 64;
+  uint8_t table_key[kTableKeyBytes] = {};
+  uint64_t table_hash = 0;
 };
 
 class Stream {
