@@ -178,6 +178,7 @@ def main():
     for _ in range(args.warmup):
         step()
     dec.set_profiling(True)
+    k1 = {}
     stage = {"host_ms": 0.0, "h2d_ms": 0.0, "destuff_ms": 0.0, "huffman_ms": 0.0, "idct_ms": 0.0, "output_ms": 0.0}
     if world > 1:
         dist.barrier()
@@ -189,6 +190,8 @@ def main():
         last = dec.last_timings()
         for k in stage:
             stage[k] += last[k]
+        for k in ("entropy_chunks_ms", "entropy_resolve_ms", "entropy_serial_ms"):
+            k1[k] = k1.get(k, 0.0) + last[k]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -256,6 +259,9 @@ def main():
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "algorithmic_bytes_per_launch": int(algo[dom]), "avg_launch_ms": round(per[dom], 4)},
             "stages_ms_per_step": {k: round(v, 4) for k, v in per.items()},
+            "huffman_detail": dict({k: round(v / K, 4) for k, v in k1.items()}, chunks=last["chunks"],
+                                   intervals=last["intervals"], split_intervals=last["split_intervals"],
+                                   serial_fallbacks=last["serial_fallbacks"]),
             "end_to_end_algorithmic_GBps": round((ecs + outb) / (elapsed / K) / 1e9, 2),
             "host_input_images_per_s_per_gpu": round(host_rate, 1) if host_rate else None,
             "parity_first_image": parity_ok,

@@ -36,6 +36,12 @@ typedef struct {
   uint64_t output_bytes;  /* bytes written to the caller's buffers */
   uint32_t images, intervals, fused_images;
   float host_ms;          /* host planning of the call (validation, layout, descriptors), wall clock */
+  float entropy_chunks_ms;   /* K1 split into its launches: chunk lanes, */
+  float entropy_resolve_ms;  /*   sync resolution, */
+  float entropy_serial_ms;   /*   serial re-decode of intervals whose chunks did not sync */
+  uint32_t chunks;           /* K1 lanes */
+  uint32_t split_intervals;  /* intervals decoded in more than one chunk */
+  uint32_t serial_fallbacks; /* of those, re-decoded serially (counted when profiling) */
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);

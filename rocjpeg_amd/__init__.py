@@ -83,7 +83,10 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("idct_ms", ctypes.c_float), ("output_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
                 ("ecs_bytes", ctypes.c_uint64), ("coef_bytes", ctypes.c_uint64), ("output_bytes", ctypes.c_uint64),
                 ("images", ctypes.c_uint32), ("intervals", ctypes.c_uint32), ("fused_images", ctypes.c_uint32),
-                ("host_ms", ctypes.c_float)]
+                ("host_ms", ctypes.c_float), ("entropy_chunks_ms", ctypes.c_float),
+                ("entropy_resolve_ms", ctypes.c_float), ("entropy_serial_ms", ctypes.c_float),
+                ("chunks", ctypes.c_uint32), ("split_intervals", ctypes.c_uint32),
+                ("serial_fallbacks", ctypes.c_uint32)]
 
 
 class RocJpegError(RuntimeError):

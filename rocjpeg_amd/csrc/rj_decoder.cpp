@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "rj_common.h"
@@ -222,7 +224,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   std::vector<RjImageDev> imgs(n);
   std::vector<RjJobDev> jobs;
   uint64_t destuff_total = 0, coef_blocks = 0, ent_total = 0, plane_bytes = 0, stage_bytes = 0;
-  uint32_t seg_total = 0, rows_total = 0, mcu_rows = 0;
+  uint32_t seg_total = 0, rows_total = 0, chunk_total = 0;
   uint64_t ecs_bytes = 0, out_bytes = 0;
   std::vector<uint64_t> stage_off(n, UINT64_MAX);
   std::vector<uint32_t> row_prefix(n), grow_prefix(n);  // K2 rows: fused images / general images
@@ -265,8 +267,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     d.ent_off = ent_total;
     ent_total += AlignUp(p.entries, RJ_ENT_GROUP);
     d.ri_mcus = in.restart_interval;
-    d.row_off = mcu_rows;
-    mcu_rows += p.mcuy;
+    d.chunk_prefix = chunk_total;
+    chunk_total += p.nchunks;
     for (int c = 0; c < in.ncomp; c++) {
       d.plane_pitch[c] = p.wblk[c] * 8;
       d.plane_rows[c] = p.hblk[c] * 8;
@@ -390,23 +392,79 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
   }
 
+  // ---- K1 lane layout (rj_device.h RjCoefBuf): one lane per chunk; an interval of at most
+  // RJ_K1_WG chunks never straddles a workgroup (padding lanes), longer ones go after them ----
+  std::vector<uint32_t> seg_lane0(seg_total);
+  uint32_t lanes_wg = 0, split_intervals = 0;
+  {
+    uint32_t gs = 0;
+    for (int i = 0; i < n; i++)
+      for (const RjSegDev &sg : streams[i]->plan().segs) {
+        const uint32_t nch = rj_chunks(sg.src_len);
+        split_intervals += nch > 1 ? 1u : 0u;
+        if (nch <= RJ_K1_WG) {
+          if (lanes_wg % RJ_K1_WG + nch > RJ_K1_WG) lanes_wg = AlignUp(lanes_wg, RJ_K1_WG);
+          seg_lane0[gs] = lanes_wg;
+          lanes_wg += nch;
+        } else {
+          seg_lane0[gs] = UINT32_MAX;
+        }
+        gs++;
+      }
+  }
+  lanes_wg = uint32_t(AlignUp(lanes_wg, RJ_K1_WG));
+  uint32_t lanes_all = lanes_wg;
+  {
+    uint32_t gs = 0;
+    for (int i = 0; i < n; i++)
+      for (const RjSegDev &sg : streams[i]->plan().segs) {
+        if (seg_lane0[gs] == UINT32_MAX) {
+          seg_lane0[gs] = lanes_all;
+          lanes_all += rj_chunks(sg.src_len);
+        }
+        gs++;
+      }
+  }
+  const uint32_t lanes_dev = lanes_all - lanes_wg;
+  std::vector<uint32_t> lane_seg(lanes_all, UINT32_MAX);
+  {
+    uint32_t gs = 0;
+    for (int i = 0; i < n; i++)
+      for (const RjSegDev &sg : streams[i]->plan().segs) {
+        const uint32_t nch = rj_chunks(sg.src_len);
+        for (uint32_t q = 0; q < nch; q++) lane_seg[seg_lane0[gs] + q] = gs;
+        gs++;
+      }
+  }
+
   // ---- one host->device upload: descriptors + non-resident bitstreams ----
   const uint64_t off_imgs = 0;
   const uint64_t off_tabs = AlignUp(off_imgs + n * sizeof(RjImageDev), 256);
   const uint64_t off_jobs = AlignUp(off_tabs + tabs.size() * sizeof(RjTableSet), 256);
   const uint64_t off_rows = AlignUp(off_jobs + std::max<size_t>(jobs.size(), 1) * sizeof(RjJobDev), 256);
   const uint64_t off_grows = AlignUp(off_rows + n * sizeof(uint32_t), 256);
-  const uint64_t off_stage = AlignUp(off_grows + n * sizeof(uint32_t), 256);
+  const uint64_t off_lane_seg = AlignUp(off_grows + n * sizeof(uint32_t), 256);
+  const uint64_t off_seg_lane0 = AlignUp(off_lane_seg + uint64_t(lanes_all) * 4, 256);
+  const uint64_t off_stage = AlignUp(off_seg_lane0 + uint64_t(seg_total) * 4, 256);
   const uint64_t blob = off_stage + stage_bytes;
   RJ_CHECK(h_stage_.Ensure(blob));
   RJ_CHECK(d_desc_.Ensure(blob));
   RJ_CHECK(d_destuff_.Ensure(std::max<uint64_t>(destuff_total, 256)));
   RJ_CHECK(d_seglen_.Ensure(std::max<uint64_t>(uint64_t(seg_total) * 4, 256)));
-  RJ_CHECK(d_rowidx_.Ensure(std::max<uint64_t>(uint64_t(mcu_rows) * 4, 256)));
+  RJ_CHECK(d_piece_.Ensure(std::max<uint64_t>(uint64_t(lanes_all) * sizeof(RjPiece), 256)));
+  RJ_CHECK(d_rec_.Ensure(std::max<uint64_t>(uint64_t(lanes_all) * RJ_MAX_RECORDS * sizeof(RjRecord), 256)));
+  RJ_CHECK(d_chunkres_.Ensure(std::max<uint64_t>(uint64_t(lanes_all) * sizeof(RjChunkRes), 256)));
+  RJ_CHECK(d_fallback_.Ensure(std::max<uint64_t>(uint64_t(seg_total) * 4, 256)));
   RJ_CHECK(d_entries_.Ensure((ent_total + RJ_ENT_SLACK) * 4));
   RjCoefBuf cbuf;
   cbuf.ent = d_entries_.as<uint32_t>();
-  cbuf.row = d_rowidx_.as<uint32_t>();
+  cbuf.piece = d_piece_.as<RjPiece>();
+  cbuf.rec = d_rec_.as<RjRecord>();
+  cbuf.res = d_chunkres_.as<RjChunkRes>();
+  cbuf.fallback = d_fallback_.as<uint32_t>();
+  // records persist across calls: a per-call epoch (28 bits, never 0) tells this call's apart
+  epoch_ = (epoch_ + 1) & 0x0FFFFFFFu;
+  if (epoch_ == 0) epoch_ = 1;
   RJ_CHECK(d_planes_.Ensure(std::max<uint64_t>(plane_bytes, 256)));
   uint8_t *h = h_stage_.data();
   uint8_t *dbase = d_desc_.as<uint8_t>();
@@ -431,6 +489,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (!jobs.empty()) std::memcpy(h + off_jobs, jobs.data(), jobs.size() * sizeof(RjJobDev));
   std::memcpy(h + off_rows, row_prefix.data(), n * sizeof(uint32_t));
   std::memcpy(h + off_grows, grow_prefix.data(), n * sizeof(uint32_t));
+  std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(lanes_all) * 4);
+  std::memcpy(h + off_seg_lane0, seg_lane0.data(), uint64_t(seg_total) * 4);
+  cbuf.lane_seg = reinterpret_cast<const uint32_t *>(dbase + off_lane_seg);
+  cbuf.seg_lane0 = reinterpret_cast<const uint32_t *>(dbase + off_seg_lane0);
   const uint32_t *d_rows = reinterpret_cast<const uint32_t *>(dbase + off_rows);
   const uint32_t *d_grows = reinterpret_cast<const uint32_t *>(dbase + off_grows);
 
@@ -444,8 +506,11 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
   RJ_HIP(LaunchDestuff(stream_, d_imgs, n, seg_total, d_destuff_.as<uint8_t>(), d_seglen_.as<uint32_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[2], stream_));
-  RJ_HIP(LaunchHuffman(stream_, d_imgs, n, seg_total, d_destuff_.as<uint8_t>(), d_seglen_.as<uint32_t>(), d_tabs,
-                       cbuf));
+  for (int stage = 0; stage < 3; stage++) {
+    RJ_HIP(LaunchEntropy(stream_, stage, d_imgs, n, lanes_wg, lanes_dev, seg_total, d_destuff_.as<uint8_t>(),
+                        d_seglen_.as<uint32_t>(), d_tabs, cbuf, epoch_));
+    if (profiling_ && stage < 2) RJ_HIP(hipEventRecord(ev_[6 + stage], stream_));
+  }
   if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
   RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, fused_rows, cbuf, d_tabs, nullptr));
   RJ_HIP(LaunchRows(stream_, true, d_imgs, n, d_grows, general_rows, cbuf, d_tabs, d_planes_.as<uint8_t>()));
@@ -456,6 +521,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
 
   timings_.images = uint32_t(n);
   timings_.intervals = seg_total;
+  timings_.chunks = lanes_all;
+  timings_.split_intervals = split_intervals;
   timings_.ecs_bytes = ecs_bytes;
   timings_.coef_bytes = coef_blocks * 128;  // dense-equivalent; the sparse bytes are data-dependent
   timings_.output_bytes = out_bytes;
@@ -469,6 +536,53 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     timings_.idct_ms = ms[3];
     timings_.output_ms = ms[4];
     RJ_HIP(hipEventElapsedTime(&timings_.total_ms, ev_[0], ev_[5]));
+    RJ_HIP(hipEventElapsedTime(&timings_.entropy_chunks_ms, ev_[2], ev_[6]));
+    RJ_HIP(hipEventElapsedTime(&timings_.entropy_resolve_ms, ev_[6], ev_[7]));
+    RJ_HIP(hipEventElapsedTime(&timings_.entropy_serial_ms, ev_[7], ev_[3]));
+    std::vector<uint32_t> fb(seg_total);
+    RJ_HIP(hipMemcpy(fb.data(), d_fallback_.as<uint32_t>(), fb.size() * 4, hipMemcpyDeviceToHost));
+    for (uint32_t f : fb) timings_.serial_fallbacks += f ? 1u : 0u;
+    if (getenv("RJ_DEBUG_K1")) {  // development diagnostics of the chunked decode
+      std::vector<RjChunkRes> cr(lanes_all);
+      RJ_HIP(hipMemcpy(cr.data(), d_chunkres_.as<RjChunkRes>(), cr.size() * sizeof(RjChunkRes), hipMemcpyDeviceToHost));
+      double sum_ov = 0, sum_it = 0;
+      uint32_t nsync = 0, ndone = 0, nfail = 0, max_ov = 0, max_it = 0;
+      uint32_t hist[8] = {};
+      for (const RjChunkRes &r : cr) {
+        if (r.status == RJ_CHUNK_SYNC) {
+          nsync++;
+          const uint32_t ov = r.pad[0] - r.pad[1];
+          sum_ov += ov;
+          max_ov = std::max(max_ov, ov);
+          int h = 0;
+          while (h < 7 && (256u << h) <= ov) h++;
+          hist[h]++;
+        } else if (r.status == RJ_CHUNK_DONE) {
+          ndone++;
+        } else if (r.status == RJ_CHUNK_FAIL) {
+          nfail++;
+        }
+        if (r.status) { sum_it += r.pad[2]; max_it = std::max(max_it, r.pad[2]); }
+      }
+      fprintf(stderr, "[K1] sync %u done %u fail %u | overlap bits mean %.0f max %u | hist(<256<<h):", nsync, ndone,
+              nfail, nsync ? sum_ov / nsync : 0.0, max_ov);
+      for (int h = 0; h < 8; h++) fprintf(stderr, " %u", hist[h]);
+      fprintf(stderr, " | iters mean %.0f max %u\n", (nsync + ndone) ? sum_it / (nsync + ndone) : 0.0, max_it);
+      if (n == 1 && getenv("RJ_DEBUG_K1_PIECES")) {  // one image: its first interval's pieces and chunks
+        const uint32_t l0 = seg_lane0[0], nch = rj_chunks(streams[0]->plan().segs[0].src_len);
+        std::vector<RjPiece> pc(nch);
+        RJ_HIP(hipMemcpy(pc.data(), d_piece_.as<RjPiece>() + l0, nch * sizeof(RjPiece), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[K1] seg0 lanes %u.. nch %u npieces %u\n", l0, nch, pc[0].npieces);
+        for (uint32_t q = 0; q < std::min<uint32_t>(pc[0].npieces, nch); q++)
+          fprintf(stderr, "  piece %u: ent %llu first %u n %u dcd %d %d %d\n", q, (unsigned long long)pc[q].ent,
+                  pc[q].first_blk, pc[q].nblk, pc[q].dcd[0], pc[q].dcd[1], pc[q].dcd[2]);
+        for (uint32_t c = 0; c < nch; c++) {
+          const RjChunkRes &r = cr[l0 + nch - 1 - c];
+          fprintf(stderr, "  chunk %u: st %u tgt %u rec %u rb %u ne %u stop %u end %u\n", c, r.status, r.tgt, r.rec,
+                  r.rb, r.ne, r.pad[0], r.pad[1]);
+        }
+      }
+    }
   }
   return kOk;
 }

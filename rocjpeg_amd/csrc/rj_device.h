@@ -6,12 +6,11 @@
 //   tabsets[]  RjTableSet          de-duplicated Huffman LUTs + natural-order quant tables
 //   segs       RjSegDev per image  restart intervals (resident with the stream's ECS bytes)
 //   destuffed  u8                  byte-unstuffed entropy data, each interval 16-B aligned
-//   entries    uint32              sparse coefficients (K1 -> K2): per restart interval one
-//                                  stream, per block its DC entry (zigzag pos 0, absolute value)
-//                                  then its nonzero AC entries; a terminator (pos 127) after the
-//                                  interval's last block.  Region per interval sized for the
-//                                  worst case (64 entries per block), 64-B aligned.
-//   row index  uint32 per MCU row  entry index (image-relative) of the row's first block
+//   entries    uint32              sparse coefficients (K1 -> K2): per K1 chunk one stream,
+//                                  per block its DC entry (zigzag pos 0) then its nonzero AC
+//                                  entries, a terminator (pos 127) at the end; regions sized
+//                                  for the worst case, 64-B aligned (RjCoefBuf)
+//   pieces     RjPiece per chunk   which part of which stream holds which blocks
 //   planes     u8                  per component, padded to the MCU grid (general path only)
 #pragma once
 #include <hip/hip_runtime.h>  // uint2/uint4 vector types (all users are built with hipcc)
@@ -29,18 +28,85 @@ __host__ __device__ inline uint32_t rj_fused_strip_mcus(uint32_t hmax, uint32_t 
 }
 
 // Sparse coefficient storage written by K1 and read by K2 (rj_fused.hip).
-//   entry = uint16 value | zigzag position << 16 (positions 0..63; RJ_ENT_TERM ends an interval)
+//   entry = uint16 value | zigzag position << 16 (positions 0..63; RJ_ENT_TERM ends a stream)
+// K1 decodes every restart interval in one or more chunks (one lane each, see rj_entropy.hip);
+// each chunk writes its own entry stream.  The pieces say which part of which stream is valid:
+// piece j of an interval covers `nblk` blocks starting at the interval's block `first_blk`,
+// read from entry `ent` (absolute index into `ent`) with `dcd` added to its DC values.
+struct RjPiece {
+  uint64_t ent;
+  uint32_t first_blk, nblk;
+  uint32_t npieces;  // valid in the interval's first piece
+  int32_t dcd[3];
+};
+// chunk-start record (speculative lanes): block start at bit `pos` of the interval, block
+// within the MCU in tag bits 0..3, call epoch in tag bits 4..31 (records persist across calls)
+struct RjRecord {
+  uint32_t pos, tag, ne, rb;  // ne: entries written before this block, rb: blocks before it
+  int32_t pred[3];
+  uint32_t pad;
+};
+// what a chunk's lane found when it stopped
+struct RjChunkRes {
+  uint32_t status;           // RJ_CHUNK_*
+  uint32_t tgt, rec;         // SYNC: later chunk (interval-relative) and its record index
+  uint32_t rb, ne;           // blocks / entries this lane produced before the stop point
+  int32_t pred[3];           // its (chunk-relative) DC predictors at the stop point
+  uint32_t rb_over;          // first block that read past the data (UINT32_MAX: none)
+  uint32_t pad[3];
+};
+#define RJ_CHUNK_SYNC 1u      // reached a block start recorded by a later chunk with equal state
+#define RJ_CHUNK_DONE 2u      // reached the end of the interval's data
+#define RJ_CHUNK_FAIL 3u      // overlap or capacity exhausted: interval re-decoded serially
+// K1 lanes: one per chunk, laid out per call by the host so that an interval of at most RJ_K1_WG
+// chunks never straddles a workgroup (its lanes exchange chunk-start records through the CU's
+// caches); longer intervals go to a second lane space whose records are exchanged device-wide.
+// Within an interval the chunks run in reverse lane order (chunk c at lane seg_lane0 + nch-1-c).
+#define RJ_K1_WG 256
 struct RjCoefBuf {
-  uint32_t *ent;  // entry streams, one region per interval (image.ent_off + seg.ent_off)
-  uint32_t *row;  // per MCU row (image.row_off + my): first entry of the row, image-relative
+  uint32_t *ent;              // entry streams
+  RjPiece *piece;             // per lane; the interval's pieces start at its seg_lane0
+  RjRecord *rec;              // per lane: RJ_MAX_RECORDS records
+  RjChunkRes *res;            // per lane
+  uint32_t *fallback;         // per interval (batch index): 1 = decode serially
+  const uint32_t *lane_seg;   // per lane: batch interval index (0xFFFFFFFF: padding)
+  const uint32_t *seg_lane0;  // per interval: its first lane
 };
 #define RJ_ENT_PER_BLOCK 64       // worst case: DC + 63 AC (each position written at most once)
 #define RJ_ENT_GROUP 16           // K1 writes entries in 64-B groups; regions are group-aligned
-#define RJ_ENT_TERM (127u << 16)  // end-of-interval marker
+#define RJ_ENT_TERM (127u << 16)  // end-of-stream marker
 #define RJ_ENT_SLACK 1024         // entries of read slack after the last region (K2 reads 512-entry windows)
-// entries reserved for an interval of `blocks` blocks: worst case + terminator, group-aligned
-__host__ __device__ inline uint64_t rj_interval_entries(uint64_t blocks) {
-  return (blocks * RJ_ENT_PER_BLOCK + 1 + RJ_ENT_GROUP - 1) / RJ_ENT_GROUP * RJ_ENT_GROUP;
+#define RJ_MAX_RECORDS 64         // chunk-start records per speculative chunk
+#define RJ_RECORD_EVERY 8         // one record every 8th block start of a chunk's head
+
+// Chunking of an interval of `bytes` raw entropy-coded bytes: about RJ_CHUNK_BYTES per lane;
+// intervals below two chunks are decoded by one lane with the exact serial semantics.
+#define RJ_CHUNK_BYTES 8192u
+#define RJ_OVERLAP_CHUNKS 3u      // a lane may decode this many chunk lengths past its own end
+#define RJ_CHUNK_ENT_PER_BYTE 4u  // region budget of a chunk lane (typical ~1.7); overflow -> serial path
+__host__ __device__ inline uint32_t rj_chunks(uint32_t bytes) {
+  const uint32_t n = (bytes + RJ_CHUNK_BYTES / 2) / RJ_CHUNK_BYTES;
+  return n < 2 ? 1u : (n > 4096 ? 4096u : n);
+}
+// chunk length in bytes (16-B multiple); chunk c covers [c*len, min((c+1)*len, bytes))
+__host__ __device__ inline uint32_t rj_chunk_len(uint32_t bytes, uint32_t nch) {
+  return ((bytes + nch - 1) / nch + 15u) & ~15u;
+}
+__host__ __device__ inline uint64_t rj_group(uint64_t n) { return (n + RJ_ENT_GROUP - 1) / RJ_ENT_GROUP * RJ_ENT_GROUP; }
+// entry region of one chunk of a split interval: a lane decodes at most its chunk +
+// RJ_OVERLAP_CHUNKS more; it stops (and the interval goes to the serial path) before it would
+// overflow.  The regions of an interval together hold its serial decode (>= 8 entries/byte).
+__host__ __device__ inline uint64_t rj_chunk_cap(uint32_t clen) {
+  return rj_group(uint64_t(RJ_CHUNK_ENT_PER_BYTE) * clen * (1 + RJ_OVERLAP_CHUNKS) + 2 * RJ_ENT_PER_BLOCK);
+}
+// entries reserved for an interval: one serial stream (zero-bit decode of the last MCU after
+// the data ends, then one zero DC entry per skipped block), or the chunk regions of a split one
+// (their sum also holds the serial re-decode of a failed split interval)
+__host__ __device__ inline uint64_t rj_interval_entries(uint32_t bytes, uint64_t blocks, uint32_t nblk_mcu) {
+  const uint32_t nch = rj_chunks(bytes);
+  if (nch == 1) return rj_group(8ull * bytes + blocks + uint64_t(nblk_mcu) * RJ_ENT_PER_BLOCK + 1);
+  return uint64_t(nch) * rj_chunk_cap(rj_chunk_len(bytes, nch)) +
+         rj_group(blocks + uint64_t(nblk_mcu) * RJ_ENT_PER_BLOCK + 1);
 }
 
 // One restart interval of one image (host parser rj_stream.cpp builds these).
@@ -51,8 +117,8 @@ struct RjSegDev {
   uint32_t mcu_first;  // first MCU of the interval
   uint32_t mcu_count;  // MCUs in the interval
   uint32_t flags;      // RJ_SEG_MISSING: marker not found -> interval decodes to zero blocks
-  uint32_t ent_off;    // first sparse-coefficient entry of the interval, relative to image.ent_off
-  uint32_t pad;
+  uint32_t ent_off;    // first entry of the interval's region(s), relative to image.ent_off
+  uint32_t chunk0;     // image-relative chunk count before this interval (rj_chunks(src_len) each)
 };
 #define RJ_SEG_MISSING 1u
 
@@ -121,7 +187,7 @@ struct RjImageDev {
   uint64_t destuff_off;  // into the destuffed buffer
   uint64_t ent_off;      // in entries (sparse coefficients), group-aligned
   uint32_t ri_mcus;      // MCUs per restart interval (0: one interval)
-  uint32_t row_off;      // first MCU row of this image in the batch's row index
+  uint32_t chunk_prefix; // exclusive prefix of K1 chunks over the batch (unpadded)
   // component planes (general path)
   uint64_t plane_off[4];
   uint32_t plane_pitch[4], plane_rows[4];

@@ -1,0 +1,557 @@
+// rj_entropy.hip -- K1: baseline Huffman entropy decode (T.81 F.2.2, libjpeg jdhuff.c semantics).
+//
+// The reference hands this step to VCN (src/rocjpeg_vaapi_decoder.cpp:677-689).  Here every
+// restart interval is decoded by one or more lanes:
+//
+//   * short intervals (< 2 chunks of RJ_CHUNK_BYTES): one lane, exact serial semantics --
+//     libjpeg's "insufficient data" rule (the MCU that runs past the data is decoded with zero
+//     bits, the rest of the interval is zero) and missing-RST intervals;
+//   * long intervals (long DRI, or no DRI at all -- every reference fixture): one lane per
+//     chunk.  Chunk 0 starts in the true state; chunk c > 0 starts speculatively at its first
+//     bit, as if a Y block began there, and records its state at every 4th block start of its
+//     head.  Huffman codes self-synchronise: a lane that runs past its own end compares its
+//     (true) state at each block start with the records of the chunk it has entered and stops
+//     at the first equal state -- from there on both decodes are identical.  k_resolve chains
+//     the sync points into pieces (which part of which chunk stream holds which blocks, and
+//     the DC-predictor correction of each piece); an interval whose chunks did not sync within
+//     RJ_OVERLAP_CHUNKS, or whose data ends before its blocks (truncated stream), is decoded
+//     again serially by k_entropy<true>.  Chunks are laid out in reverse order over the lanes,
+//     so the chunk a lane has to read records from was dispatched no later than itself.
+//
+// Per lane everything on the per-symbol dependency chain stays on-chip:
+//   * bits: 64-bit MSB-first buffer refilled 32 bits at a time from a per-lane LDS ring of the
+//     destuffed bytes (read one symbol ahead); the ring is topped up from HBM at wave-uniform
+//     phase boundaries with loads issued one phase before they are committed -- the symbol
+//     loop itself never reads HBM (a conditional global load there costs a vmcnt(0) round trip);
+//   * lookup: two-level LUT in LDS (9-bit first level + 7-bit second level, rj_device.h), one
+//     copy per workgroup of 4 waves; the extra bits come from the same 32-bit peek;
+//   * output: per-lane LDS stage, 64-B groups written at phase boundaries.
+#include <hip/hip_runtime.h>
+
+#include "rj_device.h"
+#include "rj_kernels.h"
+#include "rj_math.h"
+
+namespace rj {
+
+#define RJ_RING_CHUNKS 6   // 16-B chunks per lane in the bit ring (96 B)
+#define RJ_RING_WORDS (RJ_RING_CHUNKS * 4)
+#define RJ_PHASE 8         // symbols per phase: <= 8 ring words consumed (<= 31 bits/symbol)
+#define RJ_PREFETCH 2      // chunks fetched per phase at most
+#define RJ_STAGE 32        // staged entries per lane (two 64-B groups)
+#define RJ_WG 256          // 4 waves share one LDS copy of the tables
+// Ring invariant: after every phase commit the ring holds >= 8 unread words (or all that is
+// left).  With U unread words a phase prefetches n = min(2, 6 - used) chunks and consumes at
+// most 8 words: U >= 16 keeps U' >= 8; 8 <= U < 16 means used <= 4, so n = 2 and U' = U.
+
+struct BitReader {
+  const uint4 *src;   // 16-B aligned destuffed bytes (from the lane's start), zero-padded
+  uint32_t *ring;     // this lane's LDS ring (RJ_RING_WORDS words)
+  uint32_t nchunks;   // 16-B chunks holding data
+  uint32_t rd;        // words moved into the bit buffer (monotonic)
+  uint32_t rdw;       // rd mod RJ_RING_WORDS
+  uint32_t cm;        // chunks committed to the ring (monotonic)
+  uint32_t cms;       // cm mod RJ_RING_CHUNKS
+  uint32_t nw;        // ring word rd, read ahead
+  int nb;             // valid bits in acc (left-justified)
+  uint64_t acc;
+
+  __device__ __forceinline__ void init(const uint4 *s, uint32_t *r, uint32_t nbytes) {
+    src = s;
+    ring = r;
+    nchunks = (nbytes + 15) / 16;
+    const uint32_t first = nchunks < RJ_RING_CHUNKS ? nchunks : RJ_RING_CHUNKS;
+    for (uint32_t q = 0; q < first; q++) reinterpret_cast<uint4 *>(ring)[q] = gp(src)[q];
+    cm = first;
+    cms = first == RJ_RING_CHUNKS ? 0 : first;
+    rd = 0;
+    rdw = 0;
+    nw = ring[0];
+    nb = 0;
+    acc = 0;
+  }
+  // Phase start: issue the loads of up to RJ_PREFETCH chunks (unconditional, clamped: a
+  // conditional load would force an immediate wait).  Phase end: commit them to the ring.
+  // The loaded registers live only inside one phase (no loop-carried copy of an in-flight
+  // load, which would make the compiler wait for it at once).
+  __device__ __forceinline__ uint32_t issue(uint4 &pf0, uint4 &pf1) const {
+    static_assert(RJ_PREFETCH == 2, "two prefetch registers");
+    const uint32_t used = cm - (rd >> 2);  // live chunks, incl. the one being read
+    const uint32_t room = RJ_RING_CHUNKS - used;
+    uint32_t want = nchunks > cm ? nchunks - cm : 0u;
+    want = want < room ? want : room;
+    const uint32_t n = want < RJ_PREFETCH ? want : RJ_PREFETCH;
+    const uint32_t last = nchunks ? nchunks - 1 : 0;
+    pf0 = gp(src)[cm < last ? cm : last];
+    pf1 = gp(src)[cm + 1 < last ? cm + 1 : last];
+    return n;
+  }
+  __device__ __forceinline__ void commit(const uint4 &pf0, const uint4 &pf1, uint32_t n) {
+    uint4 *r4 = reinterpret_cast<uint4 *>(ring);
+    if (n > 0) {
+      r4[cms] = pf0;
+      cms = cms == RJ_RING_CHUNKS - 1 ? 0 : cms + 1;
+    }
+    if (n > 1) {
+      r4[cms] = pf1;
+      cms = cms == RJ_RING_CHUNKS - 1 ? 0 : cms + 1;
+    }
+    cm += n;
+    nw = ring[rdw];  // the commit may have landed the read-ahead word
+  }
+  __device__ __forceinline__ void refill() {  // branch-free
+    const bool need = nb <= 32;
+    const uint32_t w = (need && rd < 4 * cm) ? nw : 0u;  // past the data: zero bits, as libjpeg inserts
+    acc |= uint64_t(__builtin_bswap32(w)) << ((32 - nb) & 63);
+    nb += need ? 32 : 0;
+    rd += need ? 1u : 0u;
+    rdw = need ? (rdw == RJ_RING_WORDS - 1 ? 0 : rdw + 1) : rdw;
+    nw = ring[rdw];
+  }
+  __device__ __forceinline__ uint32_t consumed() const { return rd * 32u - uint32_t(nb); }  // bits
+};
+
+// canonical search for codes the LDS tables do not resolve (second-level pool exhausted, or a
+// DC code longer than 9 bits): libjpeg jpeg_huff_decode on the table in HBM
+__device__ __forceinline__ uint32_t huff_slow(const RjHuffDev *t, uint32_t peek16) {
+  uint32_t e = RJ_LUT_BAD;
+  for (int l = 1; l <= 16; l++)
+    if (peek16 < t->maxcode16[l]) {
+      e = uint32_t(l << 8) | t->vals[((peek16 >> (16 - l)) + t->valoff[l]) & 255];
+      break;
+    }
+  return e;
+}
+
+// LDS table image: DC tables first level only (512 entries each), AC tables both levels
+#define RJ_SLUT_AC0 (2 * RJ_LUT_L1)
+#define RJ_SLUT_ENTRIES (2 * RJ_LUT_L1 + 2 * RJ_LUT_ENTRIES)
+
+__device__ __forceinline__ uint64_t rec_key(uint32_t pos, uint32_t b, uint32_t epoch) {
+  return uint64_t(pos) | (uint64_t((b & 15u) | (epoch << 4)) << 32);
+}
+// Publish a chunk-start record.  The reader only looks at the 8-B key {pos, tag}; k_resolve
+// reads the rest after the kernel.  Workgroup scope: one 16-B store into the CU's coherent
+// cache level; agent scope: the key as a device-coherent atomic.
+template <int kScope>
+__device__ __forceinline__ void put_record(RjRecord *r, uint32_t pos, uint32_t b, uint32_t epoch, uint32_t ne,
+                                           uint32_t rb, int p0, int p1, int p2) {
+  *gp(reinterpret_cast<int4 *>(&r->pred[0])) = make_int4(p0, p1, p2, 0);
+  if (kScope == __HIP_MEMORY_SCOPE_WORKGROUP) {
+    *gp(reinterpret_cast<uint4 *>(r)) = make_uint4(pos, (b & 15u) | (epoch << 4), ne, rb);
+  } else {
+    *gp(reinterpret_cast<uint2 *>(&r->ne)) = make_uint2(ne, rb);
+    __hip_atomic_store(reinterpret_cast<uint64_t *>(r), rec_key(pos, b, epoch), __ATOMIC_RELAXED, kScope);
+  }
+}
+
+// The decode of one lane.  kSplit: speculative/seek chunk of a long interval (stops at a sync
+// point or the end of the data); else exact serial decode of a whole interval.
+struct LaneJob {
+  const uint4 *src;    // destuffed bytes from the lane's first byte
+  uint32_t bytes;      // bytes available from there to the end of the interval's data
+  uint32_t start_bit;  // interval bit position of the lane's first bit
+  uint32_t end_bit;    // interval bit position where the lane's own chunk ends (split)
+  uint32_t ov_bit;     // give-up point (split)
+  uint32_t nbits;      // interval data bits
+  uint32_t blocks;     // exact: blocks of the interval
+  uint32_t *ent;       // the lane's entry region
+  uint32_t cap;        // its capacity (split)
+  bool missing;        // exact: RST marker missing -> all blocks zero
+  bool spec;           // split, c > 0: write chunk-start records
+  RjRecord *rec;       // this chunk's records
+  const RjRecord *rec_next;  // records of chunk c+1 (chunk c+t at rec_next - (t-1) lanes: reverse order)
+  uint32_t next_chunks;      // chunks after this one
+  uint32_t clen_bits;
+  // exact lanes: pieces at MCU-row checkpoints, so that K2 finds any row without a long skip
+  RjPiece *pieces;     // the interval's piece slots
+  uint32_t slots;      // how many
+  uint64_t ent_abs;    // absolute entry index of J.ent
+  uint32_t mcux, mcu_first, mcu_count;
+};
+
+template <bool kSplit, int kScope>
+__device__ __forceinline__ void decode_lane(const LaneJob &J, uint64_t binfo, uint32_t nblk, uint32_t epoch,
+                                            const uint16_t *s_lut, const RjTableSet *ts, uint32_t *ring,
+                                            uint32_t *stage, RjChunkRes *res) {
+  BitReader br;
+  br.init(J.src, ring, J.bytes);
+  uint32_t ne = 0, fl = 0;  // entries produced / flushed (fl multiple of RJ_ENT_GROUP)
+  int pred0 = 0, pred1 = 0, pred2 = 0;
+  bool skip = J.missing;
+  uint32_t blocks_left = kSplit ? 0xFFFFFFFFu : J.blocks;
+  uint32_t b = 0;
+  uint32_t info = uint32_t(binfo) & 15u;
+  uint32_t dcbase = ((info >> 2) & 1u) * RJ_LUT_L1, acbase = RJ_SLUT_AC0 + ((info >> 3) & 1u) * RJ_LUT_ENTRIES;
+  int k = 0;
+  // split-lane state
+  uint32_t rb = 0;                 // blocks completed
+  uint32_t nrec = 0;
+  uint32_t tgt = 0, j = 0;         // chunk (relative to this one, 1-based) and record being sought
+  uint64_t cache = 0;              // record key of (tgt, j), loaded during the previous phase
+  uint32_t cache_tj = 0xFFFFFFFFu;
+  uint32_t status = 0, rb_over = 0xFFFFFFFFu, s_tgt = 0, s_rec = 0;
+  uint32_t next_tgt_bit = J.end_bit;  // where the next later chunk begins
+  // exact lanes: row checkpoints every `every` MCU rows of the interval (piece slots permitting)
+  uint32_t to_row = 0, rows_left = 0, every = 1, np = 1, pfirst = 0, bdone = 0;
+  if (!kSplit) {
+    const uint32_t r0 = J.mcu_first / J.mcux;
+    const uint32_t rows = (J.mcu_first + J.mcu_count - 1) / J.mcux - r0 + 1;
+    every = (rows + J.slots - 1) / J.slots;
+    to_row = J.mcux - (J.mcu_first - r0 * J.mcux);  // MCUs until the next row starts
+    rows_left = every;
+  }
+  if (kSplit && J.spec) {
+    put_record<kScope>(J.rec, J.start_bit, 0u, epoch, 0u, 0u, 0, 0, 0);
+    nrec = 1;
+  }
+  while (kSplit ? status == 0 : blocks_left > 0) {
+    // ---- phase start (same count in every active lane): prefetch, record load, stage flush ----
+    uint4 pf0, pf1;
+    const uint32_t pn = br.issue(pf0, pf1);
+    uint64_t rec_ld = 0;
+    uint32_t rec_ld_tj = 0xFFFFFFFFu;
+    if (kSplit) {  // record of the chunk being sought: compared from the next phase on
+      const uint32_t t = tgt ? tgt : 1u;
+      const bool have = t <= J.next_chunks && j < RJ_MAX_RECORDS;
+      const RjRecord *r = have ? J.rec_next - int64_t(t - 1) * RJ_MAX_RECORDS + j : J.rec;
+      rec_ld = __hip_atomic_load(reinterpret_cast<const uint64_t *>(r), __ATOMIC_RELAXED, kScope);
+      rec_ld_tj = have ? (t << 16 | j) : 0xFFFFFFFFu;
+    }
+    if (ne - fl >= RJ_ENT_GROUP) {  // one full 64-B group leaves the stage
+      const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
+      uint4 *d4 = reinterpret_cast<uint4 *>(J.ent + fl);
+#pragma unroll
+      for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = s4[q];
+      fl += RJ_ENT_GROUP;
+    }
+    for (uint32_t step = 0; step < RJ_PHASE && (kSplit ? status == 0 : blocks_left > 0); step++) {
+    uint32_t entry;
+    bool emit;
+    if (skip) {  // libjpeg: the rest of the interval decodes to zero blocks
+      entry = 0;
+      emit = true;
+      k = 64;
+    } else {
+      br.refill();
+      const uint32_t c = info & 3u;
+      const uint32_t peek32 = uint32_t(br.acc >> 32);
+      const uint32_t tbase = k == 0 ? dcbase : acbase;
+      uint32_t e = s_lut[tbase + (peek32 >> 23)];
+      if (e & 0x8000u) {
+        if (e != 0xFFFFu && k != 0) {
+          e = s_lut[tbase + RJ_LUT_L1 + (e & 0x7Fu) * 128u + ((peek32 >> 16) & 127u)];
+        } else {
+          const RjHuffDev *t = k == 0 ? &ts->dc[(info >> 2) & 1u] : &ts->ac[(info >> 3) & 1u];
+          e = huff_slow(t, peek32 >> 16);
+        }
+      }
+      const uint32_t len = e >> 8, sym = e & 255u;
+      const uint32_t s = sym & 15u, r = sym >> 4;
+      // extra bits follow the code inside the same peek (len + s <= 31); width 0 -> 0
+      const uint32_t raw = __builtin_amdgcn_ubfe(peek32, 32u - len - s, s);
+      // HUFF_EXTEND (jdhuff.h): negative when the top extra bit is 0; s == 0 gives 0
+      const int val = int(raw) + (int32_t(raw - (1u << ((s - 1) & 31))) >> 31 & int32_t(1u - (1u << s)));
+      br.acc <<= (len + s);
+      br.nb -= int(len + s);
+      // DC (k == 0): predictor per component (F.2.1.3); AC: run/size (F.2.2.2)
+      const bool isdc = k == 0;
+      const int p = (c == 0 ? pred0 : (c == 1 ? pred1 : pred2)) + val;
+      pred0 = (isdc && c == 0) ? p : pred0;
+      pred1 = (isdc && c == 1) ? p : pred1;
+      pred2 = (isdc && c == 2) ? p : pred2;
+      const int kk = isdc ? 0 : k + int(r);  // zigzag position of this coefficient
+      entry = (uint32_t(isdc ? p : val) & 0xFFFFu) | (uint32_t(kk < 63 ? kk : 63) << 16);
+      emit = isdc || s;
+      k = isdc ? 1 : (s ? kk + 1 : (r == 15 ? k + 16 : 64));  // ZRL / EOB
+    }
+    stage[ne & (RJ_STAGE - 1)] = entry;  // a non-emitted write lands in the next free slot
+    ne += emit ? 1u : 0u;
+    // block / MCU bookkeeping as selects (lanes end blocks at different iterations)
+    const bool bend = k >= 64;
+    const uint32_t bn = b + 1 == nblk ? 0u : b + 1;
+    const bool mcuend = bend && bn == 0;
+    k = bend ? 0 : k;
+    b = bend ? bn : b;
+    info = uint32_t(binfo >> (4 * b)) & 15u;
+    dcbase = ((info >> 2) & 1u) * RJ_LUT_L1;
+    acbase = RJ_SLUT_AC0 + ((info >> 3) & 1u) * RJ_LUT_ENTRIES;
+    if (!kSplit) {
+      blocks_left -= bend ? 1u : 0u;
+      bdone += bend ? 1u : 0u;
+      // libjpeg: after an MCU that ran past the data the rest of the interval stays zero
+      skip = skip || (mcuend && br.consumed() > J.nbits);
+      to_row -= mcuend ? 1u : 0u;
+      if (to_row == 0) {  // the next MCU starts a row (rare)
+        to_row = J.mcux;
+        if (--rows_left == 0) {
+          rows_left = every;
+          if (blocks_left && np < J.slots) {  // checkpoint: a new piece starts here
+            gp(J.pieces + np - 1)->nblk = bdone - pfirst;
+            *gp(J.pieces + np) = RjPiece{J.ent_abs + ne, bdone, 0u, 0u, {0, 0, 0}};
+            pfirst = bdone;
+            np++;
+          }
+        }
+      }
+    } else if (bend) {  // block start: records, sync search, stop conditions
+      rb++;
+      const uint32_t pos = J.start_bit + br.consumed();
+      if (J.spec && nrec < RJ_MAX_RECORDS && rb % RJ_RECORD_EVERY == 0 && pos < J.end_bit) {
+        put_record<kScope>(J.rec + nrec, pos, b, epoch, ne, rb, pred0, pred1, pred2);
+        nrec++;
+      }
+      if (pos >= next_tgt_bit && tgt < J.next_chunks) {  // entered the next later chunk
+        tgt++;
+        j = 0;
+        next_tgt_bit += J.clen_bits;
+      }
+      if (tgt) {  // records exist for the head of chunk c+tgt only
+        if (cache_tj == (tgt << 16 | j) && uint32_t(cache >> 36) == (epoch & 0x0FFFFFFFu)) {
+          const uint32_t cpos = uint32_t(cache);
+          if (cpos == pos && uint32_t(cache >> 32 & 15u) == b) {
+            status = RJ_CHUNK_SYNC;  // identical state from here on: the later chunk owns the rest
+            s_tgt = tgt;
+            s_rec = j;
+          } else if (cpos < pos) {
+            j++;
+          }
+        }
+      }
+      if (status == 0 && pos >= J.nbits) {  // end of the data
+        if (pos > J.nbits) rb_over = rb - 1;
+        status = RJ_CHUNK_DONE;
+      }
+      if (status == 0 && (pos > J.ov_bit || ne + 2 * RJ_ENT_PER_BLOCK > J.cap)) status = RJ_CHUNK_FAIL;
+    }
+    }
+    // ---- phase end: the prefetch (one phase old) lands in the ring ----
+    br.commit(pf0, pf1, pn);
+    if (kSplit) {
+      cache = rec_ld;
+      cache_tj = rec_ld_tj;
+    }
+  }
+  // terminator, then everything still staged (whole groups; the slack is reserved)
+  stage[ne & (RJ_STAGE - 1)] = RJ_ENT_TERM;
+  while (fl < ne + 1) {
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
+    uint4 *d4 = reinterpret_cast<uint4 *>(J.ent + fl);
+#pragma unroll
+    for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = s4[q];
+    fl += RJ_ENT_GROUP;
+  }
+  if (!kSplit) {
+    gp(J.pieces + np - 1)->nblk = bdone - pfirst;
+    gp(J.pieces)->npieces = np;
+  }
+  if (kSplit) {
+    RjChunkRes o;
+    o.status = status;
+    o.tgt = s_tgt;
+    o.rec = s_rec;
+    o.rb = rb;
+    o.ne = ne;
+    o.pred[0] = pred0;
+    o.pred[1] = pred1;
+    o.pred[2] = pred2;
+    o.rb_over = rb_over;
+    o.pad[0] = J.start_bit + br.consumed();  // stop position (diagnostics)
+    o.pad[1] = J.end_bit;
+    o.pad[2] = 0;
+    *gp(res) = o;
+  }
+}
+
+// kFallback = false: one lane per chunk (all intervals).  kFallback = true: one lane per
+// interval, only those k_resolve flagged, exact serial decode over the interval's regions.
+// kFallback = false: one lane per chunk, lanes [lane0, lane0 + nlanes) of the call's lane
+// layout (kScope: how records travel -- workgroup for intervals inside one workgroup, agent for
+// the rest).  kFallback = true: one lane per interval, only those k_resolve flagged, exact
+// serial decode over the interval's regions.
+template <bool kFallback, int kScope>
+__global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0,
+                                                      uint32_t nlanes, const uint8_t *__restrict__ destuffed,
+                                                      const uint32_t *__restrict__ seg_len,
+                                                      const RjTableSet *__restrict__ tabsets, RjCoefBuf coefs,
+                                                      uint32_t epoch) {
+  static_assert(RJ_WG == RJ_K1_WG, "lane layout granule");
+  // strides padded by 16 B so the 8-lane groups of ds_*_b128 hit distinct banks
+  __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_WG][RJ_RING_WORDS + 4];
+  __shared__ __attribute__((aligned(16))) uint32_t s_stage[RJ_WG][RJ_STAGE + 4];
+  __shared__ __attribute__((aligned(16))) uint16_t s_lut[RJ_SLUT_ENTRIES];
+  __shared__ uint32_t s_T;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t g = lane0 + blockIdx.x * RJ_WG + tid;  // lane (kFallback: interval)
+  bool pending = g < lane0 + nlanes;
+  int i = 0;
+  uint32_t gseg = 0, c = 0, nch = 1;
+  if (pending) {
+    gseg = kFallback ? g : gp(coefs.lane_seg)[g];
+    pending = kFallback ? gp(coefs.fallback)[g] != 0 : gseg != 0xFFFFFFFFu;
+  }
+  if (pending) {
+    i = upper_index(nimg, gseg, [&](int q) { return imgs[q].seg_prefix; });
+    if (!kFallback) {
+      nch = rj_chunks(gp(imgs[i].segs)[gseg - imgs[i].seg_prefix].src_len);
+      c = nch - 1 - (g - gp(coefs.seg_lane0)[gseg]);  // reverse order: later chunks on earlier lanes
+    }
+  }
+  const RjImageDev &im = imgs[i];
+  const uint32_t seg = gseg - im.seg_prefix;
+  const uint32_t my_ts = im.tabset;
+  // one pass per distinct table set among the workgroup's lanes (normally exactly one)
+  while (__syncthreads_or(pending)) {
+    if (tid == 0) s_T = 0xFFFFFFFFu;
+    __syncthreads();
+    if (pending) atomicMin(&s_T, my_ts);
+    __syncthreads();
+    const uint32_t T = s_T;
+    {
+      const RjTableSet &ts = tabsets[T];
+      uint4 *d4 = reinterpret_cast<uint4 *>(s_lut);
+      constexpr uint32_t L1Q = RJ_LUT_L1 * 2 / 16, FQ = RJ_LUT_ENTRIES * 2 / 16;
+      for (uint32_t q = tid; q < 2 * L1Q + 2 * FQ; q += RJ_WG) {
+        const uint4 *s4;
+        if (q < L1Q) s4 = reinterpret_cast<const uint4 *>(ts.dc[0].lut) + q;
+        else if (q < 2 * L1Q) s4 = reinterpret_cast<const uint4 *>(ts.dc[1].lut) + (q - L1Q);
+        else if (q < 2 * L1Q + FQ) s4 = reinterpret_cast<const uint4 *>(ts.ac[0].lut) + (q - 2 * L1Q);
+        else s4 = reinterpret_cast<const uint4 *>(ts.ac[1].lut) + (q - 2 * L1Q - FQ);
+        d4[q] = *gp(s4);
+      }
+    }
+    __syncthreads();
+    if (pending && my_ts == T) {
+      pending = false;
+      const RjSegDev sg = gp(im.segs)[seg];
+      const uint32_t nblk = im.nblk_mcu;
+      // per block-in-MCU b: component (2 bits) | dc table (1) | ac table (1), 4 bits each
+      uint64_t binfo = 0;
+      for (uint32_t b = 0; b < nblk; b++) {
+        const uint32_t cc = im.blk_comp[b] & 3;
+        binfo |= uint64_t(cc | ((im.comp_td[cc] & 1) << 2) | ((im.comp_ta[cc] & 1) << 3)) << (4 * b);
+      }
+      const uint32_t nbytes = gp(seg_len)[gseg];
+      const uint32_t blocks = sg.mcu_count * nblk;
+      const uint8_t *data = destuffed + im.destuff_off + sg.dst_off;
+      uint32_t *ent_base = coefs.ent + im.ent_off + sg.ent_off;
+      const uint64_t ent_abs = im.ent_off + sg.ent_off;
+      const uint32_t lane_first = gp(coefs.seg_lane0)[gseg];
+      const RjTableSet *ts = tabsets + T;
+      LaneJob J;
+      J.nbits = nbytes * 8u;
+      J.blocks = blocks;
+      J.missing = (sg.flags & RJ_SEG_MISSING) != 0;
+      if (kFallback || nch == 1) {
+        J.src = reinterpret_cast<const uint4 *>(data);
+        J.bytes = nbytes;
+        J.start_bit = 0;
+        J.ent = ent_base;
+        J.pieces = coefs.piece + lane_first;
+        J.slots = rj_chunks(sg.src_len);
+        J.ent_abs = ent_abs;
+        J.mcux = im.mcux;
+        J.mcu_first = sg.mcu_first;
+        J.mcu_count = sg.mcu_count;
+        *gp(J.pieces) = RjPiece{ent_abs, 0u, blocks, 1u, {0, 0, 0}};
+        decode_lane<false, kScope>(J, binfo, nblk, epoch, s_lut, ts, s_ring[tid], s_stage[tid], nullptr);
+      } else {
+        const uint32_t clen = rj_chunk_len(nbytes, nch);
+        const uint32_t b0 = min(c * clen, nbytes), b1 = min(b0 + clen, nbytes);
+        if (c > 0 && b0 >= nbytes) {  // no data left for this chunk (16-B rounding): nothing to decode
+          RjChunkRes o = {};
+          o.status = RJ_CHUNK_DONE;
+          o.rb_over = 0xFFFFFFFFu;
+          *gp(coefs.res + g) = o;
+          put_record<kScope>(coefs.rec + uint64_t(g) * RJ_MAX_RECORDS, 0xFFFFFFFFu, 0u, epoch, 0u, 0u, 0, 0, 0);
+          continue;
+        }
+        J.src = reinterpret_cast<const uint4 *>(data + b0);
+        J.bytes = nbytes - b0;
+        J.start_bit = b0 * 8u;
+        J.end_bit = b1 * 8u;
+        J.clen_bits = clen * 8u;
+        J.ov_bit = J.end_bit + RJ_OVERLAP_CHUNKS * clen * 8u;
+        const uint32_t rcap = uint32_t(rj_chunk_cap(rj_chunk_len(sg.src_len, nch)));
+        J.ent = ent_base + uint64_t(c) * rcap;
+        J.cap = rcap;
+        J.spec = c > 0;
+        J.rec = coefs.rec + uint64_t(g) * RJ_MAX_RECORDS;
+        J.rec_next = J.rec - RJ_MAX_RECORDS;  // chunk c+1 sits on lane g-1
+        J.next_chunks = nch - 1 - c;
+        decode_lane<true, kScope>(J, binfo, nblk, epoch, s_lut, ts, s_ring[tid], s_stage[tid], coefs.res + g);
+      }
+    }
+  }
+}
+
+// Chains the chunks of every split interval into pieces; flags intervals for the serial path.
+__global__ __launch_bounds__(256) void k_resolve(const RjImageDev *__restrict__ imgs, int nimg, uint32_t nseg,
+                                                 RjCoefBuf coefs) {
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  if (g >= nseg) return;
+  const int i = upper_index(nimg, g, [&](int q) { return imgs[q].seg_prefix; });
+  const RjImageDev &im = imgs[i];
+  const RjSegDev sg = gp(im.segs)[g - im.seg_prefix];
+  const uint32_t nch = rj_chunks(sg.src_len);
+  bool ok = true;
+  if (nch > 1) {
+    const uint32_t total = sg.mcu_count * im.nblk_mcu;
+    const uint32_t lane_first = gp(coefs.seg_lane0)[g];  // lane of chunk c: lane_first + nch-1-c
+    const uint64_t rcap = rj_chunk_cap(rj_chunk_len(sg.src_len, nch));
+    const uint64_t ent0 = im.ent_off + sg.ent_off;
+    RjPiece *pieces = coefs.piece + lane_first;
+    uint32_t c = 0, vs_rb = 0, vs_ne = 0, T = 0, np = 0;
+    int32_t D[3] = {0, 0, 0};
+    while (true) {
+      const RjChunkRes r = gp(coefs.res)[lane_first + nch - 1 - c];
+      if (r.status != RJ_CHUNK_SYNC && r.status != RJ_CHUNK_DONE) { ok = false; break; }
+      if (r.rb < vs_rb) { ok = false; break; }
+      uint32_t nb = r.rb - vs_rb;
+      if (r.status == RJ_CHUNK_DONE) {
+        // a block the interval needs read past the data, or the data ended early: libjpeg's
+        // insufficient-data semantics need the serial decode
+        if (r.rb_over != 0xFFFFFFFFu && r.rb_over >= vs_rb && T + (r.rb_over - vs_rb) < total) { ok = false; break; }
+        if (T + nb < total) { ok = false; break; }
+      }
+      if (T + nb > total) nb = total - T;
+      gp(pieces)[np] = RjPiece{ent0 + uint64_t(c) * rcap + vs_ne, T, nb, 0u, {D[0], D[1], D[2]}};
+      np++;
+      T += nb;
+      if (r.status == RJ_CHUNK_DONE || T >= total) break;
+      const uint32_t t = c + r.tgt;
+      if (t >= nch || r.rec >= RJ_MAX_RECORDS) { ok = false; break; }
+      const RjRecord rec = gp(coefs.rec)[uint64_t(lane_first + nch - 1 - t) * RJ_MAX_RECORDS + r.rec];
+      for (int q = 0; q < 3; q++) D[q] = r.pred[q] + D[q] - rec.pred[q];
+      c = t;
+      vs_rb = rec.rb;
+      vs_ne = rec.ne;
+    }
+    if (ok && T == total) gp(pieces)->npieces = np;
+    else ok = false;
+  }
+  gp(coefs.fallback)[g] = ok ? 0u : 1u;
+}
+
+hipError_t LaunchEntropy(hipStream_t st, int stage, const RjImageDev *imgs, int nimg, uint32_t lanes_wg,
+                         uint32_t lanes_dev, uint32_t nseg, const uint8_t *destuffed, const uint32_t *seg_len,
+                         const RjTableSet *tabsets, RjCoefBuf coefs, uint32_t epoch) {
+  if (nseg == 0) return hipSuccess;
+  if (stage == 0) {
+    if (lanes_wg)
+      hipLaunchKernelGGL((k_entropy<false, __HIP_MEMORY_SCOPE_WORKGROUP>), dim3((lanes_wg + RJ_WG - 1) / RJ_WG),
+                         dim3(RJ_WG), 0, st, imgs, nimg, 0u, lanes_wg, destuffed, seg_len, tabsets, coefs, epoch);
+    if (lanes_dev)
+      hipLaunchKernelGGL((k_entropy<false, __HIP_MEMORY_SCOPE_AGENT>), dim3((lanes_dev + RJ_WG - 1) / RJ_WG),
+                         dim3(RJ_WG), 0, st, imgs, nimg, lanes_wg, lanes_dev, destuffed, seg_len, tabsets, coefs,
+                         epoch);
+  } else if (stage == 1) {
+    hipLaunchKernelGGL(k_resolve, dim3((nseg + 255) / 256), dim3(256), 0, st, imgs, nimg, nseg, coefs);
+  } else {
+    hipLaunchKernelGGL((k_entropy<true, __HIP_MEMORY_SCOPE_WORKGROUP>), dim3((nseg + RJ_WG - 1) / RJ_WG),
+                       dim3(RJ_WG), 0, st, imgs, nimg, 0u, nseg, destuffed, seg_len, tabsets, coefs, epoch);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace rj

@@ -68,38 +68,70 @@ __device__ __forceinline__ void store_bytes(uint8_t *d, uint32_t n, const uint32
 #define RJ_WIN_ROWS 8
 struct EntWin {
   uint32_t w[RJ_WIN_ROWS];
-  uint32_t base;
-  __device__ __forceinline__ void load(const uint32_t *__restrict__ ent, uint32_t at, uint32_t lane) {
-    base = at;
+  uint32_t base_lo, base_hi;
+  __device__ __forceinline__ void load(const uint32_t *__restrict__ ent, uint64_t at, uint32_t lane) {
+    base_lo = U(uint32_t(at));
+    base_hi = U(uint32_t(at >> 32));
+    const uint32_t *p = ent + at;
 #pragma unroll
-    for (int r = 0; r < RJ_WIN_ROWS; r++) w[r] = ent[at + r * 64u + lane];
+    for (int r = 0; r < RJ_WIN_ROWS; r++) w[r] = gp(p)[r * 64u + lane];
   }
 };
 
-// Expand the next `nb` blocks of the image's entry stream into the zeroed LDS blocks [0, nb)
-// (block j at s_buf + j * RJ_BLK_STRIDE, int16 in zigzag order).  A block starts at its DC
-// entry (pos 0); the terminator (pos 127) closes an interval; a block has <= 64 entries.
-// Entries are consumed row by row from the window; the ordinal of an entry's block is the
-// number of block starts at or before it, so rows need no alignment to block starts.
-//   cur    image-relative entry index of the next block's DC entry (== win.base on entry)
-//   bleft  blocks left in the current restart interval; at 0 the cursor moves to the next one
-//   gblk   image-relative index of the next block (locates the next interval)
-__device__ __forceinline__ void parse_blocks(const RjImageDev &im, const uint32_t *__restrict__ ent, uint32_t lane,
-                                             uint32_t nb, uint32_t nblk, EntWin &win, uint32_t &cur,
-                                             uint32_t &bleft, uint32_t &gblk, uint8_t *s_buf) {
+// Position in the image's entry streams: the next block's DC entry inside the current piece
+// (RjPiece: which part of which K1 chunk stream holds which blocks of an interval).
+struct Nav {
+  uint32_t cur_lo, cur_hi;  // absolute entry index (64-bit, kept as two SGPR-able halves)
+  uint32_t bleft;           // blocks left in the current piece
+  uint32_t seg, pj;         // interval (image-relative) and piece within it
+  int32_t dcd[3];           // DC correction of the current piece, per component
+  __device__ __forceinline__ uint64_t cur() const { return uint64_t(cur_hi) << 32 | cur_lo; }
+  __device__ __forceinline__ void set_cur(uint64_t v) {
+    cur_lo = U(uint32_t(v));
+    cur_hi = U(uint32_t(v >> 32));
+  }
+  __device__ __forceinline__ void take(const RjPiece *pc) {
+    const RjPiece p = *gp(pc);
+    set_cur(p.ent);
+    bleft = U(p.nblk);
+    dcd[0] = int32_t(U(uint32_t(p.dcd[0])));
+    dcd[1] = int32_t(U(uint32_t(p.dcd[1])));
+    dcd[2] = int32_t(U(uint32_t(p.dcd[2])));
+  }
+};
+
+// Expand the next `nb` blocks of the entry streams into the zeroed LDS blocks [0, nb) (block j
+// at s_buf + j * RJ_BLK_STRIDE, int16 in zigzag order), after discarding `drop` blocks.  A
+// block starts at its DC entry (pos 0); a terminator (pos 127) ends a stream; a block has
+// <= 64 entries.  Entries are consumed row by row from the window; the ordinal of an entry's
+// block is the number of block starts at or before it, so rows need no alignment to blocks.
+// cbits: component of each block within the MCU (2 bits each), for the DC corrections.
+__device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefBuf &coefs,
+                                             const uint32_t *__restrict__ ent, uint32_t lane, uint32_t nb,
+                                             uint32_t drop, uint32_t nblk, uint32_t cbits, EntWin &win, Nav &nv,
+                                             uint8_t *s_buf) {
   uint32_t done = 0;
-  while (done < nb) {
-    if (bleft == 0) {  // the next block opens a new restart interval (rare: synchronous reload)
-      const uint32_t ri = im.ri_mcus;
-      const RjSegDev sg = gp(im.segs)[ri ? gblk / nblk / ri : 0];
-      cur = U(sg.ent_off);
-      bleft = U(sg.mcu_count * nblk);
-      win.load(ent, cur, lane);
+  const uint32_t need = nb + drop;
+  for (uint32_t moves = 0; done < need && moves < (1u << 16); moves++) {  // bounded on corrupt pieces
+    if (nv.bleft == 0) {  // next piece, or the first piece of the next interval (synchronous reload)
+      if (nv.seg >= im.nseg) break;
+      const RjPiece *pb = coefs.piece + gp(coefs.seg_lane0)[im.seg_prefix + nv.seg];
+      if (nv.pj + 1 < gp(pb)->npieces) {
+        nv.pj++;
+      } else {
+        nv.seg++;
+        nv.pj = 0;
+        if (nv.seg >= im.nseg) break;
+        pb = coefs.piece + gp(coefs.seg_lane0)[im.seg_prefix + nv.seg];
+      }
+      nv.take(pb + nv.pj);
+      win.load(ent, nv.cur(), lane);
     }
-    const uint32_t piece = min(nb - done, bleft);  // blocks taken from this interval
-    uint32_t seen = 0;                              // block starts before the current row
+    const uint32_t piece = min(need - done, nv.bleft);  // blocks taken from this piece
+    const bool fix_dc = (nv.dcd[0] | nv.dcd[1] | nv.dcd[2]) != 0;
+    uint32_t seen = 0;                                  // block starts before the current row
     bool found = false;
-    for (int guard = 0; !found && guard < 64; guard++) {  // <= 64 entries per block: bounded
+    for (uint32_t guard = 0; !found && guard < (1u << 20); guard++) {  // bounded even on a corrupt stream
 #pragma unroll
       for (int r = 0; r < RJ_WIN_ROWS; r++) {
         const uint32_t e = win.w[r];
@@ -108,21 +140,29 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const uint32_
         const uint64_t m = __ballot(st);
         const uint32_t below = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
         const uint32_t ord = seen + below + (st ? 1u : 0u) - 1u;
-        if (ord < piece && p < 64u)
-          *reinterpret_cast<int16_t *>(s_buf + (done + ord) * RJ_BLK_STRIDE + p * 2) = int16_t(e & 0xFFFFu);
+        const uint32_t blk = done + ord;  // block index counted from the first dropped one
+        if (ord < piece && p < 64u && blk >= drop) {
+          int v = int16_t(e & 0xFFFFu);
+          if (fix_dc && p == 0) {
+            const uint32_t bi = (blk - drop) % nblk;  // strips start at an MCU boundary
+            const uint32_t cc = (cbits >> (2 * bi)) & 3u;
+            v += cc == 0 ? nv.dcd[0] : (cc == 1 ? nv.dcd[1] : nv.dcd[2]);
+          }
+          *reinterpret_cast<int16_t *>(s_buf + (blk - drop) * RJ_BLK_STRIDE + p * 2) = int16_t(v);
+        }
         const uint64_t hit = __ballot(st && ord == piece);  // start of the first block past the piece
         seen += __popcll(m);
         if (hit) {
-          cur = win.base + uint32_t(r) * 64u + uint32_t(__ffsll((long long)hit) - 1);
+          nv.set_cur((uint64_t(win.base_hi) << 32 | win.base_lo) + uint32_t(r) * 64u +
+                     uint32_t(__ffsll((long long)hit) - 1));
           found = true;
           break;
         }
       }
-      if (!found) win.load(ent, win.base + RJ_WIN_ROWS * 64u, lane);  // block longer than the window
+      if (!found) win.load(ent, (uint64_t(win.base_hi) << 32 | win.base_lo) + RJ_WIN_ROWS * 64u, lane);
     }
     done += piece;
-    bleft -= piece;
-    gblk += piece;
+    nv.bleft -= piece;
   }
 }
 
@@ -188,18 +228,28 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
 
   const uint32_t mcux = U(im.mcux);
   const uint32_t strips_x = (mcux + S - 1) / S;
-  const uint32_t *ent = coefs.ent + im.ent_off;
-  // entry cursor at the row's first block, blocks left in its restart interval
-  uint32_t cur = U(coefs.row[im.row_off + my]);
-  uint32_t gblk = my * mcux * nblk;
-  uint32_t bleft;
+  const uint32_t *ent = coefs.ent;
+  uint32_t cbits = 0;  // component of each block within the MCU
+  for (uint32_t b = 0; b < nblk; b++) cbits |= (inter ? uint32_t(im.blk_comp[b] & 3) : 0u) << (2 * b);
+  cbits = U(cbits);
+  // the row's first block: its interval, the piece holding it, blocks to skip inside the piece
+  Nav nv;
+  uint32_t drop;
   {
     const uint32_t ri = U(im.ri_mcus);
-    const RjSegDev sg = gp(im.segs)[ri ? (my * mcux) / ri : 0];
-    bleft = U((sg.mcu_first + sg.mcu_count - my * mcux) * nblk);
+    nv.seg = U(ri ? (my * mcux) / ri : 0);
+    const RjSegDev sg = gp(im.segs)[nv.seg];
+    const uint32_t rel = (my * mcux - sg.mcu_first) * nblk;
+    const RjPiece *pb = coefs.piece + gp(coefs.seg_lane0)[im.seg_prefix + nv.seg];
+    const uint32_t np = U(min(gp(pb)->npieces, 4096u));
+    uint32_t pj = 0;
+    while (pj + 1 < np && U(gp(pb + pj + 1)->first_blk) <= rel) pj++;
+    nv.pj = pj;
+    nv.take(pb + pj);
+    drop = U(rel - gp(pb + pj)->first_blk);
   }
   EntWin win;
-  win.load(ent, cur, tid);
+  win.load(ent, nv.cur(), tid);
 
   // output descriptor, read once before the strip loop (the output stores could otherwise
   // force re-reads of the descriptor inside the pixel loops)
@@ -225,8 +275,9 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
     for (uint32_t k = tid; k < nb * 8; k += 64)
       *reinterpret_cast<uint4 *>(s_buf + (k >> 3) * RJ_BLK_STRIDE + (k & 7) * 16) = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    parse_blocks(im, ent, tid, nb, nblk, win, cur, bleft, gblk, s_buf);
-    if (sx + 1 < strips_x) win.load(ent, cur, tid);  // next strip's window: lands behind B and C
+    parse_blocks(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf);
+    drop = 0;
+    if (sx + 1 < strips_x && nv.bleft) win.load(ent, nv.cur(), tid);  // next strip's window: lands behind B and C
     __syncthreads();
 
     // ---- B: lane-per-block IDCT in registers ----

@@ -11,9 +11,12 @@ namespace rj {
 hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nseg, uint8_t *destuffed,
                          uint32_t *seg_len);
 
-// K1: Huffman entropy decode, one lane per restart interval -> sparse coefficients.
-hipError_t LaunchHuffman(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nseg, const uint8_t *destuffed,
-                         const uint32_t *seg_len, const RjTableSet *tabsets, RjCoefBuf coefs);
+// K1 (rj_entropy.hip): Huffman entropy decode -> sparse entry streams + pieces.  stage 0: one
+// lane per interval chunk; 1: sync resolution; 2: serial re-decode of the flagged intervals.
+// lanes_wg: lanes of intervals that fit one workgroup (laid out first); lanes_dev: the others.
+hipError_t LaunchEntropy(hipStream_t st, int stage, const RjImageDev *imgs, int nimg, uint32_t lanes_wg,
+                         uint32_t lanes_dev, uint32_t nseg, const uint8_t *destuffed, const uint32_t *seg_len,
+                         const RjTableSet *tabsets, RjCoefBuf coefs, uint32_t epoch);
 
 // K2b (general path): every output format / ROI of rocjpeg_decoder.cpp:143-180 from the planes.
 hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobDev *jobs, int njobs, uint32_t total_rows,

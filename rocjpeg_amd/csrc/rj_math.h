@@ -45,6 +45,18 @@ __device__ __forceinline__ const RJ_GLOBAL T *gp(const T *p) {
 
 __device__ __forceinline__ int32_t m24(int32_t a, int32_t k) { return __mul24(a, k); }
 
+// index of the last entry with prefix <= key (prefix[0] == 0, monotone)
+template <typename F>
+__device__ __forceinline__ int upper_index(int n, uint32_t key, F prefix_of) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (prefix_of(mid) <= key) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
 // One 8-point ISLOW butterfly on x0..x7 (dequantised coefficients or pass-1 outputs).  `rnd`
 // is added to the even part, so it reaches all eight outputs: callers fold the descale
 // rounding (and the range-limit offset) into it.  Writes the pre-shift sums t[0..7].

@@ -317,8 +317,9 @@ void Stream::BuildPlan() {
     sg.mcu_count = ri ? std::min(ri, total_mcus - sg.mcu_first) : total_mcus;
     sg.flags = 0;
     sg.ent_off = uint32_t(ent);
-    sg.pad = 0;
-    ent += rj_interval_entries(uint64_t(sg.mcu_count) * p.nblk_mcu);
+    sg.chunk0 = p.nchunks;
+    p.nchunks += rj_chunks(sg.src_len);
+    ent += rj_interval_entries(sg.src_len, uint64_t(sg.mcu_count) * p.nblk_mcu, p.nblk_mcu);
     dst += (uint64_t(sg.src_len) + 16 + 15) & ~uint64_t(15);  // >= 16 B of slack after each interval
     p.segs.push_back(sg);
   };
@@ -355,8 +356,9 @@ void Stream::BuildPlan() {
     sg.mcu_count = std::min(ri, total_mcus - sg.mcu_first);
     sg.flags = RJ_SEG_MISSING;
     sg.ent_off = uint32_t(ent);
-    sg.pad = 0;
-    ent += rj_interval_entries(uint64_t(sg.mcu_count) * p.nblk_mcu);
+    sg.chunk0 = p.nchunks;
+    p.nchunks += 1;
+    ent += rj_interval_entries(0, uint64_t(sg.mcu_count) * p.nblk_mcu, p.nblk_mcu);
     dst += 16;
     p.segs.push_back(sg);
   }

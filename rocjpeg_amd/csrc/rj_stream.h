@@ -49,6 +49,7 @@ struct DecodePlan {
   std::vector<RjSegDev> segs;      // one per restart interval
   uint64_t destuff_bytes = 0;      // destuffed buffer size incl. per-interval alignment
   uint64_t entries = 0;            // sparse-coefficient entries reserved (worst case)
+  uint32_t nchunks = 0;            // K1 lanes (chunks) over all intervals
   RjTableSet tables;               // derived tables
   // De-duplication key: the raw DHT/DQT content the derived tables are a function of (the
   // batch planner compares these ~670 B instead of the 14.5 KB RjTableSet) and its hash.
