@@ -131,3 +131,76 @@ def test_error_statuses(dec):
     assert dec.decode(s, R.decode_params(R.OutputFormat.RGB), img) == R.Status.JPEG_NOT_SUPPORTED
     # empty batch succeeds
     assert dec.decode_batched([], R.decode_params(R.OutputFormat.RGB), []) in (0, R.Status.INVALID_PARAMETER)
+
+
+# ---- chunked (self-synchronising) entropy decode of long intervals ----
+BIG_NORI = [f for f in DECODABLE if f["ref_parse"]["restart_interval"] == 0 and f["bytes"] > 200_000]
+
+
+def _ecs_span(data):
+    """(start, end) of the entropy-coded segment after the (only) SOS."""
+    i = data.index(b"\xff\xda")
+    start = i + 2 + int.from_bytes(data[i + 2:i + 4], "big")
+    end = data.rindex(b"\xff\xd9")
+    return start, end
+
+
+def _variants(data):
+    """Damaged copies of a long no-restart stream: truncated (libjpeg's insufficient-data path,
+    which the chunked decode hands to the serial re-decode) and with flipped bits mid-stream
+    (the chunks must still agree with the true decode wherever they synchronise)."""
+    s, e = _ecs_span(data)
+    out = {}
+    for frac in (0.37, 0.81):
+        cut = s + int((e - s) * frac)
+        if data[cut - 1] == 0xFF:
+            cut -= 1
+        out[f"trunc{int(frac * 100)}"] = data[:cut] + b"\xff\xd9"
+    buf = bytearray(data)
+    rng = np.random.default_rng(7)
+    for pos in rng.integers(s + 1000, e - 1000, 24):
+        if buf[pos] != 0xFF and buf[pos - 1] != 0xFF and buf[pos + 1] != 0x00:
+            nb = buf[pos] ^ (1 << int(rng.integers(0, 8)))
+            if nb != 0xFF:
+                buf[pos] = nb
+    out["bitflips"] = bytes(buf)
+    return out
+
+
+@pytest.mark.parametrize("ent", BIG_NORI, ids=[f["name"] for f in BIG_NORI])
+def test_long_interval_damaged_streams(dec, ent):
+    """Parity on damaged long no-restart streams, where the chunked K1 meets truncation and
+    corrupt codes (the oracle restates libjpeg's semantics for both)."""
+    from tests import gpu_util as G
+    for name, data in _variants(O.fixture_bytes(ent)).items():
+        st, ost, got, want = run_both(dec, data, R.OutputFormat.RGB)
+        assert st == ost, name
+        if st == 0:
+            assert G.first_mismatch(got[0], want[0]) is None, (name, G.first_mismatch(got[0], want[0]))
+
+
+def test_long_interval_batch_mixed(dec):
+    """A batch mixing long no-restart streams (chunked), restart-interval streams (one lane per
+    interval) and their damaged variants, decoded in one call."""
+    from tests import gpu_util as G
+    datas = []
+    for ent in BIG_NORI + SMALL[:4]:
+        d = O.fixture_bytes(ent)
+        datas.append(d)
+        if ent in BIG_NORI:
+            datas.extend(_variants(d).values())
+    streams = [R.JpegStream(d) for d in datas]
+    shapes_all, bufs_all, imgs = [], [], []
+    for s in streams:
+        nc, css, w, h = dec.image_info(s)
+        shapes = G.channel_shapes(R.OutputFormat.RGB, css, w, h)
+        bufs, img = G.gpu_buffers(shapes)
+        shapes_all.append(shapes)
+        bufs_all.append(bufs)
+        imgs.append(img)
+    st = dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs)
+    assert st == 0
+    for d, shapes, bufs in zip(datas, shapes_all, bufs_all):
+        ost, want = O.oracle_decode(d, int(R.OutputFormat.RGB), shapes)
+        assert ost == 0
+        assert G.first_mismatch(G.to_host(bufs)[0], want[0]) is None
