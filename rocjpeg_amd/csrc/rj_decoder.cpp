@@ -154,8 +154,10 @@ int Decoder::StreamsToDevice(Stream *const *streams, int n) {
     r.generation = s->generation();
     RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.ecs), std::max<size_t>(in.ecs_size, 16)));
     RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.segs), std::max<size_t>(p.segs.size() * sizeof(RjSegDev), 16)));
+    RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.ds), std::max<size_t>(p.ds.size() * sizeof(RjDsBlock), 16)));
     RJ_HIP(hipMemcpy(r.ecs, in.ecs, in.ecs_size, hipMemcpyHostToDevice));
     RJ_HIP(hipMemcpy(r.segs, p.segs.data(), p.segs.size() * sizeof(RjSegDev), hipMemcpyHostToDevice));
+    if (!p.ds.empty()) RJ_HIP(hipMemcpy(r.ds, p.ds.data(), p.ds.size() * sizeof(RjDsBlock), hipMemcpyHostToDevice));
     s->resident = r;
   }
   return kOk;
@@ -224,7 +226,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   std::vector<RjImageDev> imgs(n);
   std::vector<RjJobDev> jobs;
   uint64_t destuff_total = 0, coef_blocks = 0, ent_total = 0, plane_bytes = 0, stage_bytes = 0;
-  uint32_t seg_total = 0, rows_total = 0, chunk_total = 0;
+  uint32_t seg_total = 0, rows_total = 0, chunk_total = 0, ds_total = 0;
   uint64_t ecs_bytes = 0, out_bytes = 0;
   std::vector<uint64_t> stage_off(n, UINT64_MAX);
   std::vector<uint32_t> row_prefix(n), grow_prefix(n);  // K2 rows: fused images / general images
@@ -261,6 +263,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     d.nseg = uint32_t(p.segs.size());
     d.seg_prefix = seg_total;
     seg_total += d.nseg;
+    d.ds_prefix = ds_total;
+    ds_total += uint32_t(p.ds.size());
     d.destuff_off = destuff_total;
     destuff_total += AlignUp(p.destuff_bytes, 256);
     coef_blocks += uint64_t(p.mcux) * p.mcuy * p.nblk_mcu;
@@ -276,7 +280,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     ecs_bytes += in.ecs_size;
     if (!(s->resident.device == device_ && s->resident.generation == s->generation())) {
       stage_off[i] = stage_bytes;
-      stage_bytes += AlignUp(p.segs.size() * sizeof(RjSegDev), 256) + AlignUp(in.ecs_size + 16, 256);
+      stage_bytes += AlignUp(p.segs.size() * sizeof(RjSegDev), 256) + AlignUp(p.ds.size() * sizeof(RjDsBlock), 256) +
+                     AlignUp(in.ecs_size + 16, 256);
     }
 
     // output window: ROI semantics of rocjpeg_decoder.cpp:124-141 (no ROI decode on gfx950)
@@ -450,7 +455,6 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   RJ_CHECK(h_stage_.Ensure(blob));
   RJ_CHECK(d_desc_.Ensure(blob));
   RJ_CHECK(d_destuff_.Ensure(std::max<uint64_t>(destuff_total, 256)));
-  RJ_CHECK(d_seglen_.Ensure(std::max<uint64_t>(uint64_t(seg_total) * 4, 256)));
   RJ_CHECK(d_piece_.Ensure(std::max<uint64_t>(uint64_t(lanes_all) * sizeof(RjPiece), 256)));
   RJ_CHECK(d_rec_.Ensure(std::max<uint64_t>(uint64_t(lanes_all) * RJ_MAX_RECORDS * sizeof(RjRecord), 256)));
   RJ_CHECK(d_chunkres_.Ensure(std::max<uint64_t>(uint64_t(lanes_all) * sizeof(RjChunkRes), 256)));
@@ -474,10 +478,14 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (stage_off[i] == UINT64_MAX) {
       d.ecs = s->resident.ecs;
       d.segs = s->resident.segs;
+      d.ds = s->resident.ds;
     } else {
       const DecodePlan &p = s->plan();
       const uint64_t so = off_stage + stage_off[i];
-      const uint64_t eo = so + AlignUp(p.segs.size() * sizeof(RjSegDev), 256);
+      const uint64_t bo = so + AlignUp(p.segs.size() * sizeof(RjSegDev), 256);
+      const uint64_t eo = bo + AlignUp(p.ds.size() * sizeof(RjDsBlock), 256);
+      if (!p.ds.empty()) std::memcpy(h + bo, p.ds.data(), p.ds.size() * sizeof(RjDsBlock));
+      d.ds = reinterpret_cast<const RjDsBlock *>(dbase + bo);
       std::memcpy(h + so, p.segs.data(), p.segs.size() * sizeof(RjSegDev));
       std::memcpy(h + eo, s->info().ecs, s->info().ecs_size);
       d.segs = reinterpret_cast<const RjSegDev *>(dbase + so);
@@ -504,11 +512,11 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (profiling_) RJ_HIP(hipEventRecord(ev_[0], stream_));
   RJ_HIP(hipMemcpyAsync(dbase, h, blob, hipMemcpyHostToDevice, stream_));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
-  RJ_HIP(LaunchDestuff(stream_, d_imgs, n, seg_total, d_destuff_.as<uint8_t>(), d_seglen_.as<uint32_t>()));
+  RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[2], stream_));
   for (int stage = 0; stage < 3; stage++) {
-    RJ_HIP(LaunchEntropy(stream_, stage, d_imgs, n, lanes_wg, lanes_dev, seg_total, d_destuff_.as<uint8_t>(),
-                        d_seglen_.as<uint32_t>(), d_tabs, cbuf, epoch_));
+    RJ_HIP(LaunchEntropy(stream_, stage, d_imgs, n, lanes_wg, lanes_dev, seg_total, d_destuff_.as<uint8_t>(), d_tabs,
+                        cbuf, epoch_));
     if (profiling_ && stage < 2) RJ_HIP(hipEventRecord(ev_[6 + stage], stream_));
   }
   if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));

@@ -69,7 +69,7 @@ class Decoder {
   RocJpegAmdTimings timings_ = {};
   hipEvent_t ev_[8] = {};  // 0..5 stage boundaries, 6..7 inside K1
 
-  DeviceBuffer d_desc_, d_stage_, d_destuff_, d_seglen_, d_entries_, d_planes_;
+  DeviceBuffer d_desc_, d_stage_, d_destuff_, d_entries_, d_planes_;
   DeviceBuffer d_piece_, d_rec_, d_chunkres_, d_fallback_;  // K1 chunk bookkeeping
   uint32_t epoch_ = 0;
   PinnedBuffer h_stage_;

@@ -119,6 +119,19 @@ struct RjSegDev {
   uint32_t flags;      // RJ_SEG_MISSING: marker not found -> interval decodes to zero blocks
   uint32_t ent_off;    // first entry of the interval's region(s), relative to image.ent_off
   uint32_t chunk0;     // image-relative chunk count before this interval (rj_chunks(src_len) each)
+  uint32_t dst_len;    // destuffed bytes (src_len minus the stuffed 00 and fill FF bytes)
+  uint32_t pad[3];
+};
+
+// K0 work unit: up to RJ_DS_BLOCK raw bytes of one interval.  The host parser knows where every
+// stuffed byte is (its marker scan visits each FF), so each block's output offset is known up
+// front and the blocks are independent.
+#define RJ_DS_BLOCK 2048u
+struct RjDsBlock {
+  uint32_t src_off;   // ECS-relative raw offset
+  uint32_t len;       // raw bytes
+  uint32_t dst_off;   // output offset relative to image.destuff_off
+  uint32_t zero_end;  // last block of its interval: zero the output up to here (0: not last)
 };
 #define RJ_SEG_MISSING 1u
 
@@ -182,6 +195,8 @@ struct RjImageDev {
   // inputs
   const uint8_t *ecs;
   const RjSegDev *segs;
+  const RjDsBlock *ds;   // K0 blocks of this image
+  uint32_t ds_prefix;    // exclusive prefix of K0 blocks over the batch
   uint32_t nseg;
   uint32_t seg_prefix;   // exclusive prefix of segments over the batch
   uint64_t destuff_off;  // into the destuffed buffer

@@ -372,7 +372,6 @@ __device__ __forceinline__ void decode_lane(const LaneJob &J, uint64_t binfo, ui
 template <bool kFallback, int kScope>
 __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0,
                                                       uint32_t nlanes, const uint8_t *__restrict__ destuffed,
-                                                      const uint32_t *__restrict__ seg_len,
                                                       const RjTableSet *__restrict__ tabsets, RjCoefBuf coefs,
                                                       uint32_t epoch) {
   static_assert(RJ_WG == RJ_K1_WG, "lane layout granule");
@@ -431,7 +430,7 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
         const uint32_t cc = im.blk_comp[b] & 3;
         binfo |= uint64_t(cc | ((im.comp_td[cc] & 1) << 2) | ((im.comp_ta[cc] & 1) << 3)) << (4 * b);
       }
-      const uint32_t nbytes = gp(seg_len)[gseg];
+      const uint32_t nbytes = sg.dst_len;
       const uint32_t blocks = sg.mcu_count * nblk;
       const uint8_t *data = destuffed + im.destuff_off + sg.dst_off;
       uint32_t *ent_base = coefs.ent + im.ent_off + sg.ent_off;
@@ -534,22 +533,22 @@ __global__ __launch_bounds__(256) void k_resolve(const RjImageDev *__restrict__ 
 }
 
 hipError_t LaunchEntropy(hipStream_t st, int stage, const RjImageDev *imgs, int nimg, uint32_t lanes_wg,
-                         uint32_t lanes_dev, uint32_t nseg, const uint8_t *destuffed, const uint32_t *seg_len,
-                         const RjTableSet *tabsets, RjCoefBuf coefs, uint32_t epoch) {
+                         uint32_t lanes_dev, uint32_t nseg, const uint8_t *destuffed, const RjTableSet *tabsets,
+                         RjCoefBuf coefs, uint32_t epoch) {
   if (nseg == 0) return hipSuccess;
   if (stage == 0) {
     if (lanes_wg)
       hipLaunchKernelGGL((k_entropy<false, __HIP_MEMORY_SCOPE_WORKGROUP>), dim3((lanes_wg + RJ_WG - 1) / RJ_WG),
-                         dim3(RJ_WG), 0, st, imgs, nimg, 0u, lanes_wg, destuffed, seg_len, tabsets, coefs, epoch);
+                         dim3(RJ_WG), 0, st, imgs, nimg, 0u, lanes_wg, destuffed, tabsets, coefs, epoch);
     if (lanes_dev)
       hipLaunchKernelGGL((k_entropy<false, __HIP_MEMORY_SCOPE_AGENT>), dim3((lanes_dev + RJ_WG - 1) / RJ_WG),
-                         dim3(RJ_WG), 0, st, imgs, nimg, lanes_wg, lanes_dev, destuffed, seg_len, tabsets, coefs,
+                         dim3(RJ_WG), 0, st, imgs, nimg, lanes_wg, lanes_dev, destuffed, tabsets, coefs,
                          epoch);
   } else if (stage == 1) {
     hipLaunchKernelGGL(k_resolve, dim3((nseg + 255) / 256), dim3(256), 0, st, imgs, nimg, nseg, coefs);
   } else {
     hipLaunchKernelGGL((k_entropy<true, __HIP_MEMORY_SCOPE_WORKGROUP>), dim3((nseg + RJ_WG - 1) / RJ_WG),
-                       dim3(RJ_WG), 0, st, imgs, nimg, 0u, nseg, destuffed, seg_len, tabsets, coefs, epoch);
+                       dim3(RJ_WG), 0, st, imgs, nimg, 0u, nseg, destuffed, tabsets, coefs, epoch);
   }
   return hipGetLastError();
 }

@@ -7,16 +7,15 @@
 
 namespace rj {
 
-// K0: byte-unstuffing of every restart interval (one wavefront per interval).
-hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nseg, uint8_t *destuffed,
-                         uint32_t *seg_len);
+// K0: byte-unstuffing of the entropy-coded data (one wavefront per RjDsBlock).
+hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nblocks, uint8_t *destuffed);
 
 // K1 (rj_entropy.hip): Huffman entropy decode -> sparse entry streams + pieces.  stage 0: one
 // lane per interval chunk; 1: sync resolution; 2: serial re-decode of the flagged intervals.
 // lanes_wg: lanes of intervals that fit one workgroup (laid out first); lanes_dev: the others.
 hipError_t LaunchEntropy(hipStream_t st, int stage, const RjImageDev *imgs, int nimg, uint32_t lanes_wg,
-                         uint32_t lanes_dev, uint32_t nseg, const uint8_t *destuffed, const uint32_t *seg_len,
-                         const RjTableSet *tabsets, RjCoefBuf coefs, uint32_t epoch);
+                         uint32_t lanes_dev, uint32_t nseg, const uint8_t *destuffed, const RjTableSet *tabsets,
+                         RjCoefBuf coefs, uint32_t epoch);
 
 // K2b (general path): every output format / ROI of rocjpeg_decoder.cpp:143-180 from the planes.
 hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobDev *jobs, int njobs, uint32_t total_rows,

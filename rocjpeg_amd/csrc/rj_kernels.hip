@@ -3,8 +3,9 @@
 // Replaces the VCN fixed-function decode of the reference (src/rocjpeg_vaapi_decoder.cpp:
 // 574-692) and rewrites its post-processing kernels (src/rocjpeg_hip_kernels.cpp).
 //
-//   K0 k_destuff      one wavefront per restart interval: coalesced byte loads, FF00/fill
-//                     removal by per-lane keep masks + wave prefix sum, compacted stores.
+//   K0 k_destuff      one wavefront per 2-KB block of entropy-coded bytes (output offsets from
+//                     the host parser): FF00/fill removal by per-lane keep masks + wave prefix
+//                     sum, compacted stores.
 //   K1 k_entropy      (rj_entropy.hip) Huffman decode, one lane per interval chunk, with
 //                     self-synchronising speculative chunks for long intervals.
 //   K2 k_rows         (rj_fused.hip) one wave per MCU row: entry stream -> LDS blocks ->
@@ -40,23 +41,26 @@ __device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v, uint32_t lan
 // (b[i] == 00 && b[i-1] == FF) or (b[i] == FF && b[i+1] == FF).
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ imgs, int nimg,
-                                                uint8_t *__restrict__ destuffed, uint32_t *__restrict__ seg_len) {
+                                                uint8_t *__restrict__ destuffed) {
   const uint32_t g = blockIdx.x;
   const uint32_t lane = threadIdx.x;
-  const int i = upper_index(nimg, g, [&](int k) { return imgs[k].seg_prefix; });
+  const int i = __builtin_amdgcn_readfirstlane(upper_index(nimg, g, [&](int k) { return imgs[k].ds_prefix; }));
   const RjImageDev &im = imgs[i];
-  const RjSegDev sg = gp(im.segs)[g - im.seg_prefix];
-  const RJ_GLOBAL uint8_t *src = gp(im.ecs + sg.src_off);
-  uint8_t *dst = destuffed + im.destuff_off + sg.dst_off;
-  const uint32_t len = sg.src_len;
+  const RjDsBlock blk = gp(im.ds)[g - im.ds_prefix];
+  const RJ_GLOBAL uint8_t *src = gp(im.ecs + blk.src_off);
+  uint8_t *dst = destuffed + im.destuff_off + blk.dst_off;
+  const bool first = (blk.len >> 31) != 0;  // first block of its interval
+  const uint32_t len = blk.len & 0x7FFFFFFFu;
+  const bool last = blk.zero_end != 0;
   uint32_t out = 0;
-  uint32_t prev_byte = 0;  // byte before the current 256-B chunk
+  uint32_t prev_byte = first ? 0u : uint32_t(src[-1]);  // byte before the current 256-B chunk
   for (uint32_t base = 0; base < len; base += 256) {
     const uint32_t p = base + 4 * lane;
     uint32_t b[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) b[k] = (p + k < len) ? src[p + k] : 0x100u;  // 0x100 = past the end
-    const uint32_t nb_next = (base + 256 < len) ? src[base + 256] : 0x100u;
+    // the byte after this chunk: inside the block, the next block's first byte, or past the end
+    const uint32_t nb_next = (base + 256 < len) ? src[base + 256] : ((base + 256 == len && !last) ? src[len] : 0x100u);
     uint32_t prev = __shfl_up(b[3], 1, 64);
     if (lane == 0) prev = prev_byte;
     uint32_t next = __shfl_down(b[0], 1, 64);
@@ -65,7 +69,9 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t pv = k == 0 ? prev : b[k - 1];
-      const uint32_t nx = k == 3 ? next : b[k + 1];
+      uint32_t nx = k == 3 ? next : b[k + 1];
+      // the block's last byte: its successor is the next block's first byte (or past the end)
+      if (p + k + 1 == len) nx = last ? 0x100u : uint32_t(src[len]);
       const bool drop = b[k] == 0x100u || (b[k] == 0x00u && pv == 0xFFu) || (b[k] == 0xFFu && nx == 0xFFu);
       keep |= (drop ? 0u : 1u) << k;
     }
@@ -73,21 +79,21 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
     uint32_t o = wave_exclusive_scan(__popc(keep), lane, total) + out;
 #pragma unroll
     for (int k = 0; k < 4; k++)
-      if (keep & (1u << k)) dst[o++] = uint8_t(b[k]);
+      if (keep & (1u << k)) gp(dst)[o++] = uint8_t(b[k]);
     out += total;
     prev_byte = __shfl(b[3], 63, 64);
   }
-  // zero the slack after the data (>= 16 B, see rj_stream.cpp BuildPlan): K1 reads whole 16-B
-  // chunks and must see zero bits past the end, as libjpeg inserts after a marker
-  const uint32_t pad_end = (len + 16u + 15u) & ~15u;
-  for (uint32_t b = out + lane; b < pad_end; b += 64) dst[b] = 0;
-  if (lane == 0) seg_len[g] = out;
+  // last block: zero the interval's slack after the data (>= 16 B, rj_stream.cpp BuildPlan):
+  // K1 reads whole 16-B chunks and must see zero bits past the end, as libjpeg inserts
+  if (last) {
+    uint8_t *base = destuffed + im.destuff_off;
+    for (uint32_t q = blk.dst_off + out + lane; q < blk.zero_end; q += 64) gp(base)[q] = 0;
+  }
 }
 
-hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nseg, uint8_t *destuffed,
-                         uint32_t *seg_len) {
-  if (nseg == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_destuff, dim3(nseg), dim3(64), 0, st, imgs, nimg, destuffed, seg_len);
+hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nblocks, uint8_t *destuffed) {
+  if (nblocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_destuff, dim3(nblocks), dim3(64), 0, st, imgs, nimg, destuffed);
   return hipGetLastError();
 }
 

@@ -306,13 +306,32 @@ void Stream::BuildPlan() {
   const uint32_t n = s.ecs_size;
   uint32_t start = 0, i = 0;
   uint64_t dst = 0, ent = 0;
+  // bytes the destuffing drops (the 00 of FF 00, a fill FF followed by FF), in stream order
+  std::vector<uint32_t> drops;
+  size_t dq = 0;
   auto emit = [&](uint32_t b, uint32_t stop) {
     while (stop > b && e[stop - 1] == 0xFF) stop--;  // trailing fill
     if (p.segs.size() >= expected) return;
     RjSegDev sg;
+    std::memset(&sg, 0, sizeof(sg));
     sg.src_off = b;
     sg.src_len = stop - b;
     sg.dst_off = uint32_t(dst);
+    // K0 blocks: output offset of each = its raw offset minus the bytes dropped before it
+    while (dq < drops.size() && drops[dq] < b) dq++;
+    uint32_t dropped = 0;
+    for (uint32_t o = 0; o < sg.src_len; o += RJ_DS_BLOCK) {
+      const uint32_t blen = std::min(RJ_DS_BLOCK, sg.src_len - o);
+      RjDsBlock blk;
+      blk.src_off = b + o;
+      blk.len = blen | (o == 0 ? 0x80000000u : 0u);  // high bit: first block of the interval
+      blk.dst_off = sg.dst_off + o - dropped;
+      blk.zero_end = 0;
+      while (dq < drops.size() && drops[dq] < b + o + blen) { dq++; dropped++; }
+      p.ds.push_back(blk);
+    }
+    sg.dst_len = sg.src_len - dropped;
+    if (sg.src_len) p.ds.back().zero_end = uint32_t(dst + ((uint64_t(sg.src_len) + 16 + 15) & ~uint64_t(15)));
     sg.mcu_first = uint32_t(p.segs.size()) * (ri ? ri : total_mcus);
     sg.mcu_count = ri ? std::min(ri, total_mcus - sg.mcu_first) : total_mcus;
     sg.flags = 0;
@@ -333,8 +352,10 @@ void Stream::BuildPlan() {
     if (i + 1 >= n) break;
     const uint8_t m = e[i + 1];
     if (m == 0x00) {
+      drops.push_back(i + 1);
       i += 2;
     } else if (m == 0xFF) {
+      drops.push_back(i);
       i += 1;
     } else if (ri && m >= 0xD0 && m <= 0xD7) {
       emit(start, std::min(i, cut));
@@ -349,6 +370,7 @@ void Stream::BuildPlan() {
   emit(start, std::min(n, cut));
   while (p.segs.size() < expected) {  // intervals whose RST marker never came: zero blocks
     RjSegDev sg;
+    std::memset(&sg, 0, sizeof(sg));
     sg.src_off = n;
     sg.src_len = 0;
     sg.dst_off = uint32_t(dst);
@@ -373,6 +395,7 @@ void Stream::ReleaseResident() {
       (void)hipSetDevice(resident.device);
       (void)hipFree(resident.ecs);
       (void)hipFree(resident.segs);
+      (void)hipFree(resident.ds);
       (void)hipSetDevice(cur);
     }
   }

@@ -47,6 +47,7 @@ struct DecodePlan {
   uint8_t comp_blk0[4] = {};
   uint32_t wblk[4] = {}, hblk[4] = {};
   std::vector<RjSegDev> segs;      // one per restart interval
+  std::vector<RjDsBlock> ds;       // K0 blocks over all intervals
   uint64_t destuff_bytes = 0;      // destuffed buffer size incl. per-interval alignment
   uint64_t entries = 0;            // sparse-coefficient entries reserved (worst case)
   uint32_t nchunks = 0;            // K1 lanes (chunks) over all intervals
@@ -73,6 +74,7 @@ class Stream {
     uint64_t generation = 0;
     uint8_t *ecs = nullptr;
     RjSegDev *segs = nullptr;
+    RjDsBlock *ds = nullptr;
   } resident;
   void ReleaseResident();
   ~Stream() { ReleaseResident(); }
