@@ -398,17 +398,22 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   }
 
   // ---- K1 lane layout (rj_device.h RjCoefBuf): one lane per chunk; an interval of at most
-  // RJ_K1_WG chunks never straddles a workgroup (padding lanes), longer ones go after them ----
-  std::vector<uint32_t> seg_lane0(seg_total);
-  uint32_t lanes_wg = 0, split_intervals = 0;
-  {
+  // RJ_K1_WG chunks never straddles a workgroup (padding lanes), longer ones go after them.
+  // Common case -- no interval split -- is the identity (lane = interval), nothing uploaded. ----
+  bool any_split = false;
+  for (int i = 0; i < n && !any_split; i++) any_split = streams[i]->plan().nchunks != streams[i]->plan().segs.size();
+  std::vector<uint32_t> seg_lane0, lane_seg;
+  uint32_t lanes_wg = seg_total, split_intervals = 0;
+  if (any_split) {
+    seg_lane0.resize(seg_total);
+    lanes_wg = 0;
     uint32_t gs = 0;
     for (int i = 0; i < n; i++)
       for (const RjSegDev &sg : streams[i]->plan().segs) {
         const uint32_t nch = rj_chunks(sg.src_len);
         split_intervals += nch > 1 ? 1u : 0u;
         if (nch <= RJ_K1_WG) {
-          if (lanes_wg % RJ_K1_WG + nch > RJ_K1_WG) lanes_wg = AlignUp(lanes_wg, RJ_K1_WG);
+          if (lanes_wg % RJ_K1_WG + nch > RJ_K1_WG) lanes_wg = uint32_t(AlignUp(lanes_wg, RJ_K1_WG));
           seg_lane0[gs] = lanes_wg;
           lanes_wg += nch;
         } else {
@@ -416,10 +421,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         }
         gs++;
       }
+    lanes_wg = uint32_t(AlignUp(lanes_wg, RJ_K1_WG));
   }
-  lanes_wg = uint32_t(AlignUp(lanes_wg, RJ_K1_WG));
   uint32_t lanes_all = lanes_wg;
-  {
+  if (any_split) {
     uint32_t gs = 0;
     for (int i = 0; i < n; i++)
       for (const RjSegDev &sg : streams[i]->plan().segs) {
@@ -429,11 +434,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         }
         gs++;
       }
-  }
-  const uint32_t lanes_dev = lanes_all - lanes_wg;
-  std::vector<uint32_t> lane_seg(lanes_all, UINT32_MAX);
-  {
-    uint32_t gs = 0;
+    lane_seg.assign(lanes_all, UINT32_MAX);
+    gs = 0;
     for (int i = 0; i < n; i++)
       for (const RjSegDev &sg : streams[i]->plan().segs) {
         const uint32_t nch = rj_chunks(sg.src_len);
@@ -441,6 +443,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         gs++;
       }
   }
+  const uint32_t lanes_dev = lanes_all - lanes_wg;
 
   // ---- one host->device upload: descriptors + non-resident bitstreams ----
   const uint64_t off_imgs = 0;
@@ -449,8 +452,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t off_rows = AlignUp(off_jobs + std::max<size_t>(jobs.size(), 1) * sizeof(RjJobDev), 256);
   const uint64_t off_grows = AlignUp(off_rows + n * sizeof(uint32_t), 256);
   const uint64_t off_lane_seg = AlignUp(off_grows + n * sizeof(uint32_t), 256);
-  const uint64_t off_seg_lane0 = AlignUp(off_lane_seg + uint64_t(lanes_all) * 4, 256);
-  const uint64_t off_stage = AlignUp(off_seg_lane0 + uint64_t(seg_total) * 4, 256);
+  const uint64_t off_seg_lane0 = AlignUp(off_lane_seg + uint64_t(lane_seg.size()) * 4, 256);
+  const uint64_t off_stage = AlignUp(off_seg_lane0 + uint64_t(seg_lane0.size()) * 4, 256);
   const uint64_t blob = off_stage + stage_bytes;
   RJ_CHECK(h_stage_.Ensure(blob));
   RJ_CHECK(d_desc_.Ensure(blob));
@@ -497,10 +500,15 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (!jobs.empty()) std::memcpy(h + off_jobs, jobs.data(), jobs.size() * sizeof(RjJobDev));
   std::memcpy(h + off_rows, row_prefix.data(), n * sizeof(uint32_t));
   std::memcpy(h + off_grows, grow_prefix.data(), n * sizeof(uint32_t));
-  std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(lanes_all) * 4);
-  std::memcpy(h + off_seg_lane0, seg_lane0.data(), uint64_t(seg_total) * 4);
-  cbuf.lane_seg = reinterpret_cast<const uint32_t *>(dbase + off_lane_seg);
-  cbuf.seg_lane0 = reinterpret_cast<const uint32_t *>(dbase + off_seg_lane0);
+  if (any_split) {
+    std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(lane_seg.size()) * 4);
+    std::memcpy(h + off_seg_lane0, seg_lane0.data(), uint64_t(seg_lane0.size()) * 4);
+    cbuf.lane_seg = reinterpret_cast<const uint32_t *>(dbase + off_lane_seg);
+    cbuf.seg_lane0 = reinterpret_cast<const uint32_t *>(dbase + off_seg_lane0);
+  } else {  // identity layout
+    cbuf.lane_seg = nullptr;
+    cbuf.seg_lane0 = nullptr;
+  }
   const uint32_t *d_rows = reinterpret_cast<const uint32_t *>(dbase + off_rows);
   const uint32_t *d_grows = reinterpret_cast<const uint32_t *>(dbase + off_grows);
 

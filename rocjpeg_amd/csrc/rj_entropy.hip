@@ -386,14 +386,14 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
   int i = 0;
   uint32_t gseg = 0, c = 0, nch = 1;
   if (pending) {
-    gseg = kFallback ? g : gp(coefs.lane_seg)[g];
+    gseg = kFallback ? g : rj_lane_seg(coefs, g);
     pending = kFallback ? gp(coefs.fallback)[g] != 0 : gseg != 0xFFFFFFFFu;
   }
   if (pending) {
     i = upper_index(nimg, gseg, [&](int q) { return imgs[q].seg_prefix; });
     if (!kFallback) {
       nch = rj_chunks(gp(imgs[i].segs)[gseg - imgs[i].seg_prefix].src_len);
-      c = nch - 1 - (g - gp(coefs.seg_lane0)[gseg]);  // reverse order: later chunks on earlier lanes
+      c = nch - 1 - (g - rj_seg_lane0(coefs, gseg));  // reverse order: later chunks on earlier lanes
     }
   }
   const RjImageDev &im = imgs[i];
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
       const uint8_t *data = destuffed + im.destuff_off + sg.dst_off;
       uint32_t *ent_base = coefs.ent + im.ent_off + sg.ent_off;
       const uint64_t ent_abs = im.ent_off + sg.ent_off;
-      const uint32_t lane_first = gp(coefs.seg_lane0)[gseg];
+      const uint32_t lane_first = rj_seg_lane0(coefs, gseg);
       const RjTableSet *ts = tabsets + T;
       LaneJob J;
       J.nbits = nbytes * 8u;
@@ -496,7 +496,7 @@ __global__ __launch_bounds__(256) void k_resolve(const RjImageDev *__restrict__ 
   bool ok = true;
   if (nch > 1) {
     const uint32_t total = sg.mcu_count * im.nblk_mcu;
-    const uint32_t lane_first = gp(coefs.seg_lane0)[g];  // lane of chunk c: lane_first + nch-1-c
+    const uint32_t lane_first = rj_seg_lane0(coefs, g);  // lane of chunk c: lane_first + nch-1-c
     const uint64_t rcap = rj_chunk_cap(rj_chunk_len(sg.src_len, nch));
     const uint64_t ent0 = im.ent_off + sg.ent_off;
     RjPiece *pieces = coefs.piece + lane_first;

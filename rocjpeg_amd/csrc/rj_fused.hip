@@ -115,14 +115,14 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
   for (uint32_t moves = 0; done < need && moves < (1u << 16); moves++) {  // bounded on corrupt pieces
     if (nv.bleft == 0) {  // next piece, or the first piece of the next interval (synchronous reload)
       if (nv.seg >= im.nseg) break;
-      const RjPiece *pb = coefs.piece + gp(coefs.seg_lane0)[im.seg_prefix + nv.seg];
+      const RjPiece *pb = coefs.piece + rj_seg_lane0(coefs, im.seg_prefix + nv.seg);
       if (nv.pj + 1 < gp(pb)->npieces) {
         nv.pj++;
       } else {
         nv.seg++;
         nv.pj = 0;
         if (nv.seg >= im.nseg) break;
-        pb = coefs.piece + gp(coefs.seg_lane0)[im.seg_prefix + nv.seg];
+        pb = coefs.piece + rj_seg_lane0(coefs, im.seg_prefix + nv.seg);
       }
       nv.take(pb + nv.pj);
       win.load(ent, nv.cur(), lane);
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
     nv.seg = U(ri ? (my * mcux) / ri : 0);
     const RjSegDev sg = gp(im.segs)[nv.seg];
     const uint32_t rel = (my * mcux - sg.mcu_first) * nblk;
-    const RjPiece *pb = coefs.piece + gp(coefs.seg_lane0)[im.seg_prefix + nv.seg];
+    const RjPiece *pb = coefs.piece + rj_seg_lane0(coefs, im.seg_prefix + nv.seg);
     const uint32_t np = U(min(gp(pb)->npieces, 4096u));
     uint32_t pj = 0;
     while (pj + 1 < np && U(gp(pb + pj + 1)->first_blk) <= rel) pj++;

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rj_device.h"
+
 namespace rj {
 
 // Global-address-space views of generic pointers.  Pointers read from descriptors are generic,
@@ -44,6 +46,14 @@ __device__ __forceinline__ const RJ_GLOBAL T *gp(const T *p) {
 #define RJ_FIX_3_072711026 25172
 
 __device__ __forceinline__ int32_t m24(int32_t a, int32_t k) { return __mul24(a, k); }
+
+// K1 lane layout lookups (RjCoefBuf); null tables mean the identity layout
+__device__ __forceinline__ uint32_t rj_lane_seg(const RjCoefBuf &c, uint32_t lane) {
+  return c.lane_seg ? *gp(c.lane_seg + lane) : lane;
+}
+__device__ __forceinline__ uint32_t rj_seg_lane0(const RjCoefBuf &c, uint32_t seg) {
+  return c.seg_lane0 ? *gp(c.seg_lane0 + seg) : seg;
+}
 
 // index of the last entry with prefix <= key (prefix[0] == 0, monotone)
 template <typename F>
