@@ -42,6 +42,9 @@ typedef struct {
   uint32_t chunks;           /* K1 lanes */
   uint32_t split_intervals;  /* intervals decoded in more than one chunk */
   uint32_t serial_fallbacks; /* of those, re-decoded serially (counted when profiling) */
+  uint32_t pipe_groups;      /* interval length classes of a pipelined launch (1: sequential
+                                K1 -> K2; >1: huffman_ms ends at the last class's K1 and idct_ms
+                                is the K2 work left after it) */
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);

@@ -9,7 +9,8 @@ import enum
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librocjpeg_amd.so")
+# RJ_LIB_PATH: an experimental build variant of the same library (development A/B runs)
+LIB_PATH = os.environ.get("RJ_LIB_PATH") or os.path.join(_HERE, "librocjpeg_amd.so")
 
 # exported symbols declared by include/rocjpeg.h and include/rocjpeg_amd.h
 API_SYMBOLS = (
@@ -86,7 +87,7 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("host_ms", ctypes.c_float), ("entropy_chunks_ms", ctypes.c_float),
                 ("entropy_resolve_ms", ctypes.c_float), ("entropy_serial_ms", ctypes.c_float),
                 ("chunks", ctypes.c_uint32), ("split_intervals", ctypes.c_uint32),
-                ("serial_fallbacks", ctypes.c_uint32)]
+                ("serial_fallbacks", ctypes.c_uint32), ("pipe_groups", ctypes.c_uint32)]
 
 
 class RocJpegError(RuntimeError):

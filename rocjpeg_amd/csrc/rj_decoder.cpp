@@ -98,6 +98,14 @@ Decoder::~Decoder() {
     (void)hipStreamSynchronize(stream_);
     for (auto &e : ev_)
       if (e) (void)hipEventDestroy(e);
+    for (auto &e : pev_)
+      if (e) (void)hipEventDestroy(e);
+    for (auto &e : pk1_)
+      if (e) (void)hipEventDestroy(e);
+    for (auto &e : kev_)
+      if (e) (void)hipEventDestroy(e);
+    for (auto &q : pstream_)
+      if (q) (void)hipStreamDestroy(q);
     (void)hipStreamDestroy(stream_);
   }
 }
@@ -123,6 +131,13 @@ int Decoder::Initialize() {
   }
   RJ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   for (auto &e : ev_) RJ_HIP(hipEventCreate(&e));
+  if (const char *g = getenv("RJ_PIPE_GROUPS")) pipe_groups_ = std::max(1, std::min(kMaxPipe, atoi(g)));
+  if (const char *m = getenv("RJ_PIPE_MIN")) pipe_min_ = uint32_t(std::max(1, atoi(m)));
+  if (const char *o = getenv("RJ_SORT_LANES")) sort_lanes_ = atoi(o) != 0;
+  for (auto &q : pstream_) RJ_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+  for (auto &e : pev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto &e : pk1_) RJ_HIP(hipEventCreate(&e));
+  for (auto &e : kev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   (void)backend_;  // HARDWARE and HYBRID both run the HIP decoder
   return kOk;
 }
@@ -231,6 +246,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   std::vector<uint64_t> stage_off(n, UINT64_MAX);
   std::vector<uint32_t> row_prefix(n), grow_prefix(n);  // K2 rows: fused images / general images
   uint32_t fused_rows = 0, general_rows = 0, fused_images = 0;
+  std::vector<uint8_t> is_fused(n, 0);
   for (int i = 0; i < n; i++) {
     Stream *s = streams[i];
     const StreamInfo &in = s->info();
@@ -388,6 +404,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       jobs.resize(jobs_before);
       fused_rows += p.mcuy;  // k_fused: one workgroup per MCU row
       fused_images++;
+      is_fused[i] = 1;
     } else {
       for (int c = 0; c < in.ncomp; c++) {
         d.plane_off[c] = plane_bytes;
@@ -445,6 +462,81 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   }
   const uint32_t lanes_dev = lanes_all - lanes_wg;
 
+  // ---- lane order (no interval split): K1 is issue-bound and a wave lasts as long as its
+  // longest lane, so lanes are sorted by interval length (shortest first; 32-B buckets) -- the
+  // lanes of a wave then do about equal work.
+  // Pipelined launch: the sorted lanes are cut into `ngroups` classes of equal count; class g's
+  // K1 lanes run on stream g, then the K2 rows of class g once K1 of classes 0..g is done, so
+  // K2 work overlaps the K1 tail.  A row's class = the latest class among the intervals it
+  // touches (a row can span intervals of several classes). ----
+  const bool sorted = !any_split && sort_lanes_ && (seg_total >= 256 || seg_total >= pipe_min_);
+  int ngroups = 1;
+  if (sorted && pipe_groups_ > 1 && seg_total >= pipe_min_) ngroups = pipe_groups_;
+  uint32_t lane_off[kMaxPipe + 1] = {}, frow_off[kMaxPipe + 1] = {}, grow_off[kMaxPipe + 1] = {};
+  uint32_t class_max[kMaxPipe] = {};  // longest interval (bytes) of each class
+  std::vector<uint2> row_list;
+  if (sorted) {
+    constexpr uint32_t kBuckets = 4096;  // 32-B length buckets up to 128 KB
+    auto bucket = [](uint32_t len) { return std::min<uint32_t>(len >> 5, kBuckets - 1); };
+    std::vector<uint32_t> pos(kBuckets, 0);
+    for (int i = 0; i < n; i++)
+      for (const RjSegDev &sg : streams[i]->plan().segs) pos[bucket(sg.src_len)]++;
+    for (uint32_t b = 0, cum = 0; b < kBuckets; b++) {
+      const uint32_t c = pos[b];
+      pos[b] = cum;
+      cum += c;
+    }
+    std::vector<uint32_t> seg_pos(seg_total);
+    lane_seg.resize(seg_total);
+    uint32_t gs = 0;
+    for (int i = 0; i < n; i++)
+      for (const RjSegDev &sg : streams[i]->plan().segs) {
+        const uint32_t l = pos[bucket(sg.src_len)]++;
+        lane_seg[l] = gs;
+        seg_pos[gs++] = l;
+      }
+    for (int g = 0; g <= ngroups; g++) lane_off[g] = uint32_t(uint64_t(seg_total) * g / ngroups);
+    if (ngroups > 1) {
+      auto class_of = [&](uint32_t l) {  // no division in the per-interval loop
+        uint8_t g = 0;
+        while (g + 1 < ngroups && l >= lane_off[g + 1]) g++;
+        return g;
+      };
+      std::vector<uint8_t> row_group(uint64_t(fused_rows) + general_rows, 0);
+      uint32_t frow_cnt[kMaxPipe] = {}, grow_cnt[kMaxPipe] = {};
+      gs = 0;
+      for (int i = 0; i < n; i++) {
+        const DecodePlan &p = streams[i]->plan();
+        uint8_t *rg = row_group.data() + (is_fused[i] ? row_prefix[i] : fused_rows + grow_prefix[i]);
+        for (const RjSegDev &sg : p.segs) {
+          const uint8_t g = class_of(seg_pos[gs++]);
+          class_max[g] = std::max(class_max[g], sg.src_len);
+          if (sg.mcu_count == 0 || p.mcux == 0) continue;
+          const uint32_t r0 = sg.mcu_first / p.mcux;
+          const uint32_t r1 = std::min<uint32_t>((sg.mcu_first + sg.mcu_count - 1) / p.mcux, p.mcuy - 1);
+          for (uint32_t r = r0; r <= r1; r++) rg[r] = std::max(rg[r], g);
+        }
+        for (uint32_t r = 0; r < p.mcuy; r++) (is_fused[i] ? frow_cnt : grow_cnt)[rg[r]]++;
+      }
+      for (int g = 0; g < ngroups; g++) {
+        frow_off[g + 1] = frow_off[g] + frow_cnt[g];
+        grow_off[g + 1] = grow_off[g] + grow_cnt[g];
+      }
+      uint32_t fpos[kMaxPipe], gpos[kMaxPipe];
+      for (int g = 0; g < ngroups; g++) {
+        fpos[g] = frow_off[g];
+        gpos[g] = fused_rows + grow_off[g];
+      }
+      row_list.resize(uint64_t(fused_rows) + general_rows);
+      for (int i = 0; i < n; i++) {
+        const DecodePlan &p = streams[i]->plan();
+        const uint8_t *rg = row_group.data() + (is_fused[i] ? row_prefix[i] : fused_rows + grow_prefix[i]);
+        uint32_t *wp = is_fused[i] ? fpos : gpos;
+        for (uint32_t r = 0; r < p.mcuy; r++) row_list[wp[rg[r]]++] = uint2{uint32_t(i), r};
+      }
+    }
+  }
+
   // ---- one host->device upload: descriptors + non-resident bitstreams ----
   const uint64_t off_imgs = 0;
   const uint64_t off_tabs = AlignUp(off_imgs + n * sizeof(RjImageDev), 256);
@@ -453,7 +545,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t off_grows = AlignUp(off_rows + n * sizeof(uint32_t), 256);
   const uint64_t off_lane_seg = AlignUp(off_grows + n * sizeof(uint32_t), 256);
   const uint64_t off_seg_lane0 = AlignUp(off_lane_seg + uint64_t(lane_seg.size()) * 4, 256);
-  const uint64_t off_stage = AlignUp(off_seg_lane0 + uint64_t(seg_lane0.size()) * 4, 256);
+  const uint64_t off_row_list = AlignUp(off_seg_lane0 + uint64_t(seg_lane0.size()) * 4, 256);
+  const uint64_t off_stage = AlignUp(off_row_list + uint64_t(row_list.size()) * sizeof(uint2), 256);
   const uint64_t blob = off_stage + stage_bytes;
   RJ_CHECK(h_stage_.Ensure(blob));
   RJ_CHECK(d_desc_.Ensure(blob));
@@ -505,10 +598,16 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     std::memcpy(h + off_seg_lane0, seg_lane0.data(), uint64_t(seg_lane0.size()) * 4);
     cbuf.lane_seg = reinterpret_cast<const uint32_t *>(dbase + off_lane_seg);
     cbuf.seg_lane0 = reinterpret_cast<const uint32_t *>(dbase + off_seg_lane0);
+  } else if (sorted) {  // lanes in length order; pieces stay at the interval's own slot
+    std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(lane_seg.size()) * 4);
+    cbuf.lane_seg = reinterpret_cast<const uint32_t *>(dbase + off_lane_seg);
+    cbuf.seg_lane0 = nullptr;
   } else {  // identity layout
     cbuf.lane_seg = nullptr;
     cbuf.seg_lane0 = nullptr;
   }
+  if (!row_list.empty()) std::memcpy(h + off_row_list, row_list.data(), row_list.size() * sizeof(uint2));
+  const uint2 *d_row_list = reinterpret_cast<const uint2 *>(dbase + off_row_list);
   const uint32_t *d_rows = reinterpret_cast<const uint32_t *>(dbase + off_rows);
   const uint32_t *d_grows = reinterpret_cast<const uint32_t *>(dbase + off_grows);
 
@@ -522,14 +621,41 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
   RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[2], stream_));
-  for (int stage = 0; stage < 3; stage++) {
-    RJ_HIP(LaunchEntropy(stream_, stage, d_imgs, n, lanes_wg, lanes_dev, seg_total, d_destuff_.as<uint8_t>(), d_tabs,
-                        cbuf, epoch_));
-    if (profiling_ && stage < 2) RJ_HIP(hipEventRecord(ev_[6 + stage], stream_));
+  if (ngroups > 1) {
+    RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0 done
+    if (getenv("RJ_DEBUG_PIPE_SERIAL")) {  // development: each class's K1 alone, one after another
+      for (int g = 0; g < ngroups; g++) {
+        RJ_HIP(LaunchEntropyLanes(stream_, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g],
+                                  d_destuff_.as<uint8_t>(), d_tabs, cbuf, epoch_));
+        if (profiling_) RJ_HIP(hipEventRecord(pk1_[g], stream_));
+      }
+    }
+    for (int g = 0; g < ngroups && !getenv("RJ_DEBUG_PIPE_SERIAL"); g++) {
+      hipStream_t st = g == ngroups - 1 ? stream_ : pstream_[g];
+      if (st != stream_) RJ_HIP(hipStreamWaitEvent(st, pev_[kMaxPipe - 1], 0));
+      RJ_HIP(LaunchEntropyLanes(st, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g], d_destuff_.as<uint8_t>(),
+                                d_tabs, cbuf, epoch_));
+      if (profiling_) RJ_HIP(hipEventRecord(pk1_[g], st));
+      RJ_HIP(hipEventRecord(kev_[g], st));
+      for (int q = 0; q < g; q++) RJ_HIP(hipStreamWaitEvent(st, kev_[q], 0));  // rows spanning classes
+      RJ_HIP(LaunchRows(st, false, d_imgs, n, d_rows, d_row_list + frow_off[g], frow_off[g + 1] - frow_off[g], cbuf,
+                        d_tabs, nullptr));
+      RJ_HIP(LaunchRows(st, true, d_imgs, n, d_grows, d_row_list + fused_rows + grow_off[g],
+                        grow_off[g + 1] - grow_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>()));
+      if (st != stream_) RJ_HIP(hipEventRecord(pev_[g], st));
+    }
+    for (int g = 0; g + 1 < ngroups; g++) RJ_HIP(hipStreamWaitEvent(stream_, pev_[g], 0));
+  } else {
+    for (int stage = 0; stage < 3; stage++) {
+      RJ_HIP(LaunchEntropy(stream_, stage, d_imgs, n, lanes_wg, lanes_dev, seg_total, d_destuff_.as<uint8_t>(),
+                           d_tabs, cbuf, epoch_));
+      if (profiling_ && stage < 2) RJ_HIP(hipEventRecord(ev_[6 + stage], stream_));
+    }
+    if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
+    RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr));
+    RJ_HIP(LaunchRows(stream_, true, d_imgs, n, d_grows, nullptr, general_rows, cbuf, d_tabs,
+                      d_planes_.as<uint8_t>()));
   }
-  if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
-  RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, fused_rows, cbuf, d_tabs, nullptr));
-  RJ_HIP(LaunchRows(stream_, true, d_imgs, n, d_grows, general_rows, cbuf, d_tabs, d_planes_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[4], stream_));
   RJ_HIP(LaunchOutputJobs(stream_, d_imgs, d_jobs, int(jobs.size()), rows_total, d_planes_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[5], stream_));
@@ -539,25 +665,53 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   timings_.intervals = seg_total;
   timings_.chunks = lanes_all;
   timings_.split_intervals = split_intervals;
+  timings_.pipe_groups = uint32_t(ngroups);
   timings_.ecs_bytes = ecs_bytes;
   timings_.coef_bytes = coef_blocks * 128;  // dense-equivalent; the sparse bytes are data-dependent
   timings_.output_bytes = out_bytes;
   timings_.fused_images = fused_images;
   if (profiling_) {
     float ms[5];
-    for (int k = 0; k < 5; k++) RJ_HIP(hipEventElapsedTime(&ms[k], ev_[k], ev_[k + 1]));
+    RJ_HIP(hipEventElapsedTime(&ms[0], ev_[0], ev_[1]));
+    RJ_HIP(hipEventElapsedTime(&ms[1], ev_[1], ev_[2]));
+    RJ_HIP(hipEventElapsedTime(&ms[4], ev_[4], ev_[5]));
+    RJ_HIP(hipEventElapsedTime(&timings_.total_ms, ev_[0], ev_[5]));
+    if (ngroups > 1) {  // K1 ends with the last class; K2 of the earlier classes overlaps it
+      float k1 = 0, k12 = 0;
+      for (int g = 0; g < ngroups; g++) {
+        float t = 0;
+        RJ_HIP(hipEventElapsedTime(&t, ev_[2], pk1_[g]));
+        k1 = std::max(k1, t);
+      }
+      RJ_HIP(hipEventElapsedTime(&k12, ev_[2], ev_[4]));
+      if (getenv("RJ_DEBUG_K1")) {
+        float prev = 0;
+        for (int g = 0; g < ngroups; g++) {
+          float t = 0;
+          RJ_HIP(hipEventElapsedTime(&t, ev_[2], pk1_[g]));
+          fprintf(stderr, "[rj] class %d: %u lanes, max %u B, K1 end %.3f ms (+%.3f)\n", g,
+                  lane_off[g + 1] - lane_off[g], class_max[g], t, t - prev);
+          prev = t;
+        }
+      }
+      ms[2] = k1;
+      ms[3] = k12 - k1;
+      timings_.entropy_chunks_ms = k1;
+    } else {
+      RJ_HIP(hipEventElapsedTime(&ms[2], ev_[2], ev_[3]));
+      RJ_HIP(hipEventElapsedTime(&ms[3], ev_[3], ev_[4]));
+      RJ_HIP(hipEventElapsedTime(&timings_.entropy_chunks_ms, ev_[2], ev_[6]));
+      RJ_HIP(hipEventElapsedTime(&timings_.entropy_resolve_ms, ev_[6], ev_[7]));
+      RJ_HIP(hipEventElapsedTime(&timings_.entropy_serial_ms, ev_[7], ev_[3]));
+      std::vector<uint32_t> fb(seg_total);
+      RJ_HIP(hipMemcpy(fb.data(), d_fallback_.as<uint32_t>(), fb.size() * 4, hipMemcpyDeviceToHost));
+      for (uint32_t f : fb) timings_.serial_fallbacks += f ? 1u : 0u;
+    }
     timings_.h2d_ms = ms[0];
     timings_.destuff_ms = ms[1];
     timings_.huffman_ms = ms[2];
     timings_.idct_ms = ms[3];
     timings_.output_ms = ms[4];
-    RJ_HIP(hipEventElapsedTime(&timings_.total_ms, ev_[0], ev_[5]));
-    RJ_HIP(hipEventElapsedTime(&timings_.entropy_chunks_ms, ev_[2], ev_[6]));
-    RJ_HIP(hipEventElapsedTime(&timings_.entropy_resolve_ms, ev_[6], ev_[7]));
-    RJ_HIP(hipEventElapsedTime(&timings_.entropy_serial_ms, ev_[7], ev_[3]));
-    std::vector<uint32_t> fb(seg_total);
-    RJ_HIP(hipMemcpy(fb.data(), d_fallback_.as<uint32_t>(), fb.size() * 4, hipMemcpyDeviceToHost));
-    for (uint32_t f : fb) timings_.serial_fallbacks += f ? 1u : 0u;
     if (getenv("RJ_DEBUG_K1")) {  // development diagnostics of the chunked decode
       std::vector<RjChunkRes> cr(lanes_all);
       RJ_HIP(hipMemcpy(cr.data(), d_chunkres_.as<RjChunkRes>(), cr.size() * sizeof(RjChunkRes), hipMemcpyDeviceToHost));

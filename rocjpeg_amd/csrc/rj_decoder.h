@@ -68,6 +68,16 @@ class Decoder {
   int path_policy_ = 0;
   RocJpegAmdTimings timings_ = {};
   hipEvent_t ev_[8] = {};  // 0..5 stage boundaries, 6..7 inside K1
+  // pipelined launch (rj_decoder.cpp): interval length classes 0..pipe_groups_-2 on pstream_,
+  // the last class on stream_; pev_ joins them (no timing), pk1_ times each class's K1
+  static constexpr int kMaxPipe = 4;  // = HIP's default hardware queues per process
+  int pipe_groups_ = kMaxPipe;     // env RJ_PIPE_GROUPS (1 = sequential)
+  uint32_t pipe_min_ = 2048;       // env RJ_PIPE_MIN: fewest intervals worth pipelining
+  bool sort_lanes_ = true;         // env RJ_SORT_LANES=0: K1 lanes in interval order
+  hipStream_t pstream_[kMaxPipe - 1] = {};
+  hipEvent_t pev_[kMaxPipe] = {};
+  hipEvent_t pk1_[kMaxPipe] = {};
+  hipEvent_t kev_[kMaxPipe] = {};  // K1 of class g done (K2 of later classes waits on it)
 
   DeviceBuffer d_desc_, d_stage_, d_destuff_, d_entries_, d_planes_;
   DeviceBuffer d_piece_, d_rec_, d_chunkres_, d_fallback_;  // K1 chunk bookkeeping

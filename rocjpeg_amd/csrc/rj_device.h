@@ -81,7 +81,9 @@ struct RjCoefBuf {
 
 // Chunking of an interval of `bytes` raw entropy-coded bytes: about RJ_CHUNK_BYTES per lane;
 // intervals below two chunks are decoded by one lane with the exact serial semantics.
+#ifndef RJ_CHUNK_BYTES
 #define RJ_CHUNK_BYTES 8192u
+#endif
 #define RJ_OVERLAP_CHUNKS 3u      // a lane may decode this many chunk lengths past its own end
 #define RJ_CHUNK_ENT_PER_BYTE 4u  // region budget of a chunk lane (typical ~1.7); overflow -> serial path
 __host__ __device__ inline uint32_t rj_chunks(uint32_t bytes) {

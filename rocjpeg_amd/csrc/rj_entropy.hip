@@ -170,6 +170,153 @@ struct LaneJob {
   uint32_t mcux, mcu_first, mcu_count;
 };
 
+// empty asm with a read-write VGPR operand: the value is computed unconditionally before it,
+// which keeps selects on it as v_cndmask (otherwise the structurizer may sink each operand's
+// computation into its own branch, with the exec-mask SALU that brings)
+__device__ __forceinline__ void opaque(uint32_t &v) { asm volatile("" : "+v"(v)); }
+
+// 32 zero bytes: what the exact decoder reads past the end of an interval's data
+__device__ const uint4 rj_zero_chunks[RJ_PREFETCH] = {};
+
+// Exact serial decode of one whole interval (one lane).  Every lane of the wave runs the same
+// number of symbol steps per phase (no per-lane loop exit: a lane that has finished its blocks
+// keeps stepping with its effects masked), and the per-symbol bookkeeping is select-only, so
+// the loop carries no exec-mask juggling.  Past the data the ring receives zero chunks -- the
+// zero bits libjpeg inserts -- so the refill needs no end-of-data test.
+__device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, uint32_t nblk, const uint16_t *s_lut,
+                                             const RjTableSet *ts, uint32_t *ring, uint32_t *stage) {
+  BitReader br;
+  br.init(J.src, ring, J.bytes);
+  for (uint32_t q = br.cm; q < RJ_RING_CHUNKS; q++) reinterpret_cast<uint4 *>(ring)[q] = make_uint4(0, 0, 0, 0);
+  br.cm = RJ_RING_CHUNKS;  // chunks past the data count as committed zero chunks
+  br.cms = 0;
+  uint32_t ne = 0, fl = 0;
+  int pred0 = 0, pred1 = 0, pred2 = 0;
+  bool skip = J.missing;
+  uint32_t blocks_left = J.blocks;
+  uint32_t b = 0;
+  uint32_t info = uint32_t(binfo) & 15u;
+  uint32_t acbase = RJ_SLUT_AC0 + ((info >> 3) & 1u) * RJ_LUT_ENTRIES;
+  uint32_t tbase = ((info >> 2) & 1u) * RJ_LUT_L1;  // table of the next symbol (DC of block 0)
+  uint32_t k = 0;
+  // row checkpoints every `every` MCU rows of the interval (piece slots permitting)
+  uint32_t np = 1, pfirst = 0, bdone = 0;
+  const uint32_t r0 = J.mcu_first / J.mcux;
+  const uint32_t rows = (J.mcu_first + J.mcu_count - 1) / J.mcux - r0 + 1;
+  const uint32_t every = (rows + J.slots - 1) / J.slots;
+  uint32_t to_row = J.mcux - (J.mcu_first - r0 * J.mcux);  // MCUs until the next row starts
+  uint32_t rows_left = every;
+  while (__builtin_amdgcn_ballot_w64(blocks_left > 0) != 0) {
+    // ---- phase start (wave-uniform): prefetch (zero chunks past the data), stage flush ----
+    const uint32_t used = br.cm - (br.rd >> 2);
+    const uint32_t n = min(RJ_RING_CHUNKS - used, uint32_t(RJ_PREFETCH));
+    const uint4 pf0 = *gp(br.cm < br.nchunks ? br.src + br.cm : rj_zero_chunks);
+    const uint4 pf1 = *gp(br.cm + 1 < br.nchunks ? br.src + br.cm + 1 : rj_zero_chunks + 1);
+    if (ne - fl >= RJ_ENT_GROUP) {
+      const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
+      uint4 *d4 = reinterpret_cast<uint4 *>(J.ent + fl);
+#pragma unroll
+      for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = s4[q];
+      fl += RJ_ENT_GROUP;
+    }
+    for (uint32_t step = 0; step < RJ_PHASE; step++) {
+      const bool act = blocks_left > 0;
+      // refill (32 bits when <= 32 are left); the ring always holds the next words
+      const bool need = br.nb <= 32;
+      br.acc |= uint64_t(__builtin_bswap32(need ? br.nw : 0u)) << ((32 - br.nb) & 63);
+      br.nb += need ? 32 : 0;
+      br.rd += need ? 1u : 0u;
+      br.rdw = need ? (br.rdw == RJ_RING_WORDS - 1 ? 0u : br.rdw + 1u) : br.rdw;
+      br.nw = ring[br.rdw];
+      const uint32_t peek32 = uint32_t(br.acc >> 32);
+      const bool isdc = k == 0;
+      uint32_t e = s_lut[tbase + (peek32 >> 23)];
+      if (e & 0x8000u) {
+        if (e != 0xFFFFu && !isdc) {
+          e = s_lut[tbase + RJ_LUT_L1 + (e & 0x7Fu) * 128u + ((peek32 >> 16) & 127u)];
+        } else {
+          const RjHuffDev *t = isdc ? &ts->dc[(info >> 2) & 1u] : &ts->ac[(info >> 3) & 1u];
+          e = huff_slow(t, peek32 >> 16);
+        }
+      }
+      const uint32_t len = e >> 8, sym = e & 255u;
+      const uint32_t sz = sym & 15u, r = sym >> 4;
+      const uint32_t raw = __builtin_amdgcn_ubfe(peek32, 32u - len - sz, sz);
+      const int val = int(raw) + (int32_t(raw - (1u << ((sz - 1) & 31))) >> 31 & int32_t(1u - (1u << sz)));
+      br.acc <<= (len + sz);
+      br.nb -= int(len + sz);
+      const uint32_t c = info & 3u;
+      const int p = (c == 0 ? pred0 : (c == 1 ? pred1 : pred2)) + val;
+      pred0 = (isdc && c == 0) ? p : pred0;
+      pred1 = (isdc && c == 1) ? p : pred1;
+      pred2 = (isdc && c == 2) ? p : pred2;
+      const uint32_t kk = isdc ? 0u : k + r;  // zigzag position of this coefficient
+      // AC: EOB (size 0, run != 15) ends the block; ZRL and coefficients advance k to kk + 1
+      const bool eob = !isdc && sz == 0 && r != 15;
+      uint32_t entry = (uint32_t(isdc ? p : val) & 0xFFFFu) | (min(kk, 63u) << 16);
+      bool emit = isdc || sz != 0;
+      uint32_t knew = kk + 1u;
+      opaque(knew);
+      knew = eob ? 64u : knew;
+      entry = skip ? 0u : entry;  // libjpeg: the rest of the interval decodes to zero blocks
+      emit = skip || emit;
+      knew = skip ? 64u : knew;
+      stage[ne & (RJ_STAGE - 1)] = entry;  // a non-emitted write lands in the next free slot
+      ne += (emit && act) ? 1u : 0u;
+      const bool bend = knew >= 64u;
+      const uint32_t bn = b + 1 == nblk ? 0u : b + 1;
+      const bool mcuend = bend && bn == 0;
+      k = bend ? 0u : knew;
+      b = bend ? bn : b;
+      info = uint32_t(binfo >> (4 * b)) & 15u;
+      acbase = RJ_SLUT_AC0 + ((info >> 3) & 1u) * RJ_LUT_ENTRIES;
+      uint32_t dcb = ((info >> 2) & 1u) * RJ_LUT_L1;
+      opaque(dcb);  // both operands materialised: the select stays a v_cndmask, not a branch
+      opaque(acbase);
+      tbase = bend ? dcb : acbase;
+      const bool done_blk = bend && act;
+      blocks_left -= done_blk ? 1u : 0u;
+      bdone += done_blk ? 1u : 0u;
+      skip = skip || (mcuend && br.consumed() > J.nbits);
+      to_row -= (mcuend && act) ? 1u : 0u;
+      if (to_row == 0) {  // the next MCU starts a row (rare)
+        to_row = J.mcux;
+        if (--rows_left == 0) {
+          rows_left = every;
+          if (blocks_left && np < J.slots) {  // checkpoint: a new piece starts here
+            gp(J.pieces + np - 1)->nblk = bdone - pfirst;
+            *gp(J.pieces + np) = RjPiece{J.ent_abs + ne, bdone, 0u, 0u, {0, 0, 0}};
+            pfirst = bdone;
+            np++;
+          }
+        }
+      }
+    }
+    // ---- phase end: the prefetch lands in the ring (zero chunks past the data) ----
+    uint4 *r4 = reinterpret_cast<uint4 *>(ring);
+    if (n > 0) {
+      r4[br.cms] = pf0;
+      br.cms = br.cms == RJ_RING_CHUNKS - 1 ? 0 : br.cms + 1;
+    }
+    if (n > 1) {
+      r4[br.cms] = pf1;
+      br.cms = br.cms == RJ_RING_CHUNKS - 1 ? 0 : br.cms + 1;
+    }
+    br.cm += n;
+    br.nw = ring[br.rdw];
+  }
+  stage[ne & (RJ_STAGE - 1)] = RJ_ENT_TERM;
+  while (fl < ne + 1) {
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
+    uint4 *d4 = reinterpret_cast<uint4 *>(J.ent + fl);
+#pragma unroll
+    for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = s4[q];
+    fl += RJ_ENT_GROUP;
+  }
+  gp(J.pieces + np - 1)->nblk = bdone - pfirst;
+  gp(J.pieces)->npieces = np;
+}
+
 template <bool kSplit, int kScope>
 __device__ __forceinline__ void decode_lane(const LaneJob &J, uint64_t binfo, uint32_t nblk, uint32_t epoch,
                                             const uint16_t *s_lut, const RjTableSet *ts, uint32_t *ring,
@@ -205,6 +352,12 @@ __device__ __forceinline__ void decode_lane(const LaneJob &J, uint64_t binfo, ui
     put_record<kScope>(J.rec, J.start_bit, 0u, epoch, 0u, 0u, 0, 0, 0);
     nrec = 1;
   }
+  // a record taken mid-phase is stored at the next phase start: a store issued inside the
+  // symbol loop would hold up the phase-end wait for the prefetch (vmcnt counts stores too).
+  // Records are >= 8 blocks (>= 16 symbols, two phases) apart, so one register copy suffices.
+  bool rp = false;
+  uint32_t rp_pos = 0, rp_b = 0, rp_ne = 0, rp_rb = 0;
+  int rp_p0 = 0, rp_p1 = 0, rp_p2 = 0;
   while (kSplit ? status == 0 : blocks_left > 0) {
     // ---- phase start (same count in every active lane): prefetch, record load, stage flush ----
     uint4 pf0, pf1;
@@ -217,6 +370,11 @@ __device__ __forceinline__ void decode_lane(const LaneJob &J, uint64_t binfo, ui
       const RjRecord *r = have ? J.rec_next - int64_t(t - 1) * RJ_MAX_RECORDS + j : J.rec;
       rec_ld = __hip_atomic_load(reinterpret_cast<const uint64_t *>(r), __ATOMIC_RELAXED, kScope);
       rec_ld_tj = have ? (t << 16 | j) : 0xFFFFFFFFu;
+    }
+    if (kSplit && rp) {
+      put_record<kScope>(J.rec + nrec, rp_pos, rp_b, epoch, rp_ne, rp_rb, rp_p0, rp_p1, rp_p2);
+      nrec++;
+      rp = false;
     }
     if (ne - fl >= RJ_ENT_GROUP) {  // one full 64-B group leaves the stage
       const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
@@ -298,8 +456,14 @@ __device__ __forceinline__ void decode_lane(const LaneJob &J, uint64_t binfo, ui
       rb++;
       const uint32_t pos = J.start_bit + br.consumed();
       if (J.spec && nrec < RJ_MAX_RECORDS && rb % RJ_RECORD_EVERY == 0 && pos < J.end_bit) {
-        put_record<kScope>(J.rec + nrec, pos, b, epoch, ne, rb, pred0, pred1, pred2);
-        nrec++;
+        rp = true;
+        rp_pos = pos;
+        rp_b = b;
+        rp_ne = ne;
+        rp_rb = rb;
+        rp_p0 = pred0;
+        rp_p1 = pred1;
+        rp_p2 = pred2;
       }
       if (pos >= next_tgt_bit && tgt < J.next_chunks) {  // entered the next later chunk
         tgt++;
@@ -332,6 +496,7 @@ __device__ __forceinline__ void decode_lane(const LaneJob &J, uint64_t binfo, ui
       cache_tj = rec_ld_tj;
     }
   }
+  if (kSplit && rp) put_record<kScope>(J.rec + nrec, rp_pos, rp_b, epoch, rp_ne, rp_rb, rp_p0, rp_p1, rp_p2);
   // terminator, then everything still staged (whole groups; the slack is reserved)
   stage[ne & (RJ_STAGE - 1)] = RJ_ENT_TERM;
   while (fl < ne + 1) {
@@ -453,7 +618,7 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
         J.mcu_first = sg.mcu_first;
         J.mcu_count = sg.mcu_count;
         *gp(J.pieces) = RjPiece{ent_abs, 0u, blocks, 1u, {0, 0, 0}};
-        decode_lane<false, kScope>(J, binfo, nblk, epoch, s_lut, ts, s_ring[tid], s_stage[tid], nullptr);
+        decode_exact(J, binfo, nblk, s_lut, ts, s_ring[tid], s_stage[tid]);
       } else {
         const uint32_t clen = rj_chunk_len(nbytes, nch);
         const uint32_t b0 = min(c * clen, nbytes), b1 = min(b0 + clen, nbytes);
@@ -550,6 +715,14 @@ hipError_t LaunchEntropy(hipStream_t st, int stage, const RjImageDev *imgs, int 
     hipLaunchKernelGGL((k_entropy<true, __HIP_MEMORY_SCOPE_WORKGROUP>), dim3((nseg + RJ_WG - 1) / RJ_WG),
                        dim3(RJ_WG), 0, st, imgs, nimg, 0u, nseg, destuffed, tabsets, coefs, epoch);
   }
+  return hipGetLastError();
+}
+
+hipError_t LaunchEntropyLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
+                              const uint8_t *destuffed, const RjTableSet *tabsets, RjCoefBuf coefs, uint32_t epoch) {
+  if (nlanes == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_entropy<false, __HIP_MEMORY_SCOPE_WORKGROUP>), dim3((nlanes + RJ_WG - 1) / RJ_WG), dim3(RJ_WG),
+                     0, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, coefs, epoch);
   return hipGetLastError();
 }
 

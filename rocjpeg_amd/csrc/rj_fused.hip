@@ -172,6 +172,7 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
 template <bool kPlanes>
 __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ imgs, int nimg,
                                              const uint32_t *__restrict__ row_prefix,
+                                             const uint2 *__restrict__ row_list,
                                              RjCoefBuf coefs,
                                              const RjTableSet *__restrict__ tabsets,
                                              uint8_t *__restrict__ planes) {
@@ -179,9 +180,14 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
   __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
 
   const uint32_t tid = threadIdx.x;
-  const uint32_t row = blockIdx.x;
   int i;
-  {
+  uint32_t my;  // MCU row inside image i
+  if (row_list != nullptr) {  // pipelined launch: an explicit (image, row) list for this group
+    const uint2 e = row_list[blockIdx.x];
+    i = int(U(e.x));
+    my = U(e.y);
+  } else {
+    const uint32_t row = blockIdx.x;
     int lo = 0, hi = nimg - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
@@ -189,13 +195,13 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
       else hi = mid - 1;
     }
     i = __builtin_amdgcn_readfirstlane(lo);  // wave-uniform: image fields become scalar loads
+    my = row - row_prefix[i];
   }
   const RjImageDev &im = imgs[i];
   const uint32_t hmax = U(im.hmax), vmax = U(im.vmax);
   const uint32_t mcu_w = 8 * hmax, mcu_h = 8 * vmax;
   const uint32_t nblk = U(im.nblk_mcu);
   const uint32_t S = U(rj_fused_strip_mcus(hmax, nblk));  // MCUs per strip
-  const uint32_t my = row - row_prefix[i];
   const bool inter = U(im.interleaved) != 0;
   const uint32_t ncomp = inter ? U(im.ncomp) : 1;
 
@@ -416,12 +422,15 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
 }
 
 hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
-                      uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets, uint8_t *planes) {
+                      const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
+                      uint8_t *planes) {
   if (nrows == 0) return hipSuccess;
   if (to_planes)
-    hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, coefs, tabsets, planes);
+    hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs, tabsets,
+                       planes);
   else
-    hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, coefs, tabsets, planes);
+    hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs, tabsets,
+                       planes);
   return hipGetLastError();
 }
 

@@ -17,15 +17,22 @@ hipError_t LaunchEntropy(hipStream_t st, int stage, const RjImageDev *imgs, int 
                          uint32_t lanes_dev, uint32_t nseg, const uint8_t *destuffed, const RjTableSet *tabsets,
                          RjCoefBuf coefs, uint32_t epoch);
 
+// K1 exact lanes [lane0, lane0 + nlanes) only (pipelined launch: no interval is split, so the
+// chunk pass alone is the whole entropy decode of those lanes' intervals).
+hipError_t LaunchEntropyLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
+                              const uint8_t *destuffed, const RjTableSet *tabsets, RjCoefBuf coefs, uint32_t epoch);
+
 // K2b (general path): every output format / ROI of rocjpeg_decoder.cpp:143-180 from the planes.
 hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobDev *jobs, int njobs, uint32_t total_rows,
                             const uint8_t *planes);
 
 // K2: one wavefront per MCU row (row_prefix[i] = first row of image i in this launch; images
-// with no rows in it have equal consecutive prefixes).  Sparse entries -> dequant + ISLOW IDCT
+// with no rows in it have equal consecutive prefixes; or, when row_list is given, wave w takes
+// the (image, MCU row) pair row_list[w]).  Sparse entries -> dequant + ISLOW IDCT
 // -> either the fused output (upsample + CSC / layout straight into the caller's buffers, only
 // for rj_decoder.cpp::FusedEligible images) or the MCU-padded component planes (to_planes).
 hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
-                      uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets, uint8_t *planes);
+                      const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
+                      uint8_t *planes);
 
 }  // namespace rj

@@ -204,3 +204,60 @@ def test_long_interval_batch_mixed(dec):
         ost, want = O.oracle_decode(d, int(R.OutputFormat.RGB), shapes)
         assert ost == 0
         assert G.first_mismatch(G.to_host(bufs)[0], want[0]) is None
+
+
+@pytest.fixture(scope="module", params=[(0, 4), (1, 4), (0, 1)], ids=["auto_g4", "general_g4", "auto_g1"])
+def pdec(request):
+    """A decoder that sorts the K1 lanes of every call with no split interval by length
+    (RJ_PIPE_MIN=1) and, with 4 groups, pipelines it: interval length classes on separate
+    streams, each class's K2 rows after the K1 lanes of its class and all earlier ones."""
+    import os
+    from tests import gpu_util as G
+    G.torch()
+    policy, groups = request.param
+    env = {"RJ_PIPE_MIN": "1", "RJ_PIPE_GROUPS": str(groups)}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        d = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    d.set_path_policy(policy)
+    d.groups = groups
+    d.set_profiling(True)
+    yield d
+    d.close()
+
+
+@pytest.mark.parametrize("fmt", [R.OutputFormat.RGB, R.OutputFormat.YUV_PLANAR, R.OutputFormat.NATIVE])
+def test_pipelined_batch_matches_oracle(pdec, fmt):
+    """Pipelined launch over a batch of restart-interval and short streams (no interval split):
+    rows of every length class, damaged variants included, byte-identical to the oracle."""
+    from tests import gpu_util as G
+    big = [e for e in DECODABLE if e["name"] == "p420_q90_ri_1920x1080"]
+    datas = [O.fixture_bytes(e) for e in SMALL for _ in range(3)]
+    for e in big:
+        d = O.fixture_bytes(e)
+        datas.append(d)
+        datas.extend(_variants(d).values())
+    streams = [R.JpegStream(d) for d in datas]
+    shapes_all, bufs_all, imgs = [], [], []
+    for s in streams:
+        nc, css, w, h = pdec.image_info(s)
+        shapes = G.channel_shapes(fmt, css, w, h)
+        bufs, img = G.gpu_buffers(shapes)
+        shapes_all.append(shapes)
+        bufs_all.append(bufs)
+        imgs.append(img)
+    assert pdec.decode_batched(streams, R.decode_params(fmt), imgs) == 0
+    t = pdec.last_timings()
+    assert t["split_intervals"] == 0 and t["pipe_groups"] == pdec.groups, (t["split_intervals"], t["pipe_groups"])
+    for k, (d, shapes, bufs) in enumerate(zip(datas, shapes_all, bufs_all)):
+        ost, want = O.oracle_decode(d, int(fmt), shapes)
+        assert ost == 0
+        for c, (g, w) in enumerate(zip(G.to_host(bufs), want)):
+            assert G.first_mismatch(g, w) is None, (k, c, G.first_mismatch(g, w))
