@@ -45,6 +45,8 @@ typedef struct {
   uint32_t pipe_groups;      /* interval length classes of a pipelined launch (1: sequential
                                 K1 -> K2; >1: huffman_ms ends at the last class's K1 and idct_ms
                                 is the K2 work left after it) */
+  uint32_t pipe_lane_rows;   /* pipelined K2 rows taken from the K1 lane order (every interval
+                                one MCU row) rather than from uploaded row lists */
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);

@@ -87,7 +87,8 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("host_ms", ctypes.c_float), ("entropy_chunks_ms", ctypes.c_float),
                 ("entropy_resolve_ms", ctypes.c_float), ("entropy_serial_ms", ctypes.c_float),
                 ("chunks", ctypes.c_uint32), ("split_intervals", ctypes.c_uint32),
-                ("serial_fallbacks", ctypes.c_uint32), ("pipe_groups", ctypes.c_uint32)]
+                ("serial_fallbacks", ctypes.c_uint32), ("pipe_groups", ctypes.c_uint32),
+                ("pipe_lane_rows", ctypes.c_uint32)]
 
 
 class RocJpegError(RuntimeError):

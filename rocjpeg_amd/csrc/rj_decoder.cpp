@@ -77,7 +77,7 @@ int PinnedBuffer::Ensure(size_t bytes) {
   if (bytes <= cap_) return kOk;
   Release();
   const size_t want = std::max<size_t>(AlignUp(bytes + bytes / 4, 1 << 20), 1 << 20);
-  if (hipHostMalloc(&ptr_, want, hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc(&ptr_, want, hipHostMallocNonCoherent) != hipSuccess) {
     ptr_ = nullptr;
     (void)hipGetLastError();
     return kOutOfMemory;
@@ -206,8 +206,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (p.status != 0) return p.status;
   }
 
+  const auto t_dedupe = std::chrono::steady_clock::now();
   // ---- table de-duplication ----
-  std::vector<uint32_t> tab_of(n);
+  std::vector<uint32_t> &tab_of = sc_.tab_of;
+  tab_of.resize(n);
   std::vector<const RjTableSet *> tabs;
   {
     std::vector<const DecodePlan *> owner;  // plan whose derived tables tabs[idx] points at
@@ -237,16 +239,23 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
   }
 
+  const auto t_layout = std::chrono::steady_clock::now();
   // ---- layout ----
-  std::vector<RjImageDev> imgs(n);
-  std::vector<RjJobDev> jobs;
+  std::vector<RjImageDev> &imgs = sc_.imgs;
+  imgs.resize(n);
+  std::vector<RjJobDev> &jobs = sc_.jobs;
+  jobs.clear();
   uint64_t destuff_total = 0, coef_blocks = 0, ent_total = 0, plane_bytes = 0, stage_bytes = 0;
   uint32_t seg_total = 0, rows_total = 0, chunk_total = 0, ds_total = 0;
   uint64_t ecs_bytes = 0, out_bytes = 0;
-  std::vector<uint64_t> stage_off(n, UINT64_MAX);
-  std::vector<uint32_t> row_prefix(n), grow_prefix(n);  // K2 rows: fused images / general images
+  std::vector<uint64_t> &stage_off = sc_.stage_off;
+  stage_off.assign(n, UINT64_MAX);
+  std::vector<uint32_t> &row_prefix = sc_.row_prefix, &grow_prefix = sc_.grow_prefix;  // K2 rows: fused / general
+  row_prefix.resize(n);
+  grow_prefix.resize(n);
   uint32_t fused_rows = 0, general_rows = 0, fused_images = 0;
-  std::vector<uint8_t> is_fused(n, 0);
+  std::vector<uint8_t> &is_fused = sc_.is_fused;
+  is_fused.assign(n, 0);
   for (int i = 0; i < n; i++) {
     Stream *s = streams[i];
     const StreamInfo &in = s->info();
@@ -414,12 +423,15 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
   }
 
+  const auto t_lanes = std::chrono::steady_clock::now();
   // ---- K1 lane layout (rj_device.h RjCoefBuf): one lane per chunk; an interval of at most
   // RJ_K1_WG chunks never straddles a workgroup (padding lanes), longer ones go after them.
   // Common case -- no interval split -- is the identity (lane = interval), nothing uploaded. ----
   bool any_split = false;
   for (int i = 0; i < n && !any_split; i++) any_split = streams[i]->plan().nchunks != streams[i]->plan().segs.size();
-  std::vector<uint32_t> seg_lane0, lane_seg;
+  std::vector<uint32_t> &seg_lane0 = sc_.seg_lane0, &lane_seg = sc_.lane_seg;
+  seg_lane0.clear();
+  lane_seg.clear();
   uint32_t lanes_wg = seg_total, split_intervals = 0;
   if (any_split) {
     seg_lane0.resize(seg_total);
@@ -462,92 +474,25 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   }
   const uint32_t lanes_dev = lanes_all - lanes_wg;
 
-  // ---- lane order (no interval split): K1 is issue-bound and a wave lasts as long as its
-  // longest lane, so lanes are sorted by interval length (shortest first; 32-B buckets) -- the
-  // lanes of a wave then do about equal work.
-  // Pipelined launch: the sorted lanes are cut into `ngroups` classes of equal count; class g's
-  // K1 lanes run on stream g, then the K2 rows of class g once K1 of classes 0..g is done, so
-  // K2 work overlaps the K1 tail.  A row's class = the latest class among the intervals it
-  // touches (a row can span intervals of several classes). ----
+  // ---- one pinned staging blob, uploaded in two parts: A (descriptors, tables, non-resident
+  // bitstreams) before K0; B (K1 lane order, K2 row lists) after K0 is launched -- the lane
+  // sort and row classes below are host work that then runs while K0 executes. ----
   const bool sorted = !any_split && sort_lanes_ && (seg_total >= 256 || seg_total >= pipe_min_);
   int ngroups = 1;
   if (sorted && pipe_groups_ > 1 && seg_total >= pipe_min_) ngroups = pipe_groups_;
-  uint32_t lane_off[kMaxPipe + 1] = {}, frow_off[kMaxPipe + 1] = {}, grow_off[kMaxPipe + 1] = {};
-  uint32_t class_max[kMaxPipe] = {};  // longest interval (bytes) of each class
-  std::vector<uint2> row_list;
-  if (sorted) {
-    constexpr uint32_t kBuckets = 4096;  // 32-B length buckets up to 128 KB
-    auto bucket = [](uint32_t len) { return std::min<uint32_t>(len >> 5, kBuckets - 1); };
-    std::vector<uint32_t> pos(kBuckets, 0);
-    for (int i = 0; i < n; i++)
-      for (const RjSegDev &sg : streams[i]->plan().segs) pos[bucket(sg.src_len)]++;
-    for (uint32_t b = 0, cum = 0; b < kBuckets; b++) {
-      const uint32_t c = pos[b];
-      pos[b] = cum;
-      cum += c;
-    }
-    std::vector<uint32_t> seg_pos(seg_total);
-    lane_seg.resize(seg_total);
-    uint32_t gs = 0;
-    for (int i = 0; i < n; i++)
-      for (const RjSegDev &sg : streams[i]->plan().segs) {
-        const uint32_t l = pos[bucket(sg.src_len)]++;
-        lane_seg[l] = gs;
-        seg_pos[gs++] = l;
-      }
-    for (int g = 0; g <= ngroups; g++) lane_off[g] = uint32_t(uint64_t(seg_total) * g / ngroups);
-    if (ngroups > 1) {
-      auto class_of = [&](uint32_t l) {  // no division in the per-interval loop
-        uint8_t g = 0;
-        while (g + 1 < ngroups && l >= lane_off[g + 1]) g++;
-        return g;
-      };
-      std::vector<uint8_t> row_group(uint64_t(fused_rows) + general_rows, 0);
-      uint32_t frow_cnt[kMaxPipe] = {}, grow_cnt[kMaxPipe] = {};
-      gs = 0;
-      for (int i = 0; i < n; i++) {
-        const DecodePlan &p = streams[i]->plan();
-        uint8_t *rg = row_group.data() + (is_fused[i] ? row_prefix[i] : fused_rows + grow_prefix[i]);
-        for (const RjSegDev &sg : p.segs) {
-          const uint8_t g = class_of(seg_pos[gs++]);
-          class_max[g] = std::max(class_max[g], sg.src_len);
-          if (sg.mcu_count == 0 || p.mcux == 0) continue;
-          const uint32_t r0 = sg.mcu_first / p.mcux;
-          const uint32_t r1 = std::min<uint32_t>((sg.mcu_first + sg.mcu_count - 1) / p.mcux, p.mcuy - 1);
-          for (uint32_t r = r0; r <= r1; r++) rg[r] = std::max(rg[r], g);
-        }
-        for (uint32_t r = 0; r < p.mcuy; r++) (is_fused[i] ? frow_cnt : grow_cnt)[rg[r]]++;
-      }
-      for (int g = 0; g < ngroups; g++) {
-        frow_off[g + 1] = frow_off[g] + frow_cnt[g];
-        grow_off[g + 1] = grow_off[g] + grow_cnt[g];
-      }
-      uint32_t fpos[kMaxPipe], gpos[kMaxPipe];
-      for (int g = 0; g < ngroups; g++) {
-        fpos[g] = frow_off[g];
-        gpos[g] = fused_rows + grow_off[g];
-      }
-      row_list.resize(uint64_t(fused_rows) + general_rows);
-      for (int i = 0; i < n; i++) {
-        const DecodePlan &p = streams[i]->plan();
-        const uint8_t *rg = row_group.data() + (is_fused[i] ? row_prefix[i] : fused_rows + grow_prefix[i]);
-        uint32_t *wp = is_fused[i] ? fpos : gpos;
-        for (uint32_t r = 0; r < p.mcuy; r++) row_list[wp[rg[r]]++] = uint2{uint32_t(i), r};
-      }
-    }
-  }
-
-  // ---- one host->device upload: descriptors + non-resident bitstreams ----
   const uint64_t off_imgs = 0;
   const uint64_t off_tabs = AlignUp(off_imgs + n * sizeof(RjImageDev), 256);
   const uint64_t off_jobs = AlignUp(off_tabs + tabs.size() * sizeof(RjTableSet), 256);
   const uint64_t off_rows = AlignUp(off_jobs + std::max<size_t>(jobs.size(), 1) * sizeof(RjJobDev), 256);
   const uint64_t off_grows = AlignUp(off_rows + n * sizeof(uint32_t), 256);
-  const uint64_t off_lane_seg = AlignUp(off_grows + n * sizeof(uint32_t), 256);
-  const uint64_t off_seg_lane0 = AlignUp(off_lane_seg + uint64_t(lane_seg.size()) * 4, 256);
+  const uint64_t off_stage = AlignUp(off_grows + n * sizeof(uint32_t), 256);
+  const uint64_t blob_a = AlignUp(off_stage + stage_bytes, 256);
+  const uint64_t n_lane_seg = any_split ? lane_seg.size() : (sorted ? seg_total : 0);
+  const uint64_t off_lane_seg = blob_a;
+  const uint64_t off_seg_lane0 = AlignUp(off_lane_seg + n_lane_seg * 4, 256);
   const uint64_t off_row_list = AlignUp(off_seg_lane0 + uint64_t(seg_lane0.size()) * 4, 256);
-  const uint64_t off_stage = AlignUp(off_row_list + uint64_t(row_list.size()) * sizeof(uint2), 256);
-  const uint64_t blob = off_stage + stage_bytes;
+  const uint64_t n_row_list = ngroups > 1 ? uint64_t(fused_rows) + general_rows : 0;  // upper bound
+  const uint64_t blob = AlignUp(off_row_list + n_row_list * sizeof(uint2), 256);
   RJ_CHECK(h_stage_.Ensure(blob));
   RJ_CHECK(d_desc_.Ensure(blob));
   RJ_CHECK(d_destuff_.Ensure(std::max<uint64_t>(destuff_total, 256)));
@@ -593,36 +538,145 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (!jobs.empty()) std::memcpy(h + off_jobs, jobs.data(), jobs.size() * sizeof(RjJobDev));
   std::memcpy(h + off_rows, row_prefix.data(), n * sizeof(uint32_t));
   std::memcpy(h + off_grows, grow_prefix.data(), n * sizeof(uint32_t));
+  const uint32_t *d_rows = reinterpret_cast<const uint32_t *>(dbase + off_rows);
+  const uint32_t *d_grows = reinterpret_cast<const uint32_t *>(dbase + off_grows);
+  const RjImageDev *d_imgs = reinterpret_cast<const RjImageDev *>(dbase + off_imgs);
+  const RjTableSet *d_tabs = reinterpret_cast<const RjTableSet *>(dbase + off_tabs);
+  const RjJobDev *d_jobs = reinterpret_cast<const RjJobDev *>(dbase + off_jobs);
+  const uint2 *d_row_list = reinterpret_cast<const uint2 *>(dbase + off_row_list);
+  const uint32_t *d_lane_seg = reinterpret_cast<const uint32_t *>(dbase + off_lane_seg);
+
+  const auto t_k0 = std::chrono::steady_clock::now();
+  if (profiling_) RJ_HIP(hipEventRecord(ev_[0], stream_));
+  RJ_HIP(hipMemcpyAsync(dbase, h, blob_a, hipMemcpyHostToDevice, stream_));
+  if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
+  RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>()));
+  if (profiling_) RJ_HIP(hipEventRecord(ev_[2], stream_));
+
+  // ---- (host, while K0 runs) lane order: with no interval split K1 is issue-bound and a wave
+  // lasts as long as its longest lane, so lanes are sorted by interval length (shortest first;
+  // 32-B buckets) -- the lanes of a wave then do about equal work.
+  // Pipelined launch: the sorted lanes are cut into `ngroups` classes of equal count; class g's
+  // K1 lanes run on stream g, then the K2 rows of class g once K1 of classes 0..g is done, so
+  // K2 work overlaps the K1 tail.  A row's class = the latest class among the intervals it
+  // touches (a row can span intervals of several classes).  When every interval of every image
+  // is exactly one MCU row and all rows take the same K2 path, class g's rows are its lanes'
+  // intervals (K2 reads lane_seg); otherwise explicit (image, row) lists are uploaded. ----
+  uint32_t lane_off[kMaxPipe + 1] = {}, frow_off[kMaxPipe + 1] = {}, grow_off[kMaxPipe + 1] = {};
+  uint32_t class_max[kMaxPipe] = {};  // longest interval (bytes) of each class
+  bool rows_from_lanes = false;
+  if (sorted) {
+    constexpr uint32_t kBuckets = 4096;  // 32-B length buckets up to 128 KB
+    auto bucket = [](uint32_t len) { return std::min<uint32_t>(len >> 5, kBuckets - 1); };
+    std::vector<uint32_t> &pos = sc_.bucket_pos;
+    pos.assign(kBuckets, 0);
+    bool aligned = fused_images == uint32_t(n) || fused_images == 0;
+    for (int i = 0; i < n; i++) {
+      const DecodePlan &p = streams[i]->plan();
+      aligned = aligned && p.segs.size() == p.mcuy;
+      uint32_t m = 0;
+      for (const RjSegDev &sg : p.segs) {
+        pos[bucket(sg.src_len)]++;
+        aligned = aligned && sg.mcu_first == m && sg.mcu_count == p.mcux;
+        m += p.mcux;
+      }
+    }
+    for (uint32_t b = 0, cum = 0; b < kBuckets; b++) {
+      const uint32_t c = pos[b];
+      pos[b] = cum;
+      cum += c;
+    }
+    lane_seg.resize(seg_total);  // built in cached memory, copied into the pinned blob below
+    uint32_t *ls = lane_seg.data();
+    std::vector<uint32_t> &seg_pos = sc_.seg_pos;
+    seg_pos.resize(seg_total);
+    uint32_t gs = 0;
+    for (int i = 0; i < n; i++)
+      for (const RjSegDev &sg : streams[i]->plan().segs) {
+        const uint32_t l = pos[bucket(sg.src_len)]++;
+        ls[l] = gs;
+        seg_pos[gs++] = l;
+      }
+    for (int g = 0; g <= ngroups; g++) lane_off[g] = uint32_t(uint64_t(seg_total) * g / ngroups);
+    rows_from_lanes = ngroups > 1 && aligned;
+    if (ngroups > 1) {
+      auto class_of = [&](uint32_t l) {  // no division in the per-interval loop
+        uint8_t g = 0;
+        while (g + 1 < ngroups && l >= lane_off[g + 1]) g++;
+        return g;
+      };
+      if (rows_from_lanes) {
+        for (int g = 0; g < ngroups; g++) {  // class g's rows = its lanes
+          frow_off[g + 1] = fused_images ? lane_off[g + 1] : 0;
+          grow_off[g + 1] = fused_images ? 0 : lane_off[g + 1];
+        }
+      } else {
+        std::vector<uint8_t> &row_group = sc_.row_group;
+        row_group.assign(uint64_t(fused_rows) + general_rows, 0);
+        uint32_t frow_cnt[kMaxPipe] = {}, grow_cnt[kMaxPipe] = {};
+        gs = 0;
+        for (int i = 0; i < n; i++) {
+          const DecodePlan &p = streams[i]->plan();
+          uint8_t *rg = row_group.data() + (is_fused[i] ? row_prefix[i] : fused_rows + grow_prefix[i]);
+          for (const RjSegDev &sg : p.segs) {
+            const uint8_t g = class_of(seg_pos[gs++]);
+            class_max[g] = std::max(class_max[g], sg.src_len);
+            if (sg.mcu_count == 0 || p.mcux == 0) continue;
+            const uint32_t r0 = sg.mcu_first / p.mcux;
+            const uint32_t r1 = std::min<uint32_t>((sg.mcu_first + sg.mcu_count - 1) / p.mcux, p.mcuy - 1);
+            for (uint32_t r = r0; r <= r1; r++) rg[r] = std::max(rg[r], g);
+          }
+          for (uint32_t r = 0; r < p.mcuy; r++) (is_fused[i] ? frow_cnt : grow_cnt)[rg[r]]++;
+        }
+        for (int g = 0; g < ngroups; g++) {
+          frow_off[g + 1] = frow_off[g] + frow_cnt[g];
+          grow_off[g + 1] = grow_off[g] + grow_cnt[g];
+        }
+        uint32_t fpos[kMaxPipe], gpos[kMaxPipe];
+        for (int g = 0; g < ngroups; g++) {
+          fpos[g] = frow_off[g];
+          gpos[g] = fused_rows + grow_off[g];
+        }
+        std::vector<uint2> &row_list = sc_.row_list;
+        row_list.resize(uint64_t(fused_rows) + general_rows);
+        uint2 *rl = row_list.data();
+        for (int i = 0; i < n; i++) {
+          const DecodePlan &p = streams[i]->plan();
+          const uint8_t *rg = row_group.data() + (is_fused[i] ? row_prefix[i] : fused_rows + grow_prefix[i]);
+          uint32_t *wp = is_fused[i] ? fpos : gpos;
+          for (uint32_t r = 0; r < p.mcuy; r++) rl[wp[rg[r]]++] = uint2{uint32_t(i), r};
+        }
+        std::memcpy(h + off_row_list, rl, row_list.size() * sizeof(uint2));
+      }
+    }
+  }
   if (any_split) {
     std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(lane_seg.size()) * 4);
     std::memcpy(h + off_seg_lane0, seg_lane0.data(), uint64_t(seg_lane0.size()) * 4);
-    cbuf.lane_seg = reinterpret_cast<const uint32_t *>(dbase + off_lane_seg);
+    cbuf.lane_seg = d_lane_seg;
     cbuf.seg_lane0 = reinterpret_cast<const uint32_t *>(dbase + off_seg_lane0);
   } else if (sorted) {  // lanes in length order; pieces stay at the interval's own slot
-    std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(lane_seg.size()) * 4);
-    cbuf.lane_seg = reinterpret_cast<const uint32_t *>(dbase + off_lane_seg);
+    std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(seg_total) * 4);
+    cbuf.lane_seg = d_lane_seg;
     cbuf.seg_lane0 = nullptr;
   } else {  // identity layout
     cbuf.lane_seg = nullptr;
     cbuf.seg_lane0 = nullptr;
   }
-  if (!row_list.empty()) std::memcpy(h + off_row_list, row_list.data(), row_list.size() * sizeof(uint2));
-  const uint2 *d_row_list = reinterpret_cast<const uint2 *>(dbase + off_row_list);
-  const uint32_t *d_rows = reinterpret_cast<const uint32_t *>(dbase + off_rows);
-  const uint32_t *d_grows = reinterpret_cast<const uint32_t *>(dbase + off_grows);
+  if (blob > blob_a) RJ_HIP(hipMemcpyAsync(dbase + blob_a, h + blob_a, blob - blob_a, hipMemcpyHostToDevice, stream_));
 
-  const RjImageDev *d_imgs = reinterpret_cast<const RjImageDev *>(dbase + off_imgs);
-  const RjTableSet *d_tabs = reinterpret_cast<const RjTableSet *>(dbase + off_tabs);
-  const RjJobDev *d_jobs = reinterpret_cast<const RjJobDev *>(dbase + off_jobs);
-
-  timings_.host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
-  if (profiling_) RJ_HIP(hipEventRecord(ev_[0], stream_));
-  RJ_HIP(hipMemcpyAsync(dbase, h, blob, hipMemcpyHostToDevice, stream_));
-  if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
-  RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>()));
-  if (profiling_) RJ_HIP(hipEventRecord(ev_[2], stream_));
+  const auto t_end = std::chrono::steady_clock::now();
+  timings_.host_ms = std::chrono::duration<float, std::milli>(t_end - t_host0).count();
+  if (getenv("RJ_DEBUG_HOST")) {  // development: where the host planning time goes
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    fprintf(stderr, "[rj host] validate %.3f dedupe %.3f layout %.3f lanes+blob-A %.3f sort/rows+blob-B %.3f ms\n",
+            ms(t_host0, t_dedupe), ms(t_dedupe, t_layout), ms(t_layout, t_lanes), ms(t_lanes, t_k0),
+            ms(t_k0, t_end));
+  }
   if (ngroups > 1) {
-    RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0 done
+    RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0 and upload B done
     if (getenv("RJ_DEBUG_PIPE_SERIAL")) {  // development: each class's K1 alone, one after another
       for (int g = 0; g < ngroups; g++) {
         RJ_HIP(LaunchEntropyLanes(stream_, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g],
@@ -638,10 +692,15 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       if (profiling_) RJ_HIP(hipEventRecord(pk1_[g], st));
       RJ_HIP(hipEventRecord(kev_[g], st));
       for (int q = 0; q < g; q++) RJ_HIP(hipStreamWaitEvent(st, kev_[q], 0));  // rows spanning classes
-      RJ_HIP(LaunchRows(st, false, d_imgs, n, d_rows, d_row_list + frow_off[g], frow_off[g + 1] - frow_off[g], cbuf,
-                        d_tabs, nullptr));
-      RJ_HIP(LaunchRows(st, true, d_imgs, n, d_grows, d_row_list + fused_rows + grow_off[g],
-                        grow_off[g + 1] - grow_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>()));
+      if (rows_from_lanes) {
+        RJ_HIP(LaunchRowsOfLanes(st, fused_images == 0, d_imgs, n, d_lane_seg + lane_off[g],
+                                 lane_off[g + 1] - lane_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>()));
+      } else {
+        RJ_HIP(LaunchRows(st, false, d_imgs, n, d_rows, d_row_list + frow_off[g], frow_off[g + 1] - frow_off[g],
+                          cbuf, d_tabs, nullptr));
+        RJ_HIP(LaunchRows(st, true, d_imgs, n, d_grows, d_row_list + fused_rows + grow_off[g],
+                          grow_off[g + 1] - grow_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>()));
+      }
       if (st != stream_) RJ_HIP(hipEventRecord(pev_[g], st));
     }
     for (int g = 0; g + 1 < ngroups; g++) RJ_HIP(hipStreamWaitEvent(stream_, pev_[g], 0));
@@ -666,6 +725,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   timings_.chunks = lanes_all;
   timings_.split_intervals = split_intervals;
   timings_.pipe_groups = uint32_t(ngroups);
+  timings_.pipe_lane_rows = rows_from_lanes ? 1u : 0u;
   timings_.ecs_bytes = ecs_bytes;
   timings_.coef_bytes = coef_blocks * 128;  // dense-equivalent; the sparse bytes are data-dependent
   timings_.output_bytes = out_bytes;

@@ -71,13 +71,25 @@ class Decoder {
   // pipelined launch (rj_decoder.cpp): interval length classes 0..pipe_groups_-2 on pstream_,
   // the last class on stream_; pev_ joins them (no timing), pk1_ times each class's K1
   static constexpr int kMaxPipe = 4;  // = HIP's default hardware queues per process
-  int pipe_groups_ = kMaxPipe;     // env RJ_PIPE_GROUPS (1 = sequential)
+  // 2 by default: the caller's own stream (e.g. torch's) takes a hardware queue too, and two
+  // streams sharing one queue serialise (measured: 4 classes sometimes double the K1 span)
+  int pipe_groups_ = 2;            // env RJ_PIPE_GROUPS (1 = sequential)
   uint32_t pipe_min_ = 2048;       // env RJ_PIPE_MIN: fewest intervals worth pipelining
   bool sort_lanes_ = true;         // env RJ_SORT_LANES=0: K1 lanes in interval order
   hipStream_t pstream_[kMaxPipe - 1] = {};
   hipEvent_t pev_[kMaxPipe] = {};
   hipEvent_t pk1_[kMaxPipe] = {};
   hipEvent_t kev_[kMaxPipe] = {};  // K1 of class g done (K2 of later classes waits on it)
+
+  // host planning scratch, reused across calls (no per-call allocation / page faults)
+  struct Scratch {
+    std::vector<RjImageDev> imgs;
+    std::vector<RjJobDev> jobs;
+    std::vector<uint64_t> stage_off;
+    std::vector<uint32_t> tab_of, row_prefix, grow_prefix, seg_lane0, lane_seg, bucket_pos, seg_pos;
+    std::vector<uint8_t> is_fused, row_group;
+    std::vector<uint2> row_list;
+  } sc_;
 
   DeviceBuffer d_desc_, d_stage_, d_destuff_, d_entries_, d_planes_;
   DeviceBuffer d_piece_, d_rec_, d_chunkres_, d_fallback_;  // K1 chunk bookkeeping

@@ -115,7 +115,8 @@ struct BitReader {
 // DC code longer than 9 bits): libjpeg jpeg_huff_decode on the table in HBM
 __device__ __forceinline__ uint32_t huff_slow(const RjHuffDev *t, uint32_t peek16) {
   uint32_t e = RJ_LUT_BAD;
-  for (int l = 1; l <= 16; l++)
+#pragma unroll 1
+  for (int l = 1; l <= 16; l++)  // a loop: rare path, kept small in the unrolled symbol loop
     if (peek16 < t->maxcode16[l]) {
       e = uint32_t(l << 8) | t->vals[((peek16 >> (16 - l)) + t->valoff[l]) & 255];
       break;
@@ -219,6 +220,11 @@ __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, u
       for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = s4[q];
       fl += RJ_ENT_GROUP;
     }
+#ifdef RJ_EXACT_NOUNROLL
+#pragma unroll 1
+#else
+#pragma unroll
+#endif
     for (uint32_t step = 0; step < RJ_PHASE; step++) {
       const bool act = blocks_left > 0;
       // refill (32 bits when <= 32 are left); the ring always holds the next words

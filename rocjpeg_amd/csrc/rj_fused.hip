@@ -173,6 +173,7 @@ template <bool kPlanes>
 __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ imgs, int nimg,
                                              const uint32_t *__restrict__ row_prefix,
                                              const uint2 *__restrict__ row_list,
+                                             const uint32_t *__restrict__ row_segs,
                                              RjCoefBuf coefs,
                                              const RjTableSet *__restrict__ tabsets,
                                              uint8_t *__restrict__ planes) {
@@ -186,6 +187,10 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
     const uint2 e = row_list[blockIdx.x];
     i = int(U(e.x));
     my = U(e.y);
+  } else if (row_segs != nullptr) {  // pipelined, every interval one MCU row: the class's intervals
+    const uint32_t gseg = U(row_segs[blockIdx.x]);
+    i = __builtin_amdgcn_readfirstlane(upper_index(nimg, gseg, [&](int q) { return imgs[q].seg_prefix; }));
+    my = U(gp(imgs[i].segs)[gseg - imgs[i].seg_prefix].mcu_first / imgs[i].mcux);
   } else {
     const uint32_t row = blockIdx.x;
     int lo = 0, hi = nimg - 1;
@@ -425,12 +430,28 @@ hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, in
                       const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
                       uint8_t *planes) {
   if (nrows == 0) return hipSuccess;
+  const uint32_t *no_segs = nullptr;
   if (to_planes)
-    hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs, tabsets,
-                       planes);
+    hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, no_segs, coefs,
+                       tabsets, planes);
   else
-    hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs, tabsets,
-                       planes);
+    hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, no_segs, coefs,
+                       tabsets, planes);
+  return hipGetLastError();
+}
+
+hipError_t LaunchRowsOfLanes(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg,
+                             const uint32_t *row_segs, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
+                             uint8_t *planes) {
+  if (nrows == 0) return hipSuccess;
+  const uint32_t *no_prefix = nullptr;
+  const uint2 *no_list = nullptr;
+  if (to_planes)
+    hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, no_prefix, no_list, row_segs, coefs,
+                       tabsets, planes);
+  else
+    hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, no_prefix, no_list, row_segs, coefs,
+                       tabsets, planes);
   return hipGetLastError();
 }
 

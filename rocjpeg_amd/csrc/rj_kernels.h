@@ -34,5 +34,10 @@ hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobD
 hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
                       const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
                       uint8_t *planes);
+// K2 over the MCU rows of the intervals row_segs[0, nrows) (batch-global interval indices), for
+// batches whose every interval is exactly one MCU row.
+hipError_t LaunchRowsOfLanes(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg,
+                             const uint32_t *row_segs, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
+                             uint8_t *planes);
 
 }  // namespace rj

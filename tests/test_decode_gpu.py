@@ -261,3 +261,36 @@ def test_pipelined_batch_matches_oracle(pdec, fmt):
         assert ost == 0
         for c, (g, w) in enumerate(zip(G.to_host(bufs), want)):
             assert G.first_mismatch(g, w) is None, (k, c, G.first_mismatch(g, w))
+
+
+@pytest.mark.parametrize("fmt", [R.OutputFormat.RGB, R.OutputFormat.YUV_PLANAR])
+def test_pipelined_row_aligned_batch(pdec, fmt):
+    """Every interval exactly one MCU row (DRI = MCUs per row): the pipelined K2 takes its rows
+    straight from the sorted K1 lane order.  Damaged variants included."""
+    from tests import gpu_util as G
+    datas = []
+    for e in DECODABLE:
+        if e["name"] in ("p420_q90_ri_1920x1080", "p420_trunc_192x128"):
+            d = O.fixture_bytes(e)
+            datas += [d, d]
+            if e["name"] == "p420_q90_ri_1920x1080":
+                datas.extend(_variants(d).values())
+    streams = [R.JpegStream(d) for d in datas]
+    shapes_all, bufs_all, imgs = [], [], []
+    for s in streams:
+        nc, css, w, h = pdec.image_info(s)
+        shapes = G.channel_shapes(fmt, css, w, h)
+        bufs, img = G.gpu_buffers(shapes)
+        shapes_all.append(shapes)
+        bufs_all.append(bufs)
+        imgs.append(img)
+    assert pdec.decode_batched(streams, R.decode_params(fmt), imgs) == 0
+    t = pdec.last_timings()
+    assert t["pipe_groups"] == pdec.groups
+    if pdec.groups > 1:
+        assert t["pipe_lane_rows"] == 1
+    for k, (d, shapes, bufs) in enumerate(zip(datas, shapes_all, bufs_all)):
+        ost, want = O.oracle_decode(d, int(fmt), shapes)
+        assert ost == 0
+        for c, (g, w) in enumerate(zip(G.to_host(bufs), want)):
+            assert G.first_mismatch(g, w) is None, (k, c, G.first_mismatch(g, w))
