@@ -167,7 +167,7 @@ int Decoder::StreamsToDevice(Stream *const *streams, int n) {
     Stream::Resident r;
     r.device = device_;
     r.generation = s->generation();
-    RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.ecs), std::max<size_t>(in.ecs_size, 16)));
+    RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.ecs), in.ecs_size + 16));  // K0 reads <= 8 B past the end
     RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.segs), std::max<size_t>(p.segs.size() * sizeof(RjSegDev), 16)));
     RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.ds), std::max<size_t>(p.ds.size() * sizeof(RjDsBlock), 16)));
     RJ_HIP(hipMemcpy(r.ecs, in.ecs, in.ecs_size, hipMemcpyHostToDevice));

@@ -42,6 +42,8 @@ __device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v, uint32_t lan
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ imgs, int nimg,
                                                 uint8_t *__restrict__ destuffed) {
+  static_assert(RJ_DS_BLOCK == 2048u, "8 chunks of 256 B per block");
+  constexpr int kIt = RJ_DS_BLOCK / 256;
   const uint32_t g = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   const int i = __builtin_amdgcn_readfirstlane(upper_index(nimg, g, [&](int k) { return imgs[k].ds_prefix; }));
@@ -52,15 +54,33 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
   const bool first = (blk.len >> 31) != 0;  // first block of its interval
   const uint32_t len = blk.len & 0x7FFFFFFFu;
   const bool last = blk.zero_end != 0;
+  // every load of the block is issued up front (one memory latency per block, not per chunk):
+  // lane l of chunk c takes bytes [256c + 4l, +4) from two aligned dwords (alignbyte), the
+  // dword index clamped into the block (the ECS buffers carry >= 16 B of slack)
+  const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(src)) & 3u;
+  const RJ_GLOBAL uint32_t *A = reinterpret_cast<const RJ_GLOBAL uint32_t *>(src - mis);
+  const uint32_t last_dw = len ? (len - 1 + mis) >> 2 : 0u;
+  uint32_t w[kIt];
+#pragma unroll
+  for (int c = 0; c < kIt; c++) {
+    const uint32_t q = min(uint32_t(c) * 64u + lane, last_dw);
+    w[c] = __builtin_amdgcn_alignbyte(A[q + 1], A[q], mis);
+  }
+  const uint32_t before = first ? 0u : uint32_t(src[-1]);       // byte in front of the block
+  const uint32_t after = last ? 0x100u : uint32_t(src[len]);     // byte behind it (0x100: none)
   uint32_t out = 0;
-  uint32_t prev_byte = first ? 0u : uint32_t(src[-1]);  // byte before the current 256-B chunk
-  for (uint32_t base = 0; base < len; base += 256) {
+  uint32_t prev_byte = before;  // byte in front of the current chunk
+#pragma unroll
+  for (int c = 0; c < kIt; c++) {
+    const uint32_t base = uint32_t(c) * 256u;
+    if (base >= len) break;  // wave-uniform
     const uint32_t p = base + 4 * lane;
     uint32_t b[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) b[k] = (p + k < len) ? src[p + k] : 0x100u;  // 0x100 = past the end
-    // the byte after this chunk: inside the block, the next block's first byte, or past the end
-    const uint32_t nb_next = (base + 256 < len) ? src[base + 256] : ((base + 256 == len && !last) ? src[len] : 0x100u);
+    for (int k = 0; k < 4; k++) b[k] = (p + k < len) ? (w[c] >> (8 * k)) & 255u : 0x100u;  // 0x100 = past the end
+    // the byte after this chunk: the next chunk's first byte, or the one behind the block
+    uint32_t nb_next = after;
+    if (c + 1 < kIt && base + 256 < len) nb_next = __builtin_amdgcn_readfirstlane(w[c + 1]) & 255u;
     uint32_t prev = __shfl_up(b[3], 1, 64);
     if (lane == 0) prev = prev_byte;
     uint32_t next = __shfl_down(b[0], 1, 64);
@@ -70,8 +90,7 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
     for (int k = 0; k < 4; k++) {
       const uint32_t pv = k == 0 ? prev : b[k - 1];
       uint32_t nx = k == 3 ? next : b[k + 1];
-      // the block's last byte: its successor is the next block's first byte (or past the end)
-      if (p + k + 1 == len) nx = last ? 0x100u : uint32_t(src[len]);
+      if (p + k + 1 == len) nx = after;  // the block's last byte
       const bool drop = b[k] == 0x100u || (b[k] == 0x00u && pv == 0xFFu) || (b[k] == 0xFFu && nx == 0xFFu);
       keep |= (drop ? 0u : 1u) << k;
     }
