@@ -61,7 +61,7 @@ struct BitReader {
     ring = r;
     nchunks = (nbytes + 15) / 16;
     const uint32_t first = nchunks < RJ_RING_CHUNKS ? nchunks : RJ_RING_CHUNKS;
-    for (uint32_t q = 0; q < first; q++) reinterpret_cast<uint4 *>(ring)[q] = gp(src)[q];
+    for (uint32_t q = 0; q < first; q++) put4(q, gp(src)[q]);
     cm = first;
     cms = first == RJ_RING_CHUNKS ? 0 : first;
     rd = 0;
@@ -86,14 +86,20 @@ struct BitReader {
     pf1 = gp(src)[cm + 1 < last ? cm + 1 : last];
     return n;
   }
+  __device__ __forceinline__ void put4(uint32_t slot, const uint4 &v) {  // ring rows are 4-B aligned
+    uint32_t *r = ring + 4 * slot;
+    r[0] = v.x;
+    r[1] = v.y;
+    r[2] = v.z;
+    r[3] = v.w;
+  }
   __device__ __forceinline__ void commit(const uint4 &pf0, const uint4 &pf1, uint32_t n) {
-    uint4 *r4 = reinterpret_cast<uint4 *>(ring);
     if (n > 0) {
-      r4[cms] = pf0;
+      put4(cms, pf0);
       cms = cms == RJ_RING_CHUNKS - 1 ? 0 : cms + 1;
     }
     if (n > 1) {
-      r4[cms] = pf1;
+      put4(cms, pf1);
       cms = cms == RJ_RING_CHUNKS - 1 ? 0 : cms + 1;
     }
     cm += n;
@@ -182,15 +188,41 @@ __device__ const uint4 rj_zero_chunks[RJ_PREFETCH] = {};
 // Exact serial decode of one whole interval (one lane).  Every lane of the wave runs the same
 // number of symbol steps per phase (no per-lane loop exit: a lane that has finished its blocks
 // keeps stepping with its effects masked), and the per-symbol bookkeeping is select-only, so
-// the loop carries no exec-mask juggling.  Past the data the ring receives zero chunks -- the
-// zero bits libjpeg inserts -- so the refill needs no end-of-data test.
+// the loop carries no exec-mask juggling.
+// Bits: a 32-word LDS ring (+ a mirror of word 0 at index 32) of big-endian stream words,
+// read at random bit positions: word i = pos >> 5 and the next one (one ds_read2_b32) and a
+// 64-bit shift by pos & 31 give the 32-bit peek -- no refill state.  Chunks are byte-swapped
+// once, when they land in the ring; past the data the ring receives zero chunks (the zero
+// bits libjpeg inserts).  Ring invariant: >= 8 unread words at every phase start (a phase
+// reads <= 8: 8 symbols of <= 27 bits plus the next word); with U unread words a phase
+// commits n = min(2, 8 - live chunks) chunks and reads <= 7: U >= 16 keeps U' >= 9, and
+// 8 <= U < 16 means <= 4 live chunks, so n = 2 and U' >= U + 1.
+// kCkpt: MCU-row checkpoint pieces (the serial fallback of long intervals); the main pass's
+// exact lanes have one piece slot and skip that bookkeeping.
+#define RJ_XRING_CHUNKS 8
+#define RJ_XRING_WORDS (RJ_XRING_CHUNKS * 4)
+#define RJ_XRING_STRIDE (RJ_XRING_WORDS + 1)  // odd: random per-lane words spread over the banks
+
+__device__ __forceinline__ void xring_put(uint32_t *ring, uint32_t slot, const uint4 &v) {
+  const uint32_t w0 = __builtin_bswap32(v.x), w1 = __builtin_bswap32(v.y);
+  const uint32_t w2 = __builtin_bswap32(v.z), w3 = __builtin_bswap32(v.w);
+  uint32_t *r = ring + 4 * slot;
+  r[0] = w0;
+  r[1] = w1;
+  r[2] = w2;
+  r[3] = w3;
+  if (slot == 0) ring[RJ_XRING_WORDS] = w0;  // mirror: word 31's successor
+}
+
+template <bool kCkpt>
 __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, uint32_t nblk, const uint16_t *s_lut,
                                              const RjTableSet *ts, uint32_t *ring, uint32_t *stage) {
-  BitReader br;
-  br.init(J.src, ring, J.bytes);
-  for (uint32_t q = br.cm; q < RJ_RING_CHUNKS; q++) reinterpret_cast<uint4 *>(ring)[q] = make_uint4(0, 0, 0, 0);
-  br.cm = RJ_RING_CHUNKS;  // chunks past the data count as committed zero chunks
-  br.cms = 0;
+  const uint4 *src = J.src;
+  const uint32_t nchunks = (J.bytes + 15) / 16;
+  for (uint32_t q = 0; q < RJ_XRING_CHUNKS; q++)
+    xring_put(ring, q, *gp(q < nchunks ? src + q : rj_zero_chunks));
+  uint32_t cm = RJ_XRING_CHUNKS;  // chunks committed (past the data: zero chunks)
+  uint32_t pos = 0;               // bits consumed
   uint32_t ne = 0, fl = 0;
   int pred0 = 0, pred1 = 0, pred2 = 0;
   bool skip = J.missing;
@@ -201,18 +233,20 @@ __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, u
   uint32_t tbase = ((info >> 2) & 1u) * RJ_LUT_L1;  // table of the next symbol (DC of block 0)
   uint32_t k = 0;
   // row checkpoints every `every` MCU rows of the interval (piece slots permitting)
-  uint32_t np = 1, pfirst = 0, bdone = 0;
-  const uint32_t r0 = J.mcu_first / J.mcux;
-  const uint32_t rows = (J.mcu_first + J.mcu_count - 1) / J.mcux - r0 + 1;
-  const uint32_t every = (rows + J.slots - 1) / J.slots;
-  uint32_t to_row = J.mcux - (J.mcu_first - r0 * J.mcux);  // MCUs until the next row starts
-  uint32_t rows_left = every;
+  uint32_t np = 1, pfirst = 0, to_row = 0, rows_left = 0, every = 1;
+  if (kCkpt) {
+    const uint32_t r0 = J.mcu_first / J.mcux;
+    const uint32_t rows = (J.mcu_first + J.mcu_count - 1) / J.mcux - r0 + 1;
+    every = (rows + J.slots - 1) / J.slots;
+    to_row = J.mcux - (J.mcu_first - r0 * J.mcux);  // MCUs until the next row starts
+    rows_left = every;
+  }
   while (__builtin_amdgcn_ballot_w64(blocks_left > 0) != 0) {
     // ---- phase start (wave-uniform): prefetch (zero chunks past the data), stage flush ----
-    const uint32_t used = br.cm - (br.rd >> 2);
-    const uint32_t n = min(RJ_RING_CHUNKS - used, uint32_t(RJ_PREFETCH));
-    const uint4 pf0 = *gp(br.cm < br.nchunks ? br.src + br.cm : rj_zero_chunks);
-    const uint4 pf1 = *gp(br.cm + 1 < br.nchunks ? br.src + br.cm + 1 : rj_zero_chunks + 1);
+    const uint32_t used = cm - (pos >> 7);
+    const uint32_t n = min(RJ_XRING_CHUNKS - used, 2u);
+    const uint4 pf0 = *gp(cm < nchunks ? src + cm : rj_zero_chunks);
+    const uint4 pf1 = *gp(cm + 1 < nchunks ? src + cm + 1 : rj_zero_chunks + 1);
     if (ne - fl >= RJ_ENT_GROUP) {
       const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
       uint4 *d4 = reinterpret_cast<uint4 *>(J.ent + fl);
@@ -220,21 +254,12 @@ __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, u
       for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = s4[q];
       fl += RJ_ENT_GROUP;
     }
-#ifdef RJ_EXACT_NOUNROLL
-#pragma unroll 1
-#else
 #pragma unroll
-#endif
     for (uint32_t step = 0; step < RJ_PHASE; step++) {
       const bool act = blocks_left > 0;
-      // refill (32 bits when <= 32 are left); the ring always holds the next words
-      const bool need = br.nb <= 32;
-      br.acc |= uint64_t(__builtin_bswap32(need ? br.nw : 0u)) << ((32 - br.nb) & 63);
-      br.nb += need ? 32 : 0;
-      br.rd += need ? 1u : 0u;
-      br.rdw = need ? (br.rdw == RJ_RING_WORDS - 1 ? 0u : br.rdw + 1u) : br.rdw;
-      br.nw = ring[br.rdw];
-      const uint32_t peek32 = uint32_t(br.acc >> 32);
+      const uint32_t wi = (pos >> 5) & (RJ_XRING_WORDS - 1);
+      const uint64_t win = (uint64_t(ring[wi]) << 32) | ring[wi + 1];
+      const uint32_t peek32 = uint32_t((win << (pos & 31)) >> 32);
       const bool isdc = k == 0;
       uint32_t e = s_lut[tbase + (peek32 >> 23)];
       if (e & 0x8000u) {
@@ -249,8 +274,7 @@ __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, u
       const uint32_t sz = sym & 15u, r = sym >> 4;
       const uint32_t raw = __builtin_amdgcn_ubfe(peek32, 32u - len - sz, sz);
       const int val = int(raw) + (int32_t(raw - (1u << ((sz - 1) & 31))) >> 31 & int32_t(1u - (1u << sz)));
-      br.acc <<= (len + sz);
-      br.nb -= int(len + sz);
+      pos += len + sz;
       const uint32_t c = info & 3u;
       const int p = (c == 0 ? pred0 : (c == 1 ? pred1 : pred2)) + val;
       pred0 = (isdc && c == 0) ? p : pred0;
@@ -280,36 +304,29 @@ __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, u
       opaque(dcb);  // both operands materialised: the select stays a v_cndmask, not a branch
       opaque(acbase);
       tbase = bend ? dcb : acbase;
-      const bool done_blk = bend && act;
-      blocks_left -= done_blk ? 1u : 0u;
-      bdone += done_blk ? 1u : 0u;
-      skip = skip || (mcuend && br.consumed() > J.nbits);
-      to_row -= (mcuend && act) ? 1u : 0u;
-      if (to_row == 0) {  // the next MCU starts a row (rare)
-        to_row = J.mcux;
-        if (--rows_left == 0) {
-          rows_left = every;
-          if (blocks_left && np < J.slots) {  // checkpoint: a new piece starts here
-            gp(J.pieces + np - 1)->nblk = bdone - pfirst;
-            *gp(J.pieces + np) = RjPiece{J.ent_abs + ne, bdone, 0u, 0u, {0, 0, 0}};
-            pfirst = bdone;
-            np++;
+      blocks_left -= (bend && act) ? 1u : 0u;
+      skip = skip || (mcuend && pos > J.nbits);
+      if (kCkpt) {
+        to_row -= (mcuend && act) ? 1u : 0u;
+        if (to_row == 0) {  // the next MCU starts a row (rare)
+          to_row = J.mcux;
+          if (--rows_left == 0) {
+            rows_left = every;
+            if (blocks_left && np < J.slots) {  // checkpoint: a new piece starts here
+              const uint32_t bdone = J.blocks - blocks_left;
+              gp(J.pieces + np - 1)->nblk = bdone - pfirst;
+              *gp(J.pieces + np) = RjPiece{J.ent_abs + ne, bdone, 0u, 0u, {0, 0, 0}};
+              pfirst = bdone;
+              np++;
+            }
           }
         }
       }
     }
     // ---- phase end: the prefetch lands in the ring (zero chunks past the data) ----
-    uint4 *r4 = reinterpret_cast<uint4 *>(ring);
-    if (n > 0) {
-      r4[br.cms] = pf0;
-      br.cms = br.cms == RJ_RING_CHUNKS - 1 ? 0 : br.cms + 1;
-    }
-    if (n > 1) {
-      r4[br.cms] = pf1;
-      br.cms = br.cms == RJ_RING_CHUNKS - 1 ? 0 : br.cms + 1;
-    }
-    br.cm += n;
-    br.nw = ring[br.rdw];
+    if (n > 0) xring_put(ring, cm & (RJ_XRING_CHUNKS - 1), pf0);
+    if (n > 1) xring_put(ring, (cm + 1) & (RJ_XRING_CHUNKS - 1), pf1);
+    cm += n;
   }
   stage[ne & (RJ_STAGE - 1)] = RJ_ENT_TERM;
   while (fl < ne + 1) {
@@ -319,7 +336,7 @@ __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, u
     for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = s4[q];
     fl += RJ_ENT_GROUP;
   }
-  gp(J.pieces + np - 1)->nblk = bdone - pfirst;
+  gp(J.pieces + np - 1)->nblk = J.blocks - pfirst;
   gp(J.pieces)->npieces = np;
 }
 
@@ -547,8 +564,9 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
                                                       uint32_t epoch) {
   static_assert(RJ_WG == RJ_K1_WG, "lane layout granule");
   // strides padded by 16 B so the 8-lane groups of ds_*_b128 hit distinct banks
-  __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_WG][RJ_RING_WORDS + 4];
-  __shared__ __attribute__((aligned(16))) uint32_t s_stage[RJ_WG][RJ_STAGE + 4];
+  // ring rows: 33 words (the exact decoder's 32-word ring + mirror; the chunk decoder uses 24)
+  __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_WG][RJ_XRING_STRIDE];
+  __shared__ __attribute__((aligned(16))) uint32_t s_stage[RJ_WG][RJ_STAGE];
   __shared__ __attribute__((aligned(16))) uint16_t s_lut[RJ_SLUT_ENTRIES];
   __shared__ uint32_t s_T;
   const uint32_t tid = threadIdx.x;
@@ -624,7 +642,7 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
         J.mcu_first = sg.mcu_first;
         J.mcu_count = sg.mcu_count;
         *gp(J.pieces) = RjPiece{ent_abs, 0u, blocks, 1u, {0, 0, 0}};
-        decode_exact(J, binfo, nblk, s_lut, ts, s_ring[tid], s_stage[tid]);
+        decode_exact<kFallback>(J, binfo, nblk, s_lut, ts, s_ring[tid], s_stage[tid]);
       } else {
         const uint32_t clen = rj_chunk_len(nbytes, nch);
         const uint32_t b0 = min(c * clen, nbytes), b1 = min(b0 + clen, nbytes);
