@@ -44,9 +44,26 @@ namespace rj {
 // left).  With U unread words a phase prefetches n = min(2, 6 - used) chunks and consumes at
 // most 8 words: U >= 16 keeps U' >= 8; 8 <= U < 16 means used <= 4, so n = 2 and U' = U.
 
+// One lane's column of a lane-interleaved LDS array: word w of lane l at [w][l], so that the
+// lanes' private rings and stages sit in distinct banks whatever word each lane touches.
+struct LRow {
+  uint32_t *base;  // &array[0][lane]
+  __device__ __forceinline__ uint32_t &operator[](uint32_t w) const { return base[w * RJ_WG]; }
+};
+
+// one 64-B group of staged entries (16 words from slot `from`, a multiple of 16) to HBM
+__device__ __forceinline__ void flush_group(const LRow &stage, uint32_t from, uint32_t *dst) {
+  uint32_t w[RJ_ENT_GROUP];
+#pragma unroll
+  for (int q = 0; q < RJ_ENT_GROUP; q++) w[q] = stage[(from & (RJ_STAGE - 1)) + q];
+  uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+#pragma unroll
+  for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
 struct BitReader {
   const uint4 *src;   // 16-B aligned destuffed bytes (from the lane's start), zero-padded
-  uint32_t *ring;     // this lane's LDS ring (RJ_RING_WORDS words)
+  LRow ring;          // this lane's LDS ring (RJ_RING_WORDS words)
   uint32_t nchunks;   // 16-B chunks holding data
   uint32_t rd;        // words moved into the bit buffer (monotonic)
   uint32_t rdw;       // rd mod RJ_RING_WORDS
@@ -56,7 +73,7 @@ struct BitReader {
   int nb;             // valid bits in acc (left-justified)
   uint64_t acc;
 
-  __device__ __forceinline__ void init(const uint4 *s, uint32_t *r, uint32_t nbytes) {
+  __device__ __forceinline__ void init(const uint4 *s, LRow r, uint32_t nbytes) {
     src = s;
     ring = r;
     nchunks = (nbytes + 15) / 16;
@@ -86,12 +103,11 @@ struct BitReader {
     pf1 = gp(src)[cm + 1 < last ? cm + 1 : last];
     return n;
   }
-  __device__ __forceinline__ void put4(uint32_t slot, const uint4 &v) {  // ring rows are 4-B aligned
-    uint32_t *r = ring + 4 * slot;
-    r[0] = v.x;
-    r[1] = v.y;
-    r[2] = v.z;
-    r[3] = v.w;
+  __device__ __forceinline__ void put4(uint32_t slot, const uint4 &v) {
+    ring[4 * slot] = v.x;
+    ring[4 * slot + 1] = v.y;
+    ring[4 * slot + 2] = v.z;
+    ring[4 * slot + 3] = v.w;
   }
   __device__ __forceinline__ void commit(const uint4 &pf0, const uint4 &pf1, uint32_t n) {
     if (n > 0) {
@@ -201,22 +217,20 @@ __device__ const uint4 rj_zero_chunks[RJ_PREFETCH] = {};
 // exact lanes have one piece slot and skip that bookkeeping.
 #define RJ_XRING_CHUNKS 8
 #define RJ_XRING_WORDS (RJ_XRING_CHUNKS * 4)
-#define RJ_XRING_STRIDE (RJ_XRING_WORDS + 1)  // odd: random per-lane words spread over the banks
 
-__device__ __forceinline__ void xring_put(uint32_t *ring, uint32_t slot, const uint4 &v) {
+__device__ __forceinline__ void xring_put(const LRow &ring, uint32_t slot, const uint4 &v) {
   const uint32_t w0 = __builtin_bswap32(v.x), w1 = __builtin_bswap32(v.y);
   const uint32_t w2 = __builtin_bswap32(v.z), w3 = __builtin_bswap32(v.w);
-  uint32_t *r = ring + 4 * slot;
-  r[0] = w0;
-  r[1] = w1;
-  r[2] = w2;
-  r[3] = w3;
+  ring[4 * slot] = w0;
+  ring[4 * slot + 1] = w1;
+  ring[4 * slot + 2] = w2;
+  ring[4 * slot + 3] = w3;
   if (slot == 0) ring[RJ_XRING_WORDS] = w0;  // mirror: word 31's successor
 }
 
 template <bool kCkpt>
 __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, uint32_t nblk, const uint16_t *s_lut,
-                                             const RjTableSet *ts, uint32_t *ring, uint32_t *stage) {
+                                             const RjTableSet *ts, LRow ring, LRow stage) {
   const uint4 *src = J.src;
   const uint32_t nchunks = (J.bytes + 15) / 16;
   for (uint32_t q = 0; q < RJ_XRING_CHUNKS; q++)
@@ -248,10 +262,7 @@ __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, u
     const uint4 pf0 = *gp(cm < nchunks ? src + cm : rj_zero_chunks);
     const uint4 pf1 = *gp(cm + 1 < nchunks ? src + cm + 1 : rj_zero_chunks + 1);
     if (ne - fl >= RJ_ENT_GROUP) {
-      const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
-      uint4 *d4 = reinterpret_cast<uint4 *>(J.ent + fl);
-#pragma unroll
-      for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = s4[q];
+      flush_group(stage, fl, J.ent + fl);
       fl += RJ_ENT_GROUP;
     }
 #pragma unroll
@@ -330,10 +341,7 @@ __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, u
   }
   stage[ne & (RJ_STAGE - 1)] = RJ_ENT_TERM;
   while (fl < ne + 1) {
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
-    uint4 *d4 = reinterpret_cast<uint4 *>(J.ent + fl);
-#pragma unroll
-    for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = s4[q];
+    flush_group(stage, fl, J.ent + fl);
     fl += RJ_ENT_GROUP;
   }
   gp(J.pieces + np - 1)->nblk = J.blocks - pfirst;
@@ -342,8 +350,8 @@ __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, u
 
 template <bool kSplit, int kScope>
 __device__ __forceinline__ void decode_lane(const LaneJob &J, uint64_t binfo, uint32_t nblk, uint32_t epoch,
-                                            const uint16_t *s_lut, const RjTableSet *ts, uint32_t *ring,
-                                            uint32_t *stage, RjChunkRes *res) {
+                                            const uint16_t *s_lut, const RjTableSet *ts, LRow ring,
+                                            LRow stage, RjChunkRes *res) {
   BitReader br;
   br.init(J.src, ring, J.bytes);
   uint32_t ne = 0, fl = 0;  // entries produced / flushed (fl multiple of RJ_ENT_GROUP)
@@ -400,10 +408,7 @@ __device__ __forceinline__ void decode_lane(const LaneJob &J, uint64_t binfo, ui
       rp = false;
     }
     if (ne - fl >= RJ_ENT_GROUP) {  // one full 64-B group leaves the stage
-      const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
-      uint4 *d4 = reinterpret_cast<uint4 *>(J.ent + fl);
-#pragma unroll
-      for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = s4[q];
+      flush_group(stage, fl, J.ent + fl);
       fl += RJ_ENT_GROUP;
     }
     for (uint32_t step = 0; step < RJ_PHASE && (kSplit ? status == 0 : blocks_left > 0); step++) {
@@ -523,10 +528,7 @@ __device__ __forceinline__ void decode_lane(const LaneJob &J, uint64_t binfo, ui
   // terminator, then everything still staged (whole groups; the slack is reserved)
   stage[ne & (RJ_STAGE - 1)] = RJ_ENT_TERM;
   while (fl < ne + 1) {
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(stage + (fl & (RJ_STAGE - 1)));
-    uint4 *d4 = reinterpret_cast<uint4 *>(J.ent + fl);
-#pragma unroll
-    for (int q = 0; q < RJ_ENT_GROUP / 4; q++) gp(d4)[q] = s4[q];
+    flush_group(stage, fl, J.ent + fl);
     fl += RJ_ENT_GROUP;
   }
   if (!kSplit) {
@@ -564,9 +566,10 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
                                                       uint32_t epoch) {
   static_assert(RJ_WG == RJ_K1_WG, "lane layout granule");
   // strides padded by 16 B so the 8-lane groups of ds_*_b128 hit distinct banks
-  // ring rows: 33 words (the exact decoder's 32-word ring + mirror; the chunk decoder uses 24)
-  __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_WG][RJ_XRING_STRIDE];
-  __shared__ __attribute__((aligned(16))) uint32_t s_stage[RJ_WG][RJ_STAGE];
+  // lane-interleaved (LRow): 33 ring words per lane (the exact decoder's 32-word ring + mirror;
+  // the chunk decoder uses 24) and RJ_STAGE staged entries per lane
+  __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_XRING_WORDS + 1][RJ_WG];
+  __shared__ __attribute__((aligned(16))) uint32_t s_stage[RJ_STAGE][RJ_WG];
   __shared__ __attribute__((aligned(16))) uint16_t s_lut[RJ_SLUT_ENTRIES];
   __shared__ uint32_t s_T;
   const uint32_t tid = threadIdx.x;
@@ -642,7 +645,7 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
         J.mcu_first = sg.mcu_first;
         J.mcu_count = sg.mcu_count;
         *gp(J.pieces) = RjPiece{ent_abs, 0u, blocks, 1u, {0, 0, 0}};
-        decode_exact<kFallback>(J, binfo, nblk, s_lut, ts, s_ring[tid], s_stage[tid]);
+        decode_exact<kFallback>(J, binfo, nblk, s_lut, ts, LRow{&s_ring[0][tid]}, LRow{&s_stage[0][tid]});
       } else {
         const uint32_t clen = rj_chunk_len(nbytes, nch);
         const uint32_t b0 = min(c * clen, nbytes), b1 = min(b0 + clen, nbytes);
@@ -667,7 +670,8 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
         J.rec = coefs.rec + uint64_t(g) * RJ_MAX_RECORDS;
         J.rec_next = J.rec - RJ_MAX_RECORDS;  // chunk c+1 sits on lane g-1
         J.next_chunks = nch - 1 - c;
-        decode_lane<true, kScope>(J, binfo, nblk, epoch, s_lut, ts, s_ring[tid], s_stage[tid], coefs.res + g);
+        decode_lane<true, kScope>(J, binfo, nblk, epoch, s_lut, ts, LRow{&s_ring[0][tid]}, LRow{&s_stage[0][tid]},
+                                  coefs.res + g);
       }
     }
   }

@@ -375,6 +375,9 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
         if (fmt == 3) {
           uint8_t *d = dst0 + (__umul24(py, pitch) + px * 3);
           if (n == 4 && a4) {
+#ifdef RJ_EXP_NOSTORE
+            if (w[0] == 0x12345679u && w[1] == 0x9abcdef1u)
+#endif
             *gp(reinterpret_cast<uint3 *>(d)) = make_uint3(w[0], w[1], w[2]);
           } else {
             store_bytes(d, 3 * n, w);
