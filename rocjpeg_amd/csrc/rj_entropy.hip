@@ -28,6 +28,8 @@
 //   * output: per-lane LDS stage, 64-B groups written at phase boundaries.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "rj_device.h"
 #include "rj_kernels.h"
 #include "rj_math.h"
@@ -228,6 +230,80 @@ __device__ __forceinline__ void xring_put(const LRow &ring, uint32_t slot, const
   if (slot == 0) ring[RJ_XRING_WORDS] = w0;  // mirror: word 31's successor
 }
 
+// One symbol step of decode_exact (SAFE: per-lane activity mask and insufficient-data handling).
+#define RJ_EXACT_STEP(SAFE) \
+  do { \
+      const bool act = !(SAFE) || blocks_left > 0; \
+      const uint32_t wi = (pos >> 5) & (RJ_XRING_WORDS - 1); \
+      const uint64_t win = (uint64_t(ring[wi]) << 32) | ring[wi + 1]; \
+      const uint32_t peek32 = uint32_t((win << (pos & 31)) >> 32); \
+      const bool isdc = k == 0; \
+      uint32_t e = s_lut[tbase + (peek32 >> 23)]; \
+      if (e & 0x8000u) { \
+        if (e != 0xFFFFu && !isdc) { \
+          e = s_lut[tbase + RJ_LUT_L1 + (e & 0x7Fu) * 128u + ((peek32 >> 16) & 127u)]; \
+        } else { \
+          const RjHuffDev *t = isdc ? &ts->dc[(info >> 2) & 1u] : &ts->ac[(info >> 3) & 1u]; \
+          e = huff_slow(t, peek32 >> 16); \
+        } \
+      } \
+      const uint32_t len = e >> 8, sym = e & 255u; \
+      const uint32_t sz = sym & 15u, r = sym >> 4; \
+      const uint32_t raw = __builtin_amdgcn_ubfe(peek32, 32u - len - sz, sz); \
+      const int val = int(raw) + (int32_t(raw - (1u << ((sz - 1) & 31))) >> 31 & int32_t(1u - (1u << sz))); \
+      pos += len + sz; \
+      const uint32_t c = info & 3u; \
+      const int p = (c == 0 ? pred0 : (c == 1 ? pred1 : pred2)) + val; \
+      pred0 = (isdc && c == 0) ? p : pred0; \
+      pred1 = (isdc && c == 1) ? p : pred1; \
+      pred2 = (isdc && c == 2) ? p : pred2; \
+      const uint32_t kk = isdc ? 0u : k + r;  /* zigzag position of this coefficient */ \
+      /* AC: EOB (size 0, run != 15) ends the block; ZRL and coefficients advance k to kk + 1 */ \
+      const bool eob = !isdc && sz == 0 && r != 15; \
+      uint32_t entry = (uint32_t(isdc ? p : val) & 0xFFFFu) | (min(kk, 63u) << 16); \
+      bool emit = isdc || sz != 0; \
+      uint32_t knew = kk + 1u; \
+      opaque(knew); \
+      knew = eob ? 64u : knew; \
+      if (SAFE) { \
+        entry = skip ? 0u : entry;  /* libjpeg: the rest of the interval decodes to zero blocks */ \
+        emit = skip || emit; \
+        knew = skip ? 64u : knew; \
+      } \
+      stage[ne & (RJ_STAGE - 1)] = entry;  /* a non-emitted write lands in the next free slot */ \
+      ne += (emit && act) ? 1u : 0u; \
+      const bool bend = knew >= 64u; \
+      const uint32_t bn = b + 1 == nblk ? 0u : b + 1; \
+      const bool mcuend = bend && bn == 0; \
+      k = bend ? 0u : knew; \
+      b = bend ? bn : b; \
+      info = uint32_t(binfo >> (4 * b)) & 15u; \
+      acbase = RJ_SLUT_AC0 + ((info >> 3) & 1u) * RJ_LUT_ENTRIES; \
+      uint32_t dcb = ((info >> 2) & 1u) * RJ_LUT_L1; \
+      opaque(dcb);  /* both operands materialised: the select stays a v_cndmask, not a branch */ \
+      opaque(acbase); \
+      tbase = bend ? dcb : acbase; \
+      blocks_left -= (bend && act) ? 1u : 0u; \
+      if (SAFE) skip = skip || (mcuend && pos > J.nbits); \
+      if (kCkpt) { \
+        to_row -= (mcuend && act) ? 1u : 0u; \
+        if (to_row == 0) {  /* the next MCU starts a row (rare) */ \
+          to_row = J.mcux; \
+          if (--rows_left == 0) { \
+            rows_left = every; \
+            if (blocks_left && np < J.slots) {  /* checkpoint: a new piece starts here */ \
+              const uint32_t bdone = J.blocks - blocks_left; \
+              gp(J.pieces + np - 1)->nblk = bdone - pfirst; \
+              *gp(J.pieces + np) = RjPiece{J.ent_abs + ne, bdone, 0u, 0u, {0, 0, 0}}; \
+              pfirst = bdone; \
+              np++; \
+            } \
+          } \
+        } \
+      } \
+     \
+  } while (0)
+
 template <bool kCkpt>
 __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, uint32_t nblk, const uint16_t *s_lut,
                                              const RjTableSet *ts, LRow ring, LRow stage) {
@@ -255,89 +331,36 @@ __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, u
     to_row = J.mcux - (J.mcu_first - r0 * J.mcux);  // MCUs until the next row starts
     rows_left = every;
   }
+  // Prefetch issued at the end of a phase (after that phase's stage flush) lands in the ring at
+  // the end of the next one: the wait for it then also covers the flush stores (vmcnt counts
+  // stores too, in issue order), which have had a whole phase to complete.
+  uint32_t n = 0;  // chunks in flight (issued at the end of the previous phase)
+  uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = make_uint4(0, 0, 0, 0);
   while (__builtin_amdgcn_ballot_w64(blocks_left > 0) != 0) {
-    // ---- phase start (wave-uniform): prefetch (zero chunks past the data), stage flush ----
-    const uint32_t used = cm - (pos >> 7);
-    const uint32_t n = min(RJ_XRING_CHUNKS - used, 2u);
-    const uint4 pf0 = *gp(cm < nchunks ? src + cm : rj_zero_chunks);
-    const uint4 pf1 = *gp(cm + 1 < nchunks ? src + cm + 1 : rj_zero_chunks + 1);
+    // A phase in which no lane can finish its blocks or reach the end of its data (each step
+    // ends at most one block and reads at most 31 bits) needs neither the per-lane activity
+    // mask nor libjpeg's insufficient-data handling: that body is the common one.
+    const bool fast = !kCkpt && __builtin_amdgcn_ballot_w64(!(blocks_left >= RJ_PHASE && !skip &&
+                                                              pos + RJ_PHASE * 31u < J.nbits)) == 0;
+    if (fast) {
+#pragma unroll
+      for (uint32_t q = 0; q < RJ_PHASE; q++) RJ_EXACT_STEP(false);
+    } else {
+#pragma unroll
+      for (uint32_t q = 0; q < RJ_PHASE; q++) RJ_EXACT_STEP(true);
+    }
+    // ---- phase end (wave-uniform): the previous prefetch lands in the ring, a full stage
+    // group leaves, the next prefetch is issued (zero chunks past the data) ----
+    if (n > 0) xring_put(ring, cm & (RJ_XRING_CHUNKS - 1), pf0);
+    if (n > 1) xring_put(ring, (cm + 1) & (RJ_XRING_CHUNKS - 1), pf1);
+    cm += n;
     if (ne - fl >= RJ_ENT_GROUP) {
       flush_group(stage, fl, J.ent + fl);
       fl += RJ_ENT_GROUP;
     }
-#pragma unroll
-    for (uint32_t step = 0; step < RJ_PHASE; step++) {
-      const bool act = blocks_left > 0;
-      const uint32_t wi = (pos >> 5) & (RJ_XRING_WORDS - 1);
-      const uint64_t win = (uint64_t(ring[wi]) << 32) | ring[wi + 1];
-      const uint32_t peek32 = uint32_t((win << (pos & 31)) >> 32);
-      const bool isdc = k == 0;
-      uint32_t e = s_lut[tbase + (peek32 >> 23)];
-      if (e & 0x8000u) {
-        if (e != 0xFFFFu && !isdc) {
-          e = s_lut[tbase + RJ_LUT_L1 + (e & 0x7Fu) * 128u + ((peek32 >> 16) & 127u)];
-        } else {
-          const RjHuffDev *t = isdc ? &ts->dc[(info >> 2) & 1u] : &ts->ac[(info >> 3) & 1u];
-          e = huff_slow(t, peek32 >> 16);
-        }
-      }
-      const uint32_t len = e >> 8, sym = e & 255u;
-      const uint32_t sz = sym & 15u, r = sym >> 4;
-      const uint32_t raw = __builtin_amdgcn_ubfe(peek32, 32u - len - sz, sz);
-      const int val = int(raw) + (int32_t(raw - (1u << ((sz - 1) & 31))) >> 31 & int32_t(1u - (1u << sz)));
-      pos += len + sz;
-      const uint32_t c = info & 3u;
-      const int p = (c == 0 ? pred0 : (c == 1 ? pred1 : pred2)) + val;
-      pred0 = (isdc && c == 0) ? p : pred0;
-      pred1 = (isdc && c == 1) ? p : pred1;
-      pred2 = (isdc && c == 2) ? p : pred2;
-      const uint32_t kk = isdc ? 0u : k + r;  // zigzag position of this coefficient
-      // AC: EOB (size 0, run != 15) ends the block; ZRL and coefficients advance k to kk + 1
-      const bool eob = !isdc && sz == 0 && r != 15;
-      uint32_t entry = (uint32_t(isdc ? p : val) & 0xFFFFu) | (min(kk, 63u) << 16);
-      bool emit = isdc || sz != 0;
-      uint32_t knew = kk + 1u;
-      opaque(knew);
-      knew = eob ? 64u : knew;
-      entry = skip ? 0u : entry;  // libjpeg: the rest of the interval decodes to zero blocks
-      emit = skip || emit;
-      knew = skip ? 64u : knew;
-      stage[ne & (RJ_STAGE - 1)] = entry;  // a non-emitted write lands in the next free slot
-      ne += (emit && act) ? 1u : 0u;
-      const bool bend = knew >= 64u;
-      const uint32_t bn = b + 1 == nblk ? 0u : b + 1;
-      const bool mcuend = bend && bn == 0;
-      k = bend ? 0u : knew;
-      b = bend ? bn : b;
-      info = uint32_t(binfo >> (4 * b)) & 15u;
-      acbase = RJ_SLUT_AC0 + ((info >> 3) & 1u) * RJ_LUT_ENTRIES;
-      uint32_t dcb = ((info >> 2) & 1u) * RJ_LUT_L1;
-      opaque(dcb);  // both operands materialised: the select stays a v_cndmask, not a branch
-      opaque(acbase);
-      tbase = bend ? dcb : acbase;
-      blocks_left -= (bend && act) ? 1u : 0u;
-      skip = skip || (mcuend && pos > J.nbits);
-      if (kCkpt) {
-        to_row -= (mcuend && act) ? 1u : 0u;
-        if (to_row == 0) {  // the next MCU starts a row (rare)
-          to_row = J.mcux;
-          if (--rows_left == 0) {
-            rows_left = every;
-            if (blocks_left && np < J.slots) {  // checkpoint: a new piece starts here
-              const uint32_t bdone = J.blocks - blocks_left;
-              gp(J.pieces + np - 1)->nblk = bdone - pfirst;
-              *gp(J.pieces + np) = RjPiece{J.ent_abs + ne, bdone, 0u, 0u, {0, 0, 0}};
-              pfirst = bdone;
-              np++;
-            }
-          }
-        }
-      }
-    }
-    // ---- phase end: the prefetch lands in the ring (zero chunks past the data) ----
-    if (n > 0) xring_put(ring, cm & (RJ_XRING_CHUNKS - 1), pf0);
-    if (n > 1) xring_put(ring, (cm + 1) & (RJ_XRING_CHUNKS - 1), pf1);
-    cm += n;
+    n = min(RJ_XRING_CHUNKS - (cm - (pos >> 7)), 2u);  // slots free now stay free until it lands
+    pf0 = *gp(cm < nchunks ? src + cm : rj_zero_chunks);
+    pf1 = *gp(cm + 1 < nchunks ? src + cm + 1 : rj_zero_chunks + 1);
   }
   stage[ne & (RJ_STAGE - 1)] = RJ_ENT_TERM;
   while (fl < ne + 1) {

@@ -7,6 +7,7 @@ STEPS=${STEPS:-10}
 for spec in "$@"; do
   tag=${spec%%:*}
   envs=${spec#*:}
-  ( IFS=','; for kv in $envs; do [ -n "$kv" ] && export "$kv"; done
+  ( IFS=',' read -ra kvs <<< "$envs"
+    for kv in "${kvs[@]}"; do [ -n "$kv" ] && export "$kv"; done
     timeout -k 10 300 python bench.py --steps $STEPS --warmup 2 --no-cpu-baseline ${BENCH_EXTRA:-} > gpurun_out/ab_$tag.log 2>&1 ) || exit $?
 done
