@@ -207,9 +207,10 @@ __device__ const uint4 rj_zero_chunks[RJ_PREFETCH] = {};
 // number of symbol steps per phase (no per-lane loop exit: a lane that has finished its blocks
 // keeps stepping with its effects masked), and the per-symbol bookkeeping is select-only, so
 // the loop carries no exec-mask juggling.
-// Bits: a 32-word LDS ring (+ a mirror of word 0 at index 32) of big-endian stream words,
-// read at random bit positions: word i = pos >> 5 and the next one (one ds_read2_b32) and a
-// 64-bit shift by pos & 31 give the 32-bit peek -- no refill state.  Chunks are byte-swapped
+// Bits: a 32-word LDS ring (+ a mirror of word 0 at index 32) of big-endian stream words.  The
+// words i = pos >> 5 and i + 1 sit in registers and a 64-bit shift by pos & 31 gives the
+// 32-bit peek; word i + 2 is read one step ahead, so a step that crosses a word boundary
+// shifts registers instead of waiting on the ring (off the symbol dependency chain).  Chunks are byte-swapped
 // once, when they land in the ring; past the data the ring receives zero chunks (the zero
 // bits libjpeg inserts).  Ring invariant: >= 8 unread words at every phase start (a phase
 // reads <= 8: 8 symbols of <= 27 bits plus the next word); with U unread words a phase
@@ -234,9 +235,7 @@ __device__ __forceinline__ void xring_put(const LRow &ring, uint32_t slot, const
 #define RJ_EXACT_STEP(SAFE) \
   do { \
       const bool act = !(SAFE) || blocks_left > 0; \
-      const uint32_t wi = (pos >> 5) & (RJ_XRING_WORDS - 1); \
-      const uint64_t win = (uint64_t(ring[wi]) << 32) | ring[wi + 1]; \
-      const uint32_t peek32 = uint32_t((win << (pos & 31)) >> 32); \
+      const uint32_t peek32 = uint32_t((((uint64_t(w0) << 32) | w1) << (pos & 31)) >> 32); \
       const bool isdc = k == 0; \
       uint32_t e = s_lut[tbase + (peek32 >> 23)]; \
       if (e & 0x8000u) { \
@@ -251,7 +250,14 @@ __device__ __forceinline__ void xring_put(const LRow &ring, uint32_t slot, const
       const uint32_t sz = sym & 15u, r = sym >> 4; \
       const uint32_t raw = __builtin_amdgcn_ubfe(peek32, 32u - len - sz, sz); \
       const int val = int(raw) + (int32_t(raw - (1u << ((sz - 1) & 31))) >> 31 & int32_t(1u - (1u << sz))); \
-      pos += len + sz; \
+      { /* words i, i+1 in w0, w1; word i+2 (read one step ahead) in w2 */ \
+        const uint32_t npos = pos + len + sz; \
+        const bool adv = (npos >> 5) != (pos >> 5); \
+        w0 = adv ? w1 : w0; \
+        w1 = adv ? w2 : w1; \
+        w2 = ring[((npos >> 5) + 2) & (RJ_XRING_WORDS - 1)]; \
+        pos = npos; \
+      } \
       const uint32_t c = info & 3u; \
       const int p = (c == 0 ? pred0 : (c == 1 ? pred1 : pred2)) + val; \
       pred0 = (isdc && c == 0) ? p : pred0; \
@@ -313,6 +319,7 @@ __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, u
     xring_put(ring, q, *gp(q < nchunks ? src + q : rj_zero_chunks));
   uint32_t cm = RJ_XRING_CHUNKS;  // chunks committed (past the data: zero chunks)
   uint32_t pos = 0;               // bits consumed
+  uint32_t w0 = ring[0], w1 = ring[1], w2 = ring[2];
   uint32_t ne = 0, fl = 0;
   int pred0 = 0, pred1 = 0, pred2 = 0;
   bool skip = J.missing;
@@ -354,6 +361,9 @@ __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, u
     if (n > 0) xring_put(ring, cm & (RJ_XRING_CHUNKS - 1), pf0);
     if (n > 1) xring_put(ring, (cm + 1) & (RJ_XRING_CHUNKS - 1), pf1);
     cm += n;
+    // the last step's read-ahead word may predate this commit (words i, i+1 never do: >= 9
+    // unread words were committed at the phase start)
+    w2 = ring[((pos >> 5) + 2) & (RJ_XRING_WORDS - 1)];
     if (ne - fl >= RJ_ENT_GROUP) {
       flush_group(stage, fl, J.ent + fl);
       fl += RJ_ENT_GROUP;
