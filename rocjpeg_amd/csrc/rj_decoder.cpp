@@ -719,6 +719,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   RJ_HIP(LaunchOutputJobs(stream_, d_imgs, d_jobs, int(jobs.size()), rows_total, d_planes_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[5], stream_));
   RJ_HIP(hipStreamSynchronize(stream_));
+#ifdef RJ_EXP_STAMPS
+  if (getenv("RJ_DEBUG_STAMPS")) DumpRowStamps();
+#endif
 
   timings_.images = uint32_t(n);
   timings_.intervals = seg_total;

@@ -21,6 +21,8 @@
 // pitch == width) is decided on the host (rj_decoder.cpp FusedEligible).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include "rj_device.h"
 #include "rj_kernels.h"
 #include "rj_math.h"
@@ -28,6 +30,15 @@
 namespace rj {
 
 #define RJ_BLK_STRIDE 144  // bytes per staged block in LDS (128 + 16 pad)
+
+#ifdef RJ_EXP_STAMPS  // diagnostic build: cycles per K2 phase, summed over waves (rj_decoder.cpp prints)
+__device__ unsigned long long rj_stamp[8];
+#define RJ_STAMP(var) const uint64_t var = __builtin_amdgcn_s_memtime()
+#define RJ_STAMP_ADD(slot, d) acc[slot] += (d)
+#else
+#define RJ_STAMP(var)
+#define RJ_STAMP_ADD(slot, d)
+#endif
 
 // byte b of w as float: the backend selects v_cvt_f32_ubyte{0..3} for this pattern
 __device__ __forceinline__ float u8f(uint32_t w, int b) { return float((w >> (8 * b)) & 255u); }
@@ -180,6 +191,7 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];  // A/B, then tiles
   __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
 
+  RJ_STAMP(t_start);
   const uint32_t tid = threadIdx.x;
   int i;
   uint32_t my;  // MCU row inside image i
@@ -275,7 +287,13 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
                          reinterpret_cast<uintptr_t>(dst2) | pitch0) & 3) == 0;
   const bool al_uv = ((reinterpret_cast<uintptr_t>(dst1) | reinterpret_cast<uintptr_t>(dst2) | pitch1) & 3) == 0;
 
+#ifdef RJ_EXP_STAMPS
+  uint64_t acc[4] = {0, 0, 0, 0};
+  RJ_STAMP(t_loop);
+  acc[3] = t_loop - t_start;
+#endif
   for (uint32_t sx = 0; sx < strips_x; sx++) {
+    RJ_STAMP(ta);
     const uint32_t mx0 = sx * S;
     const uint32_t nm = min(S, mcux - mx0);
     const uint32_t nb = nm * nblk;
@@ -291,6 +309,8 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
     if (sx + 1 < strips_x && nv.bleft) win.load(ent, nv.cur(), tid);  // next strip's window: lands behind B and C
     __syncthreads();
 
+    RJ_STAMP(tb);
+    RJ_STAMP_ADD(0, tb - ta);
     // ---- B: lane-per-block IDCT in registers ----
     const uint32_t c_b = lane_blk >> 12;
     int32_t v[64];
@@ -322,6 +342,8 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
     }
     __syncthreads();
 
+  RJ_STAMP(tc);
+  RJ_STAMP_ADD(1, tc - tb);
   // ---- C: output, lane = 4 consecutive pixels ----
   const uint32_t strip_w = nm * mcu_w;
   const uint32_t px0 = mx0 * mcu_w, py0 = my * mcu_h;
@@ -426,7 +448,14 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
       else store_bytes(d, n, &s4);
     }
   }
+  RJ_STAMP(te);
+  RJ_STAMP_ADD(2, te - tc);
   }  // strips
+#ifdef RJ_EXP_STAMPS
+  if (tid == 0)
+    for (int q = 0; q < 4; q++) atomicAdd(&rj_stamp[q], (unsigned long long)acc[q]);
+  if (tid == 0) atomicAdd(&rj_stamp[4], 1ull);
+#endif
 }
 
 hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
@@ -442,6 +471,18 @@ hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, in
                        tabsets, planes);
   return hipGetLastError();
 }
+
+#ifdef RJ_EXP_STAMPS
+void DumpRowStamps() {
+  unsigned long long h[8];
+  (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(rj_stamp), sizeof(h));
+  const double w = h[4] ? double(h[4]) : 1.0;
+  fprintf(stderr, "[rj stamps] waves %llu  per wave cycles: A %.0f B %.0f C %.0f prologue %.0f\n", h[4], h[0] / w,
+          h[1] / w, h[2] / w, h[3] / w);
+  unsigned long long z[8] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(rj_stamp), z, sizeof(z));
+}
+#endif
 
 hipError_t LaunchRowsOfLanes(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg,
                              const uint32_t *row_segs, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,

@@ -40,4 +40,8 @@ hipError_t LaunchRowsOfLanes(hipStream_t st, bool to_planes, const RjImageDev *i
                              const uint32_t *row_segs, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
                              uint8_t *planes);
 
+#ifdef RJ_EXP_STAMPS
+void DumpRowStamps();
+#endif
+
 }  // namespace rj
