@@ -101,16 +101,17 @@ def turbo_baseline(data_list, procs):
             "lib": "Pillow bundled libjpeg-turbo (BT.601 + fancy upsampling: throughput context only)"}
 
 
-def pmc_traffic(kernel, batch):
+def pmc_traffic(kernel, batch, launches):
     """HBM bytes per launch of `kernel` from the committed PMC profile (tools/gpu_pmc.sh +
     tools/pmc_traffic.py on this workload): FETCH_SIZE x 2 (gfx950 correction, MI355X_MICROARCH.md
-    HBM section) + WRITE_SIZE, per image, scaled to this launch's batch.  None if absent."""
+    HBM section) + WRITE_SIZE summed over a decode call, per image, scaled to this call's batch
+    and divided over its launches of the kernel.  None if absent."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             prof = json.load(f)
         k = prof["kernels"][kernel]
-        return int(k["hbm_bytes_per_image"] * batch)
+        return int(k["hbm_bytes_per_image"] * batch / max(1, launches))
     except (OSError, KeyError, ValueError):
         return None
 
@@ -190,7 +191,8 @@ def main():
         last = dec.last_timings()
         for k in stage:
             stage[k] += last[k]
-        for k in ("entropy_chunks_ms", "entropy_resolve_ms", "entropy_serial_ms"):
+        for k in ("entropy_chunks_ms", "entropy_resolve_ms", "entropy_serial_ms", "k1_launch_ms_sum",
+                  "k2_launch_ms_sum"):
             k1[k] = k1.get(k, 0.0) + last[k]
     torch.cuda.synchronize()
     if world > 1:
@@ -229,16 +231,21 @@ def main():
         ecs = last["ecs_bytes"]
         coef = last["coef_bytes"]
         outb = last["output_bytes"]
-        planes = args.batch * (W * H * 3 // 2)  # 4:2:0 native planes (approximate, unpadded)
-        # algorithmic bytes per launch of each kernel (DESIGN.md "Roofline")
-        algo = {"destuff_ms": 2 * ecs, "huffman_ms": ecs + coef, "idct_ms": coef + planes, "output_ms": planes + outb}
-        if last.get("fused_images", 0):
-            algo["idct_ms"] = coef + outb
-        dom = max(("huffman_ms", "idct_ms", "output_ms", "destuff_ms"), key=lambda k: per[k])
-        ach = algo[dom] / (per[dom] * 1e-3) / 1e9 if per[dom] > 0 else 0.0
-        names = {"destuff_ms": "k_destuff", "huffman_ms": "k_huffman",
-                 "idct_ms": "k_fused" if last.get("fused_images", 0) else "k_idct_planes", "output_ms": "k_output"}
-        traffic = pmc_traffic(names[dom], args.batch)
+        # per-kernel launch durations (HIP events on each launch's own stream, summed over the
+        # call's launches -- with the pipelined launch K1 and K2 run as two launches each) and
+        # the algorithmic bytes those launches move (DESIGN.md "Roofline"):
+        #   K0 k_destuff: ECS bytes read + written; K1 k_entropy: destuffed ECS read + sparse
+        #   entries written; K2 k_rows: entries read + output written
+        entb = last["entry_bytes"]
+        kern = {
+            "k_destuff": (stage["destuff_ms"] / K, 1, 2 * ecs),
+            "k_entropy": (k1["k1_launch_ms_sum"] / K, max(1, last["k1_launches"]), ecs + entb),
+            "k_rows": (k1["k2_launch_ms_sum"] / K, max(1, last["k2_launches"]), entb + outb),
+        }
+        dom = max(kern, key=lambda k: kern[k][0])
+        t_sum, launches, algo_bytes = kern[dom]
+        ach = algo_bytes / (t_sum * 1e-3) / 1e9 if t_sum > 0 else 0.0
+        traffic = pmc_traffic(dom, args.batch, launches)
         res = {
             "metric": "images/s (1080p 4:2:0 batch) at 1/2/4/8 MI355X + achieved HBM GB/s",
             "value": round(value, 2),
@@ -255,9 +262,11 @@ def main():
             "config": {"workload": "C2: batch of 1024 x 1920x1080 4:2:0 baseline JPEG q90, RI=120 MCUs, ROCJPEG_OUTPUT_RGB, bitstreams resident in HBM",
                        "batch_per_gpu": args.batch, "output_format": "RGB", "parallelism": f"images sharded, {world} rank(s)",
                        "ecs_bytes_per_image": round(ecs / args.batch)},
-            "roofline": {"bound": "hbm", "kernel": names[dom], "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": int(algo[dom]), "avg_launch_ms": round(per[dom], 4)},
+                         "algorithmic_bytes_per_launch": int(algo_bytes / launches),
+                         "avg_launch_ms": round(t_sum / launches, 4), "launches_per_step": launches,
+                         "per_kernel_launch_ms_sum": {k: round(v[0], 4) for k, v in kern.items()}},
             "stages_ms_per_step": {k: round(v, 4) for k, v in per.items()},
             "huffman_detail": dict({k: round(v / K, 4) for k, v in k1.items()}, chunks=last["chunks"],
                                    intervals=last["intervals"], split_intervals=last["split_intervals"],

@@ -47,6 +47,11 @@ typedef struct {
                                 is the K2 work left after it) */
   uint32_t pipe_lane_rows;   /* pipelined K2 rows taken from the K1 lane order (every interval
                                 one MCU row) rather than from uploaded row lists */
+  /* per-kernel launch durations (HIP events on each launch's own stream), summed over the
+     call's launches of that kernel: K1 chunk/exact pass, K2 (k_rows) */
+  float k1_launch_ms_sum, k2_launch_ms_sum;
+  uint32_t k1_launches, k2_launches;
+  uint64_t entry_bytes;      /* sparse coefficient entries K1 wrote (counted on the device) */
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);

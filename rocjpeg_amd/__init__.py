@@ -88,7 +88,10 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("entropy_resolve_ms", ctypes.c_float), ("entropy_serial_ms", ctypes.c_float),
                 ("chunks", ctypes.c_uint32), ("split_intervals", ctypes.c_uint32),
                 ("serial_fallbacks", ctypes.c_uint32), ("pipe_groups", ctypes.c_uint32),
-                ("pipe_lane_rows", ctypes.c_uint32)]
+                ("pipe_lane_rows", ctypes.c_uint32),
+                ("k1_launch_ms_sum", ctypes.c_float), ("k2_launch_ms_sum", ctypes.c_float),
+                ("k1_launches", ctypes.c_uint32), ("k2_launches", ctypes.c_uint32),
+                ("entry_bytes", ctypes.c_uint64)]
 
 
 class RocJpegError(RuntimeError):

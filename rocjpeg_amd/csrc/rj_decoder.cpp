@@ -104,6 +104,9 @@ Decoder::~Decoder() {
       if (e) (void)hipEventDestroy(e);
     for (auto &e : kev_)
       if (e) (void)hipEventDestroy(e);
+    for (auto *arr : {k1s_, k2s_, k2e_})
+      for (int q = 0; q < kMaxPipe; q++)
+        if (arr[q]) (void)hipEventDestroy(arr[q]);
     for (auto &q : pstream_)
       if (q) (void)hipStreamDestroy(q);
     (void)hipStreamDestroy(stream_);
@@ -138,6 +141,8 @@ int Decoder::Initialize() {
   for (auto &e : pev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : pk1_) RJ_HIP(hipEventCreate(&e));
   for (auto &e : kev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto *arr : {k1s_, k2s_, k2e_})
+    for (int q = 0; q < kMaxPipe; q++) RJ_HIP(hipEventCreate(&arr[q]));
   (void)backend_;  // HARDWARE and HYBRID both run the HIP decoder
   return kOk;
 }
@@ -507,6 +512,11 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   cbuf.rec = d_rec_.as<RjRecord>();
   cbuf.res = d_chunkres_.as<RjChunkRes>();
   cbuf.fallback = d_fallback_.as<uint32_t>();
+  cbuf.count = nullptr;
+  if (profiling_) {
+    RJ_CHECK(d_count_.Ensure(256));
+    cbuf.count = d_count_.as<unsigned long long>();
+  }
   // records persist across calls: a per-call epoch (28 bits, never 0) tells this call's apart
   epoch_ = (epoch_ + 1) & 0x0FFFFFFFu;
   if (epoch_ == 0) epoch_ = 1;
@@ -549,6 +559,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const auto t_k0 = std::chrono::steady_clock::now();
   if (profiling_) RJ_HIP(hipEventRecord(ev_[0], stream_));
   RJ_HIP(hipMemcpyAsync(dbase, h, blob_a, hipMemcpyHostToDevice, stream_));
+  if (cbuf.count) RJ_HIP(hipMemsetAsync(cbuf.count, 0, sizeof(unsigned long long), stream_));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
   RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[2], stream_));
@@ -687,11 +698,13 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     for (int g = 0; g < ngroups && !getenv("RJ_DEBUG_PIPE_SERIAL"); g++) {
       hipStream_t st = g == ngroups - 1 ? stream_ : pstream_[g];
       if (st != stream_) RJ_HIP(hipStreamWaitEvent(st, pev_[kMaxPipe - 1], 0));
+      if (profiling_) RJ_HIP(hipEventRecord(k1s_[g], st));
       RJ_HIP(LaunchEntropyLanes(st, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g], d_destuff_.as<uint8_t>(),
                                 d_tabs, cbuf, epoch_));
       if (profiling_) RJ_HIP(hipEventRecord(pk1_[g], st));
       RJ_HIP(hipEventRecord(kev_[g], st));
       for (int q = 0; q < g; q++) RJ_HIP(hipStreamWaitEvent(st, kev_[q], 0));  // rows spanning classes
+      if (profiling_) RJ_HIP(hipEventRecord(k2s_[g], st));
       if (rows_from_lanes) {
         RJ_HIP(LaunchRowsOfLanes(st, fused_images == 0, d_imgs, n, d_lane_seg + lane_off[g],
                                  lane_off[g + 1] - lane_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>()));
@@ -701,6 +714,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         RJ_HIP(LaunchRows(st, true, d_imgs, n, d_grows, d_row_list + fused_rows + grow_off[g],
                           grow_off[g + 1] - grow_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>()));
       }
+      if (profiling_) RJ_HIP(hipEventRecord(k2e_[g], st));
       if (st != stream_) RJ_HIP(hipEventRecord(pev_[g], st));
     }
     for (int g = 0; g + 1 < ngroups; g++) RJ_HIP(hipStreamWaitEvent(stream_, pev_[g], 0));
@@ -760,16 +774,32 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       ms[2] = k1;
       ms[3] = k12 - k1;
       timings_.entropy_chunks_ms = k1;
+      for (int g = 0; g < ngroups; g++) {
+        float a = 0, b = 0;
+        RJ_HIP(hipEventElapsedTime(&a, k1s_[g], pk1_[g]));
+        RJ_HIP(hipEventElapsedTime(&b, k2s_[g], k2e_[g]));
+        timings_.k1_launch_ms_sum += a;
+        timings_.k2_launch_ms_sum += b;
+        timings_.k1_launches += lane_off[g + 1] > lane_off[g] ? 1u : 0u;
+        timings_.k2_launches += (frow_off[g + 1] > frow_off[g] ? 1u : 0u) + (grow_off[g + 1] > grow_off[g] ? 1u : 0u);
+      }
     } else {
       RJ_HIP(hipEventElapsedTime(&ms[2], ev_[2], ev_[3]));
       RJ_HIP(hipEventElapsedTime(&ms[3], ev_[3], ev_[4]));
       RJ_HIP(hipEventElapsedTime(&timings_.entropy_chunks_ms, ev_[2], ev_[6]));
       RJ_HIP(hipEventElapsedTime(&timings_.entropy_resolve_ms, ev_[6], ev_[7]));
       RJ_HIP(hipEventElapsedTime(&timings_.entropy_serial_ms, ev_[7], ev_[3]));
+      timings_.k1_launch_ms_sum = timings_.entropy_chunks_ms;
+      timings_.k1_launches = (lanes_wg ? 1u : 0u) + (lanes_dev ? 1u : 0u);
+      timings_.k2_launch_ms_sum = ms[3];
+      timings_.k2_launches = (fused_rows ? 1u : 0u) + (general_rows ? 1u : 0u);
       std::vector<uint32_t> fb(seg_total);
       RJ_HIP(hipMemcpy(fb.data(), d_fallback_.as<uint32_t>(), fb.size() * 4, hipMemcpyDeviceToHost));
       for (uint32_t f : fb) timings_.serial_fallbacks += f ? 1u : 0u;
     }
+    unsigned long long cnt = 0;
+    RJ_HIP(hipMemcpy(&cnt, cbuf.count, sizeof(cnt), hipMemcpyDeviceToHost));
+    timings_.entry_bytes = cnt * 4;
     timings_.h2d_ms = ms[0];
     timings_.destuff_ms = ms[1];
     timings_.huffman_ms = ms[2];

@@ -80,6 +80,8 @@ class Decoder {
   hipEvent_t pev_[kMaxPipe] = {};
   hipEvent_t pk1_[kMaxPipe] = {};
   hipEvent_t kev_[kMaxPipe] = {};  // K1 of class g done (K2 of later classes waits on it)
+  hipEvent_t k1s_[kMaxPipe] = {}, k2s_[kMaxPipe] = {}, k2e_[kMaxPipe] = {};  // profiling: launch spans
+  DeviceBuffer d_count_;  // profiling: entries written by K1
 
   // host planning scratch, reused across calls (no per-call allocation / page faults)
   struct Scratch {

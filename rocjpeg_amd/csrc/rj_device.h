@@ -71,6 +71,7 @@ struct RjCoefBuf {
   uint32_t *fallback;         // per interval (batch index): 1 = decode serially
   const uint32_t *lane_seg;   // per lane: batch interval index (0xFFFFFFFF: padding); null: identity
   const uint32_t *seg_lane0;  // per interval: its first lane; null: identity (no interval split)
+  unsigned long long *count;  // profiling: entries written, summed per workgroup (null: off)
 };
 #define RJ_ENT_PER_BLOCK 64       // worst case: DC + 63 AC (each position written at most once)
 #define RJ_ENT_GROUP 16           // K1 writes entries in 64-B groups; regions are group-aligned

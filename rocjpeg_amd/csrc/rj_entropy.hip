@@ -311,7 +311,7 @@ __device__ __forceinline__ void xring_put(const LRow &ring, uint32_t slot, const
   } while (0)
 
 template <bool kCkpt>
-__device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, uint32_t nblk, const uint16_t *s_lut,
+__device__ __forceinline__ uint32_t decode_exact(const LaneJob &J, uint64_t binfo, uint32_t nblk, const uint16_t *s_lut,
                                              const RjTableSet *ts, LRow ring, LRow stage) {
   const uint4 *src = J.src;
   const uint32_t nchunks = (J.bytes + 15) / 16;
@@ -379,10 +379,11 @@ __device__ __forceinline__ void decode_exact(const LaneJob &J, uint64_t binfo, u
   }
   gp(J.pieces + np - 1)->nblk = J.blocks - pfirst;
   gp(J.pieces)->npieces = np;
+  return ne + 1;  // entries incl. the terminator
 }
 
 template <bool kSplit, int kScope>
-__device__ __forceinline__ void decode_lane(const LaneJob &J, uint64_t binfo, uint32_t nblk, uint32_t epoch,
+__device__ __forceinline__ uint32_t decode_lane(const LaneJob &J, uint64_t binfo, uint32_t nblk, uint32_t epoch,
                                             const uint16_t *s_lut, const RjTableSet *ts, LRow ring,
                                             LRow stage, RjChunkRes *res) {
   BitReader br;
@@ -584,6 +585,7 @@ __device__ __forceinline__ void decode_lane(const LaneJob &J, uint64_t binfo, ui
     o.pad[2] = 0;
     *gp(res) = o;
   }
+  return ne + 1;
 }
 
 // kFallback = false: one lane per chunk (all intervals).  kFallback = true: one lane per
@@ -598,14 +600,14 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
                                                       const RjTableSet *__restrict__ tabsets, RjCoefBuf coefs,
                                                       uint32_t epoch) {
   static_assert(RJ_WG == RJ_K1_WG, "lane layout granule");
-  // strides padded by 16 B so the 8-lane groups of ds_*_b128 hit distinct banks
   // lane-interleaved (LRow): 33 ring words per lane (the exact decoder's 32-word ring + mirror;
   // the chunk decoder uses 24) and RJ_STAGE staged entries per lane
   __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_XRING_WORDS + 1][RJ_WG];
   __shared__ __attribute__((aligned(16))) uint32_t s_stage[RJ_STAGE][RJ_WG];
   __shared__ __attribute__((aligned(16))) uint16_t s_lut[RJ_SLUT_ENTRIES];
-  __shared__ uint32_t s_T;
+  __shared__ uint32_t s_T, s_ne;
   const uint32_t tid = threadIdx.x;
+  if (tid == 0) s_ne = 0;
   const uint32_t g = lane0 + blockIdx.x * RJ_WG + tid;  // lane (kFallback: interval)
   bool pending = g < lane0 + nlanes;
   int i = 0;
@@ -678,7 +680,9 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
         J.mcu_first = sg.mcu_first;
         J.mcu_count = sg.mcu_count;
         *gp(J.pieces) = RjPiece{ent_abs, 0u, blocks, 1u, {0, 0, 0}};
-        decode_exact<kFallback>(J, binfo, nblk, s_lut, ts, LRow{&s_ring[0][tid]}, LRow{&s_stage[0][tid]});
+        const uint32_t ne = decode_exact<kFallback>(J, binfo, nblk, s_lut, ts, LRow{&s_ring[0][tid]},
+                                                    LRow{&s_stage[0][tid]});
+        if (coefs.count) atomicAdd(&s_ne, ne);
       } else {
         const uint32_t clen = rj_chunk_len(nbytes, nch);
         const uint32_t b0 = min(c * clen, nbytes), b1 = min(b0 + clen, nbytes);
@@ -703,11 +707,14 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
         J.rec = coefs.rec + uint64_t(g) * RJ_MAX_RECORDS;
         J.rec_next = J.rec - RJ_MAX_RECORDS;  // chunk c+1 sits on lane g-1
         J.next_chunks = nch - 1 - c;
-        decode_lane<true, kScope>(J, binfo, nblk, epoch, s_lut, ts, LRow{&s_ring[0][tid]}, LRow{&s_stage[0][tid]},
-                                  coefs.res + g);
+        const uint32_t ne = decode_lane<true, kScope>(J, binfo, nblk, epoch, s_lut, ts, LRow{&s_ring[0][tid]},
+                                                      LRow{&s_stage[0][tid]}, coefs.res + g);
+        if (coefs.count) atomicAdd(&s_ne, ne);
       }
     }
   }
+  // the loop exits through a barrier: every lane's count is in s_ne
+  if (tid == 0 && coefs.count != nullptr && s_ne != 0) atomicAdd(coefs.count, (unsigned long long)s_ne);
 }
 
 // Chains the chunks of every split interval into pieces; flags intervals for the serial path.

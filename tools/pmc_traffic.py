@@ -3,7 +3,9 @@
 
 FETCH_SIZE and WRITE_SIZE are reported in KiB per dispatch.  On gfx950 FETCH_SIZE counts half
 the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM section), so reads are doubled;
-WRITE_SIZE is taken as is.  Writes profiles/pmc_traffic.json for bench.py's roofline.traffic.
+WRITE_SIZE is taken as is.  Per decode call (one k_destuff dispatch per call) the dispatches of
+each kernel are summed: k_entropy = the chunk/exact pass (k_entropy<false, *>), k_rows = both
+K2 variants.  Writes profiles/pmc_traffic.json for bench.py's roofline.traffic.
 
     python3 tools/pmc_traffic.py gpurun_out/pmc_<tag> <batch> [out.json]
 """
@@ -11,25 +13,48 @@ import collections
 import csv
 import glob
 import json
+import re
 import sys
 
 root, batch = sys.argv[1], int(sys.argv[2])
 out = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json"
-vals = collections.defaultdict(lambda: collections.defaultdict(list))
+
+
+def group(name):
+    n = name.split("(")[0].replace("void ", "").replace("rj::", "").strip()
+    if n.startswith("k_entropy<false"):
+        return "k_entropy"
+    if n.startswith("k_rows"):
+        return "k_rows"
+    return re.sub(r"<.*", "", n)
+
+
+tot = collections.defaultdict(lambda: collections.defaultdict(float))
+disp = collections.defaultdict(lambda: collections.defaultdict(set))
 for f in sorted(glob.glob(f"{root}/pass*/*counter_collection.csv")):
+    p = f.split("/")[-2]
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].replace("rj::", "")
-        if r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
-            vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]) * 1024.0)
+        k = group(r["Kernel_Name"])
+        c = r["Counter_Name"]
+        if c in ("FETCH_SIZE", "WRITE_SIZE"):
+            tot[k][(p, c)] += float(r["Counter_Value"]) * 1024.0
+            disp[k][(p, c)].add(r["Dispatch_Id"])
+calls = {}
+for (p, c), ids in disp["k_destuff"].items():
+    calls[(p, c)] = len(ids)
 res = {"source": root, "batch": batch,
-       "method": "per dispatch: 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes), mean over dispatches, / batch",
+       "method": "per decode call: sum over the call's dispatches of 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes)",
        "kernels": {}}
-for k, c in sorted(vals.items()):
-    if k.startswith("__amd") or "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
+for k in sorted(tot):
+    if k.startswith("__amd"):
         continue
-    fetch = sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"]) * 2.0
-    write = sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"])
-    res["kernels"][k] = {"fetch_bytes_per_launch": int(fetch), "write_bytes_per_launch": int(write),
-                         "hbm_bytes_per_image": (fetch + write) / batch}
+    fetch = [v / calls[pc] for pc, v in tot[k].items() if pc[1] == "FETCH_SIZE" and calls.get(pc)]
+    write = [v / calls[pc] for pc, v in tot[k].items() if pc[1] == "WRITE_SIZE" and calls.get(pc)]
+    if not fetch or not write:
+        continue
+    fb, wb = 2.0 * sum(fetch) / len(fetch), sum(write) / len(write)
+    nd = max(len(ids) for pc, ids in disp[k].items()) / max(calls.values())
+    res["kernels"][k] = {"fetch_bytes_per_call": int(fb), "write_bytes_per_call": int(wb),
+                         "launches_per_call": nd, "hbm_bytes_per_image": (fb + wb) / batch}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
