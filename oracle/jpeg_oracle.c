@@ -294,6 +294,17 @@ static int next_restart(bitrd *b) {
   return 0;
 }
 
+/* One scan of a progressive (SOF2) stream: its header, the Huffman tables in force when it
+ * started (DHT may change between scans), its DRI and its entropy-coded byte range. */
+#define OJ_MAX_SCANS 64
+typedef struct {
+  int ns, comp[4];         /* component indexes (into the frame) */
+  int ss, se, ah, al;
+  int ri;
+  htab dc[4], ac[4];       /* per scan component */
+  size_t ecs_off, ecs_end;
+} pscan;
+
 typedef struct {
   oj_params p;
   int nc, hmax, vmax, mcux, mcuy, interleaved;
@@ -302,10 +313,18 @@ typedef struct {
   size_t coef_total, plane_total;
   htab dc[4], ac[4];
   uint16_t q[4][64]; /* natural order */
+  /* progressive */
+  int progressive, nscans;
+  int cwblk[4], chblk[4];  /* width/height_in_blocks: the blocks a non-interleaved scan codes */
+  pscan scans[OJ_MAX_SCANS];
 } plan;
+
+static int is_progressive(const uint8_t *d, size_t n);
+static int make_plan_prog(const uint8_t *d, size_t n, plan *pl);
 
 static int make_plan(const uint8_t *data, size_t len, plan *pl) {
   memset(pl, 0, sizeof(*pl));
+  if (is_progressive(data, len)) return make_plan_prog(data, len, pl);
   if (!oj_parse(data, len, &pl->p)) return ST_BAD_JPEG;
   oj_params *p = &pl->p;
   if (!p->sof_seen || p->ncomp == 0) return ST_NOT_SUPPORTED;
@@ -357,6 +376,346 @@ static int make_plan(const uint8_t *data, size_t len, plan *pl) {
   return ST_OK;
 }
 
+/* ---------------------------------------------------------------------------------
+ * Progressive (SOF2) decode -- SURVEY.md 8f rank 2 (config C5).  The reference parser
+ * rejects SOF2 (rocjpeg_parser.cpp:74-104 handles SOF0 only), so there is no reference
+ * arithmetic: this restates ITU-T T.81 Annex G and IJG libjpeg 9.4 (jdhuff.c
+ * decode_mcu_DC_first / _AC_first / _DC_refine / _AC_refine, process_restart;
+ * jdinput.c latch_quant_tables; jdmarker.c get_sos) and is pinned against libjpeg's own
+ * jpeg_read_coefficients output (oracle/libjpeg_golden.c).  Semantics kept from libjpeg:
+ *   - a needed bit past the data reads as 0 and sets insufficient_data; the MCUs after
+ *     that one, up to the next restart, are skipped (their coefficients keep their values);
+ *   - a restart marker that is not there keeps them skipped to the end of the interval;
+ *   - each component's quant table is latched at the first scan that contains it;
+ *   - block smoothing (libjpeg's output for incomplete progressions) is not applied: the
+ *     planes are the ISLOW transform of the final coefficients.
+ * ------------------------------------------------------------------------------- */
+static int is_progressive(const uint8_t *d, size_t n) {
+  if (!d || n < 4 || d[0] != 0xFF || d[1] != 0xD8) return 0;
+  size_t pos = 2;
+  while (pos + 4 <= n) {
+    while (pos < n && d[pos] == 0xFF) pos++;
+    if (pos + 3 > n) return 0;
+    unsigned m = d[pos++];
+    size_t len = be16(d + pos);
+    if (m == 0xC2) return 1;
+    if (m == 0xDA || m == 0xC0 || m == 0xC1 || len < 2) return 0;
+    pos += len;
+  }
+  return 0;
+}
+
+/* End of a scan's entropy-coded data: the first marker other than RSTn (FF 00 is data,
+ * FF FF is fill). */
+static size_t scan_end(const uint8_t *d, size_t pos, size_t n) {
+  while (pos + 1 < n) {
+    if (d[pos] == 0xFF) {
+      size_t q = pos + 1;
+      while (q < n && d[q] == 0xFF) q++;
+      if (q >= n) return pos;
+      if (d[q] == 0x00 || (d[q] >= 0xD0 && d[q] <= 0xD7)) { pos = q + 1; continue; }
+      return pos;
+    }
+    pos++;
+  }
+  return n;
+}
+
+static int make_plan_prog(const uint8_t *d, size_t n, plan *pl) {
+  oj_params *p = &pl->p;
+  uint8_t ht_bits[2][2][16], ht_vals[2][2][256];
+  int ht_ok[2][2] = {{0, 0}, {0, 0}};
+  uint8_t qt[4][64];
+  int qt_ok[4] = {0, 0, 0, 0}, latched[4] = {0, 0, 0, 0};
+  int ri = 0;
+  pl->progressive = 1;
+  size_t pos = 2;
+  int sof = 0, eoi = 0;
+  while (!eoi && pos + 1 < n) {
+    if (d[pos] != 0xFF) { pos++; continue; } /* garbage between segments: skip (libjpeg warns) */
+    while (pos < n && d[pos] == 0xFF) pos++;
+    if (pos >= n) break;
+    unsigned m = d[pos++];
+    if (m == 0xD9) { eoi = 1; break; }
+    if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+    if (pos + 2 > n) break;
+    size_t len = be16(d + pos), seg = pos, next = pos + len;
+    if (len < 2 || next > n) return ST_BAD_JPEG;
+    switch (m) {
+      case 0xC2: {
+        if (sof || len < 8) return ST_BAD_JPEG;
+        p->precision = d[seg + 2];
+        p->height = (uint16_t)be16(d + seg + 3);
+        p->width = (uint16_t)be16(d + seg + 5);
+        p->ncomp = d[seg + 7];
+        if (p->ncomp < 1 || p->ncomp > 3 || len < 8 + 3u * p->ncomp) return ST_BAD_JPEG;
+        for (int i = 0; i < p->ncomp; i++) {
+          const uint8_t *c = d + seg + 8 + 3 * i;
+          p->comp[i].id = c[0];
+          p->comp[i].h = c[1] >> 4;
+          p->comp[i].v = c[1] & 15;
+          p->comp[i].tq = c[2];
+          if (c[2] >= 4) return ST_BAD_JPEG;
+        }
+        p->sof_seen = 1;
+        sof = 1;
+        break;
+      }
+      case 0xC0: case 0xC1: case 0xC3: case 0xC5: case 0xC6: case 0xC7:
+      case 0xC9: case 0xCA: case 0xCB: case 0xCD: case 0xCE: case 0xCF:
+        return ST_BAD_JPEG; /* a second frame */
+      case 0xC4: {
+        size_t q = seg + 2;
+        while (q < next) {
+          if (q + 17 > next) return ST_BAD_JPEG;
+          unsigned idx = d[q++], id = idx & 15, ac = (idx >> 4) != 0;
+          if (id >= 2 || (idx >> 4) > 1) return ST_BAD_JPEG;
+          unsigned cnt = 0;
+          for (int i = 0; i < 16; i++) cnt += d[q + i];
+          memcpy(ht_bits[ac][id], d + q, 16);
+          q += 16;
+          if (cnt > 256 || q + cnt > next) return ST_BAD_JPEG;
+          memset(ht_vals[ac][id], 0, 256);
+          memcpy(ht_vals[ac][id], d + q, cnt);
+          ht_ok[ac][id] = 1;
+          q += cnt;
+        }
+        break;
+      }
+      case 0xDB: {
+        size_t q = seg + 2;
+        while (q < next) {
+          unsigned idx = d[q++];
+          if ((idx >> 4) || idx >= 4 || q + 64 > next) return ST_BAD_JPEG; /* 8-bit tables only */
+          memcpy(qt[idx], d + q, 64);
+          qt_ok[idx] = 1;
+          q += 64;
+        }
+        break;
+      }
+      case 0xDD:
+        if (len != 4) return ST_BAD_JPEG;
+        ri = (int)be16(d + seg + 2);
+        break;
+      case 0xDA: {
+        if (!sof) return ST_BAD_JPEG;
+        if (pl->nscans >= OJ_MAX_SCANS) return ST_NOT_SUPPORTED;
+        pscan *sc = &pl->scans[pl->nscans];
+        unsigned ns = d[seg + 2];
+        if (ns < 1 || ns > 4 || len != 6 + 2 * ns) return ST_BAD_JPEG;
+        sc->ns = (int)ns;
+        for (unsigned i = 0; i < ns; i++) {
+          unsigned cs = d[seg + 3 + 2 * i], t = d[seg + 4 + 2 * i];
+          int ci = -1;
+          for (int c = 0; c < p->ncomp; c++)
+            if (p->comp[c].id == cs) ci = c;
+          if (ci < 0) return ST_BAD_JPEG;
+          for (unsigned j = 0; j < i; j++)
+            if (sc->comp[j] == ci) return ST_BAD_JPEG;
+          sc->comp[i] = ci;
+          unsigned td = t >> 4, ta = t & 15;
+          if (td >= 2 || ta >= 2) return ST_BAD_JPEG;
+          /* tables are needed only by the scan kinds that use them */
+          sc->ss = d[seg + 3 + 2 * ns];
+          if (sc->ss == 0 && !(d[seg + 5 + 2 * ns] >> 4)) {
+            if (!ht_ok[0][td]) return ST_BAD_JPEG;
+            if (!build_htab(ht_bits[0][td], ht_vals[0][td], 12, &sc->dc[i])) return ST_BAD_JPEG;
+          }
+          if (sc->ss != 0) {
+            if (!ht_ok[1][ta]) return ST_BAD_JPEG;
+            if (!build_htab(ht_bits[1][ta], ht_vals[1][ta], 162, &sc->ac[i])) return ST_BAD_JPEG;
+          }
+        }
+        sc->ss = d[seg + 3 + 2 * ns];
+        sc->se = d[seg + 4 + 2 * ns];
+        sc->ah = d[seg + 5 + 2 * ns] >> 4;
+        sc->al = d[seg + 5 + 2 * ns] & 15;
+        /* jdhuff.c start_pass_huff_decoder progressive checks (JERR_BAD_PROGRESSION) */
+        if (sc->ss == 0) {
+          if (sc->se != 0) return ST_BAD_JPEG;
+        } else {
+          if (sc->se < sc->ss || sc->se > 63 || sc->ns != 1) return ST_BAD_JPEG;
+        }
+        if (sc->ah != 0 && sc->ah - 1 != sc->al) return ST_BAD_JPEG;
+        if (sc->al > 13) return ST_BAD_JPEG;
+        sc->ri = ri;
+        for (int i = 0; i < sc->ns; i++) { /* latch_quant_tables */
+          int c = sc->comp[i];
+          if (!latched[c]) {
+            int tq = p->comp[c].tq;
+            if (!qt_ok[tq]) return ST_BAD_JPEG;
+            for (int k = 0; k < 64; k++) pl->q[c][kZigzag[k]] = qt[tq][k];
+            memcpy(p->qt_zz[tq], qt[tq], 64);
+            p->qt_loaded[tq] = 1;
+            latched[c] = 1;
+          }
+        }
+        sc->ecs_off = next;
+        sc->ecs_end = scan_end(d, next, n);
+        pl->nscans++;
+        next = sc->ecs_end;
+        break;
+      }
+      default:
+        break;
+    }
+    pos = next;
+  }
+  if (!sof || pl->nscans == 0) return ST_BAD_JPEG;
+  if (p->precision != 8) return ST_NOT_SUPPORTED;
+  p->css = css_of(p);
+  pl->nc = p->ncomp;
+  for (int c = 0; c < pl->nc; c++) {
+    if (p->comp[c].h < 1 || p->comp[c].h > 4 || p->comp[c].v < 1 || p->comp[c].v > 4) return ST_BAD_JPEG;
+    if (p->comp[c].h > pl->hmax) pl->hmax = p->comp[c].h;
+    if (p->comp[c].v > pl->vmax) pl->vmax = p->comp[c].v;
+  }
+  pl->interleaved = pl->nc > 1;
+  if (pl->interleaved) {
+    int bpm = 0;
+    for (int c = 0; c < pl->nc; c++) bpm += p->comp[c].h * p->comp[c].v;
+    if (bpm > 10) return ST_BAD_JPEG;
+  }
+  pl->mcux = (p->width + 8 * pl->hmax - 1) / (8 * pl->hmax);
+  pl->mcuy = (p->height + 8 * pl->vmax - 1) / (8 * pl->vmax);
+  for (int c = 0; c < pl->nc; c++) {
+    int cw = (p->width * p->comp[c].h + pl->hmax - 1) / pl->hmax;
+    int ch = (p->height * p->comp[c].v + pl->vmax - 1) / pl->vmax;
+    pl->cwblk[c] = (cw + 7) / 8;
+    pl->chblk[c] = (ch + 7) / 8;
+    if (pl->interleaved) {
+      pl->wblk[c] = pl->mcux * p->comp[c].h;
+      pl->hblk[c] = pl->mcuy * p->comp[c].v;
+    } else {
+      pl->wblk[c] = pl->cwblk[c];
+      pl->hblk[c] = pl->chblk[c];
+      pl->mcux = pl->wblk[c];
+      pl->mcuy = pl->hblk[c];
+    }
+  }
+  for (int c = 0; c < pl->nc; c++)
+    if (!latched[c]) return ST_BAD_JPEG; /* a component no scan codes */
+  size_t co = 0;
+  for (int c = 0; c < pl->nc; c++) {
+    pl->coef_off[c] = co;
+    pl->plane_off[c] = co;
+    co += (size_t)pl->wblk[c] * pl->hblk[c] * 64;
+  }
+  pl->coef_total = pl->plane_total = co;
+  /* the fields GetImageInfo and the output stage read */
+  p->scan_ncomp = p->ncomp;
+  for (int c = 0; c < pl->nc; c++) p->scomp[c].cs = p->comp[c].id;
+  return ST_OK;
+}
+
+/* libjpeg decode_mcu_AC_refine's correction-bit step for one already-nonzero coefficient */
+static void refine_coef(bitrd *b, int16_t *c, int p1, int m1) {
+  if (getbit(b) && (*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
+}
+
+static void prog_block(bitrd *b, const pscan *sc, int i, int16_t *blk, int *pred, int *eobrun) {
+  const int al = sc->al;
+  if (sc->ss == 0) {
+    if (sc->ah == 0) { /* DC first */
+      int s = hdecode(b, &sc->dc[i]);
+      int diff = s ? extend(getbits(b, s), s) : 0;
+      *pred += diff;
+      blk[0] = (int16_t)(*pred << al);
+    } else if (getbit(b)) { /* DC refine */
+      blk[0] = (int16_t)(blk[0] | (1 << al));
+    }
+    return;
+  }
+  if (sc->ah == 0) { /* AC first */
+    if (*eobrun) { (*eobrun)--; return; }
+    for (int k = sc->ss; k <= sc->se; k++) {
+      int rs = hdecode(b, &sc->ac[i]), r = rs >> 4, s = rs & 15;
+      if (s) {
+        k += r;
+        int v = extend(getbits(b, s), s);
+        blk[kZigzag[k > 79 ? 79 : k]] = (int16_t)(v << al);
+      } else {
+        if (r != 15) {
+          if (r) *eobrun = (1 << r) + getbits(b, r) - 1;
+          break;
+        }
+        k += 15;
+      }
+    }
+    return;
+  }
+  /* AC refine */
+  const int p1 = 1 << al, m1 = -1 * (1 << al);
+  int k = sc->ss;
+  if (*eobrun == 0) {
+    do {
+      int rs = hdecode(b, &sc->ac[i]), r = rs >> 4, s = rs & 15;
+      if (s) {
+        s = getbit(b) ? p1 : m1;
+      } else if (r != 15) {
+        *eobrun = 1 << r;
+        if (r) *eobrun += getbits(b, r);
+        break;
+      }
+      do {
+        int16_t *c = &blk[kZigzag[k > 79 ? 79 : k]];
+        if (*c) refine_coef(b, c, p1, m1);
+        else if (--r < 0) break;
+        k++;
+      } while (k <= sc->se);
+      if (s) blk[kZigzag[k > 79 ? 79 : k]] = (int16_t)s;
+      k++;
+    } while (k <= sc->se);
+  }
+  if (*eobrun) {
+    for (; k <= sc->se; k++) {
+      int16_t *c = &blk[kZigzag[k]];
+      if (*c) refine_coef(b, c, p1, m1);
+    }
+    (*eobrun)--;
+  }
+}
+
+static int decode_progressive(const uint8_t *data, const plan *pl, int16_t *out) {
+  memset(out, 0, pl->coef_total * sizeof(int16_t));
+  const oj_params *p = &pl->p;
+  for (int si = 0; si < pl->nscans; si++) {
+    const pscan *sc = &pl->scans[si];
+    bitrd b;
+    memset(&b, 0, sizeof(b));
+    b.d = data;
+    b.pos = sc->ecs_off;
+    b.end = sc->ecs_end;
+    int pred[4] = {0, 0, 0, 0}, eobrun = 0, skip = 0;
+    const int inter = sc->ns > 1;
+    const int c0 = sc->comp[0];
+    const long mx_n = inter ? pl->mcux : pl->cwblk[c0];
+    const long total = inter ? (long)pl->mcux * pl->mcuy : (long)pl->cwblk[c0] * pl->chblk[c0];
+    for (long m = 0; m < total; m++) {
+      if (sc->ri && m > 0 && m % sc->ri == 0) {
+        skip = !next_restart(&b);
+        pred[0] = pred[1] = pred[2] = pred[3] = 0;
+        eobrun = 0;
+      }
+      const long mx = m % mx_n, my = m / mx_n;
+      if (!skip) {
+        for (int i = 0; i < sc->ns; i++) {
+          const int c = sc->comp[i];
+          const int hc = inter ? p->comp[c].h : 1, vc = inter ? p->comp[c].v : 1;
+          for (int by = 0; by < vc; by++)
+            for (int bx = 0; bx < hc; bx++) {
+              const long gx = mx * hc + bx, gy = my * vc + by;
+              int16_t *blk = out + pl->coef_off[c] + ((size_t)gy * pl->wblk[c] + gx) * 64;
+              prog_block(&b, sc, i, blk, &pred[c], &eobrun);
+            }
+        }
+      }
+      if (b.insufficient) skip = 1;
+    }
+  }
+  return ST_OK;
+}
+
 static void decode_block(bitrd *b, const htab *dc, const htab *ac, int *pred, int16_t *blk, int skip) {
   memset(blk, 0, 64 * sizeof(int16_t));
   if (skip) return;
@@ -380,6 +739,7 @@ static void decode_block(bitrd *b, const htab *dc, const htab *ac, int *pred, in
 }
 
 static int decode_all_coefs(const uint8_t *data, const plan *pl, int16_t *out) {
+  if (pl->progressive) return decode_progressive(data, pl, out);
   const oj_params *p = &pl->p;
   bitrd b;
   memset(&b, 0, sizeof(b));

@@ -61,6 +61,9 @@ static int dump_planes(struct jpeg_decompress_struct *ci, FILE *out) {
   ci->raw_data_out = TRUE;
   ci->dct_method = JDCT_ISLOW;
   ci->do_fancy_upsampling = FALSE;
+  /* progressive streams whose progression is incomplete (truncated): the planes are the
+     ISLOW transform of the final coefficients, without libjpeg's block smoothing */
+  ci->do_block_smoothing = FALSE;
   jpeg_start_decompress(ci);
   int nc = ci->num_components, vmax = ci->max_v_samp_factor;
   int n_imcu = (int)((ci->output_height + vmax * 8 - 1) / (vmax * 8));

@@ -91,3 +91,24 @@ def oracle_decode(data, fmt, channel_shapes, crop=(0, 0, 0, 0), fill=0xA5):
 
 def sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def frame_info(data):
+    """Frame header fields (SOF0/1/2) in the manifest's ref_parse shape -- for the progressive
+    fixtures, which the reference parser rejects (it records zeros for them)."""
+    pos = 2
+    while pos + 4 <= len(data):
+        while data[pos] == 0xFF:
+            pos += 1
+        m = data[pos]
+        ln = (data[pos + 1] << 8) | data[pos + 2]
+        if m in (0xC0, 0xC1, 0xC2):
+            seg = pos + 1
+            h = (data[seg + 3] << 8) | data[seg + 4]
+            w = (data[seg + 5] << 8) | data[seg + 6]
+            nc = data[seg + 7]
+            hv = [[data[seg + 9 + 3 * i] >> 4, data[seg + 9 + 3 * i] & 15] for i in range(nc)]
+            hv += [[0, 0]] * (4 - nc)
+            return {"ok": 1, "width": w, "height": h, "ncomp": nc, "comp_hv": hv}
+        pos += 1 + ln
+    raise ValueError("no frame header")

@@ -9,7 +9,8 @@ from tests import oracle_lib as O
 pytestmark = pytest.mark.gpu
 
 FIX = O.manifest()
-DECODABLE = [f for f in FIX if "libjpeg_coef_sha256" in f and f["ref_parse"]["css"] in (0, 1, 2, 3, 5)]
+# baseline fixtures (the reference parser accepts them); progressive ones: test_progressive_gpu.py
+DECODABLE = [f for f in FIX if "libjpeg_coef_sha256" in f and f["ref_parse"]["ok"] and f["ref_parse"]["css"] in (0, 1, 2, 3, 5)]
 SMALL = [f for f in DECODABLE if f["bytes"] < 100_000]
 FORMATS = list(R.OutputFormat)
 

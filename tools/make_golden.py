@@ -136,6 +136,16 @@ def fixtures():
     add("p420_q90_nori_1920x1080", pillow_jpeg(source_rgb(s + 17, 1920, 1080), quality=90, subsampling=2), "1080p without DRI")
     full = pillow_jpeg(source_rgb(s + 18, 192, 128), quality=90, subsampling=2, restart_marker_rows=1)
     add("p420_trunc_192x128", full[: len(full) * 3 // 5], "truncated stream (no EOI): libjpeg zero-fill semantics")
+    # progressive (SOF2), SURVEY 8f rank 2 / config C5: decoded here (the reference rejects it)
+    add("pp420_q90_1920x1080", pillow_jpeg(source_rgb(s + 19, 1920, 1080), quality=90, subsampling=2, progressive=True), "progressive 4:2:0 q90 1080p (C5 sample)")
+    add("pp420_opt_200x150", pillow_jpeg(source_rgb(s + 20, 200, 150), quality=85, subsampling=2, progressive=True, optimize=True), "progressive, optimised per-scan tables, ragged edges")
+    add("cp444_prog_ri_136x72", cjpeg_jpeg(source_rgb(s + 21, 136, 72), ["-quality", "90", "-sample", "1x1,1x1,1x1", "-progressive", "-restart", "1"]), "progressive 4:4:4, DRI = 1 MCU row in every scan")
+    add("cp422_prog_97x67", cjpeg_jpeg(source_rgb(s + 22, 97, 67), ["-quality", "80", "-sample", "2x1,1x1,1x1", "-progressive"]), "progressive 4:2:2, odd size")
+    add("cp420_prog_ri3_160x112", cjpeg_jpeg(source_rgb(s + 23, 160, 112), ["-quality", "95", "-sample", "2x2,1x1,1x1", "-progressive", "-restart", "3B"]), "progressive 4:2:0, DRI = 3 MCUs")
+    add("cp400_prog_120x80", cjpeg_jpeg(source_rgb(s + 24, 120, 80), ["-quality", "90", "-progressive"], gray=True), "progressive grayscale")
+    add("cp440_prog_96x80", cjpeg_jpeg(source_rgb(s + 25, 96, 80), ["-quality", "90", "-sample", "1x2,1x1,1x1", "-progressive"]), "progressive 4:4:0")
+    fullp = pillow_jpeg(source_rgb(s + 26, 192, 128), quality=90, subsampling=2, progressive=True)
+    add("pp420_prog_trunc_192x128", fullp[: len(fullp) * 11 // 20], "truncated progressive stream: later scans missing, insufficient-data semantics")
     return out
 
 
@@ -161,7 +171,7 @@ def main():
             cpath, ppath = os.path.join(td, "c.bin"), os.path.join(td, "p.bin")
             rc1 = subprocess.run([GOLDEN_TOOL, "coef", path, cpath], capture_output=True)
             rc2 = subprocess.run([GOLDEN_TOOL, "planes", path, ppath], capture_output=True)
-            if rc1.returncode == 0 and rc2.returncode == 0 and "prog" not in name:
+            if rc1.returncode == 0 and rc2.returncode == 0:
                 ent["libjpeg_coef_sha256"], ent["coef_dims"] = read_coef(cpath)
                 ent["libjpeg_planes_sha256"] = read_planes(ppath)
             manifest["fixtures"].append(ent)
