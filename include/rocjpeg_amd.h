@@ -11,7 +11,9 @@
 extern "C" {
 #endif
 
-/* Parse-only image info that needs no decoder handle (rocJpegGetImageInfo requires one). */
+/* Parse-only image info that needs no decoder handle (rocJpegGetImageInfo requires one).
+ * num_restart_intervals: baseline -- restart intervals of the scan; progressive (SOF2) -- the
+ * restart intervals summed over all scans. */
 RocJpegStatus rocJpegAmdStreamGetInfo(RocJpegStreamHandle stream, uint8_t *num_components,
                                       RocJpegChromaSubsampling *subsampling, uint32_t *widths, uint32_t *heights,
                                       uint32_t *num_restart_intervals);
@@ -52,6 +54,10 @@ typedef struct {
   float k1_launch_ms_sum, k2_launch_ms_sum;
   uint32_t k1_launches, k2_launches;
   uint64_t entry_bytes;      /* sparse coefficient entries K1 wrote (counted on the device) */
+  /* progressive (SOF2) images of the call: K1p (all dependency levels) and their K2 rows */
+  float prog_entropy_ms, prog_rows_ms;
+  uint32_t prog_images, prog_intervals, prog_levels, prog_pad;
+  uint64_t prog_coef_bytes;  /* dense coefficient bytes (int16 per coefficient) */
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);

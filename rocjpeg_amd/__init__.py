@@ -91,7 +91,11 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("pipe_lane_rows", ctypes.c_uint32),
                 ("k1_launch_ms_sum", ctypes.c_float), ("k2_launch_ms_sum", ctypes.c_float),
                 ("k1_launches", ctypes.c_uint32), ("k2_launches", ctypes.c_uint32),
-                ("entry_bytes", ctypes.c_uint64)]
+                ("entry_bytes", ctypes.c_uint64),
+                ("prog_entropy_ms", ctypes.c_float), ("prog_rows_ms", ctypes.c_float),
+                ("prog_images", ctypes.c_uint32), ("prog_intervals", ctypes.c_uint32),
+                ("prog_levels", ctypes.c_uint32), ("prog_pad", ctypes.c_uint32),
+                ("prog_coef_bytes", ctypes.c_uint64)]
 
 
 class RocJpegError(RuntimeError):

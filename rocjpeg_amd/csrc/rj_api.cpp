@@ -149,7 +149,7 @@ RJ_EXPORT RocJpegStatus rocJpegAmdStreamGetInfo(RocJpegStreamHandle s, uint8_t *
     int c = -1;
     const int r = rj::ImageInfo(st->info(), nc, &c, widths, heights);
     *css = RocJpegChromaSubsampling(c);
-    if (nintervals) *nintervals = uint32_t(st->plan().segs.size());
+    if (nintervals) *nintervals = uint32_t(st->plan().progressive ? st->plan().pivals.size() : st->plan().segs.size());
     return r;
   });
 }

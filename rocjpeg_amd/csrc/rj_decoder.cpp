@@ -104,6 +104,8 @@ Decoder::~Decoder() {
       if (e) (void)hipEventDestroy(e);
     for (auto &e : kev_)
       if (e) (void)hipEventDestroy(e);
+    for (auto &e : prog_ev_)
+      if (e) (void)hipEventDestroy(e);
     for (auto *arr : {k1s_, k2s_, k2e_})
       for (int q = 0; q < kMaxPipe; q++)
         if (arr[q]) (void)hipEventDestroy(arr[q]);
@@ -141,6 +143,7 @@ int Decoder::Initialize() {
   for (auto &e : pev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : pk1_) RJ_HIP(hipEventCreate(&e));
   for (auto &e : kev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto &e : prog_ev_) RJ_HIP(hipEventCreate(&e));
   for (auto *arr : {k1s_, k2s_, k2e_})
     for (int q = 0; q < kMaxPipe; q++) RJ_HIP(hipEventCreate(&arr[q]));
   (void)backend_;  // HARDWARE and HYBRID both run the HIP decoder
@@ -178,6 +181,15 @@ int Decoder::StreamsToDevice(Stream *const *streams, int n) {
     RJ_HIP(hipMemcpy(r.ecs, in.ecs, in.ecs_size, hipMemcpyHostToDevice));
     RJ_HIP(hipMemcpy(r.segs, p.segs.data(), p.segs.size() * sizeof(RjSegDev), hipMemcpyHostToDevice));
     if (!p.ds.empty()) RJ_HIP(hipMemcpy(r.ds, p.ds.data(), p.ds.size() * sizeof(RjDsBlock), hipMemcpyHostToDevice));
+    if (p.progressive) {  // scans, intervals and Huffman tables travel with the bitstream
+      RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.pscans), std::max<size_t>(p.pscans.size() * sizeof(RjProgScanDev), 16)));
+      RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.pivals), std::max<size_t>(p.pivals.size() * sizeof(RjProgIvalDev), 16)));
+      RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.ptabs), std::max<size_t>(p.ptabs.size() * sizeof(RjHuffDev), 16)));
+      RJ_HIP(hipMemcpy(r.pscans, p.pscans.data(), p.pscans.size() * sizeof(RjProgScanDev), hipMemcpyHostToDevice));
+      RJ_HIP(hipMemcpy(r.pivals, p.pivals.data(), p.pivals.size() * sizeof(RjProgIvalDev), hipMemcpyHostToDevice));
+      if (!p.ptabs.empty())
+        RJ_HIP(hipMemcpy(r.ptabs, p.ptabs.data(), p.ptabs.size() * sizeof(RjHuffDev), hipMemcpyHostToDevice));
+    }
     s->resident = r;
   }
   return kOk;
@@ -261,6 +273,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   uint32_t fused_rows = 0, general_rows = 0, fused_images = 0;
   std::vector<uint8_t> &is_fused = sc_.is_fused;
   is_fused.assign(n, 0);
+  // progressive images: their own K2 row spaces (dense coefficients), K1p intervals, buffers
+  std::vector<uint32_t> &prow_prefix = sc_.prow_prefix, &pgrow_prefix = sc_.pgrow_prefix;
+  prow_prefix.resize(n);
+  pgrow_prefix.resize(n);
+  uint32_t pfused_rows = 0, pgeneral_rows = 0, prog_images = 0, prog_levels = 0, pival_total = 0;
+  uint64_t coef_dw_total = 0, nz_total = 0;
   for (int i = 0; i < n; i++) {
     Stream *s = streams[i];
     const StreamInfo &in = s->info();
@@ -283,7 +301,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       d.comp_v[c] = in.comp[c].v;
       d.comp_td[c] = in.scomp[c].td;
       d.comp_ta[c] = in.scomp[c].ta;
-      d.comp_tq[c] = in.comp[c].tq;
+      d.comp_tq[c] = p.progressive ? uint8_t(c) : in.comp[c].tq;  // progressive: latched per component
       d.comp_blk0[c] = p.comp_blk0[c];
     }
     std::memcpy(d.blk_comp, p.blk_comp, RJ_MAX_BLK_MCU);
@@ -307,11 +325,32 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       d.plane_pitch[c] = p.wblk[c] * 8;
       d.plane_rows[c] = p.hblk[c] * 8;
     }
+    d.pival_prefix = pival_total;
+    if (p.progressive) {
+      d.progressive = 1;
+      d.coef_off = coef_dw_total;
+      coef_dw_total += AlignUp(p.coef_blocks * 32, 64);
+      d.nz_off = nz_total;
+      nz_total += AlignUp(p.nz_blocks, 8);
+      for (int c = 0; c < 3; c++) {
+        d.cblk0[c] = p.cblk0[c];
+        d.wblk[c] = p.wblk[c];
+        d.nzblk0[c] = p.nzblk0[c];
+        d.cwblk[c] = p.cwblk[c];
+      }
+      pival_total += uint32_t(p.pivals.size());
+      prog_images++;
+      prog_levels = std::max(prog_levels, p.plevels);
+    }
     ecs_bytes += in.ecs_size;
     if (!(s->resident.device == device_ && s->resident.generation == s->generation())) {
       stage_off[i] = stage_bytes;
       stage_bytes += AlignUp(p.segs.size() * sizeof(RjSegDev), 256) + AlignUp(p.ds.size() * sizeof(RjDsBlock), 256) +
                      AlignUp(in.ecs_size + 16, 256);
+      if (p.progressive)
+        stage_bytes += AlignUp(p.pscans.size() * sizeof(RjProgScanDev), 256) +
+                       AlignUp(p.pivals.size() * sizeof(RjProgIvalDev), 256) +
+                       AlignUp(p.ptabs.size() * sizeof(RjHuffDev), 256);
     }
 
     // output window: ROI semantics of rocjpeg_decoder.cpp:124-141 (no ROI decode on gfx950)
@@ -330,6 +369,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
     row_prefix[i] = fused_rows;
     grow_prefix[i] = general_rows;
+    prow_prefix[i] = pfused_rows;
+    pgrow_prefix[i] = pgeneral_rows;
 
     // ---- output jobs (general path): rocjpeg_decoder.cpp:143-180 ----
     const size_t jobs_before = jobs.size();
@@ -416,16 +457,69 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (path_policy_ == 0 && FusedEligible(in, p, fmt, roi, o)) {
       rows_total = jobs_rows_before;
       jobs.resize(jobs_before);
-      fused_rows += p.mcuy;  // k_fused: one workgroup per MCU row
-      fused_images++;
+      if (p.progressive) {
+        pfused_rows += p.mcuy;
+      } else {
+        fused_rows += p.mcuy;  // k_fused: one workgroup per MCU row
+        fused_images++;
+      }
       is_fused[i] = 1;
     } else {
       for (int c = 0; c < in.ncomp; c++) {
         d.plane_off[c] = plane_bytes;
         plane_bytes += AlignUp(uint64_t(d.plane_pitch[c]) * d.plane_rows[c], 256);
       }
-      general_rows += p.mcuy;
+      (p.progressive ? pgeneral_rows : general_rows) += p.mcuy;
     }
+  }
+
+  // ---- K1p lanes (progressive images): per dependency level, the intervals grouped by scan
+  // kind (each group padded to whole waves: the kind is wave-uniform), longest first within a
+  // group (a wave lasts as long as its longest lane) ----
+  std::vector<uint32_t> &prog_lanes = sc_.prog_lanes;
+  prog_lanes.clear();
+  uint32_t prog_level_off[257] = {};
+  const uint32_t nlev = std::min<uint32_t>(prog_levels, 256);
+  if (prog_images) {
+    constexpr uint32_t kPB = 2048;  // 64-B length buckets
+    std::vector<uint32_t> &bk = sc_.prog_bucket;
+    for (uint32_t L = 0; L < nlev; L++) {
+      prog_level_off[L] = uint32_t(prog_lanes.size());
+      for (uint32_t K = 0; K < 4; K++) {
+        bk.assign(kPB + 1, 0);
+        uint32_t cnt = 0;
+        for (int i = 0; i < n; i++) {
+          const DecodePlan &p = streams[i]->plan();
+          if (!p.progressive) continue;
+          for (const RjProgIvalDev &iv : p.pivals) {
+            const RjProgScanDev &sc = p.pscans[iv.scan];
+            if (sc.level != L || sc.kind != K || (iv.flags & RJ_SEG_MISSING)) continue;
+            bk[kPB - 1 - std::min<uint32_t>(iv.dst_len >> 6, kPB - 1)]++;
+            cnt++;
+          }
+        }
+        if (cnt == 0) continue;
+        for (uint32_t b = 0, cum = 0; b <= kPB; b++) {
+          const uint32_t c = bk[b];
+          bk[b] = cum;
+          cum += c;
+        }
+        const size_t base = prog_lanes.size();
+        prog_lanes.resize(base + AlignUp(cnt, 64), 0xFFFFFFFFu);
+        for (int i = 0; i < n; i++) {
+          const DecodePlan &p = streams[i]->plan();
+          if (!p.progressive) continue;
+          const uint32_t g0 = imgs[i].pival_prefix;
+          for (uint32_t q = 0; q < p.pivals.size(); q++) {
+            const RjProgIvalDev &iv = p.pivals[q];
+            const RjProgScanDev &sc = p.pscans[iv.scan];
+            if (sc.level != L || sc.kind != K || (iv.flags & RJ_SEG_MISSING)) continue;
+            prog_lanes[base + bk[kPB - 1 - std::min<uint32_t>(iv.dst_len >> 6, kPB - 1)]++] = g0 + q;
+          }
+        }
+      }
+    }
+    prog_level_off[nlev] = uint32_t(prog_lanes.size());
   }
 
   const auto t_lanes = std::chrono::steady_clock::now();
@@ -490,7 +584,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t off_jobs = AlignUp(off_tabs + tabs.size() * sizeof(RjTableSet), 256);
   const uint64_t off_rows = AlignUp(off_jobs + std::max<size_t>(jobs.size(), 1) * sizeof(RjJobDev), 256);
   const uint64_t off_grows = AlignUp(off_rows + n * sizeof(uint32_t), 256);
-  const uint64_t off_stage = AlignUp(off_grows + n * sizeof(uint32_t), 256);
+  const uint64_t off_prows = AlignUp(off_grows + n * sizeof(uint32_t), 256);
+  const uint64_t off_pgrows = AlignUp(off_prows + n * sizeof(uint32_t), 256);
+  const uint64_t off_plane = AlignUp(off_pgrows + n * sizeof(uint32_t), 256);
+  const uint64_t off_stage = AlignUp(off_plane + prog_lanes.size() * sizeof(uint32_t), 256);
   const uint64_t blob_a = AlignUp(off_stage + stage_bytes, 256);
   const uint64_t n_lane_seg = any_split ? lane_seg.size() : (sorted ? seg_total : 0);
   const uint64_t off_lane_seg = blob_a;
@@ -506,6 +603,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   RJ_CHECK(d_chunkres_.Ensure(std::max<uint64_t>(uint64_t(lanes_all) * sizeof(RjChunkRes), 256)));
   RJ_CHECK(d_fallback_.Ensure(std::max<uint64_t>(uint64_t(seg_total) * 4, 256)));
   RJ_CHECK(d_entries_.Ensure((ent_total + RJ_ENT_SLACK) * 4));
+  if (prog_images) {
+    RJ_CHECK(d_coef_.Ensure(coef_dw_total * 4));
+    RJ_CHECK(d_nz_.Ensure(nz_total * 8));
+  }
   RjCoefBuf cbuf;
   cbuf.ent = d_entries_.as<uint32_t>();
   cbuf.piece = d_piece_.as<RjPiece>();
@@ -513,6 +614,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   cbuf.res = d_chunkres_.as<RjChunkRes>();
   cbuf.fallback = d_fallback_.as<uint32_t>();
   cbuf.count = nullptr;
+  cbuf.dense = d_coef_.as<uint32_t>();
   if (profiling_) {
     RJ_CHECK(d_count_.Ensure(256));
     cbuf.count = d_count_.as<unsigned long long>();
@@ -541,6 +643,22 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       std::memcpy(h + eo, s->info().ecs, s->info().ecs_size);
       d.segs = reinterpret_cast<const RjSegDev *>(dbase + so);
       d.ecs = dbase + eo;
+      if (p.progressive) {
+        const uint64_t po = eo + AlignUp(s->info().ecs_size + 16, 256);
+        const uint64_t vo = po + AlignUp(p.pscans.size() * sizeof(RjProgScanDev), 256);
+        const uint64_t to = vo + AlignUp(p.pivals.size() * sizeof(RjProgIvalDev), 256);
+        std::memcpy(h + po, p.pscans.data(), p.pscans.size() * sizeof(RjProgScanDev));
+        std::memcpy(h + vo, p.pivals.data(), p.pivals.size() * sizeof(RjProgIvalDev));
+        if (!p.ptabs.empty()) std::memcpy(h + to, p.ptabs.data(), p.ptabs.size() * sizeof(RjHuffDev));
+        d.pscans = reinterpret_cast<const RjProgScanDev *>(dbase + po);
+        d.pivals = reinterpret_cast<const RjProgIvalDev *>(dbase + vo);
+        d.ptabs = reinterpret_cast<const RjHuffDev *>(dbase + to);
+      }
+    }
+    if (stage_off[i] == UINT64_MAX && s->plan().progressive) {
+      d.pscans = s->resident.pscans;
+      d.pivals = s->resident.pivals;
+      d.ptabs = s->resident.ptabs;
     }
   }
   std::memcpy(h + off_imgs, imgs.data(), n * sizeof(RjImageDev));
@@ -548,6 +666,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (!jobs.empty()) std::memcpy(h + off_jobs, jobs.data(), jobs.size() * sizeof(RjJobDev));
   std::memcpy(h + off_rows, row_prefix.data(), n * sizeof(uint32_t));
   std::memcpy(h + off_grows, grow_prefix.data(), n * sizeof(uint32_t));
+  std::memcpy(h + off_prows, prow_prefix.data(), n * sizeof(uint32_t));
+  std::memcpy(h + off_pgrows, pgrow_prefix.data(), n * sizeof(uint32_t));
+  if (!prog_lanes.empty()) std::memcpy(h + off_plane, prog_lanes.data(), prog_lanes.size() * sizeof(uint32_t));
   const uint32_t *d_rows = reinterpret_cast<const uint32_t *>(dbase + off_rows);
   const uint32_t *d_grows = reinterpret_cast<const uint32_t *>(dbase + off_grows);
   const RjImageDev *d_imgs = reinterpret_cast<const RjImageDev *>(dbase + off_imgs);
@@ -562,6 +683,21 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (cbuf.count) RJ_HIP(hipMemsetAsync(cbuf.count, 0, sizeof(unsigned long long), stream_));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
   RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>()));
+  if (prog_images) {  // progressive images: K1p level by level, then their K2 rows (dense)
+    const uint32_t *d_plane = reinterpret_cast<const uint32_t *>(dbase + off_plane);
+    if (profiling_) RJ_HIP(hipEventRecord(prog_ev_[0], stream_));
+    RJ_HIP(hipMemsetAsync(d_coef_.as<uint32_t>(), 0, coef_dw_total * 4, stream_));
+    RJ_HIP(hipMemsetAsync(d_nz_.as<unsigned long long>(), 0, nz_total * 8, stream_));
+    for (uint32_t L = 0; L < nlev; L++)
+      RJ_HIP(LaunchProgressive(stream_, d_imgs, n, d_plane + prog_level_off[L], prog_level_off[L + 1] - prog_level_off[L],
+                               d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>()));
+    if (profiling_) RJ_HIP(hipEventRecord(prog_ev_[1], stream_));
+    RJ_HIP(LaunchRowsDense(stream_, false, d_imgs, n, reinterpret_cast<const uint32_t *>(dbase + off_prows), pfused_rows,
+                           cbuf, d_tabs, nullptr));
+    RJ_HIP(LaunchRowsDense(stream_, true, d_imgs, n, reinterpret_cast<const uint32_t *>(dbase + off_pgrows),
+                           pgeneral_rows, cbuf, d_tabs, d_planes_.as<uint8_t>()));
+    if (profiling_) RJ_HIP(hipEventRecord(prog_ev_[2], stream_));
+  }
   if (profiling_) RJ_HIP(hipEventRecord(ev_[2], stream_));
 
   // ---- (host, while K0 runs) lane order: with no interval split K1 is issue-bound and a wave
@@ -581,9 +717,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     auto bucket = [](uint32_t len) { return std::min<uint32_t>(len >> 5, kBuckets - 1); };
     std::vector<uint32_t> &pos = sc_.bucket_pos;
     pos.assign(kBuckets, 0);
-    bool aligned = fused_images == uint32_t(n) || fused_images == 0;
+    bool aligned = fused_images == uint32_t(n - int(prog_images)) || fused_images == 0;
     for (int i = 0; i < n; i++) {
       const DecodePlan &p = streams[i]->plan();
+      if (p.progressive) continue;  // no K1 intervals, no rows in these launches
       aligned = aligned && p.segs.size() == p.mcuy;
       uint32_t m = 0;
       for (const RjSegDev &sg : p.segs) {
@@ -628,6 +765,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         gs = 0;
         for (int i = 0; i < n; i++) {
           const DecodePlan &p = streams[i]->plan();
+          if (p.progressive) continue;
           uint8_t *rg = row_group.data() + (is_fused[i] ? row_prefix[i] : fused_rows + grow_prefix[i]);
           for (const RjSegDev &sg : p.segs) {
             const uint8_t g = class_of(seg_pos[gs++]);
@@ -653,6 +791,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         uint2 *rl = row_list.data();
         for (int i = 0; i < n; i++) {
           const DecodePlan &p = streams[i]->plan();
+          if (p.progressive) continue;
           const uint8_t *rg = row_group.data() + (is_fused[i] ? row_prefix[i] : fused_rows + grow_prefix[i]);
           uint32_t *wp = is_fused[i] ? fpos : gpos;
           for (uint32_t r = 0; r < p.mcuy; r++) rl[wp[rg[r]]++] = uint2{uint32_t(i), r};
@@ -747,6 +886,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   timings_.coef_bytes = coef_blocks * 128;  // dense-equivalent; the sparse bytes are data-dependent
   timings_.output_bytes = out_bytes;
   timings_.fused_images = fused_images;
+  timings_.prog_images = prog_images;
+  timings_.prog_intervals = pival_total;
+  timings_.prog_levels = prog_levels;
+  timings_.prog_coef_bytes = coef_dw_total * 4;
   if (profiling_) {
     float ms[5];
     RJ_HIP(hipEventElapsedTime(&ms[0], ev_[0], ev_[1]));
@@ -796,6 +939,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       std::vector<uint32_t> fb(seg_total);
       RJ_HIP(hipMemcpy(fb.data(), d_fallback_.as<uint32_t>(), fb.size() * 4, hipMemcpyDeviceToHost));
       for (uint32_t f : fb) timings_.serial_fallbacks += f ? 1u : 0u;
+    }
+    if (prog_images) {
+      RJ_HIP(hipEventElapsedTime(&timings_.prog_entropy_ms, prog_ev_[0], prog_ev_[1]));
+      RJ_HIP(hipEventElapsedTime(&timings_.prog_rows_ms, prog_ev_[1], prog_ev_[2]));
     }
     unsigned long long cnt = 0;
     RJ_HIP(hipMemcpy(&cnt, cbuf.count, sizeof(cnt), hipMemcpyDeviceToHost));

@@ -91,10 +91,13 @@ class Decoder {
     std::vector<uint32_t> tab_of, row_prefix, grow_prefix, seg_lane0, lane_seg, bucket_pos, seg_pos;
     std::vector<uint8_t> is_fused, row_group;
     std::vector<uint2> row_list;
+    std::vector<uint32_t> prow_prefix, pgrow_prefix, prog_lanes, prog_bucket;  // progressive images
   } sc_;
+  hipEvent_t prog_ev_[3] = {};  // profiling: K1p start, K1p end (dense K2 start), dense K2 end
 
   DeviceBuffer d_desc_, d_stage_, d_destuff_, d_entries_, d_planes_;
   DeviceBuffer d_piece_, d_rec_, d_chunkres_, d_fallback_;  // K1 chunk bookkeeping
+  DeviceBuffer d_coef_, d_nz_;  // progressive images: dense coefficients, nonzero masks
   uint32_t epoch_ = 0;
   PinnedBuffer h_stage_;
 };

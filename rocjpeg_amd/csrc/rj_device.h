@@ -72,6 +72,7 @@ struct RjCoefBuf {
   const uint32_t *lane_seg;   // per lane: batch interval index (0xFFFFFFFF: padding); null: identity
   const uint32_t *seg_lane0;  // per interval: its first lane; null: identity (no interval split)
   unsigned long long *count;  // profiling: entries written, summed per workgroup (null: off)
+  const uint32_t *dense;      // progressive images: dense coefficients (RjImageDev.coef_off)
 };
 #define RJ_ENT_PER_BLOCK 64       // worst case: DC + 63 AC (each position written at most once)
 #define RJ_ENT_GROUP 16           // K1 writes entries in 64-B groups; regions are group-aligned
@@ -185,6 +186,32 @@ struct RjJobDev {
   uint32_t pad;
 };
 
+// ---- progressive (SOF2) images (rj_prog.hip) ----
+// Coefficients are accumulated densely: per component an MCU-padded raster of blocks, each 64
+// int16 in zigzag order (32 dwords).  DC is two's complement (libjpeg's DC refinement ORs bit Al
+// into it); AC is sign-magnitude (bit 15 = negative), so that every AC successive-approximation
+// update -- first-scan value, refinement correction bit, newly nonzero coefficient -- is an OR
+// into a word that no other scan of the same dependency level touches (rj_stream.cpp levels).
+// A per-block 64-bit mask of nonzero AC positions (component raster of the blocks the AC scans
+// code, no MCU padding) feeds the refinement scans.
+enum RjProgKind : uint8_t { RJ_PK_DC_FIRST = 0, RJ_PK_DC_REFINE = 1, RJ_PK_AC_FIRST = 2, RJ_PK_AC_REFINE = 3 };
+struct RjProgScanDev {
+  uint8_t kind, ns, ss, se;  // RjProgKind; components in the scan; spectral band
+  uint8_t al, level, pad0, pad1;
+  uint8_t comp[3];           // frame component of each scan component
+  uint8_t hs[3], vs[3];      // blocks per unit of each scan component (1 x 1 unless interleaved)
+  uint8_t tsel[3];           // which of the lane's two LDS tables (DC first)
+  uint16_t tab[2];           // RjImageDev.ptabs index of table 0 / 1 (0xFFFF: none)
+  uint32_t units_x, units;   // units (MCUs if interleaved, else blocks) per row / in total
+  uint32_t ri;               // units per restart interval (0: one interval)
+};
+struct RjProgIvalDev {       // one restart interval of one scan
+  uint32_t dst_off, dst_len; // destuffed bytes, relative to RjImageDev.destuff_off
+  uint32_t unit0, nunits;
+  uint16_t scan, flags;      // flags: RJ_SEG_MISSING (no marker: the interval is skipped)
+  uint32_t pad;
+};
+
 struct RjImageDev {
   uint32_t width, height;
   uint32_t mcux, mcuy;
@@ -213,4 +240,14 @@ struct RjImageDev {
   int32_t out_w, out_h, top, left;
   uint8_t *dst[4];
   uint32_t dst_pitch[4];
+  // progressive (SOF2) only
+  const RjProgScanDev *pscans;
+  const RjProgIvalDev *pivals;
+  const RjHuffDev *ptabs;
+  uint64_t coef_off;      // dwords into the dense coefficient buffer (32 per block)
+  uint64_t nz_off;        // masks into the nonzero-mask buffer
+  uint32_t pival_prefix;  // exclusive prefix of progressive intervals over the batch
+  uint32_t progressive;
+  uint32_t cblk0[3], wblk[3];   // dense block raster of each component (MCU-padded width)
+  uint32_t nzblk0[3], cwblk[3]; // nonzero-mask raster (blocks the AC scans code)
 };

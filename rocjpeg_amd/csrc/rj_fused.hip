@@ -177,10 +177,47 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
   }
 }
 
+// Two sign-magnitude int16 (bit 15 = negative) -> two's complement, per half (packed ops).
+__device__ __forceinline__ uint32_t sm16x2_to_tc(uint32_t w) {
+  typedef short s16x2 __attribute__((ext_vector_type(2)));
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const s16x2 sx = __builtin_bit_cast(s16x2, w) >> 15;  // 0 or -1 per half
+  const u16x2 x = __builtin_bit_cast(u16x2, (w & 0x7FFF7FFFu) ^ __builtin_bit_cast(uint32_t, sx));
+  return __builtin_bit_cast(uint32_t, u16x2(x - __builtin_bit_cast(u16x2, sx)));
+}
+
+// Progressive images: this lane's block (component c, block column bx of the strip, row by) from
+// the dense coefficients into its LDS slot, AC converted to two's complement (DC already is).
+__device__ __forceinline__ void load_dense_block(const RjImageDev &im, const uint32_t *__restrict__ dense,
+                                                 uint32_t lane_blk, uint32_t mx0, uint32_t my, bool inter,
+                                                 uint8_t *slot) {
+  const uint32_t c = lane_blk >> 12;
+  const uint32_t hc = inter ? im.comp_h[c] : 1, vc = inter ? im.comp_v[c] : 1;
+  const uint32_t bx = mx0 * hc + (lane_blk & 255u), by = my * vc + ((lane_blk >> 8) & 15u);
+  const uint32_t cb = c == 0 ? im.cblk0[0] : (c == 1 ? im.cblk0[1] : im.cblk0[2]);
+  const uint32_t wb = c == 0 ? im.wblk[0] : (c == 1 ? im.wblk[1] : im.wblk[2]);
+  const uint4 *src = reinterpret_cast<const uint4 *>(dense + im.coef_off + uint64_t(cb + by * wb + bx) * 32u);
+  uint4 v[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) v[q] = gp(src)[q];
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    uint4 o;
+    o.x = sm16x2_to_tc(v[q].x);
+    if (q == 0) o.x = (o.x & 0xFFFF0000u) | (v[q].x & 0xFFFFu);  // DC: two's complement already
+    o.y = sm16x2_to_tc(v[q].y);
+    o.z = sm16x2_to_tc(v[q].z);
+    o.w = sm16x2_to_tc(v[q].w);
+    *reinterpret_cast<uint4 *>(slot + q * 16) = o;
+  }
+}
+
 // K2: one wavefront per MCU row of one image, looping over the row's strips of S MCUs.
 //   kPlanes = false: fused output (rj_decoder.cpp FusedEligible images)
 //   kPlanes = true : general path, blocks into the MCU-padded component planes (K2b reads them)
-template <bool kPlanes>
+//   kDense = true  : progressive images -- blocks come from the dense coefficient buffer
+//                    (rj_prog.hip layout: zigzag, AC sign-magnitude) instead of entry streams
+template <bool kPlanes, bool kDense = false>
 __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ imgs, int nimg,
                                              const uint32_t *__restrict__ row_prefix,
                                              const uint2 *__restrict__ row_list,
@@ -257,8 +294,9 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
   cbits = U(cbits);
   // the row's first block: its interval, the piece holding it, blocks to skip inside the piece
   Nav nv;
-  uint32_t drop;
-  {
+  uint32_t drop = 0;
+  EntWin win;
+  if constexpr (!kDense) {
     const uint32_t ri = U(im.ri_mcus);
     nv.seg = U(ri ? (my * mcux) / ri : 0);
     const RjSegDev sg = gp(im.segs)[nv.seg];
@@ -270,9 +308,8 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
     nv.pj = pj;
     nv.take(pb + pj);
     drop = U(rel - gp(pb + pj)->first_blk);
+    win.load(ent, nv.cur(), tid);
   }
-  EntWin win;
-  win.load(ent, nv.cur(), tid);
 
   // output descriptor, read once before the strip loop (the output stores could otherwise
   // force re-reads of the descriptor inside the pixel loops)
@@ -304,9 +341,13 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
     for (uint32_t k = tid; k < nb * 8; k += 64)
       *reinterpret_cast<uint4 *>(s_buf + (k >> 3) * RJ_BLK_STRIDE + (k & 7) * 16) = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    parse_blocks(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf);
-    drop = 0;
-    if (sx + 1 < strips_x && nv.bleft) win.load(ent, nv.cur(), tid);  // next strip's window: lands behind B and C
+    if constexpr (kDense) {
+      if (has_blk) load_dense_block(im, coefs.dense, lane_blk, mx0, my, inter, s_buf + tid * RJ_BLK_STRIDE);
+    } else {
+      parse_blocks(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf);
+      drop = 0;
+      if (sx + 1 < strips_x && nv.bleft) win.load(ent, nv.cur(), tid);  // next strip's window: lands behind B and C
+    }
     __syncthreads();
 
     RJ_STAMP(tb);
@@ -469,6 +510,20 @@ hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, in
   else
     hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, no_segs, coefs,
                        tabsets, planes);
+  return hipGetLastError();
+}
+
+hipError_t LaunchRowsDense(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
+                           uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets, uint8_t *planes) {
+  if (nrows == 0) return hipSuccess;
+  const uint32_t *no_segs = nullptr;
+  const uint2 *no_list = nullptr;
+  if (to_planes)
+    hipLaunchKernelGGL((k_rows<true, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, no_list, no_segs,
+                       coefs, tabsets, planes);
+  else
+    hipLaunchKernelGGL((k_rows<false, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, no_list, no_segs,
+                       coefs, tabsets, planes);
   return hipGetLastError();
 }
 

@@ -40,6 +40,16 @@ hipError_t LaunchRowsOfLanes(hipStream_t st, bool to_planes, const RjImageDev *i
                              const uint32_t *row_segs, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
                              uint8_t *planes);
 
+// K1p (rj_prog.hip): progressive scans, one lane per restart interval of one scan; `lanes`
+// lists batch-global interval indices (RjImageDev.pival_prefix), grouped so every wave holds
+// one scan kind (0xFFFFFFFF: padding).  One launch per dependency level.
+hipError_t LaunchProgressive(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *lanes, uint32_t nlanes,
+                             const uint8_t *destuffed, uint32_t *coef, unsigned long long *nz);
+
+// K2 over progressive images' MCU rows: dense coefficients (RjCoefBuf.dense) instead of entries.
+hipError_t LaunchRowsDense(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
+                           uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets, uint8_t *planes);
+
 #ifdef RJ_EXP_STAMPS
 void DumpRowStamps();
 #endif

@@ -101,6 +101,12 @@ bool Stream::Parse(const uint8_t *d, uint32_t n) {
   StreamInfo &s = info_;
   if (d == nullptr || n < 4) return false;
   if (d[0] != 0xFF || d[1] != 0xD8) return false;  // :64-67
+  if (IsProgressiveStream(d, n)) {  // SOF2: rj_prog_stream.cpp
+    if (ParseProgressive(d, n)) return true;
+    plan_ = DecodePlan();
+    plan_.status = -3;
+    return false;
+  }
   size_t pos = 2;
   bool sos = false, dht = false, dqt = false;
   while (!sos && pos < n) {  // marker walk :74-109, bounds-checked
@@ -396,6 +402,9 @@ void Stream::ReleaseResident() {
       (void)hipFree(resident.ecs);
       (void)hipFree(resident.segs);
       (void)hipFree(resident.ds);
+      if (resident.pscans) (void)hipFree(resident.pscans);
+      if (resident.pivals) (void)hipFree(resident.pivals);
+      if (resident.ptabs) (void)hipFree(resident.ptabs);
       (void)hipSetDevice(cur);
     }
   }

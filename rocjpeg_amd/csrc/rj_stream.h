@@ -57,6 +57,20 @@ struct DecodePlan {
   static constexpr size_t kTableKeyBytes = 2 + 2 * (16 + 12 + 16 + 162) + 4 * 64;
   uint8_t table_key[kTableKeyBytes] = {};
   uint64_t table_hash = 0;
+
+  // progressive (SOF2) streams: every scan's restart intervals (K0 destuffs them like baseline
+  // intervals; `segs` stays empty), the per-scan Huffman tables, the dense coefficient layout
+  // and the scans' dependency levels (rj_prog.hip)
+  bool progressive = false;
+  std::vector<RjProgScanDev> pscans;
+  std::vector<RjProgIvalDev> pivals;
+  std::vector<RjHuffDev> ptabs;
+  uint32_t plevels = 0;            // dependency levels (max scan level + 1)
+  uint32_t cblk0[3] = {}, nzblk0[3] = {}, cwblk[3] = {}, chblk[3] = {};
+  uint64_t coef_blocks = 0;        // dense blocks (MCU-padded)
+  uint64_t nz_blocks = 0;          // nonzero masks
+  uint8_t pqlat[3][64] = {};       // each component's latched quant table (zigzag order)
+  std::vector<uint32_t> pscan_src; // per scan: absolute stream offsets of its data [begin, end)
 };
 
 class Stream {
@@ -75,12 +89,17 @@ class Stream {
     uint8_t *ecs = nullptr;
     RjSegDev *segs = nullptr;
     RjDsBlock *ds = nullptr;
+    RjProgScanDev *pscans = nullptr;  // progressive only
+    RjProgIvalDev *pivals = nullptr;
+    RjHuffDev *ptabs = nullptr;
   } resident;
   void ReleaseResident();
   ~Stream() { ReleaseResident(); }
 
  private:
   void BuildPlan();
+  bool ParseProgressive(const uint8_t *data, uint32_t size);  // SOF2 (beyond the reference)
+  void BuildProgressivePlan(const uint8_t *data);
   StreamInfo info_;
   DecodePlan plan_;
   uint64_t generation_ = 0;
@@ -89,6 +108,9 @@ class Stream {
 
 // GetImageInfo restatement (rocjpeg_decoder.cpp:307-358); returns RocJpegStatus.
 int ImageInfo(const StreamInfo &s, uint8_t *num_components, int *subsampling, uint32_t *widths, uint32_t *heights);
+
+// True when the frame header ahead of the first SOS is SOF2 (progressive Huffman).
+bool IsProgressiveStream(const uint8_t *data, uint32_t size);
 
 // Canonical Huffman table -> RjHuffDev; false for an invalid table.
 bool BuildHuffman(const uint8_t bits[16], const uint8_t *vals, bool is_dc, RjHuffDev *out);

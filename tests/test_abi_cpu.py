@@ -54,6 +54,14 @@ def test_stream_parse_matches_reference_parser(ent):
     s = R.JpegStream()
     st = s.try_parse(data)
     ref = ent["ref_parse"]
+    if _sof2(data):
+        # deliberate extension: the reference parser rejects SOF2 (rocjpeg_parser.cpp:74-104,
+        # it records zeros); this one parses it and reports the frame header
+        assert st == R.Status.SUCCESS
+        fi = O.frame_info(data)
+        info = s.info()
+        assert (info["widths"][0], info["heights"][0], info["num_components"]) == (fi["width"], fi["height"], fi["ncomp"])
+        return
     assert (st == R.Status.SUCCESS) == bool(ref["ok"])
     if st != R.Status.SUCCESS:
         assert st == R.Status.BAD_JPEG
@@ -71,6 +79,38 @@ def test_stream_parse_matches_reference_parser(ent):
     ri = ref["restart_interval"]
     if ri and "libjpeg_coef_sha256" in ent:
         assert info["restart_intervals"] == -(-ref["num_mcus"] // ri)
+
+
+def _sof2(data):
+    pos = 2
+    while pos + 4 <= len(data):
+        while data[pos] == 0xFF:
+            pos += 1
+        if data[pos] == 0xC2:
+            return True
+        if data[pos] in (0xC0, 0xC1, 0xDA):
+            return False
+        pos += 1 + ((data[pos + 1] << 8) | data[pos + 2])
+    return False
+
+
+def test_progressive_parse_errors():
+    """SOF2 streams: the marker walk's error rules (oracle make_plan_prog / libjpeg jdmarker.c)."""
+    good = O.fixture_bytes(next(f for f in O.manifest() if f["name"] == "pp420_opt_200x150"))
+    s = R.JpegStream()
+    assert s.try_parse(good) == R.Status.SUCCESS
+    # a scan naming a component the frame does not have
+    i = good.index(b"\xff\xda")
+    bad = bytearray(good)
+    bad[i + 5] = 0x77
+    assert s.try_parse(bytes(bad)) == R.Status.BAD_JPEG
+    # header cut before any scan
+    assert s.try_parse(good[:i]) == R.Status.BAD_JPEG
+    # Ah/Al inconsistent with the first scan (Ah != 0 with Al != Ah - 1): JERR_BAD_PROGRESSION
+    bad = bytearray(good)
+    ns = bad[i + 4]
+    bad[i + 4 + 1 + 2 * ns + 2] = 0x31
+    assert s.try_parse(bytes(bad)) == R.Status.BAD_JPEG
 
 
 def test_truncated_and_garbage_streams():

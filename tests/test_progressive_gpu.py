@@ -1,0 +1,158 @@
+"""Parity of the progressive (SOF2) decode path -- K0 destuff of every scan's intervals, K1p
+(rj_prog.hip) into dense coefficients, K2 over them -- with the CPU oracle, byte for byte
+(oracle/jpeg_oracle.c decode_progressive, pinned against libjpeg 9.4's coefficients and planes
+for every fixture used here, tests/test_oracle_golden.py).
+
+The reference cannot decode these streams at all (its parser handles SOF0 only,
+src/rocjpeg_parser.cpp:74-104); SURVEY.md 8f rank 2 / BASELINE config C5."""
+import numpy as np
+import pytest
+
+import rocjpeg_amd as R
+from tests import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+def is_progressive(data):
+    pos = 2
+    while pos + 4 <= len(data):
+        while data[pos] == 0xFF:
+            pos += 1
+        m = data[pos]
+        if m == 0xC2:
+            return True
+        if m in (0xC0, 0xC1, 0xDA):
+            return False
+        pos += 1 + ((data[pos + 1] << 8) | data[pos + 2])
+    return False
+
+
+FIX = O.manifest()
+PROG = [f for f in FIX if "libjpeg_coef_sha256" in f and is_progressive(O.fixture_bytes(f))]
+SMALL = [f for f in PROG if f["bytes"] < 100_000]
+BASE = [f for f in FIX if "libjpeg_coef_sha256" in f and f["ref_parse"]["ok"] and f["ref_parse"]["css"] in (0, 1, 2, 3, 5)
+        and f["bytes"] < 100_000]
+FORMATS = list(R.OutputFormat)
+
+
+@pytest.fixture(scope="module", params=[0, 1], ids=["auto_path", "general_path"])
+def dec(request):
+    from tests import gpu_util as G
+    G.torch()
+    d = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    d.set_path_policy(request.param)
+    yield d
+    d.close()
+
+
+def run_both(dec, data, fmt, crop=(0, 0, 0, 0)):
+    from tests import gpu_util as G
+    s = R.JpegStream(data)
+    nc, css, w, h = dec.image_info(s)
+    shapes = G.channel_shapes(fmt, css, w, h, roi=crop)
+    bufs, img = G.gpu_buffers(shapes)
+    st = dec.decode(s, R.decode_params(fmt, crop), img)
+    got = G.to_host(bufs)
+    ost, want = O.oracle_decode(data, int(fmt), shapes, crop)
+    return st, ost, got, want
+
+
+def test_fixture_set():
+    names = {f["name"] for f in PROG}
+    # 4:2:0 / 4:2:2 / 4:4:4 / 4:4:0 / gray, DRI, optimised tables, truncation, the C5 1080p sample
+    for n in ("pp420_q90_1920x1080", "cp444_prog_ri_136x72", "cp420_prog_ri3_160x112", "cp400_prog_120x80",
+              "cp440_prog_96x80", "cp422_prog_97x67", "pp420_opt_200x150", "pp420_prog_trunc_192x128"):
+        assert n in names, n
+
+
+@pytest.mark.parametrize("fmt", FORMATS, ids=[f.name for f in FORMATS])
+@pytest.mark.parametrize("ent", PROG, ids=[f["name"] for f in PROG])
+def test_progressive_matches_oracle(dec, ent, fmt):
+    from tests import gpu_util as G
+    st, ost, got, want = run_both(dec, O.fixture_bytes(ent), fmt)
+    assert st == ost == 0
+    for c, (g, w) in enumerate(zip(got, want)):
+        assert G.first_mismatch(g, w) is None, (c, G.first_mismatch(g, w))
+
+
+CROPS = [(8, 8, 72, 56), (3, 5, 60, 61), (0, 0, 64, 32)]
+
+
+@pytest.mark.parametrize("crop", CROPS, ids=[str(c) for c in CROPS])
+@pytest.mark.parametrize("fmt", [R.OutputFormat.RGB, R.OutputFormat.NATIVE, R.OutputFormat.YUV_PLANAR])
+@pytest.mark.parametrize("ent", SMALL[:4], ids=[f["name"] for f in SMALL[:4]])
+def test_progressive_roi(dec, ent, fmt, crop):
+    from tests import gpu_util as G
+    st, ost, got, want = run_both(dec, O.fixture_bytes(ent), fmt, crop)
+    assert st == ost == 0
+    for c, (g, w) in enumerate(zip(got, want)):
+        assert G.first_mismatch(g, w) is None, (c, G.first_mismatch(g, w))
+
+
+def _truncations(data):
+    """Cut inside each third of the stream: later scans missing, a scan ending mid-interval
+    (libjpeg's insufficient-data rule: zero bits, then the rest of the interval skipped)."""
+    out = {}
+    for frac in (0.3, 0.55, 0.8, 0.97):
+        cut = int(len(data) * frac)
+        if data[cut - 1] == 0xFF:
+            cut -= 1
+        out[f"cut{int(frac * 100)}"] = data[:cut]
+    return out
+
+
+@pytest.mark.parametrize("ent", [f for f in PROG if f["name"] in ("pp420_opt_200x150", "cp420_prog_ri3_160x112",
+                                                                   "cp444_prog_ri_136x72")],
+                         ids=lambda f: f["name"])
+def test_progressive_truncated(dec, ent):
+    from tests import gpu_util as G
+    for name, data in _truncations(O.fixture_bytes(ent)).items():
+        st, ost, got, want = run_both(dec, data, R.OutputFormat.RGB)
+        assert st == ost, (name, st, ost)
+        if st == 0:
+            assert G.first_mismatch(got[0], want[0]) is None, (name, G.first_mismatch(got[0], want[0]))
+
+
+@pytest.mark.parametrize("resident", [False, True], ids=["staged", "resident"])
+@pytest.mark.parametrize("fmt", [R.OutputFormat.RGB, R.OutputFormat.YUV_PLANAR, R.OutputFormat.NATIVE])
+def test_batch_mixed_progressive_and_baseline(dec, fmt, resident):
+    """Progressive and baseline streams in one rocJpegDecodeBatched call (both pipelines share
+    K0 and the output stage), streams staged per call or resident in HBM."""
+    from tests import gpu_util as G
+    datas = [O.fixture_bytes(e) for e in PROG] + [O.fixture_bytes(e) for e in BASE[:6]]
+    datas += [O.fixture_bytes(e) for e in SMALL]  # the same streams twice in one batch
+    streams = [R.JpegStream(d) for d in datas]
+    if resident:
+        dec.streams_to_device(streams)
+    shapes_all, bufs_all, imgs = [], [], []
+    for s in streams:
+        nc, css, w, h = dec.image_info(s)
+        shapes = G.channel_shapes(fmt, css, w, h)
+        bufs, img = G.gpu_buffers(shapes)
+        shapes_all.append(shapes)
+        bufs_all.append(bufs)
+        imgs.append(img)
+    assert dec.decode_batched(streams, R.decode_params(fmt), imgs) == 0
+    for k, (d, shapes, bufs) in enumerate(zip(datas, shapes_all, bufs_all)):
+        ost, want = O.oracle_decode(d, int(fmt), shapes)
+        assert ost == 0
+        for c, (g, w) in enumerate(zip(G.to_host(bufs), want)):
+            assert G.first_mismatch(g, w) is None, (k, c, G.first_mismatch(g, w))
+
+
+def test_progressive_timings(dec):
+    from tests import gpu_util as G
+    data = O.fixture_bytes(next(f for f in PROG if f["name"] == "pp420_q90_1920x1080"))
+    s = R.JpegStream(data)
+    nc, css, w, h = dec.image_info(s)
+    bufs, img = G.gpu_buffers(G.channel_shapes(R.OutputFormat.RGB, css, w, h))
+    dec.set_profiling(True)
+    try:
+        assert dec.decode(s, R.decode_params(R.OutputFormat.RGB), img) == 0
+        t = dec.last_timings()
+    finally:
+        dec.set_profiling(False)
+    assert t["prog_images"] == 1 and t["prog_levels"] >= 2 and t["prog_intervals"] == 10
+    assert t["prog_entropy_ms"] > 0 and t["prog_rows_ms"] > 0
+    assert t["prog_coef_bytes"] == 1920 * 1088 * 3 // 2 * 2  # 4:2:0, MCU-padded, int16
