@@ -9,7 +9,12 @@ ranks, each decoding its own batch (weak scaling; whole images are independent).
 builds the work table (one seed per image) and broadcasts it (RCCL); nothing crosses GPUs
 in the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload c2|c3|c4|c5]
+
+The other BASELINE.json configs are available as --workload (never the driver's default line):
+  c3  1024 x 1080p, 4:4:4 and 4:2:2 alternating, ROCJPEG_OUTPUT_YUV_PLANAR
+  c4  mixed resolution 4:2:0 (640x480 .. 3840x2160, uniform by seed), RGB, DRI = one MCU row
+  c5  progressive 4:2:0 1080p q90 (Pillow progressive=True, no DRI), RGB
 """
 import argparse
 import ctypes
@@ -37,10 +42,19 @@ def _init_worker():
     _BASE = np.asarray(Image.open(MUG).convert("RGB"))
 
 
+C4_SIZES = [(640, 480), (1280, 720), (1920, 1080), (2560, 1440), (3840, 2160)]
+
+
 def _make_jpeg(args):
-    """Seeded 1080p crop of the reference mug image + N(0,2) noise, encoded 4:2:0 q90 with
-    DRI = one MCU row (BASELINE.md generator)."""
-    seed, w, h, quality, sub, rst_blocks = args
+    """Seeded crop of the reference mug image + N(0,2) noise, encoded q90 with DRI = one MCU
+    row (BASELINE.md generator).  w == 0: size drawn from C4_SIZES by the seed."""
+    seed, w, h, quality, sub, rst_blocks, progressive = args
+    if w == 0:
+        w, h = C4_SIZES[seed % len(C4_SIZES)]
+        rst_blocks = (w + 15) // 16 if rst_blocks else 0  # MCUs per row
+    if sub == -1:  # C3: 4:4:4 and 4:2:2 alternating
+        sub = 0 if seed % 2 == 0 else 1
+        rst_blocks = (w + 7) // 8 if sub == 0 else (w + 15) // 16  # one MCU row
     from PIL import Image
     rng = np.random.default_rng(seed)
     y0 = int(rng.integers(0, _BASE.shape[0] - h + 1))
@@ -50,34 +64,30 @@ def _make_jpeg(args):
     kw = dict(quality=quality, subsampling=sub)
     if rst_blocks:
         kw["restart_marker_blocks"] = rst_blocks
+    if progressive:
+        kw["progressive"] = True
     Image.fromarray(np.clip(a, 0, 255).astype(np.uint8)).save(b, "JPEG", **kw)
     return b.getvalue()
 
 
-def make_dataset(seeds, w=1920, h=1080, quality=90, sub=2, rst_blocks=120, procs=16):
-    jobs = [(int(s), w, h, quality, sub, rst_blocks) for s in seeds]
+def make_dataset(seeds, w=1920, h=1080, quality=90, sub=2, rst_blocks=120, procs=16, progressive=False):
+    jobs = [(int(s), w, h, quality, sub, rst_blocks, progressive) for s in seeds]
     with get_context("fork").Pool(procs, initializer=_init_worker) as pool:
         return pool.map(_make_jpeg, jobs, chunksize=8)
 
 
-def cpu_baseline(data_list, budget_s=12.0):
+def cpu_baseline(data_list, shapes, fmt, what, budget_s=12.0):
     """The CPU oracle (oracle/jpeg_oracle.c, a plain single-threaded restatement of the same
     decode: Huffman, ISLOW IDCT, reference CSC) on a bounded sample of the same images."""
     from tests import oracle_lib as O
-    lib = O.oracle()
-    w3, h = 1920 * 3, 1080
-    out = np.zeros((h, w3), np.uint8)
-    ptrs = (ctypes.c_void_p * 4)(out.ctypes.data, None, None, None)
-    pitches = (ctypes.c_uint32 * 4)(w3, 0, 0, 0)
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < budget_s and n < len(data_list):
-        d = data_list[n]
-        st = lib.oj_decode(d, len(d), 3, 0, 0, 0, 0, ptrs, pitches)
+        st, _ = O.oracle_decode(data_list[n], fmt, shapes[n])
         assert st == 0
         n += 1
     dt = time.perf_counter() - t0
     return {"value": round(n / dt, 3), "unit": "images/s", "cores": 1, "kind": "port",
-            "sample": f"{n} of the batch's 1920x1080 4:2:0 q90 RI=120 images -> RGB, oracle/jpeg_oracle.c, 1 thread, {dt:.1f} s"}
+            "sample": f"{n} of the batch's {what}, oracle/jpeg_oracle.c, 1 thread, {dt:.1f} s"}
 
 
 def _turbo_worker(blobs):
@@ -130,7 +140,31 @@ def work_table(rank, world, batch, device):
     return table[rank].cpu().tolist()
 
 
+def _workloads():
+    import rocjpeg_amd as R
+    return {
+        "c2": {"gen": {}, "fmt": R.OutputFormat.RGB,
+               "data": "synthetic: seeded 1920x1080 crops of the reference mug_420.jpg + N(0,2) noise, Pillow q90 4:2:0 DRI=120",
+               "workload": "C2: batch of {batch} x 1920x1080 4:2:0 baseline JPEG q90, RI=120 MCUs, ROCJPEG_OUTPUT_RGB, bitstreams resident in HBM",
+               "sample": "1920x1080 4:2:0 q90 RI=120 images -> RGB"},
+        "c3": {"gen": {"sub": -1}, "fmt": R.OutputFormat.YUV_PLANAR,
+               "data": "synthetic: seeded 1920x1080 crops of mug_420.jpg + N(0,2) noise, Pillow q90, 4:4:4 / 4:2:2 alternating, DRI = 1 MCU row",
+               "workload": "C3: batch of {batch} x 1920x1080 baseline q90, 4:4:4 and 4:2:2 alternating, ROCJPEG_OUTPUT_YUV_PLANAR, resident",
+               "sample": "1920x1080 4:4:4 / 4:2:2 images -> YUV_PLANAR"},
+        "c4": {"gen": {"w": 0, "h": 0}, "fmt": R.OutputFormat.RGB,
+               "data": "synthetic: seeded crops of mug_420.jpg + N(0,2) noise, sizes 640x480..3840x2160 uniform by seed, Pillow q90 4:2:0, DRI = 1 MCU row",
+               "workload": "C4: batch of {batch} mixed-resolution 4:2:0 baseline JPEGs per GPU (640x480..3840x2160), ROCJPEG_OUTPUT_RGB, resident",
+               "sample": "mixed-resolution 4:2:0 images -> RGB"},
+        "c5": {"gen": {"rst_blocks": 0, "progressive": True}, "fmt": R.OutputFormat.RGB,
+               "data": "synthetic: seeded 1920x1080 crops of mug_420.jpg + N(0,2) noise, Pillow q90 4:2:0 progressive=True (no DRI)",
+               "workload": "C5: batch of {batch} x 1920x1080 4:2:0 progressive JPEG q90 (10 scans, no DRI), ROCJPEG_OUTPUT_RGB, resident",
+               "sample": "1920x1080 4:2:0 q90 progressive images -> RGB"},
+    }
+
+
 def main():
+    global WORKLOADS
+    WORKLOADS = _workloads()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -138,7 +172,9 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", type=int, default=0, help="0 auto (fused where legal), 1 general two-stage path")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
     args = ap.parse_args()
+    wl = WORKLOADS[args.workload]
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -153,7 +189,7 @@ def main():
     seeds = work_table(rank, world, args.batch, dev)
     procs = max(1, min(16, (os.cpu_count() or 16)))
     t_gen = time.perf_counter()
-    data = make_dataset(seeds, procs=procs)
+    data = make_dataset(seeds, procs=procs, **wl["gen"])
     t_gen = time.perf_counter() - t_gen
 
     import rocjpeg_amd as R
@@ -161,11 +197,27 @@ def main():
     dec.set_path_policy(args.path)
     streams = [R.JpegStream(b) for b in data]
     dec.streams_to_device(streams)
-    nc, css, w, h = dec.image_info(streams[0])
-    W, H = w[0], h[0]
-    out = torch.empty((args.batch, H, 3 * W), dtype=torch.uint8, device=dev)
-    imgs = [R.make_image([out[i].data_ptr()], [3 * W]) for i in range(args.batch)]
-    params = R.decode_params(R.OutputFormat.RGB)
+    # destinations: one HBM arena, every channel sized as the reference samples size them
+    # (samples/rocjpeg_samples_utils.h:318-399, tests/gpu_util.py channel_shapes)
+    from tests.gpu_util import channel_shapes
+    fmt = wl["fmt"]
+    shapes = []
+    for s in streams:
+        nc, css, w, h = dec.image_info(s)
+        shapes.append(channel_shapes(fmt, css, w, h))
+    total = sum(r * p for shp in shapes for r, p in shp)
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    imgs, views, off = [], [], 0
+    for shp in shapes:
+        ptrs, pitches, vv = [], [], []
+        for r, p in shp:
+            ptrs.append(out[off:].data_ptr())
+            pitches.append(p)
+            vv.append(out[off:off + r * p].view(r, p))
+            off += r * p
+        imgs.append(R.make_image(ptrs, pitches))
+        views.append(vv)
+    params = R.decode_params(fmt)
     n = len(streams)
     hs = (ctypes.c_void_p * n)(*[s.handle for s in streams])
     arr = (R.RocJpegImage * n)(*imgs)
@@ -192,7 +244,7 @@ def main():
         for k in stage:
             stage[k] += last[k]
         for k in ("entropy_chunks_ms", "entropy_resolve_ms", "entropy_serial_ms", "k1_launch_ms_sum",
-                  "k2_launch_ms_sum"):
+                  "k2_launch_ms_sum", "prog_entropy_ms", "prog_rows_ms"):
             k1[k] = k1.get(k, 0.0) + last[k]
     torch.cuda.synchronize()
     if world > 1:
@@ -218,10 +270,13 @@ def main():
     host_rate = host_steps * n / (time.perf_counter() - t_h) if st == 0 else None
     del host_streams
 
-    # parity spot-check of this run's output (first image vs the CPU oracle), outside timing
+    # parity spot-check of this run's output (first images vs the CPU oracle), outside timing
     from tests import oracle_lib as O
-    ost, want = O.oracle_decode(data[0], 3, [(H, 3 * W)])
-    parity_ok = bool(ost == 0 and np.array_equal(out[0].cpu().numpy(), want[0]))
+    parity_ok = True
+    for q in range(min(2, n)):
+        ost, want = O.oracle_decode(data[q], int(fmt), shapes[q])
+        parity_ok = parity_ok and ost == 0 and all(np.array_equal(v.cpu().numpy(), w_) for v, w_ in zip(views[q], want))
+    parity_ok = bool(parity_ok)
 
     if rank == 0:
         K = args.steps
@@ -242,6 +297,12 @@ def main():
             "k_entropy": (k1["k1_launch_ms_sum"] / K, max(1, last["k1_launches"]), ecs + entb),
             "k_rows": (k1["k2_launch_ms_sum"] / K, max(1, last["k2_launches"]), entb + outb),
         }
+        if last["prog_images"]:
+            # progressive: K1p reads the destuffed scans and writes the dense coefficients (incl.
+            # their zero fill); K2 (dense) reads them and writes the output
+            pc = last["prog_coef_bytes"]
+            kern["k_prog"] = (k1["prog_entropy_ms"] / K, max(1, last["prog_levels"]), ecs + pc)
+            kern["k_rows_dense"] = (k1["prog_rows_ms"] / K, 1, pc + outb)
         dom = max(kern, key=lambda k: kern[k][0])
         t_sum, launches, algo_bytes = kern[dom]
         ach = algo_bytes / (t_sum * 1e-3) / 1e9 if t_sum > 0 else 0.0
@@ -258,9 +319,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: seeded 1920x1080 crops of the reference mug_420.jpg + N(0,2) noise, Pillow q90 4:2:0 DRI=120",
-            "config": {"workload": "C2: batch of 1024 x 1920x1080 4:2:0 baseline JPEG q90, RI=120 MCUs, ROCJPEG_OUTPUT_RGB, bitstreams resident in HBM",
-                       "batch_per_gpu": args.batch, "output_format": "RGB", "parallelism": f"images sharded, {world} rank(s)",
+            "data": wl["data"],
+            "config": {"workload": wl["workload"].format(batch=args.batch),
+                       "batch_per_gpu": args.batch, "output_format": fmt.name, "parallelism": f"images sharded, {world} rank(s)",
                        "ecs_bytes_per_image": round(ecs / args.batch)},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
@@ -276,8 +337,13 @@ def main():
             "parity_first_image": parity_ok,
             "dataset_gen_s": round(t_gen, 1),
         }
+        if last["prog_images"]:
+            res["progressive_detail"] = {"images": last["prog_images"], "intervals": last["prog_intervals"],
+                                         "levels": last["prog_levels"],
+                                         "k1p_ms": round(k1["prog_entropy_ms"] / K, 4),
+                                         "k2_dense_ms": round(k1["prog_rows_ms"] / K, 4)}
         if not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(data)
+            res["cpu_baseline"] = cpu_baseline(data, shapes, int(fmt), wl["sample"])
             res["cpu_libjpeg_turbo"] = turbo_baseline(data, procs)
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -106,6 +106,7 @@ Decoder::~Decoder() {
       if (e) (void)hipEventDestroy(e);
     for (auto &e : prog_ev_)
       if (e) (void)hipEventDestroy(e);
+    for (auto &e : prog_lev_ev_) (void)hipEventDestroy(e);
     for (auto *arr : {k1s_, k2s_, k2e_})
       for (int q = 0; q < kMaxPipe; q++)
         if (arr[q]) (void)hipEventDestroy(arr[q]);
@@ -278,7 +279,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   prow_prefix.resize(n);
   pgrow_prefix.resize(n);
   uint32_t pfused_rows = 0, pgeneral_rows = 0, prog_images = 0, prog_levels = 0, pival_total = 0;
-  uint64_t coef_dw_total = 0, nz_total = 0;
+  uint64_t coef_dw_total = 0, nz_total = 0, prec_total = 0;
   for (int i = 0; i < n; i++) {
     Stream *s = streams[i];
     const StreamInfo &in = s->info();
@@ -332,11 +333,15 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       coef_dw_total += AlignUp(p.coef_blocks * 32, 64);
       d.nz_off = nz_total;
       nz_total += AlignUp(p.nz_blocks, 8);
+      d.prec_off = prec_total;
+      prec_total += AlignUp(p.prec_words, 8);
+      d.npscans = uint32_t(p.pscans.size());
       for (int c = 0; c < 3; c++) {
         d.cblk0[c] = p.cblk0[c];
         d.wblk[c] = p.wblk[c];
         d.nzblk0[c] = p.nzblk0[c];
         d.cwblk[c] = p.cwblk[c];
+        d.chblk[c] = p.chblk[c];
       }
       pival_total += uint32_t(p.pivals.size());
       prog_images++;
@@ -478,14 +483,15 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // group (a wave lasts as long as its longest lane) ----
   std::vector<uint32_t> &prog_lanes = sc_.prog_lanes;
   prog_lanes.clear();
-  uint32_t prog_level_off[257] = {};
+  uint32_t prog_level_off[257] = {}, fold_off[257] = {}, fold_chunks[257] = {}, acref_off[257] = {};
+  std::vector<RjFoldJob> &fold_jobs = sc_.fold_jobs;
   const uint32_t nlev = std::min<uint32_t>(prog_levels, 256);
   if (prog_images) {
     constexpr uint32_t kPB = 2048;  // 64-B length buckets
     std::vector<uint32_t> &bk = sc_.prog_bucket;
     for (uint32_t L = 0; L < nlev; L++) {
       prog_level_off[L] = uint32_t(prog_lanes.size());
-      for (uint32_t K = 0; K < 4; K++) {
+      for (uint32_t K = 0; K < 3; K++) {  // AC refinement: one wave per interval (below)
         bk.assign(kPB + 1, 0);
         uint32_t cnt = 0;
         for (int i = 0; i < n; i++) {
@@ -520,6 +526,51 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       }
     }
     prog_level_off[nlev] = uint32_t(prog_lanes.size());
+    // AC refinement intervals (k_prog_acref, one wave each), per level, after the lane lists
+    for (uint32_t L = 0; L < nlev; L++) {
+      acref_off[L] = uint32_t(prog_lanes.size());
+      for (int i = 0; i < n; i++) {
+        const DecodePlan &p = streams[i]->plan();
+        if (!p.progressive) continue;
+        for (uint32_t q = 0; q < p.pivals.size(); q++) {
+          const RjProgIvalDev &iv = p.pivals[q];
+          const RjProgScanDev &sc = p.pscans[iv.scan];
+          if (sc.level == L && sc.kind == RJ_PK_AC_REFINE && !(iv.flags & RJ_SEG_MISSING))
+            prog_lanes.push_back(imgs[i].pival_prefix + q);
+        }
+      }
+    }
+    acref_off[nlev] = uint32_t(prog_lanes.size());
+    // k_prog_fold jobs of every level >= 1: (image, component) pairs some refinement scan of
+    // that level covers, every block of the component's dense raster
+    fold_jobs.clear();
+    for (uint32_t L = 1; L < nlev; L++) {
+      fold_off[L] = uint32_t(fold_jobs.size());
+      uint32_t chunks = 0;
+      for (int i = 0; i < n; i++) {
+        const DecodePlan &p = streams[i]->plan();
+        if (!p.progressive) continue;
+        for (uint32_t c = 0; c < streams[i]->info().ncomp; c++) {
+          bool hit = false;
+          for (const RjProgScanDev &sc : p.pscans) {
+            if (sc.level != L) continue;
+            if (sc.kind == RJ_PK_AC_REFINE && sc.comp[0] == c) hit = true;
+            if (sc.kind == RJ_PK_DC_REFINE)
+              for (uint32_t q = 0; q < sc.ns; q++) hit = hit || sc.comp[q] == c;
+          }
+          if (!hit) continue;
+          RjFoldJob fj;
+          fj.image = uint32_t(i);
+          fj.comp = c;
+          fj.nblocks = p.wblk[c] * p.hblk[c];
+          fj.chunk0 = chunks;
+          chunks += (fj.nblocks + 63) / 64;
+          fold_jobs.push_back(fj);
+        }
+      }
+      fold_chunks[L] = chunks;
+    }
+    fold_off[nlev] = uint32_t(fold_jobs.size());
   }
 
   const auto t_lanes = std::chrono::steady_clock::now();
@@ -587,7 +638,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t off_prows = AlignUp(off_grows + n * sizeof(uint32_t), 256);
   const uint64_t off_pgrows = AlignUp(off_prows + n * sizeof(uint32_t), 256);
   const uint64_t off_plane = AlignUp(off_pgrows + n * sizeof(uint32_t), 256);
-  const uint64_t off_stage = AlignUp(off_plane + prog_lanes.size() * sizeof(uint32_t), 256);
+  const uint64_t off_fold = AlignUp(off_plane + prog_lanes.size() * sizeof(uint32_t), 256);
+  const uint64_t off_stage = AlignUp(off_fold + fold_jobs.size() * sizeof(RjFoldJob), 256);
   const uint64_t blob_a = AlignUp(off_stage + stage_bytes, 256);
   const uint64_t n_lane_seg = any_split ? lane_seg.size() : (sorted ? seg_total : 0);
   const uint64_t off_lane_seg = blob_a;
@@ -606,6 +658,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (prog_images) {
     RJ_CHECK(d_coef_.Ensure(coef_dw_total * 4));
     RJ_CHECK(d_nz_.Ensure(nz_total * 8));
+    RJ_CHECK(d_prec_.Ensure(std::max<uint64_t>(prec_total * 8, 256)));
   }
   RjCoefBuf cbuf;
   cbuf.ent = d_entries_.as<uint32_t>();
@@ -669,6 +722,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   std::memcpy(h + off_prows, prow_prefix.data(), n * sizeof(uint32_t));
   std::memcpy(h + off_pgrows, pgrow_prefix.data(), n * sizeof(uint32_t));
   if (!prog_lanes.empty()) std::memcpy(h + off_plane, prog_lanes.data(), prog_lanes.size() * sizeof(uint32_t));
+  if (!fold_jobs.empty()) std::memcpy(h + off_fold, fold_jobs.data(), fold_jobs.size() * sizeof(RjFoldJob));
   const uint32_t *d_rows = reinterpret_cast<const uint32_t *>(dbase + off_rows);
   const uint32_t *d_grows = reinterpret_cast<const uint32_t *>(dbase + off_grows);
   const RjImageDev *d_imgs = reinterpret_cast<const RjImageDev *>(dbase + off_imgs);
@@ -688,9 +742,30 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (profiling_) RJ_HIP(hipEventRecord(prog_ev_[0], stream_));
     RJ_HIP(hipMemsetAsync(d_coef_.as<uint32_t>(), 0, coef_dw_total * 4, stream_));
     RJ_HIP(hipMemsetAsync(d_nz_.as<unsigned long long>(), 0, nz_total * 8, stream_));
-    for (uint32_t L = 0; L < nlev; L++)
+    if (prec_total) RJ_HIP(hipMemsetAsync(d_prec_.as<unsigned long long>(), 0, prec_total * 8, stream_));
+    const RjFoldJob *d_fold = reinterpret_cast<const RjFoldJob *>(dbase + off_fold);
+    const bool dbg_lev = profiling_ && getenv("RJ_DEBUG_PROG") != nullptr;
+    if (dbg_lev && prog_lev_ev_.size() < nlev + 1) {
+      for (size_t q = prog_lev_ev_.size(); q < nlev + 1; q++) {
+        hipEvent_t e;
+        RJ_HIP(hipEventCreate(&e));
+        prog_lev_ev_.push_back(e);
+      }
+    }
+    if (dbg_lev) RJ_HIP(hipEventRecord(prog_lev_ev_[0], stream_));
+    for (uint32_t L = 0; L < nlev; L++) {
       RJ_HIP(LaunchProgressive(stream_, d_imgs, n, d_plane + prog_level_off[L], prog_level_off[L + 1] - prog_level_off[L],
-                               d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>()));
+                               d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
+                               d_prec_.as<unsigned long long>()));
+      RJ_HIP(LaunchProgressiveAcRefine(stream_, d_imgs, n, d_plane + acref_off[L], acref_off[L + 1] - acref_off[L],
+                                       d_destuff_.as<uint8_t>(), d_nz_.as<unsigned long long>(),
+                                       d_prec_.as<unsigned long long>()));
+      if (L >= 1)
+        RJ_HIP(LaunchProgressiveFold(stream_, d_imgs, d_fold + fold_off[L], fold_off[L + 1] - fold_off[L], fold_chunks[L],
+                                     L, d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
+                                     d_prec_.as<unsigned long long>()));
+      if (dbg_lev) RJ_HIP(hipEventRecord(prog_lev_ev_[L + 1], stream_));
+    }
     if (profiling_) RJ_HIP(hipEventRecord(prog_ev_[1], stream_));
     RJ_HIP(LaunchRowsDense(stream_, false, d_imgs, n, reinterpret_cast<const uint32_t *>(dbase + off_prows), pfused_rows,
                            cbuf, d_tabs, nullptr));
@@ -943,12 +1018,20 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (prog_images) {
       RJ_HIP(hipEventElapsedTime(&timings_.prog_entropy_ms, prog_ev_[0], prog_ev_[1]));
       RJ_HIP(hipEventElapsedTime(&timings_.prog_rows_ms, prog_ev_[1], prog_ev_[2]));
+      RJ_HIP(hipEventElapsedTime(&timings_.destuff_ms, ev_[1], prog_ev_[0]));  // K0 alone
+      if (getenv("RJ_DEBUG_PROG") && prog_lev_ev_.size() >= nlev + 1) {
+        for (uint32_t L = 0; L < nlev; L++) {
+          float t = 0;
+          RJ_HIP(hipEventElapsedTime(&t, prog_lev_ev_[L], prog_lev_ev_[L + 1]));
+          fprintf(stderr, "[rj prog] level %u: %u lanes, %.3f ms\n", L, prog_level_off[L + 1] - prog_level_off[L], t);
+        }
+      }
     }
     unsigned long long cnt = 0;
     RJ_HIP(hipMemcpy(&cnt, cbuf.count, sizeof(cnt), hipMemcpyDeviceToHost));
     timings_.entry_bytes = cnt * 4;
     timings_.h2d_ms = ms[0];
-    timings_.destuff_ms = ms[1];
+    if (!prog_images) timings_.destuff_ms = ms[1];
     timings_.huffman_ms = ms[2];
     timings_.idct_ms = ms[3];
     timings_.output_ms = ms[4];

@@ -92,12 +92,14 @@ class Decoder {
     std::vector<uint8_t> is_fused, row_group;
     std::vector<uint2> row_list;
     std::vector<uint32_t> prow_prefix, pgrow_prefix, prog_lanes, prog_bucket;  // progressive images
+    std::vector<RjFoldJob> fold_jobs;
   } sc_;
   hipEvent_t prog_ev_[3] = {};  // profiling: K1p start, K1p end (dense K2 start), dense K2 end
+  std::vector<hipEvent_t> prog_lev_ev_;  // development (RJ_DEBUG_PROG): per-level K1p spans
 
   DeviceBuffer d_desc_, d_stage_, d_destuff_, d_entries_, d_planes_;
   DeviceBuffer d_piece_, d_rec_, d_chunkres_, d_fallback_;  // K1 chunk bookkeeping
-  DeviceBuffer d_coef_, d_nz_;  // progressive images: dense coefficients, nonzero masks
+  DeviceBuffer d_coef_, d_nz_, d_prec_;  // progressive: dense coefficients, nonzero masks, refinement records
   uint32_t epoch_ = 0;
   PinnedBuffer h_stage_;
 };

@@ -193,7 +193,11 @@ struct RjJobDev {
 // update -- first-scan value, refinement correction bit, newly nonzero coefficient -- is an OR
 // into a word that no other scan of the same dependency level touches (rj_stream.cpp levels).
 // A per-block 64-bit mask of nonzero AC positions (component raster of the blocks the AC scans
-// code, no MCU padding) feeds the refinement scans.
+// code, no MCU padding) feeds the refinement scans.  Refinement scans do not touch the dense
+// coefficients while they decode: each writes per-unit records (AC: the positions whose
+// magnitude gains bit Al, the new coefficients and their signs; DC: one bit per block) with
+// plain stores, and k_prog_fold applies a level's records (and the new nonzero positions) to
+// the dense coefficients before the next level.
 enum RjProgKind : uint8_t { RJ_PK_DC_FIRST = 0, RJ_PK_DC_REFINE = 1, RJ_PK_AC_FIRST = 2, RJ_PK_AC_REFINE = 3 };
 struct RjProgScanDev {
   uint8_t kind, ns, ss, se;  // RjProgKind; components in the scan; spectral band
@@ -204,12 +208,21 @@ struct RjProgScanDev {
   uint16_t tab[2];           // RjImageDev.ptabs index of table 0 / 1 (0xFFFF: none)
   uint32_t units_x, units;   // units (MCUs if interleaved, else blocks) per row / in total
   uint32_t ri;               // units per restart interval (0: one interval)
+  uint32_t ival0;            // index of the scan's first interval in the image's interval list
+  uint32_t nblk;             // blocks per unit
+};
+// AC refinement record of one unit (block): 32 B, written once by the decoding lane
+struct RjRefineRec {
+  unsigned long long orm;    // positions whose magnitude gains bit Al (correction 1 or new)
+  unsigned long long sgn;    // new coefficients that are negative
+  unsigned long long newm;   // new nonzero positions
+  unsigned long long pad;
 };
 struct RjProgIvalDev {       // one restart interval of one scan
   uint32_t dst_off, dst_len; // destuffed bytes, relative to RjImageDev.destuff_off
   uint32_t unit0, nunits;
   uint16_t scan, flags;      // flags: RJ_SEG_MISSING (no marker: the interval is skipped)
-  uint32_t pad;
+  uint32_t rec_off;          // refinement scans: first record word (u64) of the interval, image-relative
 };
 
 struct RjImageDev {
@@ -246,8 +259,15 @@ struct RjImageDev {
   const RjHuffDev *ptabs;
   uint64_t coef_off;      // dwords into the dense coefficient buffer (32 per block)
   uint64_t nz_off;        // masks into the nonzero-mask buffer
+  uint64_t prec_off;      // u64 words into the refinement-record buffer
+  uint32_t npscans;
   uint32_t pival_prefix;  // exclusive prefix of progressive intervals over the batch
   uint32_t progressive;
   uint32_t cblk0[3], wblk[3];   // dense block raster of each component (MCU-padded width)
   uint32_t nzblk0[3], cwblk[3]; // nonzero-mask raster (blocks the AC scans code)
+  uint32_t chblk[3];
+};
+// k_prog_fold work: every block of one component of one image (64-block chunks, one wave each)
+struct RjFoldJob {
+  uint32_t image, comp, nblocks, chunk0;  // chunk0: exclusive prefix of chunks over the launch
 };

@@ -44,7 +44,16 @@ hipError_t LaunchRowsOfLanes(hipStream_t st, bool to_planes, const RjImageDev *i
 // lists batch-global interval indices (RjImageDev.pival_prefix), grouped so every wave holds
 // one scan kind (0xFFFFFFFF: padding).  One launch per dependency level.
 hipError_t LaunchProgressive(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *lanes, uint32_t nlanes,
-                             const uint8_t *destuffed, uint32_t *coef, unsigned long long *nz);
+                             const uint8_t *destuffed, uint32_t *coef, unsigned long long *nz,
+                             unsigned long long *recs);
+// K1p AC refinement, one wave per interval (n intervals listed in ivals, batch-global indices).
+hipError_t LaunchProgressiveAcRefine(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *ivals, uint32_t n,
+                                     const uint8_t *destuffed, const unsigned long long *nz,
+                                     unsigned long long *recs);
+// k_prog_fold: level `level`'s refinement records into the dense coefficients / nonzero masks.
+hipError_t LaunchProgressiveFold(hipStream_t st, const RjImageDev *imgs, const RjFoldJob *jobs, uint32_t njobs,
+                                 uint32_t nchunks, uint32_t level, uint32_t *coef, unsigned long long *nz,
+                                 const unsigned long long *recs);
 
 // K2 over progressive images' MCU rows: dense coefficients (RjCoefBuf.dense) instead of entries.
 hipError_t LaunchRowsDense(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,

@@ -35,6 +35,7 @@ namespace rj {
 #define RJ_PPHASE 8    // iterations per phase; an iteration consumes <= 32 bits and <= 1 block
 #define RJ_PRING 32    // bit ring words per lane
 #define RJ_PNZ 32      // nonzero-mask ring entries per lane
+#define RJ_PVALS 48    // symbol words per lane (AC tables: <= 162 symbols)
 
 struct PRow {  // lane-interleaved LDS column: word w of this lane at base[w * 64]
   uint32_t *base;
@@ -110,25 +111,56 @@ __device__ __forceinline__ int32_t pextend(uint32_t v, uint32_t s) {
   return (s && v < (1u << (s - 1))) ? int32_t(v) - int32_t(1u << s) + 1 : int32_t(v);
 }
 
-// canonical search (second-level pool exhausted): libjpeg jpeg_huff_decode on the HBM table
-__device__ __forceinline__ uint32_t phuff_slow(const RjHuffDev *t, uint32_t peek16) {
-  uint32_t e = RJ_LUT_BAD;
-#pragma unroll 1
-  for (int l = 1; l <= 16; l++)
-    if (peek16 < gp(t->maxcode16)[l]) {
-      e = uint32_t(l << 8) | gp(t->vals)[((peek16 >> (16 - l)) + gp(t->valoff)[l]) & 255];
-      break;
+// Codes longer than the LDS first level: canonical decode from per-lane registers (libjpeg
+// jpeg_huff_decode restated).  Left-justified to 16 bits, the codes of length l fill
+// [mc(l-1), mc(l)), mc = the monotone exclusive bound of all codes of length <= l; no global
+// access on the symbol chain (a wave in which any lane met a long code would otherwise wait a
+// full memory latency -- and with 64 lanes that is nearly every iteration).  The symbols sit in
+// the lane's LDS column (VRow); a code past mc(16) is libjpeg's bad code (17 bits, symbol 0).
+struct VRow {
+  uint32_t *base;
+  __device__ __forceinline__ uint32_t &operator[](uint32_t w) const { return base[w * RJ_PW]; }
+  __device__ __forceinline__ uint32_t byte(uint32_t b) const { return ((*this)[b >> 2] >> ((b & 3u) * 8u)) & 255u; }
+};
+struct PLong {
+  uint32_t mc[8];  // bound for lengths 9..16
+  int32_t vo[8];   // symbol index = code + vo[l - 9]
+  uint32_t vbase;  // this table's first symbol byte in the lane's VRow
+  __device__ __forceinline__ void load(const RjHuffDev *t, uint32_t vb) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int l = 1; l <= 16; l++) {
+      m = max(m, gp(t->maxcode16)[l]);
+      if (l >= 9) mc[l - 9] = m;
     }
-  return e;
-}
-// full two-level lookup in HBM (codes longer than the LDS level resolves)
-__device__ __forceinline__ uint32_t phuff_global(const RjHuffDev *t, uint32_t peek) {
-  uint32_t e = gp(t->lut)[peek >> 23];
-  if (e & 0x8000u) {
-    if (e == 0xFFFFu) e = phuff_slow(t, peek >> 16);
-    else e = gp(t->lut)[RJ_LUT_L1 + (e & 0xFFu) * 128u + ((peek >> 16) & 127u)];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      vo[j] = gp(t->valoff)[9 + j];
+    }
+    vbase = vb;
   }
-  return e;
+};
+__device__ __forceinline__ uint32_t plong_decode(const PLong &a, uint32_t peek, const VRow &vals) {
+  const uint32_t p16 = peek >> 16;
+  // the bounds are monotone, so with ge_j = (p16 >= mc[j]): l = 9 + sum ge_j and
+  // vo[l - 9] = vo[0] + sum ge_j * (vo[j+1] - vo[j]) -- masks, no select of loads (which the
+  // backend turns into a scratch array)
+  uint32_t l = 9;
+  int32_t vo = a.vo[0];
+#pragma unroll
+  for (int j = 0; j < 7; j++) {
+    const uint32_t m = 0u - (p16 >= a.mc[j] ? 1u : 0u);
+    l += m & 1u;
+    vo += int32_t(uint32_t(a.vo[j + 1] - a.vo[j]) & m);
+  }
+  const uint32_t idx = uint32_t(int32_t(p16 >> (16u - l)) + vo) & 255u;
+  const uint32_t sym = vals.byte(a.vbase + idx);
+  return p16 >= a.mc[7] ? RJ_LUT_BAD : ((l << 8) | sym);
+}
+// symbols of a table into the lane's VRow words [w0, w0 + nw)
+__device__ __forceinline__ void load_vals(const RjHuffDev *t, const VRow &vals, uint32_t w0, uint32_t nw) {
+  const uint32_t *src = reinterpret_cast<const uint32_t *>(t->vals);
+  for (uint32_t w = 0; w < nw; w++) vals[w0 + w] = gp(src)[w];
 }
 
 // ---- lane geometry shared by the kinds ----
@@ -168,7 +200,8 @@ struct PLaneIn {
 // DC first / DC refine (possibly interleaved): one block per iteration
 // ---------------------------------------------------------------------------------------
 template <bool kRefine>
-__device__ void lane_dc(const PLaneIn &L, PGeo &g, PBits &br, const HRow &lut, uint16_t *coef16, uint32_t *coef32) {
+__device__ __forceinline__ void lane_dc(const PLaneIn &L, PGeo &g, PBits &br, const HRow &lut, const VRow &vals, uint16_t *coef16,
+                        unsigned long long *rec) {
   const RjProgScanDev &sc = L.sc;
   const RjHuffDev *gt0 = nullptr, *gt1 = nullptr;
   if (!kRefine && L.active) {
@@ -188,11 +221,20 @@ __device__ void lane_dc(const PLaneIn &L, PGeo &g, PBits &br, const HRow &lut, u
       }
     }
   }
+  PLong lg0, lg1;  // DC codes longer than 8 bits (12 symbols per table: 16-byte slots)
+  if (!kRefine && L.active) {
+    lg0.load(gt0, 0);
+    lg1.load(gt1, 16);
+    load_vals(gt0, vals, 0, 4);
+    load_vals(gt1, vals, 4, 4);
+  }
   const uint32_t al = sc.al;
   const uint32_t tsel = uint32_t(sc.tsel[0]) | (uint32_t(sc.tsel[1]) << 1) | (uint32_t(sc.tsel[2]) << 2);
   const uint32_t nbits = L.iv.dst_len * 8u;
   int32_t pred0 = 0, pred1 = 0, pred2 = 0;
   uint32_t ci = 0, dx = 0, dy = 0;
+  uint64_t bacc = 0;   // DC refinement: one bit per block of the interval, in decode order
+  uint32_t bn = 0, bw = 0;
   bool active = L.active;
   while (__any(active)) {
     uint4 pa, pb;
@@ -204,12 +246,28 @@ __device__ void lane_dc(const PLaneIn &L, PGeo &g, PBits &br, const HRow &lut, u
       const uint32_t peek = br.peek();
       const uint32_t blk = pblock(g, ci, dx, dy);
       if (kRefine) {
-        if (peek >> 31) gor32(coef32 + g.coef + blk * 32u, 1u << al);
+        (void)blk;
+        bacc |= uint64_t(peek >> 31) << bn;
         br.pos += 1;
+        if (++bn == 64) {
+          *gp(rec + bw) = bacc;
+          bw++;
+          bn = 0;
+          bacc = 0;
+        }
       } else {
         const uint32_t t = (tsel >> ci) & 1u;
         uint32_t e = lut[(t << 8) | (peek >> 24)];
-        if (e & 0x8000u) e = phuff_global(t ? gt1 : gt0, peek);
+        if (e & 0x8000u) {  // element-wise select (a reference select would put both in scratch)
+          PLong a;
+#pragma unroll
+          for (int j = 0; j < 8; j++) {
+            a.mc[j] = t ? lg1.mc[j] : lg0.mc[j];
+            a.vo[j] = t ? lg1.vo[j] : lg0.vo[j];
+          }
+          a.vbase = t ? 16u : 0u;
+          e = plong_decode(a, peek, vals);
+        }
         const uint32_t len = e >> 8, s = e & 15u;
         const int32_t diff = pextend(pbits(peek, len, s), s);
         int32_t p;
@@ -228,7 +286,10 @@ __device__ void lane_dc(const PLaneIn &L, PGeo &g, PBits &br, const HRow &lut, u
           if (++ci == g.ns) {
             ci = 0;
             unit_step(g, 1);
-            if (g.u >= g.nunits || br.pos > nbits) active = false;
+            if (g.u >= g.nunits || br.pos > nbits) {
+              active = false;
+              if (kRefine && bn) *gp(rec + bw) = bacc;  // the interval's last, partial word
+            }
           }
         }
       }
@@ -240,8 +301,8 @@ __device__ void lane_dc(const PLaneIn &L, PGeo &g, PBits &br, const HRow &lut, u
 // ---------------------------------------------------------------------------------------
 // AC first (one component): one symbol (or one EOB-run skip) per iteration
 // ---------------------------------------------------------------------------------------
-__device__ void lane_ac_first(const PLaneIn &L, PGeo &g, PBits &br, const HRow &lut, uint16_t *coef16,
-                              unsigned long long *nz, uint32_t nzbase) {
+__device__ __forceinline__ void lane_ac_first(const PLaneIn &L, PGeo &g, PBits &br, const HRow &lut, const VRow &vals,
+                              uint16_t *coef16, unsigned long long *nz, uint32_t nzbase) {
   const RjProgScanDev &sc = L.sc;
   const RjHuffDev *gt = L.active ? L.im->ptabs + sc.tab[0] : nullptr;
   if (L.active) {
@@ -255,6 +316,11 @@ __device__ void lane_ac_first(const PLaneIn &L, PGeo &g, PBits &br, const HRow &
         lut[q * 8u + 2 * j + 1] = uint16_t(w[j] >> 16);
       }
     }
+  }
+  PLong lg;  // AC codes longer than 9 bits
+  if (L.active) {
+    lg.load(gt, 0);
+    load_vals(gt, vals, 0, RJ_PVALS);
   }
   const uint32_t ss = sc.ss, se = sc.se, al = sc.al;
   const uint32_t nbits = L.iv.dst_len * 8u;
@@ -277,7 +343,8 @@ __device__ void lane_ac_first(const PLaneIn &L, PGeo &g, PBits &br, const HRow &
       }
       const uint32_t peek = br.peek();
       uint32_t e = lut[peek >> 23];
-      if (e & 0x8000u) e = phuff_global(gt, peek);
+      const uint32_t el = plong_decode(lg, peek, vals);  // branch-free: both lookups in flight
+      e = (e & 0x8000u) ? el : e;
       const uint32_t len = e >> 8, r = (e >> 4) & 15u, s = e & 15u;
       if (s) {
         const uint32_t q = min(k + r, 63u);
@@ -315,8 +382,8 @@ __device__ void lane_ac_first(const PLaneIn &L, PGeo &g, PBits &br, const HRow &
 __device__ __forceinline__ uint64_t lomask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
 __device__ __forceinline__ uint32_t ctz64(uint64_t x) { return uint32_t(__builtin_ctzll(x)); }
 
-__device__ void lane_ac_refine(const PLaneIn &L, PGeo &g, PBits &br, const HRow &lut, uint32_t *coef32,
-                               unsigned long long *nz, uint32_t nzbase, PRow nzr) {
+__device__ __forceinline__ void lane_ac_refine(const PLaneIn &L, PGeo &g, PBits &br, const HRow &lut, const VRow &vals,
+                               unsigned long long *rec, const unsigned long long *nz, uint32_t nzbase, PRow nzr) {
   const RjProgScanDev &sc = L.sc;
   const RjHuffDev *gt = L.active ? L.im->ptabs + sc.tab[0] : nullptr;
   if (L.active) {
@@ -331,8 +398,12 @@ __device__ void lane_ac_refine(const PLaneIn &L, PGeo &g, PBits &br, const HRow 
       }
     }
   }
-  const uint32_t ss = sc.ss, se = sc.se, al = sc.al;
-  const uint32_t p1 = 1u << al;
+  PLong lg;  // AC codes longer than 9 bits
+  if (L.active) {
+    lg.load(gt, 0);
+    load_vals(gt, vals, 0, RJ_PVALS);
+  }
+  const uint32_t ss = sc.ss, se = sc.se;
   const uint64_t band = lomask(se + 1) & ~lomask(ss);
   const uint32_t nbits = L.iv.dst_len * 8u;
   // nonzero-mask ring: masks of units [0, ntop) relative to the interval are committed
@@ -357,9 +428,12 @@ __device__ void lane_ac_refine(const PLaneIn &L, PGeo &g, PBits &br, const HRow 
     return (uint64_t(nzr[2 * sl + 1]) << 32) | nzr[2 * sl];
   };
   uint64_t nzm = nz_get(0) & band;
-  uint32_t k = ss, eobrun = 0, t = 0, newv = 0;
+  uint32_t k = ss, eobrun = 0, t = 0, newv = 0;  // newv: 0 none, 1 positive, 2 negative
   bool walking = false, eobblk = false;
-  uint64_t blk_new = 0;
+  // this block's record: its correction bits in walk order (one per previously nonzero position
+  // of the band, ascending -- k_prog_fold deposits them onto those positions), new coefficients
+  uint64_t cstr = 0, sgn = 0, blk_new = 0;
+  uint32_t pend = 0;  // correction bits left before the walk reaches t
   bool active = L.active;
   while (__any(active)) {
     uint4 pa, pb;
@@ -376,17 +450,16 @@ __device__ void lane_ac_refine(const PLaneIn &L, PGeo &g, PBits &br, const HRow 
       uint32_t used = 0;
       if (!walking) {
         if (eobrun) {
-          t = se + 1;
-          newv = 0;
-          eobblk = true;
+          // handled below (shared with the EOB symbol)
         } else {
           uint32_t e = lut[peek >> 23];
-          if (e & 0x8000u) e = phuff_global(gt, peek);
+          const uint32_t el = plong_decode(lg, peek, vals);
+          e = (e & 0x8000u) ? el : e;
           const uint32_t len = e >> 8, r = (e >> 4) & 15u, s = e & 15u;
           used = len;
           if (s || r == 15) {
             if (s) {
-              newv = pbits(peek, used, 1) ? p1 : (0x8000u | p1);
+              newv = pbits(peek, used, 1) ? 1u : 2u;
               used++;
             } else {
               newv = 0;
@@ -395,40 +468,38 @@ __device__ void lane_ac_refine(const PLaneIn &L, PGeo &g, PBits &br, const HRow 
             uint64_t z = ~nzm & band & ~lomask(k);
             for (uint32_t j = 0; j < r; j++) z &= z - 1;
             t = z ? ctz64(z) : se + 1;
+            pend = uint32_t(__popcll(nzm & lomask(t) & ~lomask(k)));
           } else {  // EOBr: this block's rest and 2^r + bits - 1 more blocks
             eobrun = (1u << r) + pbits(peek, used, r);
             used += r;
             t = se + 1;
             newv = 0;
             eobblk = true;
+            pend = uint32_t(__popcll(nzm & ~lomask(k)));
           }
+        }
+        if (eobrun && !eobblk) {  // a block inside an EOB run: every nonzero position of the band
+          t = se + 1;
+          newv = 0;
+          eobblk = true;
+          pend = uint32_t(__popcll(nzm & ~lomask(k)));
         }
         walking = true;
       }
-      // correction bits of the nonzero positions in [k, t), at most 32 - used of them
-      uint64_t cm = nzm & lomask(t) & ~lomask(k);
-      const uint32_t cnt = uint32_t(__popcll(cm));
-      const uint32_t take = min(cnt, 32u - used);
-      const uint32_t cbits = pbits(peek, used, take);
+      // correction bits of the nonzero positions in [k, t): appended in walk order, at most
+      // 32 - used per iteration (the walk resumes next iteration)
+      const uint32_t take = min(pend, 32u - used);
+      cstr = (cstr << take) | pbits(peek, used, take);
       used += take;
-      const uint32_t dwb = g.coef + pblock(g, 0, 0, 0) * 32u;
-      uint32_t lastq = k;
-      for (uint32_t j = 0; j < take; j++) {
-        const uint32_t q = ctz64(cm);
-        cm &= cm - 1;
-        if ((cbits >> (take - 1 - j)) & 1u) gor32(coef32 + dwb + (q >> 1), p1 << ((q & 1u) * 16u));
-        lastq = q;
-      }
+      pend -= take;
       br.pos += used;
       bool blk_done = false;
-      if (take < cnt) {
-        k = lastq + 1;  // the walk continues next iteration
-      } else {
+      if (pend == 0) {
         walking = false;
         if (newv) {
-          const uint32_t q = min(t, 63u);
-          gor32(coef32 + dwb + (q >> 1), newv << ((q & 1u) * 16u));
-          blk_new |= 1ull << q;
+          const uint64_t bq = 1ull << min(t, 63u);
+          blk_new |= bq;
+          if (newv == 2) sgn |= bq;
         }
         if (eobblk) {
           eobblk = false;
@@ -440,8 +511,12 @@ __device__ void lane_ac_refine(const PLaneIn &L, PGeo &g, PBits &br, const HRow 
         }
       }
       if (blk_done) {
-        if (blk_new) gor64(nz + nzbase + g.u, blk_new);
-        blk_new = 0;
+        if (cstr | blk_new) {  // the record stays zero (memset) for a block with nothing to apply
+          uint4 *r4 = reinterpret_cast<uint4 *>(rec + uint64_t(g.u) * 4u);
+          *gp(r4) = make_uint4(uint32_t(cstr), uint32_t(cstr >> 32), uint32_t(sgn), uint32_t(sgn >> 32));
+          *gp(r4 + 1) = make_uint4(uint32_t(blk_new), uint32_t(blk_new >> 32), 0u, 0u);
+        }
+        cstr = sgn = blk_new = 0;
         k = ss;
         unit_step(g, 1);
         urel++;
@@ -457,11 +532,13 @@ __device__ void lane_ac_refine(const PLaneIn &L, PGeo &g, PBits &br, const HRow 
   }
 }
 
-__global__ __launch_bounds__(RJ_PW) void k_prog(const RjImageDev *__restrict__ imgs, int nimg,
+__global__ __launch_bounds__(RJ_PW) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_prog(const RjImageDev *__restrict__ imgs, int nimg,
                                                 const uint32_t *__restrict__ lanes, uint32_t nlanes,
                                                 const uint8_t *__restrict__ destuffed, uint32_t *__restrict__ coef,
-                                                unsigned long long *__restrict__ nz) {
+                                                unsigned long long *__restrict__ nz,
+                                                unsigned long long *__restrict__ recs) {
   __shared__ uint16_t s_lut[RJ_LUT_L1 * RJ_PW];
+  __shared__ uint32_t s_vals[RJ_PVALS * RJ_PW];
   __shared__ uint32_t s_ring[RJ_PRING * RJ_PW];
   __shared__ uint32_t s_nz[2 * RJ_PNZ * RJ_PW];
   const uint32_t lane = threadIdx.x;
@@ -507,32 +584,366 @@ __global__ __launch_bounds__(RJ_PW) void k_prog(const RjImageDev *__restrict__ i
   const uint32_t nzbase =
       L.active ? (c0 == 0 ? im.nzblk0[0] : (c0 == 1 ? im.nzblk0[1] : im.nzblk0[2])) + L.iv.unit0 : 0u;
   unsigned long long *nzi = nz + (L.active ? im.nz_off : 0ull);
+  unsigned long long *rec = recs + (L.active ? im.prec_off + L.iv.rec_off : 0ull);
 
   PBits br;
   const uint8_t *data = L.active ? destuffed + im.destuff_off + L.iv.dst_off : destuffed;
   br.init(reinterpret_cast<const uint4 *>(data), PRow{s_ring + lane}, L.active ? L.iv.dst_len : 0u);
   const HRow lut{s_lut + lane};
+  const VRow vals{s_vals + lane};
   switch (kind) {
     case RJ_PK_DC_FIRST:
-      lane_dc<false>(L, g, br, lut, coef16, coef32);
+      lane_dc<false>(L, g, br, lut, vals, coef16, rec);
       break;
     case RJ_PK_DC_REFINE:
-      lane_dc<true>(L, g, br, lut, coef16, coef32);
+      lane_dc<true>(L, g, br, lut, vals, coef16, rec);
       break;
     case RJ_PK_AC_FIRST:
-      lane_ac_first(L, g, br, lut, coef16, nzi, nzbase);
+      lane_ac_first(L, g, br, lut, vals, coef16, nzi, nzbase);
       break;
     default:
-      lane_ac_refine(L, g, br, lut, coef32, nzi, nzbase, PRow{s_nz + lane});
+      lane_ac_refine(L, g, br, lut, vals, rec, nzi, nzbase, PRow{s_nz + lane});
       break;
   }
 }
 
 hipError_t LaunchProgressive(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *lanes, uint32_t nlanes,
-                             const uint8_t *destuffed, uint32_t *coef, unsigned long long *nz) {
+                             const uint8_t *destuffed, uint32_t *coef, unsigned long long *nz,
+                             unsigned long long *recs) {
   if (nlanes == 0) return hipSuccess;
   hipLaunchKernelGGL(k_prog, dim3((nlanes + RJ_PW - 1) / RJ_PW), dim3(RJ_PW), 0, st, imgs, nimg, lanes, nlanes,
-                     destuffed, coef, nz);
+                     destuffed, coef, nz, recs);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// k_prog_acref: AC refinement, one WAVE per interval (wave-cooperative).  The lane-per-interval
+// decoder above leaves a batch's refinement levels with a few dozen waves on a 1024-SIMD chip
+// (one Y refinement scan per image), each lane walking ~10^5 divergent symbols.  Here the wave
+// owns one interval: per window step lane l peeks the 32 bits at pos + l and looks its Huffman
+// code up in the wave's LDS table (one lookup latency for 64 candidate offsets), then a scalar
+// (SGPR) chain walks the true symbol positions through readlane -- the refinement state machine
+// (zero-run targets, EOB runs, correction-bit counts on the 64-bit nonzero mask) is SALU work.
+// The bitstream window (64 + 64 words), the coming blocks' nonzero masks and the pending
+// records live one per lane in VGPRs; records leave 64 blocks at a time (coalesced).
+// Output is identical to lane_ac_refine (same records, k_prog_fold applies them).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane) {
+  return uint32_t(__builtin_amdgcn_readlane(int(v), int(lane)));
+}
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return uint32_t(__builtin_amdgcn_readfirstlane(int(v))); }
+
+__global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict__ imgs, int nimg,
+                                                   const uint32_t *__restrict__ ivals, const uint8_t *__restrict__ destuffed,
+                                                   const unsigned long long *__restrict__ nz,
+                                                   unsigned long long *__restrict__ recs) {
+  __shared__ uint16_t s_lut[RJ_LUT_ENTRIES];
+  __shared__ uint32_t s_maxc[18];
+  __shared__ int32_t s_voff[18];
+  __shared__ uint8_t s_vals[256];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t gi = rfl(*gp(ivals + blockIdx.x));
+  const int i = int(rfl(uint32_t(upper_index(nimg, gi, [&](int q) { return imgs[q].pival_prefix; }))));
+  const RjImageDev &im = imgs[i];
+  const RjProgIvalDev iv = *gp(im.pivals + (gi - im.pival_prefix));
+  if (iv.flags & RJ_SEG_MISSING) return;
+  const RjProgScanDev sc = *gp(im.pscans + iv.scan);
+  const RjHuffDev *gt = im.ptabs + sc.tab[0];
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(gt->lut);
+    uint4 *dst = reinterpret_cast<uint4 *>(s_lut);
+    for (uint32_t q = lane; q < RJ_LUT_ENTRIES * 2 / 16; q += 64) dst[q] = gp(src)[q];
+    if (lane < 18) {
+      s_maxc[lane] = gp(gt->maxcode16)[lane];
+      s_voff[lane] = gp(gt->valoff)[lane];
+    }
+    reinterpret_cast<uint32_t *>(s_vals)[lane] = gp(reinterpret_cast<const uint32_t *>(gt->vals))[lane];
+  }
+  __syncthreads();
+  const uint32_t ss = rfl(sc.ss), se = rfl(sc.se);
+  const uint64_t band = (se >= 63 ? ~0ull : ((1ull << (se + 1)) - 1)) & ~((1ull << ss) - 1);
+  const uint32_t nunits = rfl(iv.nunits), dst_len = rfl(iv.dst_len);
+  const uint32_t nbits = dst_len * 8u, nwords = (dst_len + 3) / 4;
+  const uint32_t *data = reinterpret_cast<const uint32_t *>(destuffed + im.destuff_off + iv.dst_off);
+  const uint32_t c0 = sc.comp[0] & 3u;
+  const unsigned long long *nzs =
+      nz + im.nz_off + (c0 == 0 ? im.nzblk0[0] : (c0 == 1 ? im.nzblk0[1] : im.nzblk0[2])) + iv.unit0;
+  unsigned long long *rec = recs + im.prec_off + iv.rec_off;
+  auto ldword = [&](uint32_t w) -> uint32_t {  // word w of the interval, zero past the data
+    const uint32_t v = *gp(data + min(w, nwords ? nwords - 1 : 0u));
+    return w < nwords ? __builtin_bswap32(v) : 0u;
+  };
+  auto ldnz = [&](uint32_t u) -> uint64_t { return *gp(nzs + min(u, nunits - 1)); };
+  // windows: bitstream words [wbase, wbase + 128) in win0/win1 (lane l: word wbase + l / + 64 + l),
+  // nonzero masks of units [nbase, nbase + 64)
+  uint32_t wbase = 0;
+  uint32_t win0 = ldword(lane), win1 = ldword(64 + lane);
+  uint32_t nbase = 0;
+  uint64_t nzw = ldnz(lane);
+  uint64_t r_cs = 0, r_sg = 0, r_nw = 0;  // lane b: record of unit rbase + b
+  uint32_t rbase = 0;
+  auto word = [&](uint32_t w) -> uint32_t {  // w relative to wbase, < 128
+    return w < 64 ? rl(win0, w) : rl(win1, w - 64);
+  };
+  uint32_t pos = 0, k = ss, eobrun = 0, u = 0;
+  uint64_t nzm = uint64_t(rl(uint32_t(nzw), 0)) | (uint64_t(rl(uint32_t(nzw >> 32), 0)) << 32);
+  nzm &= band;
+  uint64_t cstr = 0, sgn = 0, newm = 0;
+  uint32_t pend = 0, t = 0, newv = 0;
+  bool walking = false, eobblk = false, done = nunits == 0;
+  while (!done) {
+    // ---- window step: slide the bitstream window, then 64 candidate decodes ----
+    if ((pos >> 5) - wbase >= 64) {  // everything needed is in win1: shift, prefetch the next 64 words
+      wbase += 64;
+      win0 = win1;
+      win1 = ldword(wbase + 64 + lane);
+    }
+    const uint32_t W = (pos >> 5) - wbase, sh = pos & 31;
+    const uint32_t A = word(W), B = word(W + 1), C = word(W + 2), D = word(W + 3);
+    const uint32_t o = sh + lane;
+    const uint32_t hi = o < 32 ? A : (o < 64 ? B : C), lo = o < 32 ? B : (o < 64 ? C : D);
+    const uint32_t pk_l = uint32_t(((uint64_t(hi) << 32 | lo) << (o & 31)) >> 32);
+    uint32_t e_l = s_lut[pk_l >> 23];
+    if (e_l & 0x8000u) {
+      if (e_l == 0xFFFFu) {
+        const uint32_t p16 = pk_l >> 16;
+        e_l = RJ_LUT_BAD;
+        for (int l = 1; l <= 16; l++)
+          if (p16 < s_maxc[l]) {
+            e_l = uint32_t(l << 8) | s_vals[((p16 >> (16 - l)) + s_voff[l]) & 255];
+            break;
+          }
+      } else {
+        e_l = s_lut[RJ_LUT_L1 + (e_l & 0xFFu) * 128u + ((pk_l >> 16) & 127u)];
+      }
+    }
+    const uint32_t pos0 = pos;
+    // ---- scalar chain over the window ----
+    while (!done && pos - pos0 < 64) {
+      const uint32_t d = pos - pos0;
+      const uint32_t pk = rl(pk_l, d);
+      uint32_t used = 0;
+      if (!walking) {
+        if (eobrun == 0) {
+          const uint32_t en = rl(e_l, d);
+          const uint32_t len = en >> 8, r = (en >> 4) & 15u, s = en & 15u;
+          used = len;
+          if (s || r == 15) {
+            if (s) {
+              newv = pbits(pk, used, 1) ? 1u : 2u;
+              used++;
+            } else {
+              newv = 0;
+            }
+            uint64_t z = ~nzm & band & ~lomask(k);
+            for (uint32_t j = 0; j < r; j++) z &= z - 1;
+            t = z ? ctz64(z) : se + 1;
+            pend = uint32_t(__popcll(nzm & lomask(t) & ~lomask(k)));
+            eobblk = false;
+          } else {  // EOBr
+            eobrun = (1u << r) + pbits(pk, used, r);
+            used += r;
+            t = se + 1;
+            newv = 0;
+            eobblk = true;
+            pend = uint32_t(__popcll(nzm & ~lomask(k)));
+          }
+        } else {  // a block inside an EOB run
+          t = se + 1;
+          newv = 0;
+          eobblk = true;
+          pend = uint32_t(__popcll(nzm & ~lomask(k)));
+        }
+        walking = true;
+      }
+      const uint32_t take = min(pend, 32u - used);
+      cstr = (cstr << take) | pbits(pk, used, take);
+      used += take;
+      pend -= take;
+      pos += used;
+      if (pend) continue;  // the walk resumes at the next peek
+      walking = false;
+      if (newv) {
+        const uint64_t bq = 1ull << min(t, 63u);
+        newm |= bq;
+        if (newv == 2) sgn |= bq;
+      }
+      bool blk_done;
+      if (eobblk) {
+        eobrun--;
+        blk_done = true;
+      } else {
+        k = t + 1;
+        blk_done = k > se;
+      }
+      if (!blk_done) continue;
+      // ---- block end: its record into lane (u - rbase); 64 records leave together ----
+      const uint32_t rb = u - rbase;
+      if (lane == rb) {
+        r_cs = cstr;
+        r_sg = sgn;
+        r_nw = newm;
+      }
+      cstr = sgn = newm = 0;
+      k = ss;
+      u++;
+      done = u >= nunits || pos > nbits;
+      if (rb == 63 || done) {
+        if (rbase + lane < u) {
+          uint4 *r4 = reinterpret_cast<uint4 *>(rec + uint64_t(rbase + lane) * 4u);
+          *gp(r4) = make_uint4(uint32_t(r_cs), uint32_t(r_cs >> 32), uint32_t(r_sg), uint32_t(r_sg >> 32));
+          *gp(r4 + 1) = make_uint4(uint32_t(r_nw), uint32_t(r_nw >> 32), 0u, 0u);
+        }
+        r_cs = r_sg = r_nw = 0;
+        rbase += 64;
+      }
+      if (done) break;
+      if (u - nbase >= 64) {
+        nbase += 64;
+        nzw = ldnz(nbase + lane);
+      }
+      const uint32_t nl = u - nbase;
+      nzm = (uint64_t(rl(uint32_t(nzw), nl)) | (uint64_t(rl(uint32_t(nzw >> 32), nl)) << 32)) & band;
+    }
+  }
+}
+
+hipError_t LaunchProgressiveAcRefine(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *ivals, uint32_t n,
+                                     const uint8_t *destuffed, const unsigned long long *nz,
+                                     unsigned long long *recs) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_prog_acref, dim3(n), dim3(64), 0, st, imgs, nimg, ivals, destuffed, nz, recs);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// k_prog_fold: a dependency level's refinement records into the dense coefficients and the
+// nonzero masks.  One lane per block of one component of one image (a wave = 64 blocks of one
+// job, so the job and the image's scan list are wave-uniform); every block is owned by one lane,
+// so the read-modify-write needs no atomics.  All updates are ORs: AC magnitude bit Al (and the
+// sign of a new coefficient), DC bit Al (libjpeg decode_mcu_DC_refine: block[0] |= p1).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void or_bits(uint32_t (&w)[32], uint64_t orm, uint64_t sgn, uint32_t p1) {
+#pragma unroll
+  for (int q = 0; q < 32; q++) {
+    const uint32_t m2 = uint32_t(orm >> (2 * q)) & 3u, s2 = uint32_t(sgn >> (2 * q)) & 3u;
+    w[q] |= ((m2 & 1u) ? p1 : 0u) | ((m2 & 2u) ? (p1 << 16) : 0u) | ((s2 & 1u) << 15) | ((s2 & 2u) << 30);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_prog_fold(const RjImageDev *__restrict__ imgs, const RjFoldJob *__restrict__ jobs,
+                                                  uint32_t njobs, uint32_t level, uint32_t *__restrict__ coef,
+                                                  unsigned long long *__restrict__ nz,
+                                                  const unsigned long long *__restrict__ recs) {
+  const uint32_t chunk = blockIdx.x;
+  const int j = __builtin_amdgcn_readfirstlane(upper_index(int(njobs), chunk, [&](int q) { return jobs[q].chunk0; }));
+  const RjFoldJob J = jobs[j];
+  const uint32_t b = (chunk - J.chunk0) * 64u + threadIdx.x;
+  if (b >= J.nblocks) return;
+  const RjImageDev &im = imgs[J.image];
+  const uint32_t c = J.comp;
+  const uint32_t wb = c == 0 ? im.wblk[0] : (c == 1 ? im.wblk[1] : im.wblk[2]);
+  const uint32_t cwb = c == 0 ? im.cwblk[0] : (c == 1 ? im.cwblk[1] : im.cwblk[2]);
+  const uint32_t chb = c == 0 ? im.chblk[0] : (c == 1 ? im.chblk[1] : im.chblk[2]);
+  const uint32_t cb0 = c == 0 ? im.cblk0[0] : (c == 1 ? im.cblk0[1] : im.cblk0[2]);
+  const uint32_t nzb0 = c == 0 ? im.nzblk0[0] : (c == 1 ? im.nzblk0[1] : im.nzblk0[2]);
+  const uint32_t by = b / wb, bx = b - by * wb;
+  const bool coded = bx < cwb && by < chb;  // blocks a non-interleaved scan codes
+  const unsigned long long *rec = recs + im.prec_off;
+  uint32_t w[32];
+  bool loaded = false;
+  uint64_t newall = 0;
+  uint4 *blk4 = reinterpret_cast<uint4 *>(coef + im.coef_off + uint64_t(cb0 + b) * 32u);
+  auto load = [&]() {
+    if (loaded) return;
+    loaded = true;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint4 v = gp(blk4)[q];
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
+    }
+  };
+  unsigned long long *nzp = nz + im.nz_off + nzb0 + by * cwb + bx;
+  uint64_t nz_before = 0;
+  bool nz_loaded = false;
+  auto nzprev = [&]() -> uint64_t {  // the block's nonzero positions before this level
+    if (!nz_loaded) {
+      nz_loaded = true;
+      nz_before = *gp(nzp);
+    }
+    return nz_before;
+  };
+  const uint32_t ns_img = im.npscans;
+  for (uint32_t si = 0; si < ns_img; si++) {
+    const RjProgScanDev sc = im.pscans[si];
+    if (sc.level != level) continue;
+    if (sc.kind == RJ_PK_AC_REFINE) {
+      if (sc.comp[0] != c || !coded) continue;
+      const uint32_t unit = by * cwb + bx;
+      const RjProgIvalDev iv = *gp(im.pivals + sc.ival0 + (sc.ri ? unit / sc.ri : 0u));
+      const uint4 *r4 = reinterpret_cast<const uint4 *>(rec + iv.rec_off + uint64_t(unit - iv.unit0) * 4u);
+      const uint4 a = *gp(r4), n = *gp(r4 + 1);
+      const uint64_t cstr = uint64_t(a.y) << 32 | a.x, sgn = uint64_t(a.w) << 32 | a.z;
+      const uint64_t newm = uint64_t(n.y) << 32 | n.x;
+      if (cstr | newm) {
+        // the correction bits belong to the band's previously nonzero positions, ascending,
+        // first bit most significant (libjpeg decode_mcu_AC_refine's walk order)
+        const uint64_t band = (sc.se >= 63 ? ~0ull : ((1ull << (sc.se + 1)) - 1)) & ~((1ull << sc.ss) - 1);
+        uint64_t nzm = nzprev() & band;
+        uint32_t j = uint32_t(__popcll(nzm));
+        uint64_t orm = newm;
+        while (nzm) {
+          const uint32_t q = uint32_t(__builtin_ctzll(nzm));
+          nzm &= nzm - 1;
+          j--;
+          if ((cstr >> j) & 1u) orm |= 1ull << q;
+        }
+        load();
+        or_bits(w, orm, sgn, 1u << sc.al);
+      }
+      newall |= newm;
+    } else if (sc.kind == RJ_PK_DC_REFINE) {
+      uint32_t i = 3, slot0 = 0;
+      for (uint32_t q = 0; q < sc.ns; q++) {
+        if (sc.comp[q] == c && i == 3) i = q;
+        if (i == 3) slot0 += uint32_t(sc.hs[q]) * sc.vs[q];
+      }
+      if (i == 3) continue;
+      uint32_t unit, slot;
+      if (sc.ns > 1) {
+        const uint32_t h = sc.hs[i], v = sc.vs[i];
+        const uint32_t mx = bx / h, my = by / v;
+        unit = my * sc.units_x + mx;
+        slot = slot0 + (by - my * v) * h + (bx - mx * h);
+      } else {
+        if (!coded) continue;
+        unit = by * cwb + bx;
+        slot = 0;
+      }
+      const RjProgIvalDev iv = *gp(im.pivals + sc.ival0 + (sc.ri ? unit / sc.ri : 0u));
+      const uint32_t bit = (unit - iv.unit0) * sc.nblk + slot;
+      const uint64_t word = *gp(rec + iv.rec_off + bit / 64u);
+      if ((word >> (bit & 63u)) & 1u) {
+        load();
+        w[0] |= 1u << sc.al;  // two's complement DC: bit Al, low half
+      }
+    }
+  }
+  if (loaded) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) gp(blk4)[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  }
+  if (newall) *gp(nzp) = nzprev() | newall;
+}
+
+hipError_t LaunchProgressiveFold(hipStream_t st, const RjImageDev *imgs, const RjFoldJob *jobs, uint32_t njobs,
+                                 uint32_t nchunks, uint32_t level, uint32_t *coef, unsigned long long *nz,
+                                 const unsigned long long *recs) {
+  if (nchunks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_prog_fold, dim3(nchunks), dim3(64), 0, st, imgs, jobs, njobs, level, coef, nz, recs);
   return hipGetLastError();
 }
 

@@ -392,6 +392,8 @@ bool Stream::ParseProgressive(const uint8_t *d, uint32_t n) {
       v.hs[i] = uint8_t(inter && i < v.ns ? s.comp[c].h : 1);
       v.vs[i] = uint8_t(inter && i < v.ns ? s.comp[c].v : 1);
     }
+    v.nblk = 0;
+    for (int i = 0; i < v.ns; i++) v.nblk += uint32_t(v.hs[i]) * v.vs[i];
     if (inter) {
       v.units_x = p.mcux;
       v.units = p.mcux * p.mcuy;
@@ -453,8 +455,18 @@ void Stream::BuildProgressivePlan(const uint8_t *d) {
   std::vector<uint32_t> drops;
   p.pivals.clear();
   p.ds.clear();
+  uint64_t rec = 0;  // refinement records (u64 words): AC 4 per unit, DC one bit per block
   for (size_t si = 0; si < p.pscans.size(); si++) {
-    const RjProgScanDev &v = p.pscans[si];
+    RjProgScanDev &v = p.pscans[si];
+    v.ival0 = uint32_t(p.pivals.size());
+    const bool refine = v.kind == RJ_PK_AC_REFINE || v.kind == RJ_PK_DC_REFINE;
+    auto take_rec = [&](RjProgIvalDev &iv) {
+      if (v.kind == RJ_PK_AC_REFINE) rec = (rec + 3) & ~uint64_t(3);  // 32-B records, 16-B stores
+      iv.rec_off = uint32_t(rec);
+      if (v.kind == RJ_PK_AC_REFINE) rec += uint64_t(iv.nunits) * 4;
+      else if (v.kind == RJ_PK_DC_REFINE) rec += (uint64_t(iv.nunits) * v.nblk + 63) / 64;
+      (void)refine;
+    };
     const uint32_t b0 = p.pscan_src[2 * si] - base, b1 = p.pscan_src[2 * si + 1] - base;
     const uint32_t ri = v.ri, units = v.units;
     const uint32_t expected = ri ? (units + ri - 1) / ri : 1;
@@ -488,6 +500,7 @@ void Stream::BuildProgressivePlan(const uint8_t *d) {
       iv.unit0 = made * (ri ? ri : units);
       iv.nunits = ri ? std::min(ri, units - iv.unit0) : units;
       iv.scan = uint16_t(si);
+      take_rec(iv);
       dst += (uint64_t(src_len) + 16 + 15) & ~uint64_t(15);
       p.pivals.push_back(iv);
       made++;
@@ -524,12 +537,15 @@ void Stream::BuildProgressivePlan(const uint8_t *d) {
       iv.nunits = std::min(ri, units - iv.unit0);
       iv.scan = uint16_t(si);
       iv.flags = RJ_SEG_MISSING;
+      take_rec(iv);  // a skipped interval's records stay zero (the fold applies nothing)
       dst += 16;
       p.pivals.push_back(iv);
       made++;
     }
   }
   p.destuff_bytes = dst;
+  p.prec_words = rec;
+  if (rec >= (1ull << 32)) p.status = -4;  // record offsets are 32-bit
   p.segs.clear();
   p.entries = 0;
   p.nchunks = 0;

@@ -69,6 +69,7 @@ struct DecodePlan {
   uint32_t cblk0[3] = {}, nzblk0[3] = {}, cwblk[3] = {}, chblk[3] = {};
   uint64_t coef_blocks = 0;        // dense blocks (MCU-padded)
   uint64_t nz_blocks = 0;          // nonzero masks
+  uint64_t prec_words = 0;         // refinement records (u64 words)
   uint8_t pqlat[3][64] = {};       // each component's latched quant table (zigzag order)
   std::vector<uint32_t> pscan_src; // per scan: absolute stream offsets of its data [begin, end)
 };
