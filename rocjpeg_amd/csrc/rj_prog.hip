@@ -735,10 +735,14 @@ __global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict_
             } else {
               newv = 0;
             }
-            uint64_t z = ~nzm & band & ~lomask(k);
-            for (uint32_t j = 0; j < r; j++) z &= z - 1;
-            t = z ? ctz64(z) : se + 1;
-            pend = uint32_t(__popcll(nzm & lomask(t) & ~lomask(k)));
+            // the (r+1)-th zero-history position at or after k, lane-parallel: lane l is it when
+            // bit l of the candidate mask is set with exactly r candidates below it
+            const uint64_t zm = ~nzm & band & (~0ull << k);
+            const uint32_t below =
+                __builtin_amdgcn_mbcnt_hi(uint32_t(zm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(zm), 0u));
+            const uint64_t hit = __ballot(((zm >> lane) & 1u) && below == r);
+            t = hit ? ctz64(hit) : se + 1;
+            pend = uint32_t(__popcll(nzm & lomask(t) & (~0ull << k)));
             eobblk = false;
           } else {  // EOBr
             eobrun = (1u << r) + pbits(pk, used, r);
