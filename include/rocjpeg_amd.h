@@ -24,6 +24,31 @@ RocJpegStatus rocJpegAmdStreamGetInfo(RocJpegStreamHandle stream, uint8_t *num_c
  * re-parsed or destroyed. */
 RocJpegStatus rocJpegAmdStreamsToDevice(RocJpegHandle handle, RocJpegStreamHandle *streams, int count);
 
+/* rocJpegStreamParse of `count` streams followed by rocJpegAmdStreamsToDevice, with the O(bytes)
+ * part of the parse on the handle's GPU: the host reads only the headers; one kernel
+ * (rj_scan.hip) finds each entropy-coded segment's end (the first FF D9, as the reference's
+ * ParseEOI, src/rocjpeg_parser.cpp:400-416) and builds the restart-interval and destuffing
+ * tables in HBM.  The parsed streams are identical to host-parsed ones (same info, same tables)
+ * and resident on the handle's device.  Progressive (SOF2) streams are parsed on the host.
+ * Returns the first failure as rocJpegStreamParse would (BAD_JPEG). */
+RocJpegStatus rocJpegAmdStreamParseDevice(RocJpegHandle handle, const unsigned char *const *data,
+                                          const size_t *lengths, int count, RocJpegStreamHandle *streams);
+
+/* Introspection of a parsed stream's restart-interval table (tests / tooling). */
+typedef struct {
+  uint32_t src_off, src_len;   /* raw entropy-coded bytes of the interval (ECS-relative) */
+  uint32_t dst_off, dst_len;   /* destuffed bytes */
+  uint32_t mcu_first, mcu_count;
+  uint32_t flags;              /* 1: the interval's restart marker was missing */
+  uint32_t ent_off, chunk0, reserved;
+} RocJpegAmdInterval;
+RocJpegStatus rocJpegAmdStreamGetIntervals(RocJpegStreamHandle stream, RocJpegAmdInterval *out, uint32_t capacity,
+                                           uint32_t *count);
+/* The destuffing work units: 4 x uint32 each {src_off, len | first-of-interval << 31, dst_off,
+ * zero_end}; ecs_size: the entropy-coded segment length the parse found. */
+RocJpegStatus rocJpegAmdStreamGetDestuffBlocks(RocJpegStreamHandle stream, uint32_t *out4, uint32_t capacity,
+                                               uint32_t *count, uint32_t *ecs_size);
+
 /* Per-stage device time of the most recent decode call, measured with HIP events on the
  * handle's internal stream (enable with rocJpegAmdSetProfiling first). */
 typedef struct {
@@ -58,6 +83,9 @@ typedef struct {
   float prog_entropy_ms, prog_rows_ms;
   uint32_t prog_images, prog_intervals, prog_levels, prog_pad;
   uint64_t prog_coef_bytes;  /* dense coefficient bytes (int16 per coefficient) */
+  /* rocJpegAmdStreamParseDevice (the last call on this handle): streams whose marker scan ran on
+     the GPU, and those that fell back to the host scan (a scratch list overflowed) */
+  uint32_t scan_device_streams, scan_host_fallbacks;
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);

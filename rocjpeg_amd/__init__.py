@@ -19,7 +19,8 @@ API_SYMBOLS = (
 )
 EXT_SYMBOLS = (
     "rocJpegAmdStreamGetInfo", "rocJpegAmdStreamsToDevice", "rocJpegAmdSetProfiling", "rocJpegAmdGetLastTimings",
-    "rocJpegAmdSetPathPolicy", "rocJpegAmdGetStream",
+    "rocJpegAmdSetPathPolicy", "rocJpegAmdGetStream", "rocJpegAmdStreamParseDevice", "rocJpegAmdStreamGetIntervals",
+    "rocJpegAmdStreamGetDestuffBlocks",
 )
 
 
@@ -95,7 +96,13 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("prog_entropy_ms", ctypes.c_float), ("prog_rows_ms", ctypes.c_float),
                 ("prog_images", ctypes.c_uint32), ("prog_intervals", ctypes.c_uint32),
                 ("prog_levels", ctypes.c_uint32), ("prog_pad", ctypes.c_uint32),
-                ("prog_coef_bytes", ctypes.c_uint64)]
+                ("prog_coef_bytes", ctypes.c_uint64),
+                ("scan_device_streams", ctypes.c_uint32), ("scan_host_fallbacks", ctypes.c_uint32)]
+
+
+class RocJpegAmdInterval(ctypes.Structure):  # include/rocjpeg_amd.h
+    _fields_ = [(k, ctypes.c_uint32) for k in ("src_off", "src_len", "dst_off", "dst_len", "mcu_first", "mcu_count",
+                                               "flags", "ent_off", "chunk0", "reserved")]
 
 
 class RocJpegError(RuntimeError):
@@ -135,6 +142,12 @@ def lib():
         L.rocJpegAmdGetLastTimings.argtypes = [vp, ctypes.POINTER(RocJpegAmdTimings)]
         L.rocJpegAmdSetPathPolicy.argtypes = [vp, i32]
         L.rocJpegAmdGetStream.argtypes = [vp, ctypes.POINTER(vp)]
+        L.rocJpegAmdStreamParseDevice.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), i32,
+                                                  ctypes.POINTER(vp)]
+        L.rocJpegAmdStreamGetIntervals.argtypes = [vp, ctypes.POINTER(RocJpegAmdInterval), ctypes.c_uint32,
+                                                   ctypes.POINTER(ctypes.c_uint32)]
+        L.rocJpegAmdStreamGetDestuffBlocks.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32,
+                                                       ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
         for name in API_SYMBOLS + EXT_SYMBOLS:
             if name != "rocJpegGetErrorName":
                 getattr(L, name).restype = i32
@@ -178,6 +191,24 @@ class JpegStream:
                "rocJpegAmdStreamGetInfo")
         return {"num_components": nc.value, "subsampling": css.value, "widths": list(w), "heights": list(h),
                 "restart_intervals": nri.value}
+
+    def intervals(self):
+        """The restart-interval table the parse built (rocJpegAmdStreamGetIntervals)."""
+        n = ctypes.c_uint32()
+        _check(lib().rocJpegAmdStreamGetIntervals(self.handle, None, 0, ctypes.byref(n)), "rocJpegAmdStreamGetIntervals")
+        arr = (RocJpegAmdInterval * max(1, n.value))()
+        _check(lib().rocJpegAmdStreamGetIntervals(self.handle, arr, n.value, ctypes.byref(n)), "rocJpegAmdStreamGetIntervals")
+        return [tuple(getattr(arr[i], k) for k, _ in RocJpegAmdInterval._fields_) for i in range(n.value)]
+
+    def destuff_blocks(self):
+        """(ecs_size, [(src_off, len|first<<31, dst_off, zero_end), ...])."""
+        n, e = ctypes.c_uint32(), ctypes.c_uint32()
+        _check(lib().rocJpegAmdStreamGetDestuffBlocks(self.handle, None, 0, ctypes.byref(n), ctypes.byref(e)),
+               "rocJpegAmdStreamGetDestuffBlocks")
+        arr = (ctypes.c_uint32 * (4 * max(1, n.value)))()
+        _check(lib().rocJpegAmdStreamGetDestuffBlocks(self.handle, arr, n.value, ctypes.byref(n), ctypes.byref(e)),
+               "rocJpegAmdStreamGetDestuffBlocks")
+        return e.value, [tuple(arr[4 * i:4 * i + 4]) for i in range(n.value)]
 
     def close(self):
         if self.handle:
@@ -233,6 +264,19 @@ class JpegDecoder:
         hs = (ctypes.c_void_p * n)(*[s.handle for s in streams])
         arr = (RocJpegImage * n)(*images)
         return Status(lib().rocJpegDecodeBatched(self.handle, hs, n, ctypes.byref(params), arr))
+
+    def parse_device(self, datas):
+        """rocJpegAmdStreamParseDevice: parse `datas` (bytes) with the marker scan on this GPU;
+        returns (status, [JpegStream])."""
+        streams = [JpegStream() for _ in datas]
+        for s, d in zip(streams, datas):
+            s._data = bytes(d)
+        n = len(datas)
+        ptrs = (ctypes.c_char_p * n)(*[s._data for s in streams])
+        lens = (ctypes.c_size_t * n)(*[len(s._data) for s in streams])
+        hs = (ctypes.c_void_p * n)(*[s.handle for s in streams])
+        st = Status(lib().rocJpegAmdStreamParseDevice(self.handle, ptrs, lens, n, hs))
+        return st, streams
 
     def streams_to_device(self, streams):
         n = len(streams)

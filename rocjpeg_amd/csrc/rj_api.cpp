@@ -163,6 +163,56 @@ RJ_EXPORT RocJpegStatus rocJpegAmdStreamsToDevice(RocJpegHandle handle, RocJpegS
   });
 }
 
+RJ_EXPORT RocJpegStatus rocJpegAmdStreamParseDevice(RocJpegHandle handle, const unsigned char *const *data,
+                                                    const size_t *lengths, int count, RocJpegStreamHandle *streams) {
+  if (handle == nullptr || data == nullptr || lengths == nullptr || streams == nullptr || count < 0)
+    return ROCJPEG_STATUS_INVALID_PARAMETER;
+  return Guard([&] {
+    std::vector<rj::Stream *> v(static_cast<size_t>(count));
+    for (int i = 0; i < count; i++) {
+      if (streams[i] == nullptr) return int(ROCJPEG_STATUS_INVALID_PARAMETER);
+      v[i] = AsStream(streams[i]);
+    }
+    return AsDecoder(handle)->ParseOnDevice(v.data(), data, lengths, count);
+  });
+}
+
+RJ_EXPORT RocJpegStatus rocJpegAmdStreamGetIntervals(RocJpegStreamHandle s, RocJpegAmdInterval *out, uint32_t capacity,
+                                                     uint32_t *count) {
+  if (s == nullptr || count == nullptr) return ROCJPEG_STATUS_INVALID_PARAMETER;
+  return Guard([&] {
+    rj::Stream *st = AsStream(s);
+    std::lock_guard<std::mutex> lock(st->mutex());
+    const rj::DecodePlan &p = st->plan();
+    *count = uint32_t(p.segs.size());
+    for (uint32_t i = 0; out != nullptr && i < capacity && i < p.segs.size(); i++) {
+      const RjSegDev &g = p.segs[i];
+      out[i] = RocJpegAmdInterval{g.src_off, g.src_len, g.dst_off, g.dst_len, g.mcu_first, g.mcu_count, g.flags,
+                                  g.ent_off, g.chunk0, 0u};
+    }
+    return int(ROCJPEG_STATUS_SUCCESS);
+  });
+}
+
+RJ_EXPORT RocJpegStatus rocJpegAmdStreamGetDestuffBlocks(RocJpegStreamHandle s, uint32_t *out4, uint32_t capacity,
+                                                         uint32_t *count, uint32_t *ecs_size) {
+  if (s == nullptr || count == nullptr) return ROCJPEG_STATUS_INVALID_PARAMETER;
+  return Guard([&] {
+    rj::Stream *st = AsStream(s);
+    std::lock_guard<std::mutex> lock(st->mutex());
+    const rj::DecodePlan &p = st->plan();
+    *count = uint32_t(p.ds.size());
+    if (ecs_size) *ecs_size = st->info().ecs_size;
+    for (uint32_t i = 0; out4 != nullptr && i < capacity && i < p.ds.size(); i++) {
+      out4[4 * i] = p.ds[i].src_off;
+      out4[4 * i + 1] = p.ds[i].len;
+      out4[4 * i + 2] = p.ds[i].dst_off;
+      out4[4 * i + 3] = p.ds[i].zero_end;
+    }
+    return int(ROCJPEG_STATUS_SUCCESS);
+  });
+}
+
 RJ_EXPORT RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable) {
   if (handle == nullptr) return ROCJPEG_STATUS_INVALID_PARAMETER;
   AsDecoder(handle)->SetProfiling(enable != 0);

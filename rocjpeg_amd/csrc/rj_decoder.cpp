@@ -196,6 +196,133 @@ int Decoder::StreamsToDevice(Stream *const *streams, int n) {
   return kOk;
 }
 
+int Decoder::ParseOnDevice(Stream *const *streams, const uint8_t *const *data, const size_t *len, int n) {
+  std::lock_guard<std::mutex> lock(mu_);
+  if (streams == nullptr || data == nullptr || len == nullptr || n < 0) return kInvalidParameter;
+  RJ_HIP(hipSetDevice(device_));
+  // ---- host: headers only (O(header) per stream) ----
+  std::vector<int> pend;
+  for (int i = 0; i < n; i++) {
+    Stream *s = streams[i];
+    if (s == nullptr || data[i] == nullptr) return kInvalidParameter;
+    if (len[i] > 0xFFFFFFFFull) return kBadJpeg;
+    if (!s->Parse(data[i], uint32_t(len[i]), true)) return kBadJpeg;
+    if (s->scan_pending()) pend.push_back(i);
+    else if (!s->plan().progressive) s->Parse(data[i], uint32_t(len[i]));  // not decodable: host parse, same info
+  }
+  timings_.scan_device_streams = timings_.scan_host_fallbacks = 0;
+  if (pend.empty()) return kOk;
+  // ---- layout: one upload (bytes + jobs), one kernel, one read-back (tables + results) ----
+  struct Lay {
+    uint64_t src, segs, ds, rst, oth, drop;
+    uint32_t expected, ds_cap, drop_cap;
+  };
+  std::vector<Lay> lay(pend.size());
+  uint64_t bytes = 0, nsegs = 0, nds = 0, nrst = 0, noth = 0, ndrop = 0;
+  constexpr uint32_t kOthCap = 4096;
+  for (size_t k = 0; k < pend.size(); k++) {
+    const Stream *s = streams[pend[k]];
+    const DecodePlan &p = s->plan();
+    const uint32_t avail = s->info().ecs_size, ri = s->info().restart_interval;
+    const uint32_t total = p.mcux * p.mcuy;
+    Lay &L = lay[k];
+    L.expected = ri ? (total + ri - 1) / ri : 1;
+    L.ds_cap = avail / RJ_DS_BLOCK + L.expected + 1;
+    L.drop_cap = avail / 2 + 64;
+    L.src = bytes;
+    bytes += AlignUp(uint64_t(avail) + 16, 256);
+    L.segs = nsegs;
+    nsegs += L.expected;
+    L.ds = nds;
+    nds += L.ds_cap;
+    L.rst = nrst;
+    nrst += L.expected + 1;
+    L.oth = noth;
+    noth += kOthCap;
+    L.drop = ndrop;
+    ndrop += L.drop_cap;
+  }
+  const uint64_t np = pend.size();
+  const uint64_t off_jobs = AlignUp(bytes, 256);
+  const uint64_t up_bytes = AlignUp(off_jobs + np * sizeof(RjScanJob), 256);
+  const uint64_t off_out = up_bytes;  // read-back region: results, table copies
+  const uint64_t off_segs = AlignUp(off_out + np * sizeof(RjScanOut), 256);
+  const uint64_t off_ds = AlignUp(off_segs + nsegs * sizeof(RjSegDev), 256);
+  const uint64_t down_end = AlignUp(off_ds + nds * sizeof(RjDsBlock), 256);
+  const uint64_t off_rst = down_end;
+  const uint64_t off_oth = AlignUp(off_rst + nrst * 4, 256);
+  const uint64_t off_drop = AlignUp(off_oth + noth * 4, 256);
+  const uint64_t total_bytes = AlignUp(off_drop + ndrop * 4, 256);
+  RJ_CHECK(d_scan_.Ensure(total_bytes));
+  RJ_CHECK(h_scan_.Ensure(down_end));
+  uint8_t *h = h_scan_.data();
+  uint8_t *d = d_scan_.as<uint8_t>();
+  std::vector<Stream::Resident> res(np);
+  RjScanJob *jobs = reinterpret_cast<RjScanJob *>(h + off_jobs);
+  for (size_t k = 0; k < np; k++) {
+    const Stream *s = streams[pend[k]];
+    const DecodePlan &p = s->plan();
+    const Lay &L = lay[k];
+    const uint32_t avail = s->info().ecs_size;
+    std::memcpy(h + L.src, s->info().ecs, avail);
+    std::memset(h + L.src + avail, 0, 16);
+    Stream::Resident &r = res[k];
+    r.device = device_;
+    r.generation = s->generation();
+    RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.ecs), AlignUp(uint64_t(avail) + 32, 16)));
+    RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.segs), std::max<size_t>(L.expected * sizeof(RjSegDev), 16)));
+    RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.ds), std::max<size_t>(L.ds_cap * sizeof(RjDsBlock), 16)));
+    RjScanJob &J = jobs[k];
+    std::memset(&J, 0, sizeof(J));
+    J.src_off = L.src;
+    J.avail = avail;
+    J.ri = s->info().restart_interval;
+    J.total_mcus = p.mcux * p.mcuy;
+    J.nblk_mcu = p.nblk_mcu;
+    J.expected = L.expected;
+    J.rst_cap = L.expected + 1;
+    J.oth_cap = kOthCap;
+    J.drop_cap = L.drop_cap;
+    J.ds_cap = L.ds_cap;
+    J.ecs = r.ecs;
+    J.segs = r.segs;
+    J.segs_copy = reinterpret_cast<RjSegDev *>(d + off_segs) + L.segs;
+    J.ds = r.ds;
+    J.ds_copy = reinterpret_cast<RjDsBlock *>(d + off_ds) + L.ds;
+    J.rst = reinterpret_cast<uint32_t *>(d + off_rst) + L.rst;
+    J.oth = reinterpret_cast<uint32_t *>(d + off_oth) + L.oth;
+    J.drop = reinterpret_cast<uint32_t *>(d + off_drop) + L.drop;
+    J.out = reinterpret_cast<RjScanOut *>(d + off_out) + k;
+  }
+  RJ_HIP(hipMemcpyAsync(d, h, up_bytes, hipMemcpyHostToDevice, stream_));
+  RJ_HIP(hipMemsetAsync(d + off_out, 0, np * sizeof(RjScanOut), stream_));
+  RJ_HIP(LaunchScan(stream_, reinterpret_cast<const RjScanJob *>(d + off_jobs), uint32_t(np), d));
+  RJ_HIP(hipMemcpyAsync(h + off_out, d + off_out, down_end - off_out, hipMemcpyDeviceToHost, stream_));
+  RJ_HIP(hipStreamSynchronize(stream_));
+  // ---- host: adopt the device tables (or scan on the host where a list overflowed) ----
+  for (size_t k = 0; k < np; k++) {
+    Stream *s = streams[pend[k]];
+    const RjScanOut &o = reinterpret_cast<const RjScanOut *>(h + off_out)[k];
+    const Lay &L = lay[k];
+    Stream::Resident &r = res[k];
+    if (o.flags) {
+      (void)hipFree(r.ecs);
+      (void)hipFree(r.segs);
+      (void)hipFree(r.ds);
+      RJ_INFO("marker scan list overflow on stream %d: host scan", pend[k]);
+      s->Parse(data[pend[k]], uint32_t(len[pend[k]]));
+      timings_.scan_host_fallbacks++;
+      continue;
+    }
+    timings_.scan_device_streams++;
+    std::lock_guard<std::mutex> sl(s->mutex());
+    s->CompleteFromDevice(o.ecs_end, reinterpret_cast<const RjSegDev *>(h + off_segs) + L.segs, L.expected,
+                          reinterpret_cast<const RjDsBlock *>(h + off_ds) + L.ds, o.nds);
+    s->resident = r;
+  }
+  return kOk;
+}
+
 int Decoder::Decode(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
   std::lock_guard<std::mutex> lock(mu_);
   if (streams == nullptr || params == nullptr || dst == nullptr || n < 0) return kInvalidParameter;

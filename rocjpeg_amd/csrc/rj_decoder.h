@@ -52,6 +52,9 @@ class Decoder {
   int GetImageInfo(Stream *s, uint8_t *nc, RocJpegChromaSubsampling *css, uint32_t *w, uint32_t *h);
   int Decode(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
   int StreamsToDevice(Stream *const *streams, int n);
+  // rocJpegStreamParse + rocJpegAmdStreamsToDevice for a batch, with the O(bytes) marker scan
+  // (FF D9 end, restart intervals, destuffing tables) on this handle's GPU (rj_scan.hip)
+  int ParseOnDevice(Stream *const *streams, const uint8_t *const *data, const size_t *len, int n);
   void SetProfiling(bool on) { profiling_ = on; }
   void SetPathPolicy(int p) { path_policy_ = p; }
   RocJpegAmdTimings last_timings() const { return timings_; }
@@ -99,7 +102,9 @@ class Decoder {
 
   DeviceBuffer d_desc_, d_stage_, d_destuff_, d_entries_, d_planes_;
   DeviceBuffer d_piece_, d_rec_, d_chunkres_, d_fallback_;  // K1 chunk bookkeeping
-  DeviceBuffer d_coef_, d_nz_, d_prec_;  // progressive: dense coefficients, nonzero masks, refinement records
+  DeviceBuffer d_coef_, d_nz_, d_prec_;
+  DeviceBuffer d_scan_;  // marker scan: uploaded bytes, jobs, scratch lists, read-back tables
+  PinnedBuffer h_scan_;  // progressive: dense coefficients, nonzero masks, refinement records
   uint32_t epoch_ = 0;
   PinnedBuffer h_stage_;
 };

@@ -139,6 +139,24 @@ struct RjDsBlock {
 };
 #define RJ_SEG_MISSING 1u
 
+// GPU marker scan (rj_scan.hip): one job per stream, the post-SOS bytes at arena + src_off
+struct RjScanOut {
+  uint32_t ecs_end, nds, flags, destuff_bytes;  // flags 1: a list overflowed (host scan instead)
+  unsigned long long entries;
+  uint32_t nchunks, pad;
+};
+struct RjScanJob {
+  unsigned long long src_off;
+  uint32_t avail, ri, total_mcus, nblk_mcu;
+  uint32_t expected, rst_cap, oth_cap, drop_cap;
+  uint32_t ds_cap, pad[3];
+  uint8_t *ecs;                     // resident ECS buffer (avail + 32 B)
+  RjSegDev *segs, *segs_copy;       // resident table, and the copy the host plan reads back
+  RjDsBlock *ds, *ds_copy;
+  uint32_t *rst, *oth, *drop;       // scratch position lists
+  RjScanOut *out;
+};
+
 // Canonical Huffman decoder for one table (T.81 Annex C), laid out for the GPU.
 //   lut[0..511]      first level, indexed by the next 9 bits:
 //                      (code_len << 8) | symbol      for codes of <= 9 bits

@@ -59,6 +59,9 @@ hipError_t LaunchProgressiveFold(hipStream_t st, const RjImageDev *imgs, const R
 hipError_t LaunchRowsDense(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
                            uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets, uint8_t *planes);
 
+// GPU marker scan (rj_scan.hip): one wave per stream.
+hipError_t LaunchScan(hipStream_t st, const RjScanJob *jobs, uint32_t njobs, const uint8_t *arena);
+
 #ifdef RJ_EXP_STAMPS
 void DumpRowStamps();
 #endif

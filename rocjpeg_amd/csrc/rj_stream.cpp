@@ -91,13 +91,14 @@ bool BuildHuffman(const uint8_t bits[16], const uint8_t *vals, bool is_dc, RjHuf
   return true;
 }
 
-bool Stream::Parse(const uint8_t *d, uint32_t n) {
+bool Stream::Parse(const uint8_t *d, uint32_t n, bool defer_scan) {
   std::lock_guard<std::mutex> lock(mu_);  // rocjpeg_parser.cpp:44
   ReleaseResident();
   generation_++;
   info_ = StreamInfo();
   plan_ = DecodePlan();
   plan_.status = -3;
+  scan_pending_ = false;
   StreamInfo &s = info_;
   if (d == nullptr || n < 4) return false;
   if (d[0] != 0xFF || d[1] != 0xD8) return false;  // :64-67
@@ -203,6 +204,14 @@ bool Stream::Parse(const uint8_t *d, uint32_t n) {
     pos = next;
   }
   if (!dht || !dqt) return false;  // :111-118
+  if (defer_scan && sos) {
+    // GPU marker scan (Decoder::ParseOnDevice, rj_scan.hip): the device finds the FF D9 end and
+    // builds the interval / K0 tables; here only what the header determines
+    s.ecs = d + pos;
+    s.ecs_size = n - uint32_t(pos);  // bytes available; CompleteFromDevice sets the true end
+    scan_pending_ = BuildPlanHeader();
+    return true;
+  }
   // ParseEOI (:400-416): the entropy-coded segment runs to the first FF D9.
   size_t end = n;
   if (sos) {
@@ -221,6 +230,10 @@ bool Stream::Parse(const uint8_t *d, uint32_t n) {
 }
 
 void Stream::BuildPlan() {
+  if (BuildPlanHeader()) BuildIntervals();
+}
+
+bool Stream::BuildPlanHeader() {
   const StreamInfo &s = info_;
   DecodePlan &p = plan_;
   p.status = 0;
@@ -228,20 +241,20 @@ void Stream::BuildPlan() {
   // plus streams this baseline decoder cannot reconstruct.
   if (!s.sof_seen || s.ncomp == 0 || s.width < 64 || s.height < 64 || s.width > 16384 || s.height > 16384) {
     p.status = -4;  // JPEG_NOT_SUPPORTED
-    return;
+    return false;
   }
   if (!(s.css == kCss444 || s.css == kCss440 || s.css == kCss422 || s.css == kCss420 || s.css == kCss400)) {
     p.status = -4;
-    return;
+    return false;
   }
   if (s.precision != 8 || s.scan_ncomp != s.ncomp) {
     p.status = -4;
-    return;
+    return false;
   }
   const int nc = s.ncomp;
   p.hmax = p.vmax = 1;
   for (int c = 0; c < nc; c++) {
-    if (s.comp[c].h < 1 || s.comp[c].h > 4 || s.comp[c].v < 1 || s.comp[c].v > 4) { p.status = -3; return; }
+    if (s.comp[c].h < 1 || s.comp[c].h > 4 || s.comp[c].v < 1 || s.comp[c].v > 4) { p.status = -3; return false; }
     p.hmax = std::max(p.hmax, s.comp[c].h);
     p.vmax = std::max(p.vmax, s.comp[c].v);
   }
@@ -256,7 +269,7 @@ void Stream::BuildPlan() {
       p.hblk[c] = p.mcuy * s.comp[c].v;
       for (int y = 0; y < s.comp[c].v; y++)
         for (int x = 0; x < s.comp[c].h; x++) {
-          if (b >= RJ_MAX_BLK_MCU) { p.status = -3; return; }
+          if (b >= RJ_MAX_BLK_MCU) { p.status = -3; return false; }
           p.blk_comp[b] = uint8_t(c);
           p.blk_dx[b] = uint8_t(x);
           p.blk_dy[b] = uint8_t(y);
@@ -277,7 +290,7 @@ void Stream::BuildPlan() {
   uint64_t h = 1469598103934665603ull;
   for (int c = 0; c < nc; c++) {
     const int td = s.scomp[c].td, ta = s.scomp[c].ta, tq = s.comp[c].tq;
-    if (td >= 2 || ta >= 2 || !s.ht_loaded[td] || !s.ht_loaded[ta] || !s.qt_loaded[tq]) { p.status = -3; return; }
+    if (td >= 2 || ta >= 2 || !s.ht_loaded[td] || !s.ht_loaded[ta] || !s.qt_loaded[tq]) { p.status = -3; return false; }
   }
   for (int t = 0; t < 2; t++) {
     if (!s.ht_loaded[t]) continue;
@@ -285,7 +298,7 @@ void Stream::BuildPlan() {
         !BuildHuffman(s.ht[t].ac_bits, s.ht[t].ac_vals, false, &p.tables.ac[t])) {
       // only fatal when the scan actually uses this table
       for (int c = 0; c < nc; c++)
-        if (s.scomp[c].td == t || s.scomp[c].ta == t) { p.status = -3; return; }
+        if (s.scomp[c].td == t || s.scomp[c].ta == t) { p.status = -3; return false; }
     }
   }
   for (int q = 0; q < 4; q++)
@@ -301,7 +314,13 @@ void Stream::BuildPlan() {
   }
   h = Fnv1a(h, p.table_key, sizeof(p.table_key));
   p.table_hash = h;
+  return true;
+}
 
+// Restart-interval table (host marker scan; rj_scan.hip is the device version).
+void Stream::BuildIntervals() {
+  const StreamInfo &s = info_;
+  DecodePlan &p = plan_;
   // Restart-interval table: split the ECS at RSTn markers (FF D0..D7).  Fill FFs in front
   // of a marker are excluded; FF 00 stays (the destuff kernel removes the 00).
   const uint32_t total_mcus = p.mcux * p.mcuy;
@@ -392,6 +411,25 @@ void Stream::BuildPlan() {
   }
   p.destuff_bytes = dst;
   p.entries = ent;
+}
+
+void Stream::CompleteFromDevice(uint32_t ecs_size, const RjSegDev *segs, uint32_t nsegs, const RjDsBlock *ds,
+                                uint32_t nds) {
+  DecodePlan &p = plan_;
+  info_.ecs_size = ecs_size;
+  p.segs.assign(segs, segs + nsegs);
+  p.ds.assign(ds, ds + nds);
+  uint64_t dst = 0, ent = 0;
+  uint32_t nch = 0;
+  for (const RjSegDev &sg : p.segs) {  // the totals BuildIntervals accumulates
+    dst += (sg.flags & RJ_SEG_MISSING) ? 16u : ((uint64_t(sg.src_len) + 16 + 15) & ~uint64_t(15));
+    ent += rj_interval_entries(sg.src_len, uint64_t(sg.mcu_count) * p.nblk_mcu, p.nblk_mcu);
+    nch += rj_chunks(sg.src_len);
+  }
+  p.destuff_bytes = dst;
+  p.entries = ent;
+  p.nchunks = nch;
+  scan_pending_ = false;
 }
 
 void Stream::ReleaseResident() {

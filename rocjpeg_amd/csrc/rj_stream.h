@@ -77,7 +77,11 @@ struct DecodePlan {
 class Stream {
  public:
   // RocJpegStreamParser::ParseJpegStream semantics; true = parsed (else BAD_JPEG).
-  bool Parse(const uint8_t *data, uint32_t size);
+  bool Parse(const uint8_t *data, uint32_t size, bool defer_scan = false);
+  // defer_scan: header only; the O(bytes) marker scan runs on the GPU (Decoder::ParseOnDevice),
+  // which then hands the interval tables back through CompleteFromDevice
+  bool scan_pending() const { return scan_pending_; }
+  void CompleteFromDevice(uint32_t ecs_size, const RjSegDev *segs, uint32_t nsegs, const RjDsBlock *ds, uint32_t nds);
   const StreamInfo &info() const { return info_; }
   const DecodePlan &plan() const { return plan_; }
   uint64_t generation() const { return generation_; }
@@ -99,6 +103,9 @@ class Stream {
 
  private:
   void BuildPlan();
+  bool BuildPlanHeader();   // geometry, tables, status; false: not decodable
+  void BuildIntervals();    // host marker scan: restart intervals, K0 blocks
+  bool scan_pending_ = false;
   bool ParseProgressive(const uint8_t *data, uint32_t size);  // SOF2 (beyond the reference)
   void BuildProgressivePlan(const uint8_t *data);
   StreamInfo info_;
