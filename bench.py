@@ -270,6 +270,19 @@ def main():
     host_rate = host_steps * n / (time.perf_counter() - t_h) if st == 0 else None
     del host_streams
 
+    # parse rates (outside the timed region): host parser (rocJpegStreamParse, one thread) and
+    # the GPU marker scan (rocJpegAmdStreamParseDevice: headers on the host, O(bytes) on the GPU,
+    # streams left resident -- includes their HBM allocations)
+    t_p = time.perf_counter()
+    tmp = [R.JpegStream(b) for b in data]
+    parse_host_rate = n / (time.perf_counter() - t_p)
+    del tmp
+    dec.parse_device(data[:8])  # warm-up (first launch, buffers)
+    t_p = time.perf_counter()
+    pst, tmp = dec.parse_device(data)
+    parse_dev_rate = n / (time.perf_counter() - t_p) if pst == 0 else None
+    del tmp
+
     # parity spot-check of this run's output (first images vs the CPU oracle), outside timing
     from tests import oracle_lib as O
     parity_ok = True
@@ -334,6 +347,8 @@ def main():
                                    serial_fallbacks=last["serial_fallbacks"]),
             "end_to_end_algorithmic_GBps": round((ecs + outb) / (elapsed / K) / 1e9, 2),
             "host_input_images_per_s_per_gpu": round(host_rate, 1) if host_rate else None,
+            "parse_images_per_s": {"host_1_thread": round(parse_host_rate, 1),
+                                   "gpu_marker_scan": round(parse_dev_rate, 1) if parse_dev_rate else None},
             "parity_first_image": parity_ok,
             "dataset_gen_s": round(t_gen, 1),
         }

@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "rj_common.h"
 #include "rj_kernels.h"
@@ -200,6 +201,7 @@ int Decoder::ParseOnDevice(Stream *const *streams, const uint8_t *const *data, c
   std::lock_guard<std::mutex> lock(mu_);
   if (streams == nullptr || data == nullptr || len == nullptr || n < 0) return kInvalidParameter;
   RJ_HIP(hipSetDevice(device_));
+  const auto t0 = std::chrono::steady_clock::now();
   // ---- host: headers only (O(header) per stream) ----
   std::vector<int> pend;
   for (int i = 0; i < n; i++) {
@@ -258,20 +260,53 @@ int Decoder::ParseOnDevice(Stream *const *streams, const uint8_t *const *data, c
   uint8_t *h = h_scan_.data();
   uint8_t *d = d_scan_.as<uint8_t>();
   std::vector<Stream::Resident> res(np);
+  // one HBM block for every stream's resident buffers (ECS + 32 B, interval table, K0 table),
+  // shared by the streams and freed with the last of them (no per-stream hipMalloc)
+  uint64_t rbytes = 0;
+  std::vector<uint64_t> roff(np);
+  for (size_t k = 0; k < np; k++) {
+    roff[k] = rbytes;
+    rbytes += AlignUp(uint64_t(streams[pend[k]]->info().ecs_size) + 32, 256) +
+              AlignUp(lay[k].expected * sizeof(RjSegDev), 256) + AlignUp(lay[k].ds_cap * sizeof(RjDsBlock), 256);
+  }
+  uint8_t *rblock = nullptr;
+  RJ_HIP(hipMalloc(reinterpret_cast<void **>(&rblock), std::max<uint64_t>(rbytes, 256)));
+  const int dev = device_;
+  std::shared_ptr<uint8_t> block(rblock, [dev](uint8_t *p) {
+    int cur = 0;
+    if (hipGetDevice(&cur) == hipSuccess) {
+      (void)hipSetDevice(dev);
+      (void)hipFree(p);
+      (void)hipSetDevice(cur);
+    }
+  });
   RjScanJob *jobs = reinterpret_cast<RjScanJob *>(h + off_jobs);
+  {  // the bytes into the pinned staging blob: a plain copy, split over a few host threads
+    auto copy = [&](size_t k0, size_t k1) {
+      for (size_t k = k0; k < k1; k++) {
+        const Stream *s = streams[pend[k]];
+        std::memcpy(h + lay[k].src, s->info().ecs, s->info().ecs_size);
+        std::memset(h + lay[k].src + s->info().ecs_size, 0, 16);
+      }
+    };
+    const size_t nt = bytes > (32u << 20) ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency())) : 1;
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; t++) th.emplace_back(copy, np * t / nt, np * (t + 1) / nt);
+    copy(0, np / nt);
+    for (auto &x : th) x.join();
+  }
   for (size_t k = 0; k < np; k++) {
     const Stream *s = streams[pend[k]];
     const DecodePlan &p = s->plan();
     const Lay &L = lay[k];
     const uint32_t avail = s->info().ecs_size;
-    std::memcpy(h + L.src, s->info().ecs, avail);
-    std::memset(h + L.src + avail, 0, 16);
     Stream::Resident &r = res[k];
     r.device = device_;
     r.generation = s->generation();
-    RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.ecs), AlignUp(uint64_t(avail) + 32, 16)));
-    RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.segs), std::max<size_t>(L.expected * sizeof(RjSegDev), 16)));
-    RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.ds), std::max<size_t>(L.ds_cap * sizeof(RjDsBlock), 16)));
+    r.block = block;
+    r.ecs = rblock + roff[k];
+    r.segs = reinterpret_cast<RjSegDev *>(r.ecs + AlignUp(uint64_t(avail) + 32, 256));
+    r.ds = reinterpret_cast<RjDsBlock *>(reinterpret_cast<uint8_t *>(r.segs) + AlignUp(L.expected * sizeof(RjSegDev), 256));
     RjScanJob &J = jobs[k];
     std::memset(&J, 0, sizeof(J));
     J.src_off = L.src;
@@ -294,11 +329,17 @@ int Decoder::ParseOnDevice(Stream *const *streams, const uint8_t *const *data, c
     J.drop = reinterpret_cast<uint32_t *>(d + off_drop) + L.drop;
     J.out = reinterpret_cast<RjScanOut *>(d + off_out) + k;
   }
+  const auto t1 = std::chrono::steady_clock::now();
   RJ_HIP(hipMemcpyAsync(d, h, up_bytes, hipMemcpyHostToDevice, stream_));
   RJ_HIP(hipMemsetAsync(d + off_out, 0, np * sizeof(RjScanOut), stream_));
   RJ_HIP(LaunchScan(stream_, reinterpret_cast<const RjScanJob *>(d + off_jobs), uint32_t(np), d));
   RJ_HIP(hipMemcpyAsync(h + off_out, d + off_out, down_end - off_out, hipMemcpyDeviceToHost, stream_));
   RJ_HIP(hipStreamSynchronize(stream_));
+  const auto t2 = std::chrono::steady_clock::now();
+  if (getenv("RJ_DEBUG_SCAN"))
+    fprintf(stderr, "[rj scan] %zu streams: host headers+staging+alloc %.3f ms, upload+kernel+readback %.3f ms\n",
+            size_t(np), std::chrono::duration<double, std::milli>(t1 - t0).count(),
+            std::chrono::duration<double, std::milli>(t2 - t1).count());
   // ---- host: adopt the device tables (or scan on the host where a list overflowed) ----
   for (size_t k = 0; k < np; k++) {
     Stream *s = streams[pend[k]];
@@ -306,9 +347,7 @@ int Decoder::ParseOnDevice(Stream *const *streams, const uint8_t *const *data, c
     const Lay &L = lay[k];
     Stream::Resident &r = res[k];
     if (o.flags) {
-      (void)hipFree(r.ecs);
-      (void)hipFree(r.segs);
-      (void)hipFree(r.ds);
+      r = Stream::Resident();  // this stream keeps no share of the block
       RJ_INFO("marker scan list overflow on stream %d: host scan", pend[k]);
       s->Parse(data[pend[k]], uint32_t(len[pend[k]]));
       timings_.scan_host_fallbacks++;

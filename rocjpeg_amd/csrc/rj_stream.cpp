@@ -433,6 +433,10 @@ void Stream::CompleteFromDevice(uint32_t ecs_size, const RjSegDev *segs, uint32_
 }
 
 void Stream::ReleaseResident() {
+  if (resident.device >= 0 && resident.block) {
+    resident = Resident();  // drops this stream's share of the call's block
+    return;
+  }
   if (resident.device >= 0) {
     int cur = 0;
     if (hipGetDevice(&cur) == hipSuccess) {

@@ -9,6 +9,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -97,6 +98,9 @@ class Stream {
     RjProgScanDev *pscans = nullptr;  // progressive only
     RjProgIvalDev *pivals = nullptr;
     RjHuffDev *ptabs = nullptr;
+    // set: the buffers above are carved from a block shared by the streams of one
+    // rocJpegAmdStreamParseDevice call; the block is freed with its last stream
+    std::shared_ptr<uint8_t> block;
   } resident;
   void ReleaseResident();
   ~Stream() { ReleaseResident(); }
