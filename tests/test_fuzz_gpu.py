@@ -1,0 +1,118 @@
+"""Robustness of the GPU path on corrupt input: random byte damage inside the entropy-coded data
+of baseline and progressive streams, decoded in batches.  Every call must return (no fault, no
+hang) and be deterministic; baseline streams must still match the oracle byte for byte (its
+corrupt-data semantics are libjpeg's: bad codes read as 17 bits / symbol 0, zeros past the data),
+progressive ones are checked for determinism and status only -- corrupt codes that place a
+coefficient outside the scan's band are outside the progressive exactness domain."""
+import numpy as np
+import pytest
+
+import rocjpeg_amd as R
+from tests import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+FIX = O.manifest()
+
+
+def _is_prog(d):
+    pos = 2
+    while pos + 4 <= len(d):
+        while d[pos] == 0xFF:
+            pos += 1
+        if d[pos] == 0xC2:
+            return True
+        if d[pos] in (0xC0, 0xC1, 0xDA):
+            return False
+        pos += 1 + ((d[pos + 1] << 8) | d[pos + 2])
+    return False
+
+
+def _first_sos_end(d):
+    i = d.index(b"\xff\xda")
+    return i + 2 + int.from_bytes(d[i + 2:i + 4], "big")
+
+
+def scan_ranges(d):
+    """[start, end) of every scan's entropy-coded data (up to the next marker other than RSTn)."""
+    out, i = [], 0
+    while True:
+        i = d.find(b"\xff\xda", i)
+        if i < 0:
+            return out
+        s = i + 2 + int.from_bytes(d[i + 2:i + 4], "big")
+        e = s
+        while e + 1 < len(d) and not (d[e] == 0xFF and d[e + 1] not in (0x00, 0xFF) and not 0xD0 <= d[e + 1] <= 0xD7):
+            e += 1
+        out.append((s, e))
+        i = e
+
+
+def damage(d, seed, nhits=12):
+    """Flip bits / overwrite bytes inside the scans' entropy-coded data, never creating FF (no new
+    markers) and never touching FF or the byte after one (marker structure and headers intact)."""
+    rng = np.random.default_rng(seed)
+    buf = bytearray(d)
+    ranges = [(a, b) for a, b in scan_ranges(d) if b - a > 24]
+    pos_all = []
+    for _ in range(nhits):
+        a, b = ranges[int(rng.integers(0, len(ranges)))]
+        pos_all.append(int(rng.integers(a + 4, b - 4)))
+    for pos in pos_all:
+        if buf[pos] == 0xFF or buf[pos - 1] == 0xFF or buf[pos + 1] == 0x00:
+            continue
+        v = buf[pos] ^ (1 << int(rng.integers(0, 8))) if rng.random() < 0.7 else int(rng.integers(0, 255))
+        if v != 0xFF:
+            buf[pos] = v
+    return bytes(buf)
+
+
+BASE = [f for f in FIX if "libjpeg_coef_sha256" in f and f["ref_parse"]["ok"] and f["ref_parse"]["css"] in (0, 1, 2, 3, 5)
+        and f["bytes"] < 100_000]
+PROG = [f for f in FIX if "libjpeg_coef_sha256" in f and _is_prog(O.fixture_bytes(f)) and f["bytes"] < 100_000]
+
+
+def _decode_batch(dec, datas):
+    from tests import gpu_util as G
+    streams, bufs_all, imgs, shapes_all = [], [], [], []
+    for d in datas:
+        s = R.JpegStream(d)
+        nc, css, w, h = dec.image_info(s)
+        shapes = G.channel_shapes(R.OutputFormat.RGB, css, w, h)
+        bufs, img = G.gpu_buffers(shapes)
+        streams.append(s)
+        bufs_all.append(bufs)
+        imgs.append(img)
+        shapes_all.append(shapes)
+    st = dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs)
+    return st, [G.to_host(b)[0] for b in bufs_all], shapes_all
+
+
+@pytest.fixture(scope="module")
+def dec():
+    from tests import gpu_util as G
+    G.torch()
+    d = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    yield d
+    d.close()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_fuzz_baseline_matches_oracle(dec, seed):
+    datas = [damage(O.fixture_bytes(e), seed * 100 + k) for k, e in enumerate(BASE)]
+    st, outs, shapes = _decode_batch(dec, datas)
+    assert st == 0
+    for d, o, shp in zip(datas, outs, shapes):
+        ost, want = O.oracle_decode(d, int(R.OutputFormat.RGB), shp)
+        assert ost == 0
+        assert np.array_equal(o, want[0])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_progressive_runs_and_is_deterministic(dec, seed):
+    datas = [damage(O.fixture_bytes(e), seed * 100 + k, nhits=30) for k, e in enumerate(PROG)]
+    st1, outs1, _ = _decode_batch(dec, datas)
+    st2, outs2, _ = _decode_batch(dec, datas)
+    assert st1 == st2 == 0
+    for a, b in zip(outs1, outs2):
+        assert np.array_equal(a, b)
