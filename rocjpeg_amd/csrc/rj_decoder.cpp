@@ -107,6 +107,8 @@ Decoder::~Decoder() {
       if (e) (void)hipEventDestroy(e);
     for (auto &e : prog_ev_)
       if (e) (void)hipEventDestroy(e);
+    for (auto &e : prog_join_)
+      if (e) (void)hipEventDestroy(e);
     for (auto &e : prog_lev_ev_) (void)hipEventDestroy(e);
     for (auto *arr : {k1s_, k2s_, k2e_})
       for (int q = 0; q < kMaxPipe; q++)
@@ -146,6 +148,8 @@ int Decoder::Initialize() {
   for (auto &e : pk1_) RJ_HIP(hipEventCreate(&e));
   for (auto &e : kev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : prog_ev_) RJ_HIP(hipEventCreate(&e));
+  for (auto &e : prog_join_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (const char *pp = getenv("RJ_PROG_PIPE")) prog_pipe_enabled_ = atoi(pp) != 0;
   for (auto *arr : {k1s_, k2s_, k2e_})
     for (int q = 0; q < kMaxPipe; q++) RJ_HIP(hipEventCreate(&arr[q]));
   (void)backend_;  // HARDWARE and HYBRID both run the HIP decoder
@@ -650,6 +654,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   std::vector<uint32_t> &prog_lanes = sc_.prog_lanes;
   prog_lanes.clear();
   uint32_t prog_level_off[257] = {}, fold_off[257] = {}, fold_chunks[257] = {}, acref_off[257] = {};
+  bool prog_pipe = false;
   std::vector<RjFoldJob> &fold_jobs = sc_.fold_jobs;
   const uint32_t nlev = std::min<uint32_t>(prog_levels, 256);
   if (prog_images) {
@@ -692,6 +697,13 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       }
     }
     prog_level_off[nlev] = uint32_t(prog_lanes.size());
+    // pipelined refinement: every AC refinement interval in one k_prog_acref grid, a scan following
+    // its producer scans block by block (progress counters) -- possible when every refinement
+    // scan has at most 3 producers (rj_prog_stream.cpp); otherwise level by level
+    prog_pipe = prog_pipe_enabled_;
+    for (int i = 0; i < n && prog_pipe; i++)
+      for (const RjProgScanDev &sc : streams[i]->plan().pscans)
+        if (sc.kind == RJ_PK_AC_REFINE && sc.nprod == 0xFF) prog_pipe = false;
     // AC refinement intervals (k_prog_acref, one wave each), per level, after the lane lists
     for (uint32_t L = 0; L < nlev; L++) {
       acref_off[L] = uint32_t(prog_lanes.size());
@@ -701,7 +713,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         for (uint32_t q = 0; q < p.pivals.size(); q++) {
           const RjProgIvalDev &iv = p.pivals[q];
           const RjProgScanDev &sc = p.pscans[iv.scan];
-          if (sc.level == L && sc.kind == RJ_PK_AC_REFINE && !(iv.flags & RJ_SEG_MISSING))
+          // pipelined: missing intervals too (their wave only publishes "done" for consumers)
+          if (sc.level == L && sc.kind == RJ_PK_AC_REFINE && (prog_pipe || !(iv.flags & RJ_SEG_MISSING)))
             prog_lanes.push_back(imgs[i].pival_prefix + q);
         }
       }
@@ -710,7 +723,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     // k_prog_fold jobs of every level >= 1: (image, component) pairs some refinement scan of
     // that level covers, every block of the component's dense raster
     fold_jobs.clear();
-    for (uint32_t L = 1; L < nlev; L++) {
+    // pipelined: one fold over every level after the refinement grid (slot 0)
+    for (uint32_t L = prog_pipe ? 0u : 1u; L < (prog_pipe ? 1u : nlev); L++) {
       fold_off[L] = uint32_t(fold_jobs.size());
       uint32_t chunks = 0;
       for (int i = 0; i < n; i++) {
@@ -719,7 +733,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         for (uint32_t c = 0; c < streams[i]->info().ncomp; c++) {
           bool hit = false;
           for (const RjProgScanDev &sc : p.pscans) {
-            if (sc.level != L) continue;
+            if (!prog_pipe && sc.level != L) continue;
             if (sc.kind == RJ_PK_AC_REFINE && sc.comp[0] == c) hit = true;
             if (sc.kind == RJ_PK_DC_REFINE)
               for (uint32_t q = 0; q < sc.ns; q++) hit = hit || sc.comp[q] == c;
@@ -736,7 +750,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       }
       fold_chunks[L] = chunks;
     }
-    fold_off[nlev] = uint32_t(fold_jobs.size());
+    fold_off[prog_pipe ? 1u : nlev] = uint32_t(fold_jobs.size());
   }
 
   const auto t_lanes = std::chrono::steady_clock::now();
@@ -825,6 +839,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_CHECK(d_coef_.Ensure(coef_dw_total * 4));
     RJ_CHECK(d_nz_.Ensure(nz_total * 8));
     RJ_CHECK(d_prec_.Ensure(std::max<uint64_t>(prec_total * 8, 256)));
+    RJ_CHECK(d_pprog_.Ensure(std::max<uint64_t>(uint64_t(pival_total + 1) * 4, 256)));  // + error flag
   }
   RjCoefBuf cbuf;
   cbuf.ent = d_entries_.as<uint32_t>();
@@ -919,13 +934,43 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       }
     }
     if (dbg_lev) RJ_HIP(hipEventRecord(prog_lev_ev_[0], stream_));
-    for (uint32_t L = 0; L < nlev; L++) {
+    if (prog_pipe) {
+      // level 0 lanes (first scans); then, side by side: the DC-refinement lanes of the later
+      // levels on a second stream, and every AC refinement interval in one grid (level order,
+      // consumers following producers); one fold over all levels once both are done
+      RJ_HIP(hipMemsetAsync(d_pprog_.as<uint32_t>(), 0, uint64_t(pival_total + 1) * 4, stream_));
+      RJ_HIP(LaunchProgressive(stream_, d_imgs, n, d_plane + prog_level_off[0], prog_level_off[1] - prog_level_off[0],
+                               d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
+                               d_prec_.as<unsigned long long>()));
+      if (dbg_lev) RJ_HIP(hipEventRecord(prog_lev_ev_[1], stream_));
+      const bool side = prog_level_off[nlev] > prog_level_off[std::min<uint32_t>(1, nlev)];
+      if (side) {
+        RJ_HIP(hipEventRecord(prog_join_[0], stream_));
+        RJ_HIP(hipStreamWaitEvent(pstream_[0], prog_join_[0], 0));
+        for (uint32_t L = 1; L < nlev; L++)
+          RJ_HIP(LaunchProgressive(pstream_[0], d_imgs, n, d_plane + prog_level_off[L],
+                                   prog_level_off[L + 1] - prog_level_off[L], d_destuff_.as<uint8_t>(),
+                                   d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
+                                   d_prec_.as<unsigned long long>()));
+        RJ_HIP(hipEventRecord(prog_join_[1], pstream_[0]));
+      }
+      RJ_HIP(LaunchProgressiveAcRefine(stream_, d_imgs, n, d_plane + acref_off[0], acref_off[nlev] - acref_off[0],
+                                       d_destuff_.as<uint8_t>(), d_nz_.as<unsigned long long>(),
+                                       d_prec_.as<unsigned long long>(), d_pprog_.as<uint32_t>(), pival_total));
+      if (side) RJ_HIP(hipStreamWaitEvent(stream_, prog_join_[1], 0));
+      RJ_HIP(LaunchProgressiveFold(stream_, d_imgs, d_fold + fold_off[0], fold_off[1] - fold_off[0], fold_chunks[0],
+                                   RJ_FOLD_ALL, d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
+                                   d_prec_.as<unsigned long long>()));
+      if (dbg_lev)
+        for (uint32_t L = 2; L <= nlev; L++) RJ_HIP(hipEventRecord(prog_lev_ev_[L], stream_));
+    }
+    for (uint32_t L = 0; L < nlev && !prog_pipe; L++) {
       RJ_HIP(LaunchProgressive(stream_, d_imgs, n, d_plane + prog_level_off[L], prog_level_off[L + 1] - prog_level_off[L],
                                d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
                                d_prec_.as<unsigned long long>()));
       RJ_HIP(LaunchProgressiveAcRefine(stream_, d_imgs, n, d_plane + acref_off[L], acref_off[L + 1] - acref_off[L],
                                        d_destuff_.as<uint8_t>(), d_nz_.as<unsigned long long>(),
-                                       d_prec_.as<unsigned long long>()));
+                                       d_prec_.as<unsigned long long>(), nullptr, 0u));
       if (L >= 1)
         RJ_HIP(LaunchProgressiveFold(stream_, d_imgs, d_fold + fold_off[L], fold_off[L + 1] - fold_off[L], fold_chunks[L],
                                      L, d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
@@ -1113,6 +1158,14 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   RJ_HIP(LaunchOutputJobs(stream_, d_imgs, d_jobs, int(jobs.size()), rows_total, d_planes_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[5], stream_));
   RJ_HIP(hipStreamSynchronize(stream_));
+  if (prog_images && prog_pipe) {  // a refinement wave that gave up waiting (never expected)
+    uint32_t err = 0;
+    RJ_HIP(hipMemcpy(&err, d_pprog_.as<uint32_t>() + pival_total, 4, hipMemcpyDeviceToHost));
+    if (err) {
+      RJ_ERR("progressive refinement: a producer did not report progress");
+      return kExecutionFailed;
+    }
+  }
 #ifdef RJ_EXP_STAMPS
   if (getenv("RJ_DEBUG_STAMPS")) DumpRowStamps();
 #endif

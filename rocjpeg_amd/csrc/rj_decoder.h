@@ -99,10 +99,12 @@ class Decoder {
   } sc_;
   hipEvent_t prog_ev_[3] = {};  // profiling: K1p start, K1p end (dense K2 start), dense K2 end
   std::vector<hipEvent_t> prog_lev_ev_;  // development (RJ_DEBUG_PROG): per-level K1p spans
+  hipEvent_t prog_join_[2] = {};         // pipelined refinement: side stream fork / join
+  bool prog_pipe_enabled_ = true;        // env RJ_PROG_PIPE=0: level-by-level refinement
 
   DeviceBuffer d_desc_, d_stage_, d_destuff_, d_entries_, d_planes_;
   DeviceBuffer d_piece_, d_rec_, d_chunkres_, d_fallback_;  // K1 chunk bookkeeping
-  DeviceBuffer d_coef_, d_nz_, d_prec_;
+  DeviceBuffer d_coef_, d_nz_, d_prec_, d_pprog_;
   DeviceBuffer d_scan_;  // marker scan: uploaded bytes, jobs, scratch lists, read-back tables
   PinnedBuffer h_scan_;  // progressive: dense coefficients, nonzero masks, refinement records
   uint32_t epoch_ = 0;

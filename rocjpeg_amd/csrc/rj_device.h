@@ -228,7 +228,13 @@ struct RjProgScanDev {
   uint32_t ri;               // units per restart interval (0: one interval)
   uint32_t ival0;            // index of the scan's first interval in the image's interval list
   uint32_t nblk;             // blocks per unit
+  // AC refinement: the earlier AC refinement scans of this component whose band overlaps this
+  // one (their new coefficients change this scan's nonzero masks); 0xFF: more than 3 (the call
+  // then runs level by level instead of pipelined)
+  uint8_t nprod, prod[3];
 };
+#define RJ_PROG_DONE 0xFFFFFFFFu  // interval progress: finished
+#define RJ_FOLD_ALL 0xFFFFFFFFu   // k_prog_fold level: every level (after a pipelined launch)
 // AC refinement record of one unit (block): 32 B, written once by the decoding lane
 struct RjRefineRec {
   unsigned long long orm;    // positions whose magnitude gains bit Al (correction 1 or new)

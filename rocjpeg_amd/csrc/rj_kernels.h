@@ -48,8 +48,8 @@ hipError_t LaunchProgressive(hipStream_t st, const RjImageDev *imgs, int nimg, c
                              unsigned long long *recs);
 // K1p AC refinement, one wave per interval (n intervals listed in ivals, batch-global indices).
 hipError_t LaunchProgressiveAcRefine(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *ivals, uint32_t n,
-                                     const uint8_t *destuffed, const unsigned long long *nz,
-                                     unsigned long long *recs);
+                                     const uint8_t *destuffed, unsigned long long *nz,
+                                     unsigned long long *recs, uint32_t *progress, uint32_t progress_n);
 // k_prog_fold: level `level`'s refinement records into the dense coefficients / nonzero masks.
 hipError_t LaunchProgressiveFold(hipStream_t st, const RjImageDev *imgs, const RjFoldJob *jobs, uint32_t njobs,
                                  uint32_t nchunks, uint32_t level, uint32_t *coef, unsigned long long *nz,

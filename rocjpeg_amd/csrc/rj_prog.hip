@@ -635,8 +635,9 @@ __device__ __forceinline__ uint32_t rfl(uint32_t v) { return uint32_t(__builtin_
 
 __global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict__ imgs, int nimg,
                                                    const uint32_t *__restrict__ ivals, const uint8_t *__restrict__ destuffed,
-                                                   const unsigned long long *__restrict__ nz,
-                                                   unsigned long long *__restrict__ recs) {
+                                                   unsigned long long *__restrict__ nz,
+                                                   unsigned long long *__restrict__ recs,
+                                                   uint32_t *__restrict__ progress, uint32_t progress_n) {
   __shared__ uint16_t s_lut[RJ_LUT_ENTRIES];
   __shared__ uint32_t s_maxc[18];
   __shared__ int32_t s_voff[18];
@@ -646,7 +647,18 @@ __global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict_
   const int i = int(rfl(uint32_t(upper_index(nimg, gi, [&](int q) { return imgs[q].pival_prefix; }))));
   const RjImageDev &im = imgs[i];
   const RjProgIvalDev iv = *gp(im.pivals + (gi - im.pival_prefix));
-  if (iv.flags & RJ_SEG_MISSING) return;
+  // pipelined launch (progress != null): every refinement interval of the call in one grid, in
+  // level order; an interval publishes how many of its units have their records and nonzero
+  // masks out, and a later scan's interval waits for its producers' units before it reads masks
+  auto publish = [&](uint32_t units_out) {
+    if (progress == nullptr) return;
+    __threadfence();  // records and mask updates before the count (release)
+    if (threadIdx.x == 0) __hip_atomic_store(progress + gi, units_out, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  if (iv.flags & RJ_SEG_MISSING) {
+    publish(RJ_PROG_DONE);
+    return;
+  }
   const RjProgScanDev sc = *gp(im.pscans + iv.scan);
   const RjHuffDev *gt = im.ptabs + sc.tab[0];
   {
@@ -666,8 +678,32 @@ __global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict_
   const uint32_t nbits = dst_len * 8u, nwords = (dst_len + 3) / 4;
   const uint32_t *data = reinterpret_cast<const uint32_t *>(destuffed + im.destuff_off + iv.dst_off);
   const uint32_t c0 = sc.comp[0] & 3u;
-  const unsigned long long *nzs =
+  unsigned long long *nzs =
       nz + im.nz_off + (c0 == 0 ? im.nzblk0[0] : (c0 == 1 ? im.nzblk0[1] : im.nzblk0[2])) + iv.unit0;
+  const uint32_t nprod = progress ? min(uint32_t(sc.nprod), 3u) : 0u;
+  uint32_t *progress_err = progress ? progress + progress_n : nullptr;
+  auto wait_producers = [&](uint32_t ub) {  // producers' masks of units [ub, ub + 64) are out
+    const uint32_t lo = iv.unit0 + ub, hi = iv.unit0 + min(ub + 64, nunits);
+    for (uint32_t q = 0; q < nprod; q++) {
+      const RjProgScanDev ps = *gp(im.pscans + sc.prod[q]);
+      const uint32_t pri = ps.ri;
+      const uint32_t j0 = pri ? lo / pri : 0u, j1 = pri ? (hi - 1) / pri : 0u;
+      for (uint32_t j = j0; j <= j1; j++) {
+        const uint32_t s0 = pri ? j * pri : 0u;
+        const uint32_t need = hi - s0;  // units of producer interval j (capped by its DONE)
+        uint32_t *pp = progress + im.pival_prefix + ps.ival0 + j;
+        // bounded (~4 s): a producer that never reports would otherwise hang the GPU; the host
+        // turns the flag into EXECUTION_FAILED
+        for (uint32_t spin = 0; __hip_atomic_load(pp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need; spin++) {
+          if (spin >= (1u << 23)) {
+            if (threadIdx.x == 0) __hip_atomic_store(progress_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(8);
+        }
+      }
+    }
+  };
   unsigned long long *rec = recs + im.prec_off + iv.rec_off;
   auto ldword = [&](uint32_t w) -> uint32_t {  // word w of the interval, zero past the data
     const uint32_t v = *gp(data + min(w, nwords ? nwords - 1 : 0u));
@@ -679,6 +715,7 @@ __global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict_
   uint32_t wbase = 0;
   uint32_t win0 = ldword(lane), win1 = ldword(64 + lane);
   uint32_t nbase = 0;
+  if (nunits) wait_producers(0);
   uint64_t nzw = ldnz(lane);
   uint64_t r_cs = 0, r_sg = 0, r_nw = 0;  // lane b: record of unit rbase + b
   uint32_t rbase = 0;
@@ -797,26 +834,33 @@ __global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict_
           uint4 *r4 = reinterpret_cast<uint4 *>(rec + uint64_t(rbase + lane) * 4u);
           *gp(r4) = make_uint4(uint32_t(r_cs), uint32_t(r_cs >> 32), uint32_t(r_sg), uint32_t(r_sg >> 32));
           *gp(r4 + 1) = make_uint4(uint32_t(r_nw), uint32_t(r_nw >> 32), 0u, 0u);
+          // the new nonzero positions go to the masks now (other scans of this level may share
+          // the word: atomic); k_prog_fold peels them again where it needs the earlier state
+          if (r_nw) gor64(nzs + rbase + lane, r_nw);
         }
+        publish(done ? RJ_PROG_DONE : u);
         r_cs = r_sg = r_nw = 0;
         rbase += 64;
       }
       if (done) break;
       if (u - nbase >= 64) {
         nbase += 64;
+        wait_producers(nbase);
         nzw = ldnz(nbase + lane);
       }
       const uint32_t nl = u - nbase;
       nzm = (uint64_t(rl(uint32_t(nzw), nl)) | (uint64_t(rl(uint32_t(nzw >> 32), nl)) << 32)) & band;
     }
   }
+  publish(RJ_PROG_DONE);  // every exit (an empty interval never flushed)
 }
 
 hipError_t LaunchProgressiveAcRefine(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *ivals, uint32_t n,
-                                     const uint8_t *destuffed, const unsigned long long *nz,
-                                     unsigned long long *recs) {
+                                     const uint8_t *destuffed, unsigned long long *nz,
+                                     unsigned long long *recs, uint32_t *progress, uint32_t progress_n) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_prog_acref, dim3(n), dim3(64), 0, st, imgs, nimg, ivals, destuffed, nz, recs);
+  hipLaunchKernelGGL(k_prog_acref, dim3(n), dim3(64), 0, st, imgs, nimg, ivals, destuffed, nz, recs, progress,
+                     progress_n);
   return hipGetLastError();
 }
 
@@ -856,7 +900,6 @@ __global__ __launch_bounds__(64) void k_prog_fold(const RjImageDev *__restrict__
   const unsigned long long *rec = recs + im.prec_off;
   uint32_t w[32];
   bool loaded = false;
-  uint64_t newall = 0;
   uint4 *blk4 = reinterpret_cast<uint4 *>(coef + im.coef_off + uint64_t(cb0 + b) * 32u);
   auto load = [&]() {
     if (loaded) return;
@@ -870,20 +913,16 @@ __global__ __launch_bounds__(64) void k_prog_fold(const RjImageDev *__restrict__
       w[4 * q + 3] = v.w;
     }
   };
-  unsigned long long *nzp = nz + im.nz_off + nzb0 + by * cwb + bx;
-  uint64_t nz_before = 0;
-  bool nz_loaded = false;
-  auto nzprev = [&]() -> uint64_t {  // the block's nonzero positions before this level
-    if (!nz_loaded) {
-      nz_loaded = true;
-      nz_before = *gp(nzp);
-    }
-    return nz_before;
-  };
+  // the masks already hold every new position of the scans folded here (k_prog_acref ORs them
+  // in); walking the scans backwards and peeling each scan's new positions gives the masks each
+  // scan saw when it decoded
+  const unsigned long long *nzp = nz + im.nz_off + nzb0 + by * cwb + bx;
+  uint64_t running = coded ? *gp(nzp) : 0ull;
   const uint32_t ns_img = im.npscans;
-  for (uint32_t si = 0; si < ns_img; si++) {
+  for (uint32_t sr = ns_img; sr-- > 0;) {
+    const uint32_t si = sr;
     const RjProgScanDev sc = im.pscans[si];
-    if (sc.level != level) continue;
+    if (level != RJ_FOLD_ALL && sc.level != level) continue;
     if (sc.kind == RJ_PK_AC_REFINE) {
       if (sc.comp[0] != c || !coded) continue;
       const uint32_t unit = by * cwb + bx;
@@ -896,7 +935,8 @@ __global__ __launch_bounds__(64) void k_prog_fold(const RjImageDev *__restrict__
         // the correction bits belong to the band's previously nonzero positions, ascending,
         // first bit most significant (libjpeg decode_mcu_AC_refine's walk order)
         const uint64_t band = (sc.se >= 63 ? ~0ull : ((1ull << (sc.se + 1)) - 1)) & ~((1ull << sc.ss) - 1);
-        uint64_t nzm = nzprev() & band;
+        running &= ~newm;
+        uint64_t nzm = running & band;
         uint32_t j = uint32_t(__popcll(nzm));
         uint64_t orm = newm;
         while (nzm) {
@@ -908,7 +948,6 @@ __global__ __launch_bounds__(64) void k_prog_fold(const RjImageDev *__restrict__
         load();
         or_bits(w, orm, sgn, 1u << sc.al);
       }
-      newall |= newm;
     } else if (sc.kind == RJ_PK_DC_REFINE) {
       uint32_t i = 3, slot0 = 0;
       for (uint32_t q = 0; q < sc.ns; q++) {
@@ -940,7 +979,7 @@ __global__ __launch_bounds__(64) void k_prog_fold(const RjImageDev *__restrict__
 #pragma unroll
     for (int q = 0; q < 8; q++) gp(blk4)[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
   }
-  if (newall) *gp(nzp) = nzprev() | newall;
+
 }
 
 hipError_t LaunchProgressiveFold(hipStream_t st, const RjImageDev *imgs, const RjFoldJob *jobs, uint32_t njobs,

@@ -416,6 +416,16 @@ bool Stream::ParseProgressive(const uint8_t *d, uint32_t n) {
       for (int k = v.ss; k <= v.se; k++) lastlev[v.comp[i]][k] = lev;
     v.level = uint8_t(std::min(lev, 255));
     p.plevels = std::max<uint32_t>(p.plevels, uint32_t(v.level) + 1);
+    v.nprod = 0;
+    if (v.kind == RJ_PK_AC_REFINE) {  // producers for the pipelined refinement launch
+      for (size_t r = 0; r < p.pscans.size(); r++) {
+        const RjProgScanDev &q = p.pscans[r];
+        if (q.kind != RJ_PK_AC_REFINE || q.comp[0] != v.comp[0] || q.se < v.ss || q.ss > v.se) continue;
+        if (v.nprod < 3) v.prod[v.nprod++] = uint8_t(r);
+        else v.nprod = 0xFF;
+        if (v.nprod == 0xFF) break;
+      }
+    }
     p.pscans.push_back(v);
   }
   if (bogus) {
