@@ -156,3 +156,38 @@ def test_progressive_timings(dec):
     assert t["prog_images"] == 1 and t["prog_levels"] >= 2 and t["prog_intervals"] == 10
     assert t["prog_entropy_ms"] > 0 and t["prog_rows_ms"] > 0
     assert t["prog_coef_bytes"] == 1920 * 1088 * 3 // 2 * 2  # 4:2:0, MCU-padded, int16
+
+
+def test_level_by_level_refinement_matches_oracle():
+    """RJ_PROG_PIPE=0: the refinement scans run level by level (the path taken when a scan has
+    more than three producer scans) -- same bytes as the pipelined default."""
+    import os
+    from tests import gpu_util as G
+    G.torch()
+    old = os.environ.get("RJ_PROG_PIPE")
+    os.environ["RJ_PROG_PIPE"] = "0"
+    try:
+        d = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    finally:
+        if old is None:
+            del os.environ["RJ_PROG_PIPE"]
+        else:
+            os.environ["RJ_PROG_PIPE"] = old
+    try:
+        datas = [O.fixture_bytes(e) for e in PROG]
+        streams = [R.JpegStream(x) for x in datas]
+        bufs_all, imgs, shapes_all = [], [], []
+        for s in streams:
+            nc, css, w, h = d.image_info(s)
+            shapes = G.channel_shapes(R.OutputFormat.RGB, css, w, h)
+            bufs, img = G.gpu_buffers(shapes)
+            bufs_all.append(bufs)
+            imgs.append(img)
+            shapes_all.append(shapes)
+        assert d.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs) == 0
+        for x, shapes, bufs in zip(datas, shapes_all, bufs_all):
+            ost, want = O.oracle_decode(x, int(R.OutputFormat.RGB), shapes)
+            assert ost == 0
+            assert G.first_mismatch(G.to_host(bufs)[0], want[0]) is None
+    finally:
+        d.close()
