@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 
 MUG = os.path.join(ROOT, "tests", "golden", "img", "mug_420.jpg")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+PROG_KERNELS = ("k_prog", "k_prog_wave", "k_prog_fold")  # RocJpegAmdTimings.prog_kernel_*
 
 _BASE = None
 
@@ -111,12 +112,14 @@ def turbo_baseline(data_list, procs):
             "lib": "Pillow bundled libjpeg-turbo (BT.601 + fancy upsampling: throughput context only)"}
 
 
-def pmc_traffic(kernel, batch, launches):
+def pmc_traffic(kernel, batch, launches, workload="c2"):
     """HBM bytes per launch of `kernel` from the committed PMC profile (tools/gpu_pmc.sh +
-    tools/pmc_traffic.py on this workload): FETCH_SIZE x 2 (gfx950 correction, MI355X_MICROARCH.md
-    HBM section) + WRITE_SIZE summed over a decode call, per image, scaled to this call's batch
-    and divided over its launches of the kernel.  None if absent."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    tools/pmc_traffic.py on this workload; profiles/pmc_traffic.json for C2,
+    pmc_traffic_<workload>.json for the others): FETCH_SIZE x 2 (gfx950 correction,
+    MI355X_MICROARCH.md HBM section) + WRITE_SIZE summed over a decode call, per image, scaled to
+    this call's batch and divided over its launches of the kernel.  None if absent."""
+    name = "pmc_traffic.json" if workload == "c2" else f"pmc_traffic_{workload}.json"
+    path = os.path.join(ROOT, "profiles", name)
     try:
         with open(path) as f:
             prof = json.load(f)
@@ -246,6 +249,8 @@ def main():
         for k in ("entropy_chunks_ms", "entropy_resolve_ms", "entropy_serial_ms", "k1_launch_ms_sum",
                   "k2_launch_ms_sum", "prog_entropy_ms", "prog_rows_ms"):
             k1[k] = k1.get(k, 0.0) + last[k]
+        for j, name in enumerate(PROG_KERNELS):
+            k1[name] = k1.get(name, 0.0) + last["prog_kernel_ms"][j]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -311,15 +316,20 @@ def main():
             "k_rows": (k1["k2_launch_ms_sum"] / K, max(1, last["k2_launches"]), entb + outb),
         }
         if last["prog_images"]:
-            # progressive: K1p reads the destuffed scans and writes the dense coefficients (incl.
-            # their zero fill); K2 (dense) reads them and writes the output
+            # progressive: k_prog lanes read their destuffed scans and write the
+            # coefficient band / DC-refinement bits; k_prog_wave reads its scans and writes a
+            # first scan's band + masks, or reads the nonzero masks and writes one 32-B record per
+            # refined block; k_prog_fold reads the records and reads +
+            # writes each touched dense block; K2 (dense) reads the coefficients, writes the output
             pc = last["prog_coef_bytes"]
-            kern["k_prog"] = (k1["prog_entropy_ms"] / K, max(1, last["prog_levels"]), ecs + pc)
+            for j, name in enumerate(PROG_KERNELS):
+                if last["prog_kernel_launches"][j]:
+                    kern[name] = (k1[name] / K, last["prog_kernel_launches"][j], last["prog_kernel_bytes"][j])
             kern["k_rows_dense"] = (k1["prog_rows_ms"] / K, 1, pc + outb)
         dom = max(kern, key=lambda k: kern[k][0])
         t_sum, launches, algo_bytes = kern[dom]
         ach = algo_bytes / (t_sum * 1e-3) / 1e9 if t_sum > 0 else 0.0
-        traffic = pmc_traffic(dom, args.batch, launches)
+        traffic = pmc_traffic(dom, args.batch, launches, args.workload)
         res = {
             "metric": "images/s (1080p 4:2:0 batch) at 1/2/4/8 MI355X + achieved HBM GB/s",
             "value": round(value, 2),
@@ -356,6 +366,8 @@ def main():
             res["progressive_detail"] = {"images": last["prog_images"], "intervals": last["prog_intervals"],
                                          "levels": last["prog_levels"],
                                          "k1p_ms": round(k1["prog_entropy_ms"] / K, 4),
+                                         "k1p_launches": {n: last["prog_kernel_launches"][j]
+                                                          for j, n in enumerate(PROG_KERNELS)},
                                          "k2_dense_ms": round(k1["prog_rows_ms"] / K, 4)}
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(data, shapes, int(fmt), wl["sample"])

@@ -86,6 +86,13 @@ typedef struct {
   /* rocJpegAmdStreamParseDevice (the last call on this handle): streams whose marker scan ran on
      the GPU, and those that fell back to the host scan (a scratch list overflowed) */
   uint32_t scan_device_streams, scan_host_fallbacks;
+  /* progressive launches by kernel, [0] k_prog (first-scan and DC-refinement lanes), [1]
+     k_prog_wave (AC scan waves: refinement, and first scans when pipelined), [2] k_prog_fold: summed launch durations (HIP events on
+     each launch's stream), launch counts, and the algorithmic bytes of the call's launches
+     (destuffed scan bytes read + coefficient / mask / record bytes written) */
+  float prog_kernel_ms[3];
+  uint32_t prog_kernel_launches[3];
+  uint64_t prog_kernel_bytes[3];
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);

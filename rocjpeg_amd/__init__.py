@@ -97,7 +97,9 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("prog_images", ctypes.c_uint32), ("prog_intervals", ctypes.c_uint32),
                 ("prog_levels", ctypes.c_uint32), ("prog_pad", ctypes.c_uint32),
                 ("prog_coef_bytes", ctypes.c_uint64),
-                ("scan_device_streams", ctypes.c_uint32), ("scan_host_fallbacks", ctypes.c_uint32)]
+                ("scan_device_streams", ctypes.c_uint32), ("scan_host_fallbacks", ctypes.c_uint32),
+                ("prog_kernel_ms", ctypes.c_float * 3), ("prog_kernel_launches", ctypes.c_uint32 * 3),
+                ("prog_kernel_bytes", ctypes.c_uint64 * 3)]
 
 
 class RocJpegAmdInterval(ctypes.Structure):  # include/rocjpeg_amd.h
@@ -292,7 +294,11 @@ class JpegDecoder:
     def last_timings(self):
         t = RocJpegAmdTimings()
         _check(lib().rocJpegAmdGetLastTimings(self.handle, ctypes.byref(t)), "rocJpegAmdGetLastTimings")
-        return {k: getattr(t, k) for k, _ in RocJpegAmdTimings._fields_}
+        out = {}
+        for k, _ in RocJpegAmdTimings._fields_:
+            v = getattr(t, k)
+            out[k] = list(v) if isinstance(v, ctypes.Array) else v
+        return out
 
     def hip_stream(self):
         s = ctypes.c_void_p()

@@ -110,6 +110,7 @@ Decoder::~Decoder() {
     for (auto &e : prog_join_)
       if (e) (void)hipEventDestroy(e);
     for (auto &e : prog_lev_ev_) (void)hipEventDestroy(e);
+    for (auto &e : pk_ev_) (void)hipEventDestroy(e);
     for (auto *arr : {k1s_, k2s_, k2e_})
       for (int q = 0; q < kMaxPipe; q++)
         if (arr[q]) (void)hipEventDestroy(arr[q]);
@@ -150,6 +151,7 @@ int Decoder::Initialize() {
   for (auto &e : prog_ev_) RJ_HIP(hipEventCreate(&e));
   for (auto &e : prog_join_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   if (const char *pp = getenv("RJ_PROG_PIPE")) prog_pipe_enabled_ = atoi(pp) != 0;
+  if (const char *pw = getenv("RJ_PROG_WAVE_ALL")) prog_wave_all_ = atoi(pw) != 0;
   for (auto *arr : {k1s_, k2s_, k2e_})
     for (int q = 0; q < kMaxPipe; q++) RJ_HIP(hipEventCreate(&arr[q]));
   (void)backend_;  // HARDWARE and HYBRID both run the HIP decoder
@@ -380,6 +382,9 @@ int Decoder::Decode(Stream *const *streams, int n, const RocJpegDecodeParams *pa
   for (Stream *s : uniq) locks.emplace_back(s->mutex());
   return DecodeLocked(streams, n, params, dst);
 }
+
+// progressive images per call up to which every scan goes to the wave grid (see prog_wave_all)
+static constexpr int kProgWaveAllImages = 640;  // measured crossover (C5 1080p: 512 -> waves, 1024 -> lanes)
 
 int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
   const auto t_host0 = std::chrono::steady_clock::now();
@@ -653,16 +658,44 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // group (a wave lasts as long as its longest lane) ----
   std::vector<uint32_t> &prog_lanes = sc_.prog_lanes;
   prog_lanes.clear();
-  uint32_t prog_level_off[257] = {}, fold_off[257] = {}, fold_chunks[257] = {}, acref_off[257] = {};
-  bool prog_pipe = false;
+  uint32_t prog_level_off[257] = {}, fold_off[257] = {}, fold_chunks[257] = {}, wave_off[257] = {};
+  bool prog_pipe = false, prog_wave_all = false;
   std::vector<RjFoldJob> &fold_jobs = sc_.fold_jobs;
   const uint32_t nlev = std::min<uint32_t>(prog_levels, 256);
   if (prog_images) {
+    // pipelined launch: every interval of the call in one k_prog_wave grid, a refinement scan
+    // following its producer scans block by block (progress counters) -- possible when every
+    // refinement scan has at most 3 producers (rj_prog_stream.cpp); otherwise level by level
+    // (DC and AC-first scans in lanes, refinement waves, a fold per level)
+    prog_pipe = prog_pipe_enabled_;
+    for (int i = 0; i < n && prog_pipe; i++)
+      for (const RjProgScanDev &sc : streams[i]->plan().pscans)
+        if (sc.kind == RJ_PK_AC_REFINE && sc.nprod == 0xFF) prog_pipe = false;
+    // pipelined layouts: a small batch puts every scan in the wave grid (each image's scans run
+    // side by side: lowest latency); a large one decodes the first scans (all at level 0) in
+    // lanes before the grid and the DC refinements in lanes beside it -- a lane decodes a scan
+    // with far fewer instructions per symbol than a wave's scalar chain, and with ~10 waves per
+    // image the grid would outgrow the chip's wave slots
+    prog_wave_all = prog_pipe && (prog_wave_all_ >= 0 ? prog_wave_all_ != 0 : prog_images <= kProgWaveAllImages);
+    auto in_lanes = [&](uint32_t kind) {
+      return !prog_pipe ? kind != RJ_PK_AC_REFINE : (!prog_wave_all && kind != RJ_PK_AC_REFINE);
+    };
+    // algorithmic bytes of an interval: destuffed bytes read + what its decode writes (DC first:
+    // one halfword per block; DC refinement: one bit per block; AC first: the band's halfwords +
+    // the nonzero mask; AC refinement: mask read + one 32-B record per block)
+    auto ival_bytes = [](const RjProgScanDev &sc, const RjProgIvalDev &iv) -> uint64_t {
+      const uint64_t blocks = uint64_t(iv.nunits) * sc.nblk;
+      return iv.dst_len + (sc.kind == RJ_PK_DC_FIRST    ? blocks * 2
+                           : sc.kind == RJ_PK_DC_REFINE ? (blocks + 7) / 8
+                           : sc.kind == RJ_PK_AC_FIRST  ? blocks * ((sc.se - sc.ss + 1u) * 2u + 8u)
+                                                        : blocks * 40u);
+    };
     constexpr uint32_t kPB = 2048;  // 64-B length buckets
     std::vector<uint32_t> &bk = sc_.prog_bucket;
     for (uint32_t L = 0; L < nlev; L++) {
       prog_level_off[L] = uint32_t(prog_lanes.size());
-      for (uint32_t K = 0; K < 3; K++) {  // AC refinement: one wave per interval (below)
+      for (uint32_t K = 0; K < 3; K++) {  // AC refinement: waves, below
+        if (!in_lanes(K)) continue;
         bk.assign(kPB + 1, 0);
         uint32_t cnt = 0;
         for (int i = 0; i < n; i++) {
@@ -692,34 +725,65 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
             const RjProgScanDev &sc = p.pscans[iv.scan];
             if (sc.level != L || sc.kind != K || (iv.flags & RJ_SEG_MISSING)) continue;
             prog_lanes[base + bk[kPB - 1 - std::min<uint32_t>(iv.dst_len >> 6, kPB - 1)]++] = g0 + q;
+            timings_.prog_kernel_bytes[0] += ival_bytes(sc, iv);
           }
         }
       }
     }
     prog_level_off[nlev] = uint32_t(prog_lanes.size());
-    // pipelined refinement: every AC refinement interval in one k_prog_acref grid, a scan following
-    // its producer scans block by block (progress counters) -- possible when every refinement
-    // scan has at most 3 producers (rj_prog_stream.cpp); otherwise level by level
-    prog_pipe = prog_pipe_enabled_;
-    for (int i = 0; i < n && prog_pipe; i++)
-      for (const RjProgScanDev &sc : streams[i]->plan().pscans)
-        if (sc.kind == RJ_PK_AC_REFINE && sc.nprod == 0xFF) prog_pipe = false;
-    // AC refinement intervals (k_prog_acref, one wave each), per level, after the lane lists
-    for (uint32_t L = 0; L < nlev; L++) {
-      acref_off[L] = uint32_t(prog_lanes.size());
-      for (int i = 0; i < n; i++) {
-        const DecodePlan &p = streams[i]->plan();
-        if (!p.progressive) continue;
-        for (uint32_t q = 0; q < p.pivals.size(); q++) {
-          const RjProgIvalDev &iv = p.pivals[q];
-          const RjProgScanDev &sc = p.pscans[iv.scan];
-          // pipelined: missing intervals too (their wave only publishes "done" for consumers)
-          if (sc.level == L && sc.kind == RJ_PK_AC_REFINE && (prog_pipe || !(iv.flags & RJ_SEG_MISSING)))
-            prog_lanes.push_back(imgs[i].pival_prefix + q);
+    if (prog_pipe) {
+      // the grid's order: any order that lists a scan's producers before it is deadlock-free
+      // (workgroups dispatch in order; a waiting wave's producers are resident or done).  When
+      // the batch has more intervals than the chip has wave slots, the late ones should be those
+      // with slack: the largest component's AC scans first (its refinement chain is the critical
+      // path), then the other components' AC scans, then the DC scans; level order within each.
+      wave_off[0] = uint32_t(prog_lanes.size());
+      for (uint32_t rank = 0; rank < 4; rank++)
+        for (uint32_t L = 0; L < nlev; L++)
+          for (int i = 0; i < n; i++) {
+            const DecodePlan &p = streams[i]->plan();
+            if (!p.progressive) continue;
+            const uint32_t nc = streams[i]->info().ncomp;
+            for (uint32_t q = 0; q < p.pivals.size(); q++) {
+              const RjProgIvalDev &iv = p.pivals[q];
+              const RjProgScanDev &sc = p.pscans[iv.scan];
+              if (sc.level != L) continue;
+              uint32_t r = 3;
+              if (sc.kind == RJ_PK_AC_FIRST || sc.kind == RJ_PK_AC_REFINE) {
+                const uint32_t c = sc.comp[0];
+                const uint64_t bc = uint64_t(p.cwblk[c]) * p.chblk[c];
+                r = 0;
+                for (uint32_t o = 0; o < nc && o < 3; o++) {
+                  const uint64_t bo = uint64_t(p.cwblk[o]) * p.chblk[o];
+                  if (bo > bc || (bo == bc && o < c)) r++;
+                }
+                r = std::min<uint32_t>(r, 2);
+              }
+              if (r != rank || in_lanes(sc.kind)) continue;
+              prog_lanes.push_back(imgs[i].pival_prefix + q);  // missing ones too: they report DONE
+              if (!(iv.flags & RJ_SEG_MISSING)) timings_.prog_kernel_bytes[1] += ival_bytes(sc, iv);
+            }
+          }
+      for (uint32_t L = 1; L < nlev; L++) wave_off[L] = wave_off[0];
+    } else {
+      // AC refinement intervals (one wave each), per level, after the lane lists
+      for (uint32_t L = 0; L < nlev; L++) {
+        wave_off[L] = uint32_t(prog_lanes.size());
+        for (int i = 0; i < n; i++) {
+          const DecodePlan &p = streams[i]->plan();
+          if (!p.progressive) continue;
+          for (uint32_t q = 0; q < p.pivals.size(); q++) {
+            const RjProgIvalDev &iv = p.pivals[q];
+            const RjProgScanDev &sc = p.pscans[iv.scan];
+            if (sc.level == L && sc.kind == RJ_PK_AC_REFINE && !(iv.flags & RJ_SEG_MISSING)) {
+              prog_lanes.push_back(imgs[i].pival_prefix + q);
+              timings_.prog_kernel_bytes[1] += ival_bytes(sc, iv);
+            }
+          }
         }
       }
     }
-    acref_off[nlev] = uint32_t(prog_lanes.size());
+    wave_off[nlev] = uint32_t(prog_lanes.size());
     // k_prog_fold jobs of every level >= 1: (image, component) pairs some refinement scan of
     // that level covers, every block of the component's dense raster
     fold_jobs.clear();
@@ -744,6 +808,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
           fj.comp = c;
           fj.nblocks = p.wblk[c] * p.hblk[c];
           fj.chunk0 = chunks;
+          timings_.prog_kernel_bytes[2] += uint64_t(fj.nblocks) * 256;  // dense block read + written
           chunks += (fj.nblocks + 63) / 64;
           fold_jobs.push_back(fj);
         }
@@ -751,6 +816,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       fold_chunks[L] = chunks;
     }
     fold_off[prog_pipe ? 1u : nlev] = uint32_t(fold_jobs.size());
+    timings_.prog_kernel_bytes[2] += prec_total * 8;  // the refinement records
   }
 
   const auto t_lanes = std::chrono::steady_clock::now();
@@ -934,47 +1000,91 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       }
     }
     if (dbg_lev) RJ_HIP(hipEventRecord(prog_lev_ev_[0], stream_));
+    // profiling: an event pair around every progressive launch (on the launch's own stream)
+    pk_span_.clear();
+    uint32_t pk_used = 0;
+    if (profiling_) {
+      const size_t need = 2 * (3 * size_t(nlev) + 2);
+      while (pk_ev_.size() < need) {
+        hipEvent_t e;
+        RJ_HIP(hipEventCreate(&e));
+        pk_ev_.push_back(e);
+      }
+    }
+    auto pk_begin = [&](hipStream_t s) { return profiling_ ? hipEventRecord(pk_ev_[pk_used], s) : hipSuccess; };
+    auto pk_end = [&](hipStream_t s, uint32_t kind, uint32_t count) {
+      if (!profiling_) return hipSuccess;
+      const hipError_t e = hipEventRecord(pk_ev_[pk_used + 1], s);
+      if (count) pk_span_.push_back({kind, pk_used, pk_used + 1});
+      pk_used += 2;
+      return e;
+    };
     if (prog_pipe) {
-      // level 0 lanes (first scans); then, side by side: the DC-refinement lanes of the later
-      // levels on a second stream, and every AC refinement interval in one grid (level order,
-      // consumers following producers); one fold over all levels once both are done
+      // side by side: the DC lanes of every level (DC first, then DC refinements) on a second
+      // stream, and every AC interval in one k_prog_wave grid (level order, a scan following its
+      // producers); one fold over all levels once both are done
       RJ_HIP(hipMemsetAsync(d_pprog_.as<uint32_t>(), 0, uint64_t(pival_total + 1) * 4, stream_));
-      RJ_HIP(LaunchProgressive(stream_, d_imgs, n, d_plane + prog_level_off[0], prog_level_off[1] - prog_level_off[0],
-                               d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
-                               d_prec_.as<unsigned long long>()));
-      if (dbg_lev) RJ_HIP(hipEventRecord(prog_lev_ev_[1], stream_));
-      const bool side = prog_level_off[nlev] > prog_level_off[std::min<uint32_t>(1, nlev)];
+      // lane layout: the first scans (level 0) before the grid
+      const uint32_t L0 = prog_wave_all ? 0u : 1u;
+      if (!prog_wave_all && prog_level_off[1] > prog_level_off[0]) {
+        RJ_HIP(pk_begin(stream_));
+        RJ_HIP(LaunchProgressive(stream_, d_imgs, n, d_plane + prog_level_off[0], prog_level_off[1] - prog_level_off[0],
+                                 d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
+                                 d_prec_.as<unsigned long long>()));
+        RJ_HIP(pk_end(stream_, 0, prog_level_off[1] - prog_level_off[0]));
+      }
+      const bool side = prog_level_off[nlev] > prog_level_off[std::min(L0, nlev)];
       if (side) {
         RJ_HIP(hipEventRecord(prog_join_[0], stream_));
         RJ_HIP(hipStreamWaitEvent(pstream_[0], prog_join_[0], 0));
-        for (uint32_t L = 1; L < nlev; L++)
+        for (uint32_t L = L0; L < nlev; L++) {
+          RJ_HIP(pk_begin(pstream_[0]));
           RJ_HIP(LaunchProgressive(pstream_[0], d_imgs, n, d_plane + prog_level_off[L],
                                    prog_level_off[L + 1] - prog_level_off[L], d_destuff_.as<uint8_t>(),
                                    d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
                                    d_prec_.as<unsigned long long>()));
+          RJ_HIP(pk_end(pstream_[0], 0, prog_level_off[L + 1] - prog_level_off[L]));
+        }
         RJ_HIP(hipEventRecord(prog_join_[1], pstream_[0]));
       }
-      RJ_HIP(LaunchProgressiveAcRefine(stream_, d_imgs, n, d_plane + acref_off[0], acref_off[nlev] - acref_off[0],
-                                       d_destuff_.as<uint8_t>(), d_nz_.as<unsigned long long>(),
-                                       d_prec_.as<unsigned long long>(), d_pprog_.as<uint32_t>(), pival_total));
+      unsigned long long *wstamps = nullptr;
+      if (getenv("RJ_DEBUG_WAVES")) {
+        RJ_CHECK(d_wstamp_.Ensure(std::max<uint64_t>(uint64_t(wave_off[nlev] - wave_off[0]) * 32, 256)));
+        wstamps = d_wstamp_.as<unsigned long long>();
+      }
+      RJ_HIP(pk_begin(stream_));
+      RJ_HIP(LaunchProgressiveWave(stream_, d_imgs, n, d_plane + wave_off[0], wave_off[nlev] - wave_off[0],
+                                   d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
+                                   d_prec_.as<unsigned long long>(), d_pprog_.as<uint32_t>(), pival_total, wstamps,
+                                   prog_wave_all ? 0u : RJ_WAVE_FIRST_DONE));
+      RJ_HIP(pk_end(stream_, 1, wave_off[nlev] - wave_off[0]));
       if (side) RJ_HIP(hipStreamWaitEvent(stream_, prog_join_[1], 0));
+      RJ_HIP(pk_begin(stream_));
       RJ_HIP(LaunchProgressiveFold(stream_, d_imgs, d_fold + fold_off[0], fold_off[1] - fold_off[0], fold_chunks[0],
                                    RJ_FOLD_ALL, d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
                                    d_prec_.as<unsigned long long>()));
+      RJ_HIP(pk_end(stream_, 2, fold_chunks[0]));
       if (dbg_lev)
-        for (uint32_t L = 2; L <= nlev; L++) RJ_HIP(hipEventRecord(prog_lev_ev_[L], stream_));
+        for (uint32_t L = 1; L <= nlev; L++) RJ_HIP(hipEventRecord(prog_lev_ev_[L], stream_));
     }
     for (uint32_t L = 0; L < nlev && !prog_pipe; L++) {
+      RJ_HIP(pk_begin(stream_));
       RJ_HIP(LaunchProgressive(stream_, d_imgs, n, d_plane + prog_level_off[L], prog_level_off[L + 1] - prog_level_off[L],
                                d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
                                d_prec_.as<unsigned long long>()));
-      RJ_HIP(LaunchProgressiveAcRefine(stream_, d_imgs, n, d_plane + acref_off[L], acref_off[L + 1] - acref_off[L],
-                                       d_destuff_.as<uint8_t>(), d_nz_.as<unsigned long long>(),
-                                       d_prec_.as<unsigned long long>(), nullptr, 0u));
-      if (L >= 1)
+      RJ_HIP(pk_end(stream_, 0, prog_level_off[L + 1] - prog_level_off[L]));
+      RJ_HIP(pk_begin(stream_));
+      RJ_HIP(LaunchProgressiveWave(stream_, d_imgs, n, d_plane + wave_off[L], wave_off[L + 1] - wave_off[L],
+                                   d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
+                                   d_prec_.as<unsigned long long>(), nullptr, 0u));
+      RJ_HIP(pk_end(stream_, 1, wave_off[L + 1] - wave_off[L]));
+      if (L >= 1) {
+        RJ_HIP(pk_begin(stream_));
         RJ_HIP(LaunchProgressiveFold(stream_, d_imgs, d_fold + fold_off[L], fold_off[L + 1] - fold_off[L], fold_chunks[L],
                                      L, d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
                                      d_prec_.as<unsigned long long>()));
+        RJ_HIP(pk_end(stream_, 2, fold_chunks[L]));
+      }
       if (dbg_lev) RJ_HIP(hipEventRecord(prog_lev_ev_[L + 1], stream_));
     }
     if (profiling_) RJ_HIP(hipEventRecord(prog_ev_[1], stream_));
@@ -1165,6 +1275,40 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       RJ_ERR("progressive refinement: a producer did not report progress");
       return kExecutionFailed;
     }
+    if (getenv("RJ_DEBUG_WAVES")) {  // per scan of the batch's first image layout: wave timing
+      const uint32_t nw = wave_off[nlev] - wave_off[0];
+      std::vector<unsigned long long> st(size_t(nw) * 4);
+      RJ_HIP(hipMemcpy(st.data(), d_wstamp_.as<unsigned long long>(), st.size() * 8, hipMemcpyDeviceToHost));
+      unsigned long long t0 = ~0ull;
+      for (uint32_t w = 0; w < nw; w++) t0 = std::min(t0, st[4 * w]);
+      struct Acc {
+        double start = 0, ready = 0, end = 0, maxend = 0, nwin = 0, nstep = 0;
+        uint32_t cnt = 0;
+      };
+      std::vector<Acc> acc(256);
+      for (uint32_t w = 0; w < nw; w++) {
+        const uint32_t gi = prog_lanes[wave_off[0] + w];
+        int i = 0;
+        while (i + 1 < n && imgs[i + 1].pival_prefix <= gi) i++;
+        const uint32_t scan = streams[i]->plan().pivals[gi - imgs[i].pival_prefix].scan & 255u;
+        Acc &a = acc[scan];
+        const double us = 0.01;  // wall_clock64: 100 MHz
+        a.start += (st[4 * w] - t0) * us;
+        a.ready += (st[4 * w + 1] - t0) * us;
+        a.end += (st[4 * w + 2] - t0) * us;
+        a.maxend = std::max(a.maxend, (st[4 * w + 2] - t0) * us);
+        a.nwin += double(st[4 * w + 3] >> 32);
+        a.nstep += double(st[4 * w + 3] & 0xFFFFFFFFu);
+        a.cnt++;
+      }
+      for (uint32_t q = 0; q < 256; q++)
+        if (acc[q].cnt)
+          fprintf(stderr,
+                  "[rj waves] scan %2u: %5u waves, mean start %8.0f us, ready %8.0f, end %8.0f, max end %8.0f, "
+                  "windows %9.0f, steps %9.0f\n",
+                  q, acc[q].cnt, acc[q].start / acc[q].cnt, acc[q].ready / acc[q].cnt, acc[q].end / acc[q].cnt,
+                  acc[q].maxend, acc[q].nwin / acc[q].cnt, acc[q].nstep / acc[q].cnt);
+    }
   }
 #ifdef RJ_EXP_STAMPS
   if (getenv("RJ_DEBUG_STAMPS")) DumpRowStamps();
@@ -1238,6 +1382,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       RJ_HIP(hipEventElapsedTime(&timings_.prog_entropy_ms, prog_ev_[0], prog_ev_[1]));
       RJ_HIP(hipEventElapsedTime(&timings_.prog_rows_ms, prog_ev_[1], prog_ev_[2]));
       RJ_HIP(hipEventElapsedTime(&timings_.destuff_ms, ev_[1], prog_ev_[0]));  // K0 alone
+      for (const ProgSpan &sp : pk_span_) {
+        float t = 0;
+        RJ_HIP(hipEventElapsedTime(&t, pk_ev_[sp.e0], pk_ev_[sp.e1]));
+        timings_.prog_kernel_ms[sp.kind] += t;
+        timings_.prog_kernel_launches[sp.kind]++;
+      }
       if (getenv("RJ_DEBUG_PROG") && prog_lev_ev_.size() >= nlev + 1) {
         for (uint32_t L = 0; L < nlev; L++) {
           float t = 0;

@@ -101,10 +101,18 @@ class Decoder {
   std::vector<hipEvent_t> prog_lev_ev_;  // development (RJ_DEBUG_PROG): per-level K1p spans
   hipEvent_t prog_join_[2] = {};         // pipelined refinement: side stream fork / join
   bool prog_pipe_enabled_ = true;        // env RJ_PROG_PIPE=0: level-by-level refinement
+  int prog_wave_all_ = -1;               // env RJ_PROG_WAVE_ALL=0/1: force the pipelined layout (-1: by batch)
+  // profiling: one event pair per progressive launch, on the stream it runs on; kind 0 k_prog,
+  // 1 k_prog_wave, 2 k_prog_fold
+  struct ProgSpan {
+    uint32_t kind, e0, e1;
+  };
+  std::vector<hipEvent_t> pk_ev_;
+  std::vector<ProgSpan> pk_span_;
 
   DeviceBuffer d_desc_, d_stage_, d_destuff_, d_entries_, d_planes_;
   DeviceBuffer d_piece_, d_rec_, d_chunkres_, d_fallback_;  // K1 chunk bookkeeping
-  DeviceBuffer d_coef_, d_nz_, d_prec_, d_pprog_;
+  DeviceBuffer d_coef_, d_nz_, d_prec_, d_pprog_, d_wstamp_;  // d_wstamp_: RJ_DEBUG_WAVES
   DeviceBuffer d_scan_;  // marker scan: uploaded bytes, jobs, scratch lists, read-back tables
   PinnedBuffer h_scan_;  // progressive: dense coefficients, nonzero masks, refinement records
   uint32_t epoch_ = 0;

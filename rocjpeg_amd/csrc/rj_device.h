@@ -234,6 +234,7 @@ struct RjProgScanDev {
   uint8_t nprod, prod[3];
 };
 #define RJ_PROG_DONE 0xFFFFFFFFu  // interval progress: finished
+#define RJ_WAVE_FIRST_DONE 1u      // k_prog_wave flag: first scans decoded before the grid (no waits on them)
 #define RJ_FOLD_ALL 0xFFFFFFFFu   // k_prog_fold level: every level (after a pipelined launch)
 // AC refinement record of one unit (block): 32 B, written once by the decoding lane
 struct RjRefineRec {

@@ -46,10 +46,12 @@ hipError_t LaunchRowsOfLanes(hipStream_t st, bool to_planes, const RjImageDev *i
 hipError_t LaunchProgressive(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *lanes, uint32_t nlanes,
                              const uint8_t *destuffed, uint32_t *coef, unsigned long long *nz,
                              unsigned long long *recs);
-// K1p AC refinement, one wave per interval (n intervals listed in ivals, batch-global indices).
-hipError_t LaunchProgressiveAcRefine(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *ivals, uint32_t n,
-                                     const uint8_t *destuffed, unsigned long long *nz,
-                                     unsigned long long *recs, uint32_t *progress, uint32_t progress_n);
+// K1p AC scans, one wave per interval (n intervals listed in ivals, batch-global indices): AC
+// refinement, and AC first scans (pipelined launch: progress != null, scans in level order).
+hipError_t LaunchProgressiveWave(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *ivals, uint32_t n,
+                                 const uint8_t *destuffed, uint32_t *coef, unsigned long long *nz,
+                                 unsigned long long *recs, uint32_t *progress, uint32_t progress_n,
+                                 unsigned long long *stamps = nullptr, uint32_t flags = 0);
 // k_prog_fold: level `level`'s refinement records into the dense coefficients / nonzero masks.
 hipError_t LaunchProgressiveFold(hipStream_t st, const RjImageDev *imgs, const RjFoldJob *jobs, uint32_t njobs,
                                  uint32_t nchunks, uint32_t level, uint32_t *coef, unsigned long long *nz,

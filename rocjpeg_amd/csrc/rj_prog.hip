@@ -617,27 +617,48 @@ hipError_t LaunchProgressive(hipStream_t st, const RjImageDev *imgs, int nimg, c
 }
 
 // ---------------------------------------------------------------------------------------
-// k_prog_acref: AC refinement, one WAVE per interval (wave-cooperative).  The lane-per-interval
-// decoder above leaves a batch's refinement levels with a few dozen waves on a 1024-SIMD chip
-// (one Y refinement scan per image), each lane walking ~10^5 divergent symbols.  Here the wave
-// owns one interval: per window step lane l peeks the 32 bits at pos + l and looks its Huffman
-// code up in the wave's LDS table (one lookup latency for 64 candidate offsets), then a scalar
-// (SGPR) chain walks the true symbol positions through readlane -- the refinement state machine
-// (zero-run targets, EOB runs, correction-bit counts on the 64-bit nonzero mask) is SALU work.
-// The bitstream window (64 + 64 words), the coming blocks' nonzero masks and the pending
-// records live one per lane in VGPRs; records leave 64 blocks at a time (coalesced).
-// Output is identical to lane_ac_refine (same records, k_prog_fold applies them).
+// k_prog_wave: AC scans, one WAVE per interval (wave-cooperative) -- AC refinement always, AC
+// first scans in the pipelined launch.  The lane-per-interval decoder above leaves a batch's
+// refinement levels with a few dozen waves on a 1024-SIMD chip (one Y refinement scan per
+// image), each lane walking ~10^5 divergent symbols.  Here the wave owns one interval: per window
+// step lane l peeks the 32 bits at pos + l and looks its Huffman code up in the wave's LDS table
+// (one lookup latency for 64 candidate offsets), then a scalar (SGPR) chain walks the true symbol
+// positions through readlane -- the refinement state machine (zero-run targets, EOB runs,
+// correction-bit counts on the 64-bit nonzero mask) is SALU work.  The bitstream window (64 + 64
+// words), the coming blocks' nonzero masks and the pending records live one per lane in VGPRs;
+// records leave 64 blocks at a time (coalesced).  Refinement output is identical to
+// lane_ac_refine (same records, k_prog_fold applies them); a first scan's block is assembled
+// across the lanes (lane q = coefficient q) and leaves as one masked 16-bit store, exactly the
+// halfwords lane_ac_first writes.
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane) {
   return uint32_t(__builtin_amdgcn_readlane(int(v), int(lane)));
 }
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return uint32_t(__builtin_amdgcn_readfirstlane(int(v))); }
 
-__global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict__ imgs, int nimg,
-                                                   const uint32_t *__restrict__ ivals, const uint8_t *__restrict__ destuffed,
-                                                   unsigned long long *__restrict__ nz,
-                                                   unsigned long long *__restrict__ recs,
-                                                   uint32_t *__restrict__ progress, uint32_t progress_n) {
+__global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__ imgs, int nimg,
+                                                  const uint32_t *__restrict__ ivals, const uint8_t *__restrict__ destuffed,
+                                                  uint32_t *__restrict__ coef, unsigned long long *__restrict__ nz,
+                                                  unsigned long long *__restrict__ recs,
+                                                  uint32_t *__restrict__ progress, uint32_t progress_n,
+                                                  unsigned long long *__restrict__ stamps, uint32_t flags) {
+  // development (RJ_DEBUG_WAVES): wall-clock stamps per wave -- start, producers' first window
+  // ready, end
+  struct WaveStamp {
+    unsigned long long *p;
+    uint32_t nwin, nstep;
+    __device__ ~WaveStamp() {
+      if (p && threadIdx.x == 0) {
+        *gp(p + 2) = wall_clock64();
+        *gp(p + 3) = (uint64_t(nwin) << 32) | nstep;
+      }
+    }
+  } stamp{stamps ? stamps + 4ull * blockIdx.x : nullptr, 0u, 0u};
+  if (stamp.p && threadIdx.x == 0) {
+    const unsigned long long t = wall_clock64();
+    *gp(stamp.p) = t;
+    *gp(stamp.p + 1) = t;
+  }
   __shared__ uint16_t s_lut[RJ_LUT_ENTRIES];
   __shared__ uint32_t s_maxc[18];
   __shared__ int32_t s_voff[18];
@@ -655,23 +676,7 @@ __global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict_
     __threadfence();  // records and mask updates before the count (release)
     if (threadIdx.x == 0) __hip_atomic_store(progress + gi, units_out, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   };
-  if (iv.flags & RJ_SEG_MISSING) {
-    publish(RJ_PROG_DONE);
-    return;
-  }
-  const RjProgScanDev sc = *gp(im.pscans + iv.scan);
-  const RjHuffDev *gt = im.ptabs + sc.tab[0];
-  {
-    const uint4 *src = reinterpret_cast<const uint4 *>(gt->lut);
-    uint4 *dst = reinterpret_cast<uint4 *>(s_lut);
-    for (uint32_t q = lane; q < RJ_LUT_ENTRIES * 2 / 16; q += 64) dst[q] = gp(src)[q];
-    if (lane < 18) {
-      s_maxc[lane] = gp(gt->maxcode16)[lane];
-      s_voff[lane] = gp(gt->valoff)[lane];
-    }
-    reinterpret_cast<uint32_t *>(s_vals)[lane] = gp(reinterpret_cast<const uint32_t *>(gt->vals))[lane];
-  }
-  __syncthreads();
+  const RjProgScanDev &sc = *gp(im.pscans + iv.scan);
   const uint32_t ss = rfl(sc.ss), se = rfl(sc.se);
   const uint64_t band = (se >= 63 ? ~0ull : ((1ull << (se + 1)) - 1)) & ~((1ull << ss) - 1);
   const uint32_t nunits = rfl(iv.nunits), dst_len = rfl(iv.dst_len);
@@ -682,16 +687,20 @@ __global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict_
       nz + im.nz_off + (c0 == 0 ? im.nzblk0[0] : (c0 == 1 ? im.nzblk0[1] : im.nzblk0[2])) + iv.unit0;
   const uint32_t nprod = progress ? min(uint32_t(sc.nprod), 3u) : 0u;
   uint32_t *progress_err = progress ? progress + progress_n : nullptr;
-  auto wait_producers = [&](uint32_t ub) {  // producers' masks of units [ub, ub + 64) are out
-    const uint32_t lo = iv.unit0 + ub, hi = iv.unit0 + min(ub + 64, nunits);
+  auto wait_units = [&](uint32_t ub, uint32_t ue) {  // producers' masks of units [ub, ue) are out
+    if (ub >= ue) return;
+    const uint32_t lo = iv.unit0 + ub, hi = iv.unit0 + ue;
     for (uint32_t q = 0; q < nprod; q++) {
-      const RjProgScanDev ps = *gp(im.pscans + sc.prod[q]);
-      const uint32_t pri = ps.ri;
+      const uint32_t pq = rfl(q == 0 ? sc.prod[0] : (q == 1 ? sc.prod[1] : sc.prod[2]));
+      const RjProgScanDev *ps = im.pscans + pq;
+      // first scans decoded in lanes before this grid: nothing to wait for
+      if ((flags & RJ_WAVE_FIRST_DONE) && rfl(gp(ps)->kind) == RJ_PK_AC_FIRST) continue;
+      const uint32_t pri = rfl(gp(ps)->ri), pival0 = rfl(gp(ps)->ival0);
       const uint32_t j0 = pri ? lo / pri : 0u, j1 = pri ? (hi - 1) / pri : 0u;
       for (uint32_t j = j0; j <= j1; j++) {
         const uint32_t s0 = pri ? j * pri : 0u;
         const uint32_t need = hi - s0;  // units of producer interval j (capped by its DONE)
-        uint32_t *pp = progress + im.pival_prefix + ps.ival0 + j;
+        uint32_t *pp = progress + im.pival_prefix + pival0 + j;
         // bounded (~4 s): a producer that never reports would otherwise hang the GPU; the host
         // turns the flag into EXECUTION_FAILED
         for (uint32_t spin = 0; __hip_atomic_load(pp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need; spin++) {
@@ -704,32 +713,59 @@ __global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict_
       }
     }
   };
-  unsigned long long *rec = recs + im.prec_off + iv.rec_off;
+  auto wait_producers = [&](uint32_t ub) { wait_units(ub, min(ub + 64, nunits)); };
+  // a scan's progress stands for its producers' too (a consumer lists only the latest scan of each
+  // of its coefficients): an interval reports DONE only once its producers covered all its units
+  auto finish = [&](uint32_t ub) {
+    wait_units(ub, nunits);
+    publish(RJ_PROG_DONE);
+  };
+  if (iv.flags & RJ_SEG_MISSING) {
+    finish(0);
+    return;
+  }
+  const uint32_t kind = rfl(sc.kind);
+  // DC first: both tables' first levels (s_lut[0, 512) and [512, 1024)) and, for longer codes,
+  // table 1's canonical bounds and symbols where the AC second levels would go
+  uint32_t *const s_maxc1 = reinterpret_cast<uint32_t *>(s_lut + 1024);
+  int32_t *const s_voff1 = reinterpret_cast<int32_t *>(s_lut + 1024) + 18;
+  uint8_t *const s_vals1 = reinterpret_cast<uint8_t *>(s_lut + 1024) + 144;
+  if (kind != RJ_PK_DC_REFINE) {
+    const RjHuffDev *gt = im.ptabs + sc.tab[0];
+    const uint4 *src = reinterpret_cast<const uint4 *>(gt->lut);
+    uint4 *dst = reinterpret_cast<uint4 *>(s_lut);
+    if (kind == RJ_PK_DC_FIRST) {
+      const RjHuffDev *gt1 = im.ptabs + (sc.tab[1] == 0xFFFFu ? sc.tab[0] : sc.tab[1]);
+      dst[lane] = gp(src)[lane];
+      dst[64 + lane] = gp(reinterpret_cast<const uint4 *>(gt1->lut))[lane];
+      if (lane < 18) {
+        s_maxc1[lane] = gp(gt1->maxcode16)[lane];
+        s_voff1[lane] = gp(gt1->valoff)[lane];
+      }
+      reinterpret_cast<uint32_t *>(s_vals1)[lane] = gp(reinterpret_cast<const uint32_t *>(gt1->vals))[lane];
+    } else {
+      for (uint32_t q = lane; q < RJ_LUT_ENTRIES * 2 / 16; q += 64) dst[q] = gp(src)[q];
+    }
+    if (lane < 18) {
+      s_maxc[lane] = gp(gt->maxcode16)[lane];
+      s_voff[lane] = gp(gt->valoff)[lane];
+    }
+    reinterpret_cast<uint32_t *>(s_vals)[lane] = gp(reinterpret_cast<const uint32_t *>(gt->vals))[lane];
+  }
+  __syncthreads();
   auto ldword = [&](uint32_t w) -> uint32_t {  // word w of the interval, zero past the data
     const uint32_t v = *gp(data + min(w, nwords ? nwords - 1 : 0u));
     return w < nwords ? __builtin_bswap32(v) : 0u;
   };
-  auto ldnz = [&](uint32_t u) -> uint64_t { return *gp(nzs + min(u, nunits - 1)); };
-  // windows: bitstream words [wbase, wbase + 128) in win0/win1 (lane l: word wbase + l / + 64 + l),
-  // nonzero masks of units [nbase, nbase + 64)
+  // windows: bitstream words [wbase, wbase + 128) in win0/win1 (lane l: word wbase + l / + 64 + l)
   uint32_t wbase = 0;
   uint32_t win0 = ldword(lane), win1 = ldword(64 + lane);
-  uint32_t nbase = 0;
-  if (nunits) wait_producers(0);
-  uint64_t nzw = ldnz(lane);
-  uint64_t r_cs = 0, r_sg = 0, r_nw = 0;  // lane b: record of unit rbase + b
-  uint32_t rbase = 0;
   auto word = [&](uint32_t w) -> uint32_t {  // w relative to wbase, < 128
     return w < 64 ? rl(win0, w) : rl(win1, w - 64);
   };
-  uint32_t pos = 0, k = ss, eobrun = 0, u = 0;
-  uint64_t nzm = uint64_t(rl(uint32_t(nzw), 0)) | (uint64_t(rl(uint32_t(nzw >> 32), 0)) << 32);
-  nzm &= band;
-  uint64_t cstr = 0, sgn = 0, newm = 0;
-  uint32_t pend = 0, t = 0, newv = 0;
-  bool walking = false, eobblk = false, done = nunits == 0;
-  while (!done) {
-    // ---- window step: slide the bitstream window, then 64 candidate decodes ----
+  // window step: slide the bitstream window, then 64 candidate decodes -- lane l's 32-bit peek
+  // at pos + l and its table entry (len << 8 | r << 4 | s)
+  auto candidates = [&](uint32_t pos, uint32_t &pk_l, uint32_t &e_l) {
     if ((pos >> 5) - wbase >= 64) {  // everything needed is in win1: shift, prefetch the next 64 words
       wbase += 64;
       win0 = win1;
@@ -739,8 +775,8 @@ __global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict_
     const uint32_t A = word(W), B = word(W + 1), C = word(W + 2), D = word(W + 3);
     const uint32_t o = sh + lane;
     const uint32_t hi = o < 32 ? A : (o < 64 ? B : C), lo = o < 32 ? B : (o < 64 ? C : D);
-    const uint32_t pk_l = uint32_t(((uint64_t(hi) << 32 | lo) << (o & 31)) >> 32);
-    uint32_t e_l = s_lut[pk_l >> 23];
+    pk_l = uint32_t(((uint64_t(hi) << 32 | lo) << (o & 31)) >> 32);
+    e_l = s_lut[pk_l >> 23];
     if (e_l & 0x8000u) {
       if (e_l == 0xFFFFu) {
         const uint32_t p16 = pk_l >> 16;
@@ -754,10 +790,194 @@ __global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict_
         e_l = s_lut[RJ_LUT_L1 + (e_l & 0xFFu) * 128u + ((pk_l >> 16) & 127u)];
       }
     }
+  };
+  if (kind == RJ_PK_DC_REFINE) {
+    // ---- DC refinement: the records are the interval's bits, one per block in decode order
+    // (lane_dc<true>): record word w = stream bits [64w, 64w + 64), LSB first; zero past the data
+    unsigned long long *rec = recs + im.prec_off + iv.rec_off;
+    const uint64_t nblocks = uint64_t(nunits) * rfl(sc.nblk);
+    const uint32_t nrw = uint32_t((nblocks + 63) / 64);
+    for (uint32_t w = lane; w < nrw; w += 64) {
+      uint64_t v = __builtin_bitreverse64((uint64_t(ldword(2 * w)) << 32) | ldword(2 * w + 1));
+      const uint64_t b0 = uint64_t(w) * 64;
+      const uint64_t lim = min(uint64_t(nbits), nblocks);
+      v = b0 >= lim ? 0ull : (lim - b0 >= 64 ? v : v & ((1ull << (lim - b0)) - 1));
+      *gp(rec + w) = v;
+    }
+    finish(0);
+    return;
+  }
+  if (kind == RJ_PK_DC_FIRST) {
+    // ---- DC first (possibly interleaved): the DC of 64 consecutive blocks collects in the lanes
+    // (lane j: block j of the batch) and leaves as 64 halfword stores ----
+    const uint32_t al = rfl(sc.al), ns = rfl(sc.ns ? uint32_t(sc.ns) : 1u);
+    const uint32_t units_x = rfl(sc.units_x ? uint32_t(sc.units_x) : 1u);
+    const uint32_t tsel = rfl(uint32_t(sc.tsel[0]) | (uint32_t(sc.tsel[1]) << 1) | (uint32_t(sc.tsel[2]) << 2));
+    uint32_t cbq[3], wbq[3], hsq[3], vsq[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const uint32_t c = sc.comp[q] & 3u;
+      cbq[q] = rfl(c == 0 ? im.cblk0[0] : (c == 1 ? im.cblk0[1] : im.cblk0[2]));
+      wbq[q] = rfl(c == 0 ? im.wblk[0] : (c == 1 ? im.wblk[1] : im.wblk[2]));
+      hsq[q] = rfl(sc.hs[q] ? uint32_t(sc.hs[q]) : 1u);
+      vsq[q] = rfl(sc.vs[q] ? uint32_t(sc.vs[q]) : 1u);
+    }
+    uint16_t *coef16 = reinterpret_cast<uint16_t *>(coef + im.coef_off);
+    uint32_t ux = iv.unit0 % units_x, uy = iv.unit0 / units_x;
+    uint32_t pos = 0, u = 0, ci = 0, dx = 0, dy = 0, nb = 0, vblk = 0, vval = 0;
+    int32_t pred0 = 0, pred1 = 0, pred2 = 0;
+    bool done = nunits == 0;
+    auto canon = [&](uint32_t p16, const uint32_t *maxc, const int32_t *voff, const uint8_t *vals) -> uint32_t {
+      for (int l = 1; l <= 16; l++)
+        if (p16 < maxc[l]) return uint32_t(l << 8) | vals[((p16 >> (16 - l)) + voff[l]) & 255];
+      return RJ_LUT_BAD;
+    };
+    while (!done) {
+      // window step: lane l's peek at pos + l and its entry in both tables
+      if ((pos >> 5) - wbase >= 64) {
+        wbase += 64;
+        win0 = win1;
+        win1 = ldword(wbase + 64 + lane);
+      }
+      const uint32_t W = (pos >> 5) - wbase, sh = pos & 31;
+      const uint32_t A = word(W), B = word(W + 1), C = word(W + 2), D = word(W + 3);
+      const uint32_t o = sh + lane;
+      const uint32_t hi = o < 32 ? A : (o < 64 ? B : C), lo = o < 32 ? B : (o < 64 ? C : D);
+      const uint32_t pk_l = uint32_t(((uint64_t(hi) << 32 | lo) << (o & 31)) >> 32);
+      uint32_t e0_l = s_lut[pk_l >> 23], e1_l = s_lut[512 + (pk_l >> 23)];
+      if (e0_l & 0x8000u) e0_l = canon(pk_l >> 16, s_maxc, s_voff, s_vals);
+      if (e1_l & 0x8000u) e1_l = canon(pk_l >> 16, s_maxc1, s_voff1, s_vals1);
+      const uint32_t pos0 = pos;
+      while (!done && pos - pos0 < 64) {
+        const uint32_t d = pos - pos0;
+        const uint32_t en = ((tsel >> ci) & 1u) ? rl(e1_l, d) : rl(e0_l, d);
+        const uint32_t len = en >> 8, s = en & 15u;
+        const int32_t diff = pextend(pbits(rl(pk_l, d), len, s), s);
+        int32_t p;
+        if (ci == 0) p = pred0 += diff;
+        else if (ci == 1) p = pred1 += diff;
+        else p = pred2 += diff;
+        pos += len + s;
+        const uint32_t h = ci == 0 ? hsq[0] : (ci == 1 ? hsq[1] : hsq[2]);
+        const uint32_t v = ci == 0 ? vsq[0] : (ci == 1 ? vsq[1] : vsq[2]);
+        const uint32_t cb = ci == 0 ? cbq[0] : (ci == 1 ? cbq[1] : cbq[2]);
+        const uint32_t wb = ci == 0 ? wbq[0] : (ci == 1 ? wbq[1] : wbq[2]);
+        if (lane == nb) {
+          vblk = cb + (uy * v + dy) * wb + ux * h + dx;
+          vval = uint32_t(p) << al;
+        }
+        if (++nb == 64) {
+          gst16(coef16 + vblk * 64u, vval);
+          nb = 0;
+        }
+        // next slot of the unit
+        if (++dx == h) {
+          dx = 0;
+          if (++dy == v) {
+            dy = 0;
+            if (++ci == ns) {
+              ci = 0;
+              u++;
+              if (++ux == units_x) {
+                ux = 0;
+                uy++;
+              }
+              done = u >= nunits || pos > nbits;
+            }
+          }
+        }
+      }
+    }
+    if (lane < nb) gst16(coef16 + vblk * 64u, vval);
+    finish(0);
+    return;
+  }
+  if (kind == RJ_PK_AC_FIRST) {
+    // ---- AC first scan: coefficient q of the current block sits in lane q until the block ends ----
+    const uint32_t al = rfl(sc.al);
+    const uint32_t units_x = rfl(sc.units_x ? uint32_t(sc.units_x) : 1u);
+    const uint32_t cb = c0 == 0 ? im.cblk0[0] : (c0 == 1 ? im.cblk0[1] : im.cblk0[2]);
+    const uint32_t wb = c0 == 0 ? im.wblk[0] : (c0 == 1 ? im.wblk[1] : im.wblk[2]);
+    uint16_t *coef16 = reinterpret_cast<uint16_t *>(coef + im.coef_off);
+    uint32_t ux = iv.unit0 % units_x, uy = iv.unit0 / units_x;
+    uint32_t pos = 0, k = ss, u = 0, published = 0, cur = 0;
+    uint64_t curm = 0;
+    bool done = nunits == 0;
+    while (!done) {
+      uint32_t pk_l, e_l;
+      candidates(pos, pk_l, e_l);
+      const uint32_t pos0 = pos;
+      while (!done && pos - pos0 < 64) {
+        const uint32_t d = pos - pos0;
+        const uint32_t en = rl(e_l, d);
+        const uint32_t len = en >> 8, r = (en >> 4) & 15u, s = en & 15u;
+        uint32_t eobrun = 0;
+        if (s) {
+          const uint32_t q = min(k + r, 63u);
+          const int32_t v = pextend(pbits(rl(pk_l, d), len, s), s);
+          const uint32_t hv = ((uint32_t(v < 0 ? -v : v) << al) & 0x7FFFu) | (v < 0 ? 0x8000u : 0u);
+          if (lane == q) cur = hv;
+          curm |= 1ull << q;
+          k += r + 1;
+          pos += len + s;
+        } else if (r == 15) {
+          k += 16;
+          pos += len;
+        } else {  // EOBr: this block and eobrun more end here
+          eobrun = r ? (1u << r) + pbits(rl(pk_l, d), len, r) - 1u : 0u;
+          k = se + 1;
+          pos += len + r;
+        }
+        if (k <= se) continue;
+        // ---- block end: its coefficients (one masked halfword store) and nonzero mask ----
+        if (curm) {
+          const uint32_t blk = cb + uy * wb + ux;
+          if ((curm >> lane) & 1u) gst16(coef16 + blk * 64u + lane, cur);
+          if (lane == 0) gor64(nzs + u, curm);  // other scans of the component share the word
+          curm = 0;
+        }
+        k = ss;
+        const uint32_t step = 1u + min(eobrun, nunits - u - 1u);
+        u += step;
+        ux += step;
+        if (ux >= units_x) {
+          uy += ux / units_x;
+          ux %= units_x;
+        }
+        done = u >= nunits || pos > nbits;
+        if (done || (u >> 6) != (published >> 6)) {
+          publish(done ? RJ_PROG_DONE : u);
+          published = u;
+        }
+      }
+    }
+    publish(RJ_PROG_DONE);
+    return;
+  }
+  unsigned long long *rec = recs + im.prec_off + iv.rec_off;
+  auto ldnz = [&](uint32_t u) -> uint64_t { return *gp(nzs + min(u, nunits - 1)); };
+  // nonzero masks of units [nbase, nbase + 64)
+  uint32_t nbase = 0;
+  if (nunits) wait_producers(0);
+  if (stamp.p && threadIdx.x == 0) *gp(stamp.p + 1) = wall_clock64();
+  uint64_t nzw = ldnz(lane);
+  uint64_t r_cs = 0, r_sg = 0, r_nw = 0;  // lane b: record of unit rbase + b
+  uint32_t rbase = 0;
+  uint32_t pos = 0, k = ss, eobrun = 0, u = 0;
+  uint64_t nzm = uint64_t(rl(uint32_t(nzw), 0)) | (uint64_t(rl(uint32_t(nzw >> 32), 0)) << 32);
+  nzm &= band;
+  uint64_t cstr = 0, sgn = 0, newm = 0;
+  uint32_t pend = 0, t = 0, newv = 0;
+  bool walking = false, eobblk = false, done = nunits == 0;
+  while (!done) {
+    uint32_t pk_l, e_l;
+    candidates(pos, pk_l, e_l);
     const uint32_t pos0 = pos;
+    stamp.nwin++;
     // ---- scalar chain over the window ----
     while (!done && pos - pos0 < 64) {
       const uint32_t d = pos - pos0;
+      stamp.nstep++;
       const uint32_t pk = rl(pk_l, d);
       uint32_t used = 0;
       if (!walking) {
@@ -838,7 +1058,8 @@ __global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict_
           // the word: atomic); k_prog_fold peels them again where it needs the earlier state
           if (r_nw) gor64(nzs + rbase + lane, r_nw);
         }
-        publish(done ? RJ_PROG_DONE : u);
+        if (done) finish(nbase);
+        else publish(u);
         r_cs = r_sg = r_nw = 0;
         rbase += 64;
       }
@@ -852,15 +1073,16 @@ __global__ __launch_bounds__(64) void k_prog_acref(const RjImageDev *__restrict_
       nzm = (uint64_t(rl(uint32_t(nzw), nl)) | (uint64_t(rl(uint32_t(nzw >> 32), nl)) << 32)) & band;
     }
   }
-  publish(RJ_PROG_DONE);  // every exit (an empty interval never flushed)
+  finish(nbase);  // every exit (an empty interval never flushed)
 }
 
-hipError_t LaunchProgressiveAcRefine(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *ivals, uint32_t n,
-                                     const uint8_t *destuffed, unsigned long long *nz,
-                                     unsigned long long *recs, uint32_t *progress, uint32_t progress_n) {
+hipError_t LaunchProgressiveWave(hipStream_t st, const RjImageDev *imgs, int nimg, const uint32_t *ivals, uint32_t n,
+                                 const uint8_t *destuffed, uint32_t *coef, unsigned long long *nz,
+                                 unsigned long long *recs, uint32_t *progress, uint32_t progress_n,
+                                 unsigned long long *stamps, uint32_t flags) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_prog_acref, dim3(n), dim3(64), 0, st, imgs, nimg, ivals, destuffed, nz, recs, progress,
-                     progress_n);
+  hipLaunchKernelGGL(k_prog_wave, dim3(n), dim3(64), 0, st, imgs, nimg, ivals, destuffed, coef, nz, recs, progress,
+                     progress_n, stamps, flags);
   return hipGetLastError();
 }
 
@@ -913,7 +1135,7 @@ __global__ __launch_bounds__(64) void k_prog_fold(const RjImageDev *__restrict__
       w[4 * q + 3] = v.w;
     }
   };
-  // the masks already hold every new position of the scans folded here (k_prog_acref ORs them
+  // the masks already hold every new position of the scans folded here (k_prog_wave ORs them
   // in); walking the scans backwards and peeling each scan's new positions gives the masks each
   // scan saw when it decoded
   const unsigned long long *nzp = nz + im.nz_off + nzb0 + by * cwb + bx;

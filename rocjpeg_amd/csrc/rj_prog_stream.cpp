@@ -378,9 +378,9 @@ bool Stream::ParseProgressive(const uint8_t *d, uint32_t n) {
   // complement arithmetic only for consistent successive approximation, so such streams (and
   // first scans over already-coded coefficients) are refused with JPEG_NOT_SUPPORTED.
   int coef_bits[3][64];
-  int lastlev[3][64];
+  int lastlev[3][64], lastscan[3][64];
   for (int c = 0; c < 3; c++)
-    for (int k = 0; k < 64; k++) coef_bits[c][k] = lastlev[c][k] = -1;
+    for (int k = 0; k < 64; k++) coef_bits[c][k] = lastlev[c][k] = lastscan[c][k] = -1;
   bool bogus = false;
   p.plevels = 0;
   p.pscans.clear();
@@ -416,16 +416,23 @@ bool Stream::ParseProgressive(const uint8_t *d, uint32_t n) {
       for (int k = v.ss; k <= v.se; k++) lastlev[v.comp[i]][k] = lev;
     v.level = uint8_t(std::min(lev, 255));
     p.plevels = std::max<uint32_t>(p.plevels, uint32_t(v.level) + 1);
+    // producers for the pipelined launch: the latest earlier scan of each coefficient of the band
+    // (that scan waited for its own producers, so its progress covers theirs)
     v.nprod = 0;
-    if (v.kind == RJ_PK_AC_REFINE) {  // producers for the pipelined refinement launch
-      for (size_t r = 0; r < p.pscans.size(); r++) {
-        const RjProgScanDev &q = p.pscans[r];
-        if (q.kind != RJ_PK_AC_REFINE || q.comp[0] != v.comp[0] || q.se < v.ss || q.ss > v.se) continue;
-        if (v.nprod < 3) v.prod[v.nprod++] = uint8_t(r);
+    if (v.kind == RJ_PK_AC_REFINE) {
+      const int c = v.comp[0];
+      for (int k = v.ss; k <= v.se && v.nprod != 0xFF; k++) {
+        const int r = lastscan[c][k];
+        if (r < 0) continue;  // refinement of an uncoded coefficient: bogus, refused below
+        bool seen = false;
+        for (int q = 0; q < v.nprod; q++) seen = seen || v.prod[q] == r;
+        if (seen) continue;
+        if (v.nprod < 3 && r < 0xFF) v.prod[v.nprod++] = uint8_t(r);
         else v.nprod = 0xFF;
-        if (v.nprod == 0xFF) break;
       }
     }
+    for (int i = 0; i < v.ns; i++)
+      for (int k = v.ss; k <= v.se; k++) lastscan[v.comp[i]][k] = int(p.pscans.size());
     p.pscans.push_back(v);
   }
   if (bogus) {

@@ -156,23 +156,41 @@ def test_progressive_timings(dec):
     assert t["prog_images"] == 1 and t["prog_levels"] >= 2 and t["prog_intervals"] == 10
     assert t["prog_entropy_ms"] > 0 and t["prog_rows_ms"] > 0
     assert t["prog_coef_bytes"] == 1920 * 1088 * 3 // 2 * 2  # 4:2:0, MCU-padded, int16
+    # per-kernel launches: first-scan lanes (+ DC refinement lanes), AC refinement waves, fold
+    assert t["prog_kernel_launches"][1] >= 1 and t["prog_kernel_launches"][2] >= 1
+    assert all(t["prog_kernel_ms"][j] > 0 and t["prog_kernel_bytes"][j] > 0 for j in (1, 2))
+    assert sum(t["prog_kernel_ms"][1:]) <= t["prog_entropy_ms"] * 1.01
 
 
-def test_level_by_level_refinement_matches_oracle():
-    """RJ_PROG_PIPE=0: the refinement scans run level by level (the path taken when a scan has
-    more than three producer scans) -- same bytes as the pipelined default."""
+LAYOUTS = {
+    # the refinement scans level by level (the path taken when a scan has more than three
+    # producer scans)
+    "level_by_level": {"RJ_PROG_PIPE": "0"},
+    # pipelined, first scans in lanes before the wave grid (the large-batch layout)
+    "lanes_then_grid": {"RJ_PROG_WAVE_ALL": "0"},
+    # pipelined, every scan in the wave grid (the small-batch layout)
+    "all_waves": {"RJ_PROG_WAVE_ALL": "1"},
+}
+
+
+@pytest.mark.parametrize("layout", list(LAYOUTS))
+def test_progressive_layouts_match_oracle(layout):
+    """Each launch layout of the progressive path (rj_decoder.cpp, prog_pipe / prog_wave_all),
+    forced through its environment switch -- same bytes as the oracle for every fixture."""
     import os
     from tests import gpu_util as G
     G.torch()
-    old = os.environ.get("RJ_PROG_PIPE")
-    os.environ["RJ_PROG_PIPE"] = "0"
+    env = LAYOUTS[layout]
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         d = R.JpegDecoder(R.Backend.HARDWARE, 0)
     finally:
-        if old is None:
-            del os.environ["RJ_PROG_PIPE"]
-        else:
-            os.environ["RJ_PROG_PIPE"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     try:
         datas = [O.fixture_bytes(e) for e in PROG]
         streams = [R.JpegStream(x) for x in datas]
