@@ -673,9 +673,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         if (sc.kind == RJ_PK_AC_REFINE && sc.nprod == 0xFF) prog_pipe = false;
     // pipelined layouts: a small batch puts every scan in the wave grid (each image's scans run
     // side by side: lowest latency); a large one decodes the first scans (all at level 0) in
-    // lanes before the grid and the DC refinements in lanes beside it -- a lane decodes a scan
-    // with far fewer instructions per symbol than a wave's scalar chain, and with ~10 waves per
-    // image the grid would outgrow the chip's wave slots
+    // lanes before the grid and the DC refinements in lanes beside it -- lanes decode 64 scans
+    // per instruction stream where a wave's scalar chain decodes one, and with ~10 waves per
+    // image the grid would outgrow the chip's wave slots (C5, 1024 images: 149 ms vs 175 ms;
+    // DC scans as waves at the grid's end: 160 ms)
     prog_wave_all = prog_pipe && (prog_wave_all_ >= 0 ? prog_wave_all_ != 0 : prog_images <= kProgWaveAllImages);
     auto in_lanes = [&](uint32_t kind) {
       return !prog_pipe ? kind != RJ_PK_AC_REFINE : (!prog_wave_all && kind != RJ_PK_AC_REFINE);

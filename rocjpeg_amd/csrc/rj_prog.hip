@@ -725,11 +725,8 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
     return;
   }
   const uint32_t kind = rfl(sc.kind);
-  // DC first: both tables' first levels (s_lut[0, 512) and [512, 1024)) and, for longer codes,
-  // table 1's canonical bounds and symbols where the AC second levels would go
-  uint32_t *const s_maxc1 = reinterpret_cast<uint32_t *>(s_lut + 1024);
-  int32_t *const s_voff1 = reinterpret_cast<int32_t *>(s_lut + 1024) + 18;
-  uint8_t *const s_vals1 = reinterpret_cast<uint8_t *>(s_lut + 1024) + 144;
+  // DC first: both tables' first levels (s_lut[0, 512) and [512, 1024)); longer codes are
+  // decoded canonically in the chain
   if (kind != RJ_PK_DC_REFINE) {
     const RjHuffDev *gt = im.ptabs + sc.tab[0];
     const uint4 *src = reinterpret_cast<const uint4 *>(gt->lut);
@@ -738,11 +735,6 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
       const RjHuffDev *gt1 = im.ptabs + (sc.tab[1] == 0xFFFFu ? sc.tab[0] : sc.tab[1]);
       dst[lane] = gp(src)[lane];
       dst[64 + lane] = gp(reinterpret_cast<const uint4 *>(gt1->lut))[lane];
-      if (lane < 18) {
-        s_maxc1[lane] = gp(gt1->maxcode16)[lane];
-        s_voff1[lane] = gp(gt1->valoff)[lane];
-      }
-      reinterpret_cast<uint32_t *>(s_vals1)[lane] = gp(reinterpret_cast<const uint32_t *>(gt1->vals))[lane];
     } else {
       for (uint32_t q = lane; q < RJ_LUT_ENTRIES * 2 / 16; q += 64) dst[q] = gp(src)[q];
     }
@@ -827,9 +819,13 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
     uint32_t pos = 0, u = 0, ci = 0, dx = 0, dy = 0, nb = 0, vblk = 0, vval = 0;
     int32_t pred0 = 0, pred1 = 0, pred2 = 0;
     bool done = nunits == 0;
-    auto canon = [&](uint32_t p16, const uint32_t *maxc, const int32_t *voff, const uint8_t *vals) -> uint32_t {
+    // codes longer than 9 bits: canonical decode at the true symbol positions only (scalar loads
+    // from the table in global memory; rare), not at every candidate offset
+    const RjHuffDev *gdc0 = im.ptabs + sc.tab[0];
+    const RjHuffDev *gdc1 = im.ptabs + (sc.tab[1] == 0xFFFFu ? sc.tab[0] : sc.tab[1]);
+    auto canon = [&](uint32_t p16, const RjHuffDev *g) -> uint32_t {
       for (int l = 1; l <= 16; l++)
-        if (p16 < maxc[l]) return uint32_t(l << 8) | vals[((p16 >> (16 - l)) + voff[l]) & 255];
+        if (p16 < gp(g->maxcode16)[l]) return uint32_t(l << 8) | gp(g->vals)[((p16 >> (16 - l)) + gp(g->valoff)[l]) & 255];
       return RJ_LUT_BAD;
     };
     while (!done) {
@@ -844,15 +840,16 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
       const uint32_t o = sh + lane;
       const uint32_t hi = o < 32 ? A : (o < 64 ? B : C), lo = o < 32 ? B : (o < 64 ? C : D);
       const uint32_t pk_l = uint32_t(((uint64_t(hi) << 32 | lo) << (o & 31)) >> 32);
-      uint32_t e0_l = s_lut[pk_l >> 23], e1_l = s_lut[512 + (pk_l >> 23)];
-      if (e0_l & 0x8000u) e0_l = canon(pk_l >> 16, s_maxc, s_voff, s_vals);
-      if (e1_l & 0x8000u) e1_l = canon(pk_l >> 16, s_maxc1, s_voff1, s_vals1);
+      const uint32_t e0_l = s_lut[pk_l >> 23], e1_l = s_lut[512 + (pk_l >> 23)];
       const uint32_t pos0 = pos;
       while (!done && pos - pos0 < 64) {
         const uint32_t d = pos - pos0;
-        const uint32_t en = ((tsel >> ci) & 1u) ? rl(e1_l, d) : rl(e0_l, d);
+        const uint32_t t1 = (tsel >> ci) & 1u;
+        const uint32_t pk = rl(pk_l, d);
+        uint32_t en = t1 ? rl(e1_l, d) : rl(e0_l, d);
+        if (en & 0x8000u) en = canon(pk >> 16, t1 ? gdc1 : gdc0);
         const uint32_t len = en >> 8, s = en & 15u;
-        const int32_t diff = pextend(pbits(rl(pk_l, d), len, s), s);
+        const int32_t diff = pextend(pbits(pk, len, s), s);
         int32_t p;
         if (ci == 0) p = pred0 += diff;
         else if (ci == 1) p = pred1 += diff;
