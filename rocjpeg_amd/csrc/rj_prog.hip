@@ -347,12 +347,16 @@ __device__ __forceinline__ void lane_ac_first(const PLaneIn &L, PGeo &g, PBits &
       e = (e & 0x8000u) ? el : e;
       const uint32_t len = e >> 8, r = (e >> 4) & 15u, s = e & 15u;
       if (s) {
+        // corrupt data can run past Se; such a coefficient is dropped (libjpeg would store it
+        // outside the band, where another scan of this component may be writing concurrently)
         const uint32_t q = min(k + r, 63u);
         const int32_t v = pextend(pbits(peek, len, s), s);
         const uint32_t mag = (uint32_t(v < 0 ? -v : v) << al) & 0x7FFFu;
         const uint32_t blk = pblock(g, 0, 0, 0);
-        gst16(coef16 + (g.coef + blk * 32u) * 2u + q, mag | (v < 0 ? 0x8000u : 0u));
-        blk_nz |= 1ull << q;
+        if (q <= se) {
+          gst16(coef16 + (g.coef + blk * 32u) * 2u + q, mag | (v < 0 ? 0x8000u : 0u));
+          blk_nz |= 1ull << q;
+        }
         k += r + 1;
         br.pos += len + s;
       } else if (r == 15) {
@@ -496,7 +500,7 @@ __device__ __forceinline__ void lane_ac_refine(const PLaneIn &L, PGeo &g, PBits 
       bool blk_done = false;
       if (pend == 0) {
         walking = false;
-        if (newv) {
+        if (newv && min(t, 63u) <= se) {  // past Se (corrupt data): dropped, see lane_ac_first
           const uint64_t bq = 1ull << min(t, 63u);
           blk_new |= bq;
           if (newv == 2) sgn |= bq;
@@ -913,8 +917,10 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
           const uint32_t q = min(k + r, 63u);
           const int32_t v = pextend(pbits(rl(pk_l, d), len, s), s);
           const uint32_t hv = ((uint32_t(v < 0 ? -v : v) << al) & 0x7FFFu) | (v < 0 ? 0x8000u : 0u);
-          if (lane == q) cur = hv;
-          curm |= 1ull << q;
+          if (q <= se) {  // past Se (corrupt data): dropped, as in lane_ac_first
+            if (lane == q) cur = hv;
+            curm |= 1ull << q;
+          }
           k += r + 1;
           pos += len + s;
         } else if (r == 15) {
@@ -1021,7 +1027,7 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
       pos += used;
       if (pend) continue;  // the walk resumes at the next peek
       walking = false;
-      if (newv) {
+      if (newv && min(t, 63u) <= se) {  // past Se (corrupt data): dropped, as in lane_ac_refine
         const uint64_t bq = 1ull << min(t, 63u);
         newm |= bq;
         if (newv == 2) sgn |= bq;
