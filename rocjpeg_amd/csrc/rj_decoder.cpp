@@ -384,7 +384,7 @@ int Decoder::Decode(Stream *const *streams, int n, const RocJpegDecodeParams *pa
 }
 
 // progressive images per call up to which every scan goes to the wave grid (see prog_wave_all)
-static constexpr int kProgWaveAllImages = 640;  // measured crossover (C5 1080p: 512 -> waves, 1024 -> lanes)
+static constexpr int kProgWaveAllImages = 192;  // measured crossover (C5 1080p: 64 -> one grid, 256 -> two)
 
 int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
   const auto t_host0 = std::chrono::steady_clock::now();
@@ -660,6 +660,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   prog_lanes.clear();
   uint32_t prog_level_off[257] = {}, fold_off[257] = {}, fold_chunks[257] = {}, wave_off[257] = {};
   bool prog_pipe = false, prog_wave_all = false;
+  uint32_t wave_first_end = 0;  // pipelined, large batch: wave list [wave_off[0], here) = first scans
   std::vector<RjFoldJob> &fold_jobs = sc_.fold_jobs;
   const uint32_t nlev = std::min<uint32_t>(prog_levels, 256);
   if (prog_images) {
@@ -671,16 +672,13 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     for (int i = 0; i < n && prog_pipe; i++)
       for (const RjProgScanDev &sc : streams[i]->plan().pscans)
         if (sc.kind == RJ_PK_AC_REFINE && sc.nprod == 0xFF) prog_pipe = false;
-    // pipelined layouts: a small batch puts every scan in the wave grid (each image's scans run
-    // side by side: lowest latency); a large one decodes the first scans (all at level 0) in
-    // lanes before the grid and the DC refinements in lanes beside it -- lanes decode 64 scans
-    // per instruction stream where a wave's scalar chain decodes one, and with ~10 waves per
-    // image the grid would outgrow the chip's wave slots (C5, 1024 images: 149 ms vs 175 ms;
-    // DC scans as waves at the grid's end: 160 ms)
+    // pipelined layouts: a small batch puts every scan in one wave grid (each image's scans run
+    // side by side: lowest latency); a large one decodes the AC first scans in a grid of their
+    // own ahead of the refinement grid -- with ten waves per image one grid would outgrow the
+    // chip's wave slots and the first scans' chains would contend with the refinement chains
+    // (C5, 1024 images: 137 ms vs 175 ms one grid, 151 ms first scans in lanes)
     prog_wave_all = prog_pipe && (prog_wave_all_ >= 0 ? prog_wave_all_ != 0 : prog_images <= kProgWaveAllImages);
-    auto in_lanes = [&](uint32_t kind) {
-      return !prog_pipe ? kind != RJ_PK_AC_REFINE : (!prog_wave_all && kind != RJ_PK_AC_REFINE);
-    };
+    auto in_lanes = [&](uint32_t kind) { return !prog_pipe && kind != RJ_PK_AC_REFINE; };
     // algorithmic bytes of an interval: destuffed bytes read + what its decode writes (DC first:
     // one halfword per block; DC refinement: one bit per block; AC first: the band's halfwords +
     // the nonzero mask; AC refinement: mask read + one 32-B record per block)
@@ -739,8 +737,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       // with slack: the largest component's AC scans first (its refinement chain is the critical
       // path), then the other components' AC scans, then the DC scans; level order within each.
       wave_off[0] = uint32_t(prog_lanes.size());
-      for (uint32_t rank = 0; rank < 4; rank++)
-        for (uint32_t L = 0; L < nlev; L++)
+      // large batches: the first scans in a grid of their own ahead of the refinement grid
+      // (phase 0), the rest after (phase 1); small batches: everything in one grid
+      for (uint32_t phase = 0; phase < 2; phase++) {
+        if (phase == 1) wave_first_end = uint32_t(prog_lanes.size());
+        for (uint32_t rank = 0; rank < 4; rank++)
+          for (uint32_t L = 0; L < nlev; L++)
           for (int i = 0; i < n; i++) {
             const DecodePlan &p = streams[i]->plan();
             if (!p.progressive) continue;
@@ -760,11 +762,15 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
                 }
                 r = std::min<uint32_t>(r, 2);
               }
-              if (r != rank || in_lanes(sc.kind)) continue;
+              const bool first = sc.kind == RJ_PK_AC_FIRST;  // DC first: nothing waits, grid end
+              if (r != rank || (!prog_wave_all && first != (phase == 0)) || (prog_wave_all && phase == 1))
+                continue;
               prog_lanes.push_back(imgs[i].pival_prefix + q);  // missing ones too: they report DONE
               if (!(iv.flags & RJ_SEG_MISSING)) timings_.prog_kernel_bytes[1] += ival_bytes(sc, iv);
             }
           }
+      }
+      if (prog_wave_all) wave_first_end = wave_off[0];
       for (uint32_t L = 1; L < nlev; L++) wave_off[L] = wave_off[0];
     } else {
       // AC refinement intervals (one wave each), per level, after the lane lists
@@ -1025,20 +1031,21 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       // stream, and every AC interval in one k_prog_wave grid (level order, a scan following its
       // producers); one fold over all levels once both are done
       RJ_HIP(hipMemsetAsync(d_pprog_.as<uint32_t>(), 0, uint64_t(pival_total + 1) * 4, stream_));
-      // lane layout: the first scans (level 0) before the grid
-      const uint32_t L0 = prog_wave_all ? 0u : 1u;
-      if (!prog_wave_all && prog_level_off[1] > prog_level_off[0]) {
+      // large batch: the first scans' grid (nothing in it waits) before the refinement grid
+      if (wave_first_end > wave_off[0]) {
         RJ_HIP(pk_begin(stream_));
-        RJ_HIP(LaunchProgressive(stream_, d_imgs, n, d_plane + prog_level_off[0], prog_level_off[1] - prog_level_off[0],
-                                 d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
-                                 d_prec_.as<unsigned long long>()));
-        RJ_HIP(pk_end(stream_, 0, prog_level_off[1] - prog_level_off[0]));
+        RJ_HIP(LaunchProgressiveWave(stream_, d_imgs, n, d_plane + wave_off[0], wave_first_end - wave_off[0],
+                                     d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
+                                     d_prec_.as<unsigned long long>(), nullptr, 0u));
+        RJ_HIP(pk_end(stream_, 1, wave_first_end - wave_off[0]));
       }
-      const bool side = prog_level_off[nlev] > prog_level_off[std::min(L0, nlev)];
+      // (lanes only in the level-by-level layout; the side stream stays for scripts whose
+      // DC scans would need lanes)
+      const bool side = prog_level_off[nlev] > prog_level_off[0];
       if (side) {
         RJ_HIP(hipEventRecord(prog_join_[0], stream_));
         RJ_HIP(hipStreamWaitEvent(pstream_[0], prog_join_[0], 0));
-        for (uint32_t L = L0; L < nlev; L++) {
+        for (uint32_t L = 0; L < nlev; L++) {
           RJ_HIP(pk_begin(pstream_[0]));
           RJ_HIP(LaunchProgressive(pstream_[0], d_imgs, n, d_plane + prog_level_off[L],
                                    prog_level_off[L + 1] - prog_level_off[L], d_destuff_.as<uint8_t>(),
@@ -1050,15 +1057,15 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       }
       unsigned long long *wstamps = nullptr;
       if (getenv("RJ_DEBUG_WAVES")) {
-        RJ_CHECK(d_wstamp_.Ensure(std::max<uint64_t>(uint64_t(wave_off[nlev] - wave_off[0]) * 32, 256)));
+        RJ_CHECK(d_wstamp_.Ensure(std::max<uint64_t>(uint64_t(wave_off[nlev] - wave_first_end) * 32, 256)));
         wstamps = d_wstamp_.as<unsigned long long>();
       }
       RJ_HIP(pk_begin(stream_));
-      RJ_HIP(LaunchProgressiveWave(stream_, d_imgs, n, d_plane + wave_off[0], wave_off[nlev] - wave_off[0],
+      RJ_HIP(LaunchProgressiveWave(stream_, d_imgs, n, d_plane + wave_first_end, wave_off[nlev] - wave_first_end,
                                    d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
                                    d_prec_.as<unsigned long long>(), d_pprog_.as<uint32_t>(), pival_total, wstamps,
                                    prog_wave_all ? 0u : RJ_WAVE_FIRST_DONE));
-      RJ_HIP(pk_end(stream_, 1, wave_off[nlev] - wave_off[0]));
+      RJ_HIP(pk_end(stream_, 1, wave_off[nlev] - wave_first_end));
       if (side) RJ_HIP(hipStreamWaitEvent(stream_, prog_join_[1], 0));
       RJ_HIP(pk_begin(stream_));
       RJ_HIP(LaunchProgressiveFold(stream_, d_imgs, d_fold + fold_off[0], fold_off[1] - fold_off[0], fold_chunks[0],
@@ -1277,7 +1284,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       return kExecutionFailed;
     }
     if (getenv("RJ_DEBUG_WAVES")) {  // per scan of the batch's first image layout: wave timing
-      const uint32_t nw = wave_off[nlev] - wave_off[0];
+      const uint32_t nw = wave_off[nlev] - wave_first_end;
       std::vector<unsigned long long> st(size_t(nw) * 4);
       RJ_HIP(hipMemcpy(st.data(), d_wstamp_.as<unsigned long long>(), st.size() * 8, hipMemcpyDeviceToHost));
       unsigned long long t0 = ~0ull;
@@ -1288,7 +1295,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       };
       std::vector<Acc> acc(256);
       for (uint32_t w = 0; w < nw; w++) {
-        const uint32_t gi = prog_lanes[wave_off[0] + w];
+        const uint32_t gi = prog_lanes[wave_first_end + w];
         int i = 0;
         while (i + 1 < n && imgs[i + 1].pival_prefix <= gi) i++;
         const uint32_t scan = streams[i]->plan().pivals[gi - imgs[i].pival_prefix].scan & 255u;
