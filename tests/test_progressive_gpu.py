@@ -166,10 +166,10 @@ LAYOUTS = {
     # the refinement scans level by level (the path taken when a scan has more than three
     # producer scans)
     "level_by_level": {"RJ_PROG_PIPE": "0"},
-    # pipelined, first scans in lanes before the wave grid (the large-batch layout)
-    "lanes_then_grid": {"RJ_PROG_WAVE_ALL": "0"},
-    # pipelined, every scan in the wave grid (the small-batch layout)
-    "all_waves": {"RJ_PROG_WAVE_ALL": "1"},
+    # pipelined, the AC first scans in a wave grid ahead of the refinement grid (large batches)
+    "two_grids": {"RJ_PROG_WAVE_ALL": "0"},
+    # pipelined, every scan in one wave grid (small batches)
+    "one_grid": {"RJ_PROG_WAVE_ALL": "1"},
 }
 
 
