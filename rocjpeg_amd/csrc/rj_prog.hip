@@ -677,8 +677,10 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
   // masks out, and a later scan's interval waits for its producers' units before it reads masks
   auto publish = [&](uint32_t units_out) {
     if (progress == nullptr) return;
-    __threadfence();  // records and mask updates before the count (release)
-    if (threadIdx.x == 0) __hip_atomic_store(progress + gi, units_out, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    // mask updates before the count: one release fence (a seq_cst __threadfence would also
+    // invalidate the L2), then a relaxed store
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (threadIdx.x == 0) __hip_atomic_store(progress + gi, units_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   const RjProgScanDev &sc = *gp(im.pscans + iv.scan);
   const uint32_t ss = rfl(sc.ss), se = rfl(sc.se);
@@ -691,31 +693,47 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
       nz + im.nz_off + (c0 == 0 ? im.nzblk0[0] : (c0 == 1 ? im.nzblk0[1] : im.nzblk0[2])) + iv.unit0;
   const uint32_t nprod = progress ? min(uint32_t(sc.nprod), 3u) : 0u;
   uint32_t *progress_err = progress ? progress + progress_n : nullptr;
+  // the last count seen per producer (its interval index, count): units below it need neither a
+  // poll nor another acquire fence
+  uint32_t seen_j0 = ~0u, seen_j1 = ~0u, seen_j2 = ~0u, seen_n0 = 0, seen_n1 = 0, seen_n2 = 0;
   auto wait_units = [&](uint32_t ub, uint32_t ue) {  // producers' masks of units [ub, ue) are out
     if (ub >= ue) return;
     const uint32_t lo = iv.unit0 + ub, hi = iv.unit0 + ue;
-    for (uint32_t q = 0; q < nprod; q++) {
+    bool polled = false;
+#pragma unroll
+    for (uint32_t q = 0; q < 3; q++) {
+      if (q >= nprod) break;
       const uint32_t pq = rfl(q == 0 ? sc.prod[0] : (q == 1 ? sc.prod[1] : sc.prod[2]));
       const RjProgScanDev *ps = im.pscans + pq;
-      // first scans decoded in lanes before this grid: nothing to wait for
+      // first scans decoded before this grid: nothing to wait for
       if ((flags & RJ_WAVE_FIRST_DONE) && rfl(gp(ps)->kind) == RJ_PK_AC_FIRST) continue;
       const uint32_t pri = rfl(gp(ps)->ri), pival0 = rfl(gp(ps)->ival0);
       const uint32_t j0 = pri ? lo / pri : 0u, j1 = pri ? (hi - 1) / pri : 0u;
+      uint32_t &sj = q == 0 ? seen_j0 : (q == 1 ? seen_j1 : seen_j2);
+      uint32_t &sn = q == 0 ? seen_n0 : (q == 1 ? seen_n1 : seen_n2);
       for (uint32_t j = j0; j <= j1; j++) {
         const uint32_t s0 = pri ? j * pri : 0u;
         const uint32_t need = hi - s0;  // units of producer interval j (capped by its DONE)
+        if (j == sj && need <= sn) continue;
         uint32_t *pp = progress + im.pival_prefix + pival0 + j;
-        // bounded (~4 s): a producer that never reports would otherwise hang the GPU; the host
-        // turns the flag into EXECUTION_FAILED
-        for (uint32_t spin = 0; __hip_atomic_load(pp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need; spin++) {
+        // relaxed polls (an acquire load would invalidate the L2 on every poll), then one acquire
+        // fence; bounded (~4 s): a producer that never reports would otherwise hang the GPU --
+        // the host turns the flag into EXECUTION_FAILED
+        uint32_t got = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t spin = 0; got < need; spin++) {
           if (spin >= (1u << 23)) {
             if (threadIdx.x == 0) __hip_atomic_store(progress_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
           }
           __builtin_amdgcn_s_sleep(8);
+          got = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        sj = j;
+        sn = rfl(got);
+        polled = true;
       }
     }
+    if (polled) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   };
   auto wait_producers = [&](uint32_t ub) { wait_units(ub, min(ub + 64, nunits)); };
   // a scan's progress stands for its producers' too (a consumer lists only the latest scan of each
@@ -749,24 +767,27 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
     reinterpret_cast<uint32_t *>(s_vals)[lane] = gp(reinterpret_cast<const uint32_t *>(gt->vals))[lane];
   }
   __syncthreads();
-  auto ldword = [&](uint32_t w) -> uint32_t {  // word w of the interval, zero past the data
-    const uint32_t v = *gp(data + min(w, nwords ? nwords - 1 : 0u));
-    return w < nwords ? __builtin_bswap32(v) : 0u;
-  };
-  // windows: bitstream words [wbase, wbase + 128) in win0/win1 (lane l: word wbase + l / + 64 + l)
+  auto ldraw = [&](uint32_t w) -> uint32_t { return *gp(data + min(w, nwords ? nwords - 1 : 0u)); };
+  auto cvt = [&](uint32_t w, uint32_t v) -> uint32_t { return w < nwords ? __builtin_bswap32(v) : 0u; };
+  auto ldword = [&](uint32_t w) -> uint32_t { return cvt(w, ldraw(w)); };  // zero past the data
+  // windows: bitstream words [wbase, wbase + 128) in win0/win1 (lane l: word wbase + l / + 64 + l);
+  // the 64 words after them wait unconverted in win2 -- loaded a whole window ahead, so a slide
+  // never waits on memory (a wait would also wait for every store the wave has in flight)
   uint32_t wbase = 0;
-  uint32_t win0 = ldword(lane), win1 = ldword(64 + lane);
+  uint32_t win0 = ldword(lane), win1 = ldword(64 + lane), win2 = ldraw(128 + lane);
+  auto slide = [&]() {
+    wbase += 64;
+    win0 = win1;
+    win1 = cvt(wbase + 64 + lane, win2);
+    win2 = ldraw(wbase + 128 + lane);
+  };
   auto word = [&](uint32_t w) -> uint32_t {  // w relative to wbase, < 128
     return w < 64 ? rl(win0, w) : rl(win1, w - 64);
   };
   // window step: slide the bitstream window, then 64 candidate decodes -- lane l's 32-bit peek
   // at pos + l and its table entry (len << 8 | r << 4 | s)
   auto candidates = [&](uint32_t pos, uint32_t &pk_l, uint32_t &e_l) {
-    if ((pos >> 5) - wbase >= 64) {  // everything needed is in win1: shift, prefetch the next 64 words
-      wbase += 64;
-      win0 = win1;
-      win1 = ldword(wbase + 64 + lane);
-    }
+    if ((pos >> 5) - wbase >= 64) slide();  // everything needed is in win1
     const uint32_t W = (pos >> 5) - wbase, sh = pos & 31;
     const uint32_t A = word(W), B = word(W + 1), C = word(W + 2), D = word(W + 3);
     const uint32_t o = sh + lane;
@@ -834,11 +855,7 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
     };
     while (!done) {
       // window step: lane l's peek at pos + l and its entry in both tables
-      if ((pos >> 5) - wbase >= 64) {
-        wbase += 64;
-        win0 = win1;
-        win1 = ldword(wbase + 64 + lane);
-      }
+      if ((pos >> 5) - wbase >= 64) slide();
       const uint32_t W = (pos >> 5) - wbase, sh = pos & 31;
       const uint32_t A = word(W), B = word(W + 1), C = word(W + 2), D = word(W + 3);
       const uint32_t o = sh + lane;
@@ -948,7 +965,7 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
           ux %= units_x;
         }
         done = u >= nunits || pos > nbits;
-        if (done || (u >> 6) != (published >> 6)) {
+        if (done || (u >> 8) != (published >> 8)) {
           publish(done ? RJ_PROG_DONE : u);
           published = u;
         }
@@ -1062,7 +1079,7 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
           if (r_nw) gor64(nzs + rbase + lane, r_nw);
         }
         if (done) finish(nbase);
-        else publish(u);
+        else if ((u & 255u) == 0) publish(u);  // every 256 units: fewer release fences
         r_cs = r_sg = r_nw = 0;
         rbase += 64;
       }
