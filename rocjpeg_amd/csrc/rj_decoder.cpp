@@ -384,7 +384,7 @@ int Decoder::Decode(Stream *const *streams, int n, const RocJpegDecodeParams *pa
 }
 
 // progressive images per call up to which every scan goes to the wave grid (see prog_wave_all)
-static constexpr int kProgWaveAllImages = 192;  // measured crossover (C5 1080p: 64 -> one grid, 256 -> two)
+static constexpr int kProgWaveAllImages = 1280;  // measured crossover (C5 1080p: 1024 -> one grid, 2048 -> two)
 
 int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
   const auto t_host0 = std::chrono::steady_clock::now();
@@ -672,11 +672,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     for (int i = 0; i < n && prog_pipe; i++)
       for (const RjProgScanDev &sc : streams[i]->plan().pscans)
         if (sc.kind == RJ_PK_AC_REFINE && sc.nprod == 0xFF) prog_pipe = false;
-    // pipelined layouts: a small batch puts every scan in one wave grid (each image's scans run
-    // side by side: lowest latency); a large one decodes the AC first scans in a grid of their
-    // own ahead of the refinement grid -- with ten waves per image one grid would outgrow the
-    // chip's wave slots and the first scans' chains would contend with the refinement chains
-    // (C5, 1024 images: 137 ms vs 175 ms one grid, 151 ms first scans in lanes)
+    // pipelined layouts: up to ~1280 images every scan goes in one wave grid (each image's scans
+    // run side by side); beyond, the AC first scans get a grid of their own ahead of the
+    // refinement grid -- with ten waves per image one grid outgrows the chip's wave slots several
+    // times over (C5 1080p: 1024 images 111 ms one grid vs 117 ms two; 2048 images 243 vs 200)
     prog_wave_all = prog_pipe && (prog_wave_all_ >= 0 ? prog_wave_all_ != 0 : prog_images <= kProgWaveAllImages);
     auto in_lanes = [&](uint32_t kind) { return !prog_pipe && kind != RJ_PK_AC_REFINE; };
     // algorithmic bytes of an interval: destuffed bytes read + what its decode writes (DC first:
