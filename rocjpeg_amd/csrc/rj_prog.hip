@@ -992,26 +992,36 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
   while (!done) {
     uint32_t pk_l, e_l;
     candidates(pos, pk_l, e_l);
+    // per candidate offset, everything that depends only on the bits there (lane-parallel, off
+    // the chain): bits used by the symbol and its extra bits, run length r, EOB flag, new
+    // value (1 positive, 2 negative), EOB-run length; and the 32 bits after them (corrections)
+    uint32_t info_l, ck_l;
+    {
+      const uint32_t len = e_l >> 8, r = (e_l >> 4) & 15u, s = e_l & 15u;
+      const bool eob = s == 0 && r != 15;
+      const uint32_t extra = eob ? r : (s ? 1u : 0u);
+      const uint32_t eb = pbits(pk_l, len, extra);
+      const uint32_t used = len + extra;
+      const uint32_t nv = s ? (eb ? 1u : 2u) : 0u;
+      const uint32_t run = eob ? (1u << r) + eb : 0u;
+      info_l = used | (r << 6) | (eob ? 1u << 10 : 0u) | (nv << 11) | (run << 13);
+      ck_l = used < 32 ? pk_l << used : 0u;
+    }
     const uint32_t pos0 = pos;
     stamp.nwin++;
     // ---- scalar chain over the window ----
     while (!done && pos - pos0 < 64) {
       const uint32_t d = pos - pos0;
       stamp.nstep++;
-      const uint32_t pk = rl(pk_l, d);
-      uint32_t used = 0;
+      uint32_t used = 0, cbits;
       if (!walking) {
         if (eobrun == 0) {
-          const uint32_t en = rl(e_l, d);
-          const uint32_t len = en >> 8, r = (en >> 4) & 15u, s = en & 15u;
-          used = len;
-          if (s || r == 15) {
-            if (s) {
-              newv = pbits(pk, used, 1) ? 1u : 2u;
-              used++;
-            } else {
-              newv = 0;
-            }
+          const uint32_t info = rl(info_l, d);
+          cbits = rl(ck_l, d);
+          const uint32_t r = (info >> 6) & 15u;
+          used = info & 63u;
+          if (!(info & (1u << 10))) {
+            newv = (info >> 11) & 3u;
             // the (r+1)-th zero-history position at or after k, lane-parallel: lane l is it when
             // bit l of the candidate mask is set with exactly r candidates below it
             const uint64_t zm = ~nzm & band & (~0ull << k);
@@ -1022,23 +1032,25 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
             pend = uint32_t(__popcll(nzm & lomask(t) & (~0ull << k)));
             eobblk = false;
           } else {  // EOBr
-            eobrun = (1u << r) + pbits(pk, used, r);
-            used += r;
+            eobrun = info >> 13;
             t = se + 1;
             newv = 0;
             eobblk = true;
             pend = uint32_t(__popcll(nzm & ~lomask(k)));
           }
         } else {  // a block inside an EOB run
+          cbits = rl(pk_l, d);
           t = se + 1;
           newv = 0;
           eobblk = true;
           pend = uint32_t(__popcll(nzm & ~lomask(k)));
         }
         walking = true;
+      } else {
+        cbits = rl(pk_l, d);
       }
       const uint32_t take = min(pend, 32u - used);
-      cstr = (cstr << take) | pbits(pk, used, take);
+      cstr = (cstr << take) | pbits(cbits, 0, take);
       used += take;
       pend -= take;
       pos += used;
