@@ -209,3 +209,47 @@ def test_progressive_layouts_match_oracle(layout):
             assert G.first_mismatch(G.to_host(bufs)[0], want[0]) is None
     finally:
         d.close()
+
+
+@pytest.mark.parametrize("layout", ["one_grid", "two_grids"])
+def test_progressive_many_images_one_call(layout):
+    """Hundreds of progressive images in one call (each small fixture many times over, DRI and
+    no-DRI scripts mixed): every refinement wave follows its producers through the progress
+    counters under load, in both pipelined layouts -- every image equals the oracle."""
+    import os
+    from tests import gpu_util as G
+    G.torch()
+    env = LAYOUTS[layout]
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        d = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    try:
+        base = [O.fixture_bytes(e) for e in SMALL]
+        want = {}
+        datas = [base[i % len(base)] for i in range(320)]
+        streams = [R.JpegStream(x) for x in datas]
+        dec_bufs, imgs, shapes_all = [], [], []
+        for s in streams:
+            nc, css, w, h = d.image_info(s)
+            shapes = G.channel_shapes(R.OutputFormat.RGB, css, w, h)
+            bufs, img = G.gpu_buffers(shapes)
+            dec_bufs.append(bufs)
+            imgs.append(img)
+            shapes_all.append(shapes)
+        assert d.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs) == 0
+        for k, (x, shapes, bufs) in enumerate(zip(datas, shapes_all, dec_bufs)):
+            key = k % len(base)
+            if key not in want:
+                ost, ref = O.oracle_decode(x, int(R.OutputFormat.RGB), shapes)
+                assert ost == 0
+                want[key] = ref[0]
+            assert G.first_mismatch(G.to_host(bufs)[0], want[key]) is None, k
+    finally:
+        d.close()
