@@ -737,37 +737,51 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       // path), then the other components' AC scans, then the DC scans; level order within each.
       wave_off[0] = uint32_t(prog_lanes.size());
       // large batches: the first scans in a grid of their own ahead of the refinement grid
-      // (phase 0), the rest after (phase 1); small batches: everything in one grid
-      for (uint32_t phase = 0; phase < 2; phase++) {
-        if (phase == 1) wave_first_end = uint32_t(prog_lanes.size());
-        for (uint32_t rank = 0; rank < 4; rank++)
-          for (uint32_t L = 0; L < nlev; L++)
-          for (int i = 0; i < n; i++) {
-            const DecodePlan &p = streams[i]->plan();
-            if (!p.progressive) continue;
-            const uint32_t nc = streams[i]->info().ncomp;
-            for (uint32_t q = 0; q < p.pivals.size(); q++) {
-              const RjProgIvalDev &iv = p.pivals[q];
-              const RjProgScanDev &sc = p.pscans[iv.scan];
-              if (sc.level != L) continue;
-              uint32_t r = 3;
-              if (sc.kind == RJ_PK_AC_FIRST || sc.kind == RJ_PK_AC_REFINE) {
-                const uint32_t c = sc.comp[0];
-                const uint64_t bc = uint64_t(p.cwblk[c]) * p.chblk[c];
-                r = 0;
-                for (uint32_t o = 0; o < nc && o < 3; o++) {
-                  const uint64_t bo = uint64_t(p.cwblk[o]) * p.chblk[o];
-                  if (bo > bc || (bo == bc && o < c)) r++;
-                }
-                r = std::min<uint32_t>(r, 2);
-              }
-              const bool first = sc.kind == RJ_PK_AC_FIRST;  // DC first: nothing waits, grid end
-              if (r != rank || (!prog_wave_all && first != (phase == 0)) || (prog_wave_all && phase == 1))
-                continue;
-              prog_lanes.push_back(imgs[i].pival_prefix + q);  // missing ones too: they report DONE
-              if (!(iv.flags & RJ_SEG_MISSING)) timings_.prog_kernel_bytes[1] += ival_bytes(sc, iv);
+      // (phase 0), the rest after (phase 1); small batches: everything in one grid.  Order key
+      // (phase, rank, level), counting sort (two passes over the intervals)
+      const uint32_t nkeys = 2 * 4 * nlev;
+      std::vector<uint32_t> &bucket = sc_.prog_bucket;
+      bucket.assign(nkeys + 1, 0);
+      std::vector<uint16_t> scan_key;
+      auto keys_of = [&](const DecodePlan &p, uint32_t nc) {
+        scan_key.resize(p.pscans.size());
+        for (size_t q = 0; q < p.pscans.size(); q++) {
+          const RjProgScanDev &sc = p.pscans[q];
+          uint32_t r = 3;
+          if (sc.kind == RJ_PK_AC_FIRST || sc.kind == RJ_PK_AC_REFINE) {
+            const uint32_t c = sc.comp[0];
+            const uint64_t bc = uint64_t(p.cwblk[c]) * p.chblk[c];
+            r = 0;
+            for (uint32_t o = 0; o < nc && o < 3; o++) {
+              const uint64_t bo = uint64_t(p.cwblk[o]) * p.chblk[o];
+              if (bo > bc || (bo == bc && o < c)) r++;
             }
+            r = std::min<uint32_t>(r, 2);
           }
+          const uint32_t phase = (!prog_wave_all && sc.kind != RJ_PK_AC_FIRST) ? 1u : 0u;
+          scan_key[q] = uint16_t((phase * 4 + r) * nlev + std::min<uint32_t>(sc.level, nlev - 1));
+        }
+      };
+      for (int i = 0; i < n; i++) {
+        const DecodePlan &p = streams[i]->plan();
+        if (!p.progressive) continue;
+        keys_of(p, streams[i]->info().ncomp);
+        for (const RjProgIvalDev &iv : p.pivals) bucket[scan_key[iv.scan] + 1]++;
+      }
+      for (uint32_t b = 0; b < nkeys; b++) bucket[b + 1] += bucket[b];
+      const uint32_t base = uint32_t(prog_lanes.size());
+      wave_first_end = base + bucket[4 * nlev];  // phase 1 starts here
+      prog_lanes.resize(base + bucket[nkeys]);
+      for (int i = 0; i < n; i++) {
+        const DecodePlan &p = streams[i]->plan();
+        if (!p.progressive) continue;
+        keys_of(p, streams[i]->info().ncomp);
+        for (uint32_t q = 0; q < p.pivals.size(); q++) {
+          const RjProgIvalDev &iv = p.pivals[q];
+          // missing intervals too: they report DONE
+          prog_lanes[base + bucket[scan_key[iv.scan]]++] = imgs[i].pival_prefix + q;
+          if (!(iv.flags & RJ_SEG_MISSING)) timings_.prog_kernel_bytes[1] += ival_bytes(p.pscans[iv.scan], iv);
+        }
       }
       if (prog_wave_all) wave_first_end = wave_off[0];
       for (uint32_t L = 1; L < nlev; L++) wave_off[L] = wave_off[0];
