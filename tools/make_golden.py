@@ -47,13 +47,49 @@ def pillow_jpeg(rgb, **kw):
     return b.getvalue()
 
 
-def cjpeg_jpeg(rgb, args, gray=False):
+def cjpeg_jpeg(rgb, args, gray=False, scans=None):
     with tempfile.TemporaryDirectory() as td:
         src = os.path.join(td, "in.pgm" if gray else "in.ppm")
         im = Image.fromarray(rgb)
         (im.convert("L") if gray else im).save(src)
+        if scans is not None:  # a custom progressive scan script (cjpeg -scans)
+            sp = os.path.join(td, "scans.txt")
+            with open(sp, "w") as f:
+                f.write(scans)
+            args = args + ["-scans", sp]
         out = subprocess.run([CJPEG] + args + [src], check=True, capture_output=True).stdout
     return out
+
+
+# Y's first scans in three bands, then two successive-approximation refinements of the whole
+# band (the first has three producer scans -- the pipelined launch's limit)
+SCANS_3BANDS = """0,1,2: 0-0, 0, 1;
+0: 1-5, 0, 2;
+0: 6-20, 0, 2;
+0: 21-63, 0, 2;
+1: 1-63, 0, 1;
+2: 1-63, 0, 1;
+0: 1-63, 2, 1;
+0: 1-63, 1, 0;
+0,1,2: 0-0, 1, 0;
+1: 1-63, 1, 0;
+2: 1-63, 1, 0;
+"""
+# non-interleaved DC scans, Y's first scans in five bands and refinements of band unions (four
+# producers: the decoder falls back to level-by-level refinement)
+SCANS_5BANDS = """0: 0-0, 0, 0;
+1: 0-0, 0, 0;
+2: 0-0, 0, 0;
+0: 1-2, 0, 1;
+0: 3-5, 0, 1;
+0: 6-14, 0, 1;
+0: 15-30, 0, 1;
+0: 31-63, 0, 1;
+1: 1-63, 0, 0;
+2: 1-63, 0, 0;
+0: 1-30, 1, 0;
+0: 31-63, 1, 0;
+"""
 
 
 def read_coef(path):
@@ -144,6 +180,8 @@ def fixtures():
     add("cp420_prog_ri3_160x112", cjpeg_jpeg(source_rgb(s + 23, 160, 112), ["-quality", "95", "-sample", "2x2,1x1,1x1", "-progressive", "-restart", "3B"]), "progressive 4:2:0, DRI = 3 MCUs")
     add("cp400_prog_120x80", cjpeg_jpeg(source_rgb(s + 24, 120, 80), ["-quality", "90", "-progressive"], gray=True), "progressive grayscale")
     add("cp440_prog_96x80", cjpeg_jpeg(source_rgb(s + 25, 96, 80), ["-quality", "90", "-sample", "1x2,1x1,1x1", "-progressive"]), "progressive 4:4:0")
+    add("cp420_scans3_128x96", cjpeg_jpeg(source_rgb(s + 27, 128, 96), ["-quality", "92", "-sample", "2x2,1x1,1x1"], scans=SCANS_3BANDS), "progressive, custom script: Y first scans in 3 bands, Al 2 -> 1 -> 0")
+    add("cp420_scans5_112x80", cjpeg_jpeg(source_rgb(s + 28, 112, 80), ["-quality", "90", "-sample", "2x2,1x1,1x1", "-restart", "2B"], scans=SCANS_5BANDS), "progressive, custom script: non-interleaved DC, 5 Y bands, refinements over band unions, DRI 2 MCUs")
     fullp = pillow_jpeg(source_rgb(s + 26, 192, 128), quality=90, subsampling=2, progressive=True)
     add("pp420_prog_trunc_192x128", fullp[: len(fullp) * 11 // 20], "truncated progressive stream: later scans missing, insufficient-data semantics")
     return out
