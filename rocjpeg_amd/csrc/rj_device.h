@@ -228,9 +228,9 @@ struct RjProgScanDev {
   uint32_t ri;               // units per restart interval (0: one interval)
   uint32_t ival0;            // index of the scan's first interval in the image's interval list
   uint32_t nblk;             // blocks per unit
-  // AC refinement: the earlier AC refinement scans of this component whose band overlaps this
-  // one (their new coefficients change this scan's nonzero masks); 0xFF: more than 3 (the call
-  // then runs level by level instead of pipelined)
+  // AC refinement: its producers -- the latest earlier scan of each coefficient of its band (AC
+  // first or refinement; their nonzero masks are this scan's input, and each waited for its own
+  // producers, rj_prog_stream.cpp); 0xFF: more than 3 (the call then runs level by level)
   uint8_t nprod, prod[3];
 };
 #define RJ_PROG_DONE 0xFFFFFFFFu  // interval progress: finished
