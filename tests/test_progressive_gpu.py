@@ -258,3 +258,27 @@ def test_progressive_many_images_one_call(layout):
             assert G.first_mismatch(G.to_host(bufs)[0], want[key]) is None, k
     finally:
         d.close()
+
+
+def test_progressive_1080p_batch_one_call(dec):
+    """The C5 sample (1080p 4:2:0, ten scans, no DRI) 96 times in one call: every image equals
+    the oracle's decode (compared on the device), at the scale where the refinement waves of
+    many images share the chip."""
+    from tests import gpu_util as G
+    t = G.torch()
+    ent = next(f for f in PROG if f["name"] == "pp420_q90_1920x1080")
+    data = O.fixture_bytes(ent)
+    streams = [R.JpegStream(data) for _ in range(96)]
+    nc, css, w, h = dec.image_info(streams[0])
+    shapes = G.channel_shapes(R.OutputFormat.RGB, css, w, h)
+    bufs_all, imgs = [], []
+    for _ in streams:
+        bufs, img = G.gpu_buffers(shapes)
+        bufs_all.append(bufs)
+        imgs.append(img)
+    assert dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs) == 0
+    ost, want = O.oracle_decode(data, int(R.OutputFormat.RGB), shapes)
+    assert ost == 0
+    ref = t.from_numpy(want[0]).to("cuda")
+    bad = [k for k, bufs in enumerate(bufs_all) if not t.equal(bufs[0], ref)]
+    assert not bad, bad[:8]
