@@ -1,26 +1,31 @@
 #!/usr/bin/env python3
 """bench.py -- images/s of rocJpegDecodeBatched on MI355X (BASELINE.json `metric`).
 
-Workload (BASELINE.json configs[1], "C2"): a batch of 1024 synthetic 1920x1080 4:2:0 baseline
-JPEGs (q90, DRI = 120 MCUs = one MCU row), ROCJPEG_OUTPUT_RGB.  A step = one
-rocJpegDecodeBatched call over the whole batch with the bitstreams already resident in HBM
-(rocJpegAmdStreamsToDevice, outside the timed region) and RGB written to HBM.  N GPUs = N
-ranks, each decoding its own batch (weak scaling; whole images are independent).  Rank 0
-builds the work table (one seed per image) and broadcasts it (RCCL); nothing crosses GPUs
-in the timed region.
+Workload (BASELINE.json configs[1], "C2"): per GPU a batch of 1024 synthetic 1920x1080 4:2:0
+baseline JPEGs (q90, DRI = 120 MCUs = one MCU row), ROCJPEG_OUTPUT_RGB.  A step = one
+rocJpegDecodeBatched call per rank over that rank's shard, bitstreams already resident in HBM,
+RGB written to HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload c2|c3|c4|c5]
+Multi-GPU (rocjpeg_amd/shard.py): one process per GPU.  Every rank generates one
+part of the dataset into a file on the node (before any GPU call); rank 0 reads the headers of
+all parts, builds the 64-byte-per-image work table, assigns images to ranks by LPT and
+broadcasts the table (RCCL) -- the only collective; each rank parses its own images from the
+shared files and decodes them on its own GPU.  `--gpus N` with no WORLD_SIZE in the
+environment launches the N ranks itself (torch.distributed.run, before touching the GPU).
 
-The other BASELINE.json configs are available as --workload (never the driver's default line):
-  c3  1024 x 1080p, 4:4:4 and 4:2:2 alternating, ROCJPEG_OUTPUT_YUV_PLANAR
-  c4  mixed resolution 4:2:0 (640x480 .. 3840x2160, uniform by seed), RGB, DRI = one MCU row
-  c5  progressive 4:2:0 1080p q90 (Pillow progressive=True, no DRI), RGB
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload c2|c2nori|c3|c4|c5]
+
+At N = 1 the line also carries `extra_workloads`: the other BASELINE configs measured in the
+same run with the same contract -- c2nori (the no-DRI twin set), C3 (4:4:4 +
+4:2:2 -> YUV_PLANAR), C4 (mixed resolution, per GPU) and C5 (progressive).
 """
 import argparse
 import ctypes
 import io
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from multiprocessing import get_context
@@ -31,308 +36,489 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 MUG = os.path.join(ROOT, "tests", "golden", "img", "mug_420.jpg")
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+TABLE_BYTES = 1828          # JpegStreamParameters per image: the 8(d) basis
 PROG_KERNELS = ("k_prog", "k_prog_wave", "k_prog_fold")  # RocJpegAmdTimings.prog_kernel_*
+C4_SIZES = [(640, 480), (1280, 720), (1920, 1080), (2560, 1440), (3840, 2160)]
+SEED0 = 1234
+GEN_VERSION = 1  # bump when the generator changes (dataset files are cached per node)
 
+# generator arguments: (w, h, subsampling, restart = one MCU row, progressive); w == 0: C4 sizes
+# by seed; sub == -1: 4:4:4 / 4:2:2 alternating by seed (C3)
+WORKLOADS = {
+    "c2": {"gen": (1920, 1080, 2, True, False), "fmt": "RGB",
+           "data": "synthetic: seeded 1920x1080 crops of the reference mug_420.jpg + N(0,2) noise, Pillow q90 4:2:0 DRI=120",
+           "workload": "C2: batch of {batch} x 1920x1080 4:2:0 baseline JPEG q90, RI=120 MCUs per GPU, ROCJPEG_OUTPUT_RGB, bitstreams resident in HBM"},
+    "c2nori": {"gen": (1920, 1080, 2, False, False), "fmt": "RGB",
+               "data": "synthetic: the C2 seeds encoded without DRI (SURVEY.md 8d no-DRI twin set)",
+               "workload": "C2 no-DRI twin: batch of {batch} x 1920x1080 4:2:0 baseline q90, no restart markers, ROCJPEG_OUTPUT_RGB, resident"},
+    "c3": {"gen": (1920, 1080, -1, True, False), "fmt": "YUV_PLANAR",
+           "data": "synthetic: seeded 1920x1080 crops of mug_420.jpg + N(0,2) noise, Pillow q90, 4:4:4 / 4:2:2 alternating, DRI = 1 MCU row",
+           "workload": "C3: batch of {batch} x 1920x1080 baseline q90, 4:4:4 and 4:2:2 alternating, ROCJPEG_OUTPUT_YUV_PLANAR, resident"},
+    "c4": {"gen": (0, 0, 2, True, False), "fmt": "RGB",
+           "data": "synthetic: seeded crops of mug_420.jpg + N(0,2) noise, sizes 640x480..3840x2160 uniform by seed, Pillow q90 4:2:0, DRI = 1 MCU row",
+           "workload": "C4: batch of {batch} mixed-resolution 4:2:0 baseline JPEGs per GPU (640x480..3840x2160), LPT-sharded, ROCJPEG_OUTPUT_RGB, resident"},
+    "c5": {"gen": (1920, 1080, 2, False, True), "fmt": "RGB",
+           "data": "synthetic: seeded 1920x1080 crops of mug_420.jpg + N(0,2) noise, Pillow q90 4:2:0 progressive=True (no DRI)",
+           "workload": "C5: batch of {batch} x 1920x1080 4:2:0 progressive JPEG q90 (10 scans, no DRI), ROCJPEG_OUTPUT_RGB, resident"},
+}
+
+
+def host_cores():
+    """CPU cores this job may use: the affinity mask, capped by a cgroup CPU quota and by
+    OMP_NUM_THREADS (the GPU box sets it to the job's CPU share; nproc there shows the whole
+    machine).  Returns (cores, nproc, rule)."""
+    nproc = os.cpu_count() or 1
+    cores, rule = nproc, "nproc"
+    try:
+        aff = len(os.sched_getaffinity(0))
+        if aff < cores:
+            cores, rule = aff, "sched_getaffinity"
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            c = max(1, int(int(q) // int(p)))
+            if c < cores:
+                cores, rule = c, "cgroup cpu.max"
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and 0 < int(omp) < cores:
+        cores, rule = int(omp), "OMP_NUM_THREADS (the job's CPU share)"
+    return cores, nproc, rule
+
+
+# ------------------------------------------------------------------ dataset (host only)
 _BASE = None
 
 
-def _init_worker():
+def _init_gen():
     global _BASE
     from PIL import Image
     _BASE = np.asarray(Image.open(MUG).convert("RGB"))
 
 
-C4_SIZES = [(640, 480), (1280, 720), (1920, 1080), (2560, 1440), (3840, 2160)]
-
-
-def _make_jpeg(args):
-    """Seeded crop of the reference mug image + N(0,2) noise, encoded q90 with DRI = one MCU
-    row (BASELINE.md generator).  w == 0: size drawn from C4_SIZES by the seed."""
-    seed, w, h, quality, sub, rst_blocks, progressive = args
+def _make_jpeg(job):
+    """Seeded crop of the reference mug image + N(0,2) noise, Pillow/libjpeg-turbo q90
+    (BASELINE.md generator)."""
+    seed, (w, h, sub, rst, prog) = job
     if w == 0:
         w, h = C4_SIZES[seed % len(C4_SIZES)]
-        rst_blocks = (w + 15) // 16 if rst_blocks else 0  # MCUs per row
-    if sub == -1:  # C3: 4:4:4 and 4:2:2 alternating
+    if sub == -1:
         sub = 0 if seed % 2 == 0 else 1
-        rst_blocks = (w + 7) // 8 if sub == 0 else (w + 15) // 16  # one MCU row
     from PIL import Image
     rng = np.random.default_rng(seed)
     y0 = int(rng.integers(0, _BASE.shape[0] - h + 1))
     x0 = int(rng.integers(0, _BASE.shape[1] - w + 1))
     a = _BASE[y0:y0 + h, x0:x0 + w].astype(np.float32) + rng.normal(0.0, 2.0, (h, w, 3))
-    b = io.BytesIO()
-    kw = dict(quality=quality, subsampling=sub)
-    if rst_blocks:
-        kw["restart_marker_blocks"] = rst_blocks
-    if progressive:
+    kw = dict(quality=90, subsampling=sub)
+    if rst:
+        kw["restart_marker_blocks"] = (w + 7) // 8 if sub == 0 else (w + 15) // 16  # one MCU row
+    if prog:
         kw["progressive"] = True
+    b = io.BytesIO()
     Image.fromarray(np.clip(a, 0, 255).astype(np.uint8)).save(b, "JPEG", **kw)
     return b.getvalue()
 
 
-def make_dataset(seeds, w=1920, h=1080, quality=90, sub=2, rst_blocks=120, procs=16, progressive=False):
-    jobs = [(int(s), w, h, quality, sub, rst_blocks, progressive) for s in seeds]
-    with get_context("fork").Pool(procs, initializer=_init_worker) as pool:
-        return pool.map(_make_jpeg, jobs, chunksize=8)
+def data_dir():
+    d = os.environ.get("RJ_BENCH_DATA") or os.path.join("/tmp", f"rocjpeg_amd_bench_{os.getuid()}")
+    os.makedirs(d, exist_ok=True)
+    return d
 
 
-def cpu_baseline(data_list, shapes, fmt, what, budget_s=12.0):
-    """The CPU oracle (oracle/jpeg_oracle.c, a plain single-threaded restatement of the same
-    decode: Huffman, ISLOW IDCT, reference CSC) on a bounded sample of the same images."""
+def part_base(name, part, count):
+    return os.path.join(data_dir(), f"{name}_v{GEN_VERSION}_p{part}_n{count}")
+
+
+def dataset_part(name, part, count, pool):
+    """Part `part` of workload `name` (seeds SEED0 + part * count ...): one file of concatenated
+    JPEGs plus an index, generated once per node and shared by the ranks.  Returns
+    (path, offsets, sizes)."""
+    base = part_base(name, part, count)
+    if not (os.path.exists(base + ".bin") and os.path.exists(base + ".idx.npy")):
+        seeds = range(SEED0 + part * count, SEED0 + (part + 1) * count)
+        blobs = pool.map(_make_jpeg, [(s, WORKLOADS[name]["gen"]) for s in seeds], chunksize=4)
+        sizes = np.array([len(b) for b in blobs], dtype=np.uint64)
+        offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+        tmp = f"{base}.{os.getpid()}"
+        with open(tmp + ".bin", "wb") as f:
+            for b in blobs:
+                f.write(b)
+        np.save(tmp + ".idx.npy", np.stack([offs, sizes]))
+        os.replace(tmp + ".bin", base + ".bin")
+        os.replace(tmp + ".idx.npy", base + ".idx.npy")
+    idx = np.load(base + ".idx.npy")
+    return base + ".bin", idx[0], idx[1]
+
+
+# ------------------------------------------------------------------ CPU baselines
+def _turbo_proc(go, q, path, items, budget_s):
+    """One host core: libjpeg-turbo (Pillow) decodes of this worker's images to RGB, timed
+    around the decode loop only (samples/jpegDecodePerf/jpegdecodeperf.cpp:153-186)."""
+    from PIL import Image
+    with open(path, "rb") as f:
+        data = [None] * len(items)
+        for j, (o, s) in enumerate(items):
+            f.seek(int(o))
+            data[j] = f.read(int(s))
+    go.wait()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        for b in data:
+            Image.open(io.BytesIO(b)).convert("RGB").load()
+            n += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    q.put((n, time.perf_counter() - t0))
+
+
+class TurboBaseline:
+    """libjpeg-turbo on the job's host cores, one process per core, each decoding its shard of
+    the same files (BASELINE.md "CPU baseline plan").  The processes are forked before any GPU
+    call and wait on an event; they exit by returning (no SIGTERM)."""
+
+    def __init__(self, path, offs, sizes, cores, budget_s=1.5, per_core=24):
+        ctx = get_context("fork")
+        self.go, self.q = ctx.Event(), ctx.Queue()
+        n = len(offs)
+        self.procs = []
+        for c in range(cores):
+            sel = [(offs[(c * per_core + j) % n], sizes[(c * per_core + j) % n]) for j in range(per_core)]
+            p = ctx.Process(target=_turbo_proc, args=(self.go, self.q, path, sel, budget_s), daemon=True)
+            p.start()
+            self.procs.append(p)
+        self.cores = cores
+
+    def run(self):
+        self.go.set()
+        res = [self.q.get(timeout=600) for _ in self.procs]
+        for p in self.procs:
+            p.join(timeout=60)
+        rate = sum(n / t for n, t in res)  # the reference sums per-thread rates (jpegdecodeperf.cpp:281-300)
+        return rate, sum(n for n, _ in res), max(t for _, t in res)
+
+
+def cpu_oracle(datas, shapes, fmt, budget_s=5.0):
+    """The C restatement (oracle/jpeg_oracle.c), one thread, on a bounded sample: context."""
     from tests import oracle_lib as O
     n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s and n < len(data_list):
-        st, _ = O.oracle_decode(data_list[n], fmt, shapes[n])
+    while time.perf_counter() - t0 < budget_s and n < len(datas):
+        st, _ = O.oracle_decode(datas[n], fmt, shapes[n])
         assert st == 0
         n += 1
     dt = time.perf_counter() - t0
     return {"value": round(n / dt, 3), "unit": "images/s", "cores": 1, "kind": "port",
-            "sample": f"{n} of the batch's {what}, oracle/jpeg_oracle.c, 1 thread, {dt:.1f} s"}
-
-
-def _turbo_worker(blobs):
-    from PIL import Image
-    t0 = time.perf_counter()
-    for b in blobs:
-        Image.open(io.BytesIO(b)).convert("RGB").load()
-    return len(blobs), time.perf_counter() - t0
-
-
-def turbo_baseline(data_list, procs):
-    """Context only (not the cpu_baseline): Pillow's libjpeg-turbo on `procs` host cores."""
-    per = max(1, min(len(data_list) // procs, 48))
-    shards = [data_list[(i * per) % len(data_list):][:per] for i in range(procs)]
-    t0 = time.perf_counter()
-    with get_context("fork").Pool(procs) as pool:
-        res = pool.map(_turbo_worker, shards)
-    wall = time.perf_counter() - t0
-    n = sum(r[0] for r in res)
-    return {"value": round(n / max(wall, 1e-9), 1), "unit": "images/s", "cores": procs,
-            "lib": "Pillow bundled libjpeg-turbo (BT.601 + fancy upsampling: throughput context only)"}
+            "sample": f"{n} images of the batch, oracle/jpeg_oracle.c, 1 thread, {dt:.1f} s"}
 
 
 def pmc_traffic(kernel, batch, launches, workload="c2"):
-    """HBM bytes per launch of `kernel` from the committed PMC profile (tools/gpu_pmc.sh +
-    tools/pmc_traffic.py on this workload; profiles/pmc_traffic.json for C2,
-    pmc_traffic_<workload>.json for the others): FETCH_SIZE x 2 (gfx950 correction,
-    MI355X_MICROARCH.md HBM section) + WRITE_SIZE summed over a decode call, per image, scaled to
-    this call's batch and divided over its launches of the kernel.  None if absent."""
+    """HBM bytes per launch of `kernel` from the committed PMC profile of this workload
+    (tools/gpu_pmc.sh + tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE per decode call, the
+    gfx950 correction of MI355X_MICROARCH.md), scaled to this batch.  (bytes, source) or None."""
     name = "pmc_traffic.json" if workload == "c2" else f"pmc_traffic_{workload}.json"
     path = os.path.join(ROOT, "profiles", name)
     try:
         with open(path) as f:
             prof = json.load(f)
         k = prof["kernels"][kernel]
-        return int(k["hbm_bytes_per_image"] * batch / max(1, launches))
+        return int(k["hbm_bytes_per_image"] * batch / max(1, launches)), f"profiles/{name} ({prof.get('commit', '?')})"
     except (OSError, KeyError, ValueError):
         return None
 
 
-def work_table(rank, world, batch, device):
-    """Rank 0 builds the work table (one image seed per slot, `batch` images per rank) and one
-    broadcast (RCCL on GPUs, gloo in the CPU tests) hands every rank the whole table; each rank
-    keeps its own row.  Returns this rank's seeds."""
-    import torch
-    import torch.distributed as dist
-    table = torch.empty((world, batch), dtype=torch.int64, device=device)
-    if rank == 0:
-        table.copy_(torch.arange(world * batch, dtype=torch.int64).view(world, batch) + 1234)
-    if world > 1:
-        dist.broadcast(table, src=0)
-    return table[rank].cpu().tolist()
+# ------------------------------------------------------------------ one batch on the GPU
+class BatchRun:
+    """A rank's batch: streams parsed on the GPU (rocJpegAmdStreamParseDevice, resident), the
+    destinations in one HBM arena sized as the reference samples size them
+    (samples/rocjpeg_samples_utils.h:318-399, tests/gpu_util.py channel_shapes)."""
+
+    def __init__(self, dec, datas, fmt, dev):
+        import torch
+        import rocjpeg_amd as R
+        from tests.gpu_util import channel_shapes
+        self.R, self.dec, self.datas, self.fmt = R, dec, datas, fmt
+        t0 = time.perf_counter()
+        st, self.streams = dec.parse_device(datas)
+        if st != 0:
+            raise RuntimeError(f"rocJpegAmdStreamParseDevice: {R.error_name(st)}")
+        self.parse_s = time.perf_counter() - t0
+        dec.streams_to_device(self.streams)  # progressive streams are host-parsed: make them resident too
+        self.shapes = []
+        for s in self.streams:
+            nc, css, w, h = dec.image_info(s)
+            self.shapes.append(channel_shapes(fmt, css, w, h))
+        total = sum(r * p for shp in self.shapes for r, p in shp)
+        self.out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+        imgs, self.views, off = [], [], 0
+        for shp in self.shapes:
+            ptrs, pitches, vv = [], [], []
+            for r, p in shp:
+                ptrs.append(self.out[off:].data_ptr())
+                pitches.append(p)
+                vv.append(self.out[off:off + r * p].view(r, p))
+                off += r * p
+            imgs.append(R.make_image(ptrs, pitches))
+            self.views.append(vv)
+        self.params = R.decode_params(fmt)
+        self.n = len(self.streams)
+        self.hs = (ctypes.c_void_p * self.n)(*[s.handle for s in self.streams])
+        self.arr = (R.RocJpegImage * self.n)(*imgs)
+
+    def step(self):
+        st = self.R.lib().rocJpegDecodeBatched(self.dec.handle, self.hs, self.n, ctypes.byref(self.params), self.arr)
+        if st != 0:
+            raise RuntimeError(self.R.error_name(st))
+
+    def timed(self, steps, warmup, world=1, dev=None):
+        """W untimed steps, then K steps bracketed by barrier + synchronize; max over ranks."""
+        import torch
+        import torch.distributed as dist
+        for _ in range(warmup):
+            self.step()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed
+
+    def profiled(self, steps):
+        """Per-stage / per-kernel device times (HIP events on each launch's stream) over a
+        separate pass -- never the timed one."""
+        self.dec.set_profiling(True)
+        acc, last = {}, None
+        for _ in range(steps):
+            self.step()
+            last = self.dec.last_timings()
+            for k, v in last.items():
+                if isinstance(v, float):
+                    acc[k] = acc.get(k, 0.0) + v
+                elif isinstance(v, list) and v and isinstance(v[0], float):
+                    acc[k] = [a + b for a, b in zip(acc.get(k, [0.0] * len(v)), v)]
+        self.dec.set_profiling(False)
+        for k, v in acc.items():
+            last[k] = [x / steps for x in v] if isinstance(v, list) else v / steps
+        return last
+
+    def parity(self, idx):
+        """Images `idx` of the current outputs (the last timed step's) vs the CPU oracle."""
+        from tests import oracle_lib as O
+        ok = True
+        for q in idx:
+            ost, want = O.oracle_decode(self.datas[q], int(self.fmt), self.shapes[q])
+            ok = ok and ost == 0 and all(np.array_equal(v.cpu().numpy(), w_) for v, w_ in zip(self.views[q], want))
+        return bool(ok)
+
+    def close(self):
+        import torch
+        del self.views, self.out, self.arr
+        for s in self.streams:
+            s.close()
+        torch.cuda.empty_cache()
 
 
-def _workloads():
+def kernel_table(t, n):
+    """(summed launch ms per call, launches per call, units (images) per launch) per kernel of
+    a profiled pass; the pipelined K1/K2 launches each take an equal share of the intervals."""
+    kern = {}
+    if t["k1_launches"]:
+        kern["k_entropy"] = (t["k1_launch_ms_sum"], t["k1_launches"], n / t["k1_launches"])
+    if t["k2_launches"]:
+        kern["k_rows"] = (t["k2_launch_ms_sum"], t["k2_launches"], n / t["k2_launches"])
+    kern["k_destuff"] = (t["destuff_ms"], 1, n)
+    if t["prog_images"]:
+        for j, name in enumerate(PROG_KERNELS):
+            if t["prog_kernel_launches"][j]:
+                kern[name] = (t["prog_kernel_ms"][j], t["prog_kernel_launches"][j], n / t["prog_kernel_launches"][j])
+        kern["k_rows_dense"] = (t["prog_rows_ms"], 1, n)
+    return kern
+
+
+def roofline(t, n, workload, per_image_bytes):
+    """achieved = algorithmic bytes per image (ECS + 1,828 B tables + output)
+    x the images one launch of the dominant kernel processes / its average launch time."""
+    kern = kernel_table(t, n)
+    dom = max(kern, key=lambda k: kern[k][0])
+    ms_sum, launches, units = kern[dom]
+    avg_ms = ms_sum / launches
+    ach = units * per_image_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    r = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+         "basis": "SURVEY.md 8(d): (ECS + 1,828 B tables + output bytes) per image x images per launch / avg launch time",
+         "algorithmic_bytes_per_image": int(per_image_bytes), "images_per_launch": round(units, 2),
+         "avg_launch_ms": round(avg_ms, 4), "launches_per_step": launches,
+         "per_kernel_launch_ms_sum": {k: round(v[0], 4) for k, v in kern.items()}}
+    tr = pmc_traffic(dom, n, launches, workload)
+    if tr:
+        r["traffic"], r["traffic_source"] = tr
+    # intermediate-inclusive figures (what the kernels actually move through HBM by design)
+    entb = t["entry_bytes"]
+    if dom == "k_entropy" and t["k1_launches"]:
+        b = (t["ecs_bytes"] + entb) / t["k1_launches"]
+        r["achieved_incl_intermediates"] = round(b / (avg_ms * 1e-3) / 1e9, 2)
+    if "k_rows" in kern:
+        ms, la, _ = kern["k_rows"]
+        b = (entb + t["output_bytes"]) / la
+        r["stage2_k_rows"] = {"bytes_per_launch": int(b), "avg_launch_ms": round(ms / la, 4),
+                              "achieved": round(b / (ms / la * 1e-3) / 1e9, 2),
+                              "frac": round(b / (ms / la * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                              "basis": "sparse entries read + output written (BASELINE.md stage-2 efficiency)"}
+    return r
+
+
+def run_extra(name, dec, pool_path, steps, warmup, dev):
+    """One more BASELINE config on this GPU with the same contract (N = 1 only)."""
     import rocjpeg_amd as R
-    return {
-        "c2": {"gen": {}, "fmt": R.OutputFormat.RGB,
-               "data": "synthetic: seeded 1920x1080 crops of the reference mug_420.jpg + N(0,2) noise, Pillow q90 4:2:0 DRI=120",
-               "workload": "C2: batch of {batch} x 1920x1080 4:2:0 baseline JPEG q90, RI=120 MCUs, ROCJPEG_OUTPUT_RGB, bitstreams resident in HBM",
-               "sample": "1920x1080 4:2:0 q90 RI=120 images -> RGB"},
-        "c3": {"gen": {"sub": -1}, "fmt": R.OutputFormat.YUV_PLANAR,
-               "data": "synthetic: seeded 1920x1080 crops of mug_420.jpg + N(0,2) noise, Pillow q90, 4:4:4 / 4:2:2 alternating, DRI = 1 MCU row",
-               "workload": "C3: batch of {batch} x 1920x1080 baseline q90, 4:4:4 and 4:2:2 alternating, ROCJPEG_OUTPUT_YUV_PLANAR, resident",
-               "sample": "1920x1080 4:4:4 / 4:2:2 images -> YUV_PLANAR"},
-        "c4": {"gen": {"w": 0, "h": 0}, "fmt": R.OutputFormat.RGB,
-               "data": "synthetic: seeded crops of mug_420.jpg + N(0,2) noise, sizes 640x480..3840x2160 uniform by seed, Pillow q90 4:2:0, DRI = 1 MCU row",
-               "workload": "C4: batch of {batch} mixed-resolution 4:2:0 baseline JPEGs per GPU (640x480..3840x2160), ROCJPEG_OUTPUT_RGB, resident",
-               "sample": "mixed-resolution 4:2:0 images -> RGB"},
-        "c5": {"gen": {"rst_blocks": 0, "progressive": True}, "fmt": R.OutputFormat.RGB,
-               "data": "synthetic: seeded 1920x1080 crops of mug_420.jpg + N(0,2) noise, Pillow q90 4:2:0 progressive=True (no DRI)",
-               "workload": "C5: batch of {batch} x 1920x1080 4:2:0 progressive JPEG q90 (10 scans, no DRI), ROCJPEG_OUTPUT_RGB, resident",
-               "sample": "1920x1080 4:2:0 q90 progressive images -> RGB"},
-    }
+    path, offs, sizes = pool_path
+    with open(path, "rb") as f:
+        raw = f.read()
+    datas = [raw[int(o):int(o) + int(s)] for o, s in zip(offs, sizes)]
+    del raw
+    fmt = getattr(R.OutputFormat, WORKLOADS[name]["fmt"])
+    b = BatchRun(dec, datas, fmt, dev)
+    el = b.timed(steps, warmup)
+    t = b.profiled(2)
+    per_img = (t["ecs_bytes"] + TABLE_BYTES * b.n + t["output_bytes"]) / b.n
+    rf = roofline(t, b.n, name, per_img)
+    res = {"value": round(b.n * steps / el, 2), "unit": "images/s", "ms_per_step": round(el / steps * 1e3, 3),
+           "steps": steps, "warmup": warmup, "workload": WORKLOADS[name]["workload"].format(batch=b.n),
+           "output_format": WORKLOADS[name]["fmt"], "parity_sample": b.parity([0, b.n - 1]),
+           "roofline": {k: rf[k] for k in ("kernel", "achieved", "frac", "avg_launch_ms", "launches_per_step")},
+           "per_kernel_launch_ms_sum": rf["per_kernel_launch_ms_sum"], "host_ms": round(t["host_ms"], 3),
+           "split_intervals": t["split_intervals"], "serial_fallbacks": t["serial_fallbacks"]}
+    b.close()
+    return res
 
 
 def main():
-    global WORKLOADS
-    WORKLOADS = _workloads()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--batch", type=int, default=1024, help="images per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the other BASELINE configs at N=1")
     ap.add_argument("--path", type=int, default=0, help="0 auto (fused where legal), 1 general two-stage path")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     args = ap.parse_args()
-    wl = WORKLOADS[args.workload]
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU, launched before this process touches the GPU; exit with its code
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    wl = WORKLOADS[args.workload]
+    extras = [] if (world > 1 or args.no_extras) else [w for w in ("c2nori", "c3", "c4", "c5") if w != args.workload]
+
+    # ---- host only (no GPU call yet): this rank's dataset part, the extra configs' data,
+    # the CPU baseline's processes ----
+    cores, nproc, core_rule = host_cores()
+    t_gen = time.perf_counter()
+    gen_pool = get_context("fork").Pool(max(1, min(cores, 32)), initializer=_init_gen)
+    mine = dataset_part(args.workload, rank, args.batch, gen_pool)
+    extra_data = {w: dataset_part(w, 0, args.batch, gen_pool) for w in extras} if rank == 0 else {}
+    gen_pool.close()
+    gen_pool.join()
+    t_gen = time.perf_counter() - t_gen
+    turbo = None
+    if rank == 0 and not args.no_cpu_baseline:
+        turbo = TurboBaseline(mine[0], mine[1], mine[2], cores)
+
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-
-    seeds = work_table(rank, world, args.batch, dev)
-    procs = max(1, min(16, (os.cpu_count() or 16)))
-    t_gen = time.perf_counter()
-    data = make_dataset(seeds, procs=procs, **wl["gen"])
-    t_gen = time.perf_counter() - t_gen
+        dist.barrier()  # every part is on disk
 
     import rocjpeg_amd as R
+    from rocjpeg_amd import shard as S
+    # ---- the work table: rank 0 reads every part's headers, LPT over the ranks, one broadcast ----
+    parts = [np.memmap(mine[0], dtype=np.uint8, mode="r") if r == rank else None for r in range(world)]
+    idx = [None] * world
+    for r in range(world):
+        base = part_base(args.workload, r, args.batch)
+        if parts[r] is None:
+            parts[r] = np.memmap(base + ".bin", dtype=np.uint8, mode="r")
+        idx[r] = np.load(base + ".idx.npy")
+    blob = S.Blob(parts)
+    t_tab = time.perf_counter()
+    table, shard_cost = None, None
+    if rank == 0:
+        table = S.concat_tables([S.build_work_table(np.asarray(parts[r]), idx[r][0], idx[r][1], blob.part_base(r))
+                                 for r in range(world)])
+        shard_cost = S.assign_shards(table, world, list(range(world)))
+    t_build = time.perf_counter() - t_tab
+    table = S.broadcast_table(table, src=0, device=dev)
+    t_tab = time.perf_counter() - t_tab
+    my = S.shard_of(table, rank)
+    datas = [blob.get(o, s) for o, s in zip(my["stream_offset"], my["stream_bytes"])]
+
     dec = R.JpegDecoder(R.Backend.HARDWARE, local_rank)
     dec.set_path_policy(args.path)
-    streams = [R.JpegStream(b) for b in data]
-    dec.streams_to_device(streams)
-    # destinations: one HBM arena, every channel sized as the reference samples size them
-    # (samples/rocjpeg_samples_utils.h:318-399, tests/gpu_util.py channel_shapes)
-    from tests.gpu_util import channel_shapes
-    fmt = wl["fmt"]
-    shapes = []
-    for s in streams:
-        nc, css, w, h = dec.image_info(s)
-        shapes.append(channel_shapes(fmt, css, w, h))
-    total = sum(r * p for shp in shapes for r, p in shp)
-    out = torch.empty(total, dtype=torch.uint8, device=dev)
-    imgs, views, off = [], [], 0
-    for shp in shapes:
-        ptrs, pitches, vv = [], [], []
-        for r, p in shp:
-            ptrs.append(out[off:].data_ptr())
-            pitches.append(p)
-            vv.append(out[off:off + r * p].view(r, p))
-            off += r * p
-        imgs.append(R.make_image(ptrs, pitches))
-        views.append(vv)
-    params = R.decode_params(fmt)
-    n = len(streams)
-    hs = (ctypes.c_void_p * n)(*[s.handle for s in streams])
-    arr = (R.RocJpegImage * n)(*imgs)
-    L = R.lib()
+    fmt = getattr(R.OutputFormat, wl["fmt"])
+    run = BatchRun(dec, datas, fmt, dev)
+    n = run.n
 
-    def step():
-        st = L.rocJpegDecodeBatched(dec.handle, hs, n, ctypes.byref(params), arr)
-        if st != 0:
-            raise RuntimeError(R.error_name(st))
+    elapsed = run.timed(args.steps, args.warmup, world, dev)
+    # parity of the timed run's own output (the last step's), before anything else writes it
+    parity = run.parity(sorted({0, n // 2, n - 1}))
+    imgs = torch.tensor([n], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(imgs)
+    imgs_total = int(imgs.item()) * args.steps
 
-    for _ in range(args.warmup):
-        step()
-    dec.set_profiling(True)
-    k1 = {}
-    stage = {"host_ms": 0.0, "h2d_ms": 0.0, "destuff_ms": 0.0, "huffman_ms": 0.0, "idct_ms": 0.0, "output_ms": 0.0}
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    last = None
-    for _ in range(args.steps):
-        step()
-        last = dec.last_timings()
-        for k in stage:
-            stage[k] += last[k]
-        for k in ("entropy_chunks_ms", "entropy_resolve_ms", "entropy_serial_ms", "k1_launch_ms_sum",
-                  "k2_launch_ms_sum", "prog_entropy_ms", "prog_rows_ms"):
-            k1[k] = k1.get(k, 0.0) + last[k]
-        for j, name in enumerate(PROG_KERNELS):
-            k1[name] = k1.get(name, 0.0) + last["prog_kernel_ms"][j]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    dec.set_profiling(False)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    t = run.profiled(max(2, min(args.steps, 5)))
+    per_img = (t["ecs_bytes"] + TABLE_BYTES * n + t["output_bytes"]) / n
+    rf = roofline(t, n, args.workload, per_img)
 
-    # PCIe-inclusive rate (DESIGN.md): the same batch from host memory (fresh stream objects, so
-    # every call stages the bitstreams through pinned memory + H2D); reported, never `value`
-    host_streams = [R.JpegStream(b) for b in data]
+    # PCIe-inclusive rate (DESIGN.md 5): the same images from host memory in every call (fresh
+    # stream objects: each call stages the bitstreams through pinned memory + H2D)
+    host_streams = [R.JpegStream(b) for b in datas]
     hs2 = (ctypes.c_void_p * n)(*[s.handle for s in host_streams])
-    st = L.rocJpegDecodeBatched(dec.handle, hs2, n, ctypes.byref(params), arr)  # warm-up
+    L = R.lib()
+    st = L.rocJpegDecodeBatched(dec.handle, hs2, n, ctypes.byref(run.params), run.arr)
     torch.cuda.synchronize()
     t_h = time.perf_counter()
-    host_steps = 3
-    for _ in range(host_steps):
-        st |= L.rocJpegDecodeBatched(dec.handle, hs2, n, ctypes.byref(params), arr)
+    for _ in range(3):
+        st |= L.rocJpegDecodeBatched(dec.handle, hs2, n, ctypes.byref(run.params), run.arr)
     torch.cuda.synchronize()
-    host_rate = host_steps * n / (time.perf_counter() - t_h) if st == 0 else None
+    host_rate = 3 * n / (time.perf_counter() - t_h) if st == 0 else None
+    t_p = time.perf_counter()
+    for s in host_streams:
+        s.parse(s._data)
+    parse_host_rate = n / (time.perf_counter() - t_p)
     del host_streams
 
-    # parse rates (outside the timed region): host parser (rocJpegStreamParse, one thread) and
-    # the GPU marker scan (rocJpegAmdStreamParseDevice: headers on the host, O(bytes) on the GPU,
-    # streams left resident -- includes their HBM allocations)
-    t_p = time.perf_counter()
-    tmp = [R.JpegStream(b) for b in data]
-    parse_host_rate = n / (time.perf_counter() - t_p)
-    del tmp
-    dec.parse_device(data[:8])  # warm-up (first launch, buffers)
-    t_p = time.perf_counter()
-    pst, tmp = dec.parse_device(data)
-    parse_dev_rate = n / (time.perf_counter() - t_p) if pst == 0 else None
-    del tmp
-
-    # parity spot-check of this run's output (first images vs the CPU oracle), outside timing
-    from tests import oracle_lib as O
-    parity_ok = True
-    for q in range(min(2, n)):
-        ost, want = O.oracle_decode(data[q], int(fmt), shapes[q])
-        parity_ok = parity_ok and ost == 0 and all(np.array_equal(v.cpu().numpy(), w_) for v, w_ in zip(views[q], want))
-    parity_ok = bool(parity_ok)
-
+    res = None
     if rank == 0:
         K = args.steps
-        imgs_total = world * args.batch * K
-        value = imgs_total / elapsed
-        per = {k: v / K for k, v in stage.items()}
-        ecs = last["ecs_bytes"]
-        coef = last["coef_bytes"]
-        outb = last["output_bytes"]
-        # per-kernel launch durations (HIP events on each launch's own stream, summed over the
-        # call's launches -- with the pipelined launch K1 and K2 run as two launches each) and
-        # the algorithmic bytes those launches move (DESIGN.md "Roofline"):
-        #   K0 k_destuff: ECS bytes read + written; K1 k_entropy: destuffed ECS read + sparse
-        #   entries written; K2 k_rows: entries read + output written
-        entb = last["entry_bytes"]
-        kern = {
-            "k_destuff": (stage["destuff_ms"] / K, 1, 2 * ecs),
-            "k_entropy": (k1["k1_launch_ms_sum"] / K, max(1, last["k1_launches"]), ecs + entb),
-            "k_rows": (k1["k2_launch_ms_sum"] / K, max(1, last["k2_launches"]), entb + outb),
-        }
-        if last["prog_images"]:
-            # progressive (DESIGN.md 4a): k_prog lanes read their destuffed scans and write the
-            # coefficient band / DC-refinement bits; k_prog_wave reads its scans and writes a
-            # first scan's band + masks, or reads the nonzero masks and writes one 32-B record per
-            # refined block; k_prog_fold reads the records and reads +
-            # writes each touched dense block; K2 (dense) reads the coefficients, writes the output
-            pc = last["prog_coef_bytes"]
-            for j, name in enumerate(PROG_KERNELS):
-                if last["prog_kernel_launches"][j]:
-                    kern[name] = (k1[name] / K, last["prog_kernel_launches"][j], last["prog_kernel_bytes"][j])
-            kern["k_rows_dense"] = (k1["prog_rows_ms"] / K, 1, pc + outb)
-        dom = max(kern, key=lambda k: kern[k][0])
-        t_sum, launches, algo_bytes = kern[dom]
-        ach = algo_bytes / (t_sum * 1e-3) / 1e9 if t_sum > 0 else 0.0
-        traffic = pmc_traffic(dom, args.batch, launches, args.workload)
         res = {
             "metric": "images/s (1080p 4:2:0 batch) at 1/2/4/8 MI355X + achieved HBM GB/s",
-            "value": round(value, 2),
+            "value": round(imgs_total / elapsed, 2),
             "unit": "images/s",
             "n_gpus": world,
             "steps": K,
@@ -343,35 +529,44 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": wl["data"],
-            "config": {"workload": wl["workload"].format(batch=args.batch),
-                       "batch_per_gpu": args.batch, "output_format": fmt.name, "parallelism": f"images sharded, {world} rank(s)",
-                       "ecs_bytes_per_image": round(ecs / args.batch)},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": int(algo_bytes / launches),
-                         "avg_launch_ms": round(t_sum / launches, 4), "launches_per_step": launches,
-                         "per_kernel_launch_ms_sum": {k: round(v[0], 4) for k, v in kern.items()}},
-            "stages_ms_per_step": {k: round(v, 4) for k, v in per.items()},
-            "huffman_detail": dict({k: round(v / K, 4) for k, v in k1.items()}, chunks=last["chunks"],
-                                   intervals=last["intervals"], split_intervals=last["split_intervals"],
-                                   serial_fallbacks=last["serial_fallbacks"]),
-            "end_to_end_algorithmic_GBps": round((ecs + outb) / (elapsed / K) / 1e9, 2),
+            "config": {"workload": wl["workload"].format(batch=args.batch), "batch_per_gpu": args.batch,
+                       "output_format": wl["fmt"],
+                       "parallelism": f"images sharded over {world} rank(s) by LPT on a broadcast work table",
+                       "ecs_bytes_per_image": round(t["ecs_bytes"] / n)},
+            "roofline": rf,
+            "stages_ms_per_step": {k: round(t[k], 4) for k in ("host_ms", "h2d_ms", "destuff_ms", "huffman_ms",
+                                                                "idct_ms", "output_ms", "total_ms")},
+            "huffman_detail": {"intervals": t["intervals"], "chunks": t["chunks"],
+                               "split_intervals": t["split_intervals"], "serial_fallbacks": t["serial_fallbacks"],
+                               "entry_bytes_per_image": round(t["entry_bytes"] / n)},
+            "end_to_end_algorithmic_GBps": round(imgs_total * per_img / elapsed / 1e9, 2),
             "host_input_images_per_s_per_gpu": round(host_rate, 1) if host_rate else None,
             "parse_images_per_s": {"host_1_thread": round(parse_host_rate, 1),
-                                   "gpu_marker_scan": round(parse_dev_rate, 1) if parse_dev_rate else None},
-            "parity_first_image": parity_ok,
+                                   "gpu_marker_scan": round(n / run.parse_s, 1)},
+            "parity_timed_output": parity,
+            "work_table": {"images": int(len(table)), "bytes": int(table.nbytes), "build_ms": round(t_build * 1e3, 2),
+                           "build_and_broadcast_ms": round(t_tab * 1e3, 2),
+                           "lpt_imbalance": round(S.imbalance(shard_cost), 5),
+                           "images_per_rank": [int((table["shard"] == r).sum()) for r in range(world)]},
             "dataset_gen_s": round(t_gen, 1),
         }
-        if last["prog_images"]:
-            res["progressive_detail"] = {"images": last["prog_images"], "intervals": last["prog_intervals"],
-                                         "levels": last["prog_levels"],
-                                         "k1p_ms": round(k1["prog_entropy_ms"] / K, 4),
-                                         "k1p_launches": {n: last["prog_kernel_launches"][j]
-                                                          for j, n in enumerate(PROG_KERNELS)},
-                                         "k2_dense_ms": round(k1["prog_rows_ms"] / K, 4)}
-        if not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(data, shapes, int(fmt), wl["sample"])
-            res["cpu_libjpeg_turbo"] = turbo_baseline(data, procs)
+        if t["prog_images"]:
+            res["progressive_detail"] = {"images": t["prog_images"], "intervals": t["prog_intervals"],
+                                         "levels": t["prog_levels"], "k1p_ms": round(t["prog_entropy_ms"], 4),
+                                         "k2_dense_ms": round(t["prog_rows_ms"], 4)}
+    run.close()
+    if rank == 0 and extras:
+        res["extra_workloads"] = {w: run_extra(w, dec, extra_data[w], max(3, args.steps // 2), 1, dev) for w in extras}
+    if rank == 0:
+        if turbo is not None:
+            rate, nimg, wall = turbo.run()
+            res["cpu_baseline"] = {
+                "value": round(rate, 1), "unit": "images/s", "cores": cores, "kind": "reference",
+                "lib": "libjpeg-turbo 3.1 (Pillow bundle): the reference's host decode path of BASELINE config C1; "
+                       "BT.601 + fancy upsampling, a throughput comparator, not a parity oracle",
+                "sample": f"{nimg} decodes of this run's images, {cores} processes (one per core; {core_rule}; "
+                          f"nproc={nproc}), ~{wall:.1f} s each, per-process rates summed as jpegdecodeperf.cpp does"}
+            res["cpu_oracle_1core"] = cpu_oracle(datas, run.shapes, int(fmt))
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()

@@ -93,6 +93,9 @@ typedef struct {
   float prog_kernel_ms[3];
   uint32_t prog_kernel_launches[3];
   uint64_t prog_kernel_bytes[3];
+  /* images whose destination was not on the handle's device (another GPU or host memory):
+     decoded into device-local staging, then copied where the caller's pointers live */
+  uint32_t routed_images, reserved0;
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);
@@ -104,6 +107,47 @@ RocJpegStatus rocJpegAmdSetPathPolicy(RocJpegHandle handle, int policy);
 
 /* The handle's HIP stream (as void*), e.g. for external event timing. */
 RocJpegStatus rocJpegAmdGetStream(RocJpegHandle handle, void **hip_stream);
+
+/* ---- Multi-GPU batched decode: the per-image work table ----
+ * The reference has one device per handle (src/rocjpeg_api.cpp:107-120) and no multi-GPU path;
+ * its batched entry point (src/rocjpeg_decoder.cpp:196-292) is what each rank calls on its
+ * shard.  Rank 0 reads only the headers of the batch (O(header) per image; progressive streams
+ * are walked whole), builds one 64-byte record per image, assigns images to shards by greedy
+ * LPT on a decode-cost estimate, and broadcasts the table (RCCL over xGMI); every rank then
+ * parses and decodes the images of its own shard from the shared bitstream blob.  No pointers
+ * cross ranks: `stream_offset` is an offset into the blob every rank can read. */
+typedef struct {
+  uint64_t stream_offset;      /* the JPEG's first byte in the caller's blob */
+  uint32_t stream_bytes;       /* its length */
+  uint32_t ecs_bytes;          /* entropy-coded bytes after the first SOS header (estimate) */
+  uint32_t width, height;      /* luma size */
+  int32_t subsampling;         /* RocJpegChromaSubsampling (-1 unknown) */
+  uint32_t restart_intervals;  /* restart intervals of the scan (1 without DRI; progressive: 0) */
+  uint32_t flags;              /* ROCJPEG_AMD_WORK_* */
+  int32_t shard;               /* assigned shard (rank), -1 before rocJpegAmdAssignShards */
+  int32_t dest_device;         /* device the decoded image is written on */
+  uint32_t index;              /* position in the batch */
+  uint64_t cost;               /* LPT weight: ROCJPEG_AMD_COST_BYTE x ecs_bytes + pixels
+                                  (progressive: ROCJPEG_AMD_COST_BYTE_PROG per byte) */
+  uint64_t reserved;
+} RocJpegAmdWorkItem;
+#define ROCJPEG_AMD_WORK_PROGRESSIVE 1u
+#define ROCJPEG_AMD_WORK_BAD 2u         /* header parse failed: cost 0, still assigned */
+#define ROCJPEG_AMD_WORK_UNSUPPORTED 4u /* parsed, but the decode call would refuse it */
+#define ROCJPEG_AMD_COST_BYTE 8u        /* measured: K1 spends ~8x per ECS byte what K2 spends per pixel */
+#define ROCJPEG_AMD_COST_BYTE_PROG 120u /* progressive scans: serial refinement chains */
+
+/* Fill items[0..count) from the JPEGs at blob + offsets[i] (sizes[i] bytes each).  Returns
+ * SUCCESS even when some images fail to parse (they are flagged ROCJPEG_AMD_WORK_BAD). */
+RocJpegStatus rocJpegAmdBuildWorkTable(const unsigned char *blob, const uint64_t *offsets, const uint32_t *sizes,
+                                       int count, RocJpegAmdWorkItem *items);
+
+/* Greedy LPT (longest processing time first) over `num_shards` shards: items by decreasing
+ * cost, each to the shard with the least assigned cost (ties: lower shard).  Sets `shard` and
+ * `dest_device` (shard_devices[shard], or the shard index when shard_devices is NULL).
+ * shard_cost (optional, num_shards entries) receives each shard's summed cost. */
+RocJpegStatus rocJpegAmdAssignShards(RocJpegAmdWorkItem *items, int count, int num_shards, const int *shard_devices,
+                                     uint64_t *shard_cost);
 
 #if defined(__cplusplus)
 }

@@ -20,7 +20,7 @@ API_SYMBOLS = (
 EXT_SYMBOLS = (
     "rocJpegAmdStreamGetInfo", "rocJpegAmdStreamsToDevice", "rocJpegAmdSetProfiling", "rocJpegAmdGetLastTimings",
     "rocJpegAmdSetPathPolicy", "rocJpegAmdGetStream", "rocJpegAmdStreamParseDevice", "rocJpegAmdStreamGetIntervals",
-    "rocJpegAmdStreamGetDestuffBlocks",
+    "rocJpegAmdStreamGetDestuffBlocks", "rocJpegAmdBuildWorkTable", "rocJpegAmdAssignShards",
 )
 
 
@@ -99,7 +99,8 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("prog_coef_bytes", ctypes.c_uint64),
                 ("scan_device_streams", ctypes.c_uint32), ("scan_host_fallbacks", ctypes.c_uint32),
                 ("prog_kernel_ms", ctypes.c_float * 3), ("prog_kernel_launches", ctypes.c_uint32 * 3),
-                ("prog_kernel_bytes", ctypes.c_uint64 * 3)]
+                ("prog_kernel_bytes", ctypes.c_uint64 * 3),
+                ("routed_images", ctypes.c_uint32), ("reserved0", ctypes.c_uint32)]
 
 
 class RocJpegAmdInterval(ctypes.Structure):  # include/rocjpeg_amd.h
@@ -150,6 +151,9 @@ def lib():
                                                    ctypes.POINTER(ctypes.c_uint32)]
         L.rocJpegAmdStreamGetDestuffBlocks.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32,
                                                        ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+        L.rocJpegAmdBuildWorkTable.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
+                                               i32, vp]
+        L.rocJpegAmdAssignShards.argtypes = [vp, i32, i32, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_uint64)]
         for name in API_SYMBOLS + EXT_SYMBOLS:
             if name != "rocJpegGetErrorName":
                 getattr(L, name).restype = i32

@@ -161,6 +161,7 @@ int Decoder::Initialize() {
 int Decoder::GetImageInfo(Stream *s, uint8_t *nc, RocJpegChromaSubsampling *css, uint32_t *w, uint32_t *h) {
   std::lock_guard<std::mutex> lock(mu_);
   if (s == nullptr || nc == nullptr || css == nullptr || w == nullptr || h == nullptr) return kInvalidParameter;
+  std::lock_guard<std::mutex> sl(s->mutex());  // a concurrent re-parse must not tear the info
   int c = -1;
   const int st = ImageInfo(s->info(), nc, &c, w, h);
   *css = RocJpegChromaSubsampling(c);
@@ -180,9 +181,12 @@ int Decoder::StreamsToDevice(Stream *const *streams, int n) {
     const StreamInfo &in = s->info();
     const DecodePlan &p = s->plan();
     if (p.status != 0) continue;
-    Stream::Resident r;
+    if (s->scan_pending()) return kBadJpeg;  // header-only parse never completed
+    // every allocation lands in s->resident at once: an error part-way is freed by
+    // ReleaseResident (the stream's destructor or its next parse)
+    Stream::Resident &r = s->resident;
     r.device = device_;
-    r.generation = s->generation();
+    r.generation = s->generation() - 1;  // not valid until every copy below succeeded
     RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.ecs), in.ecs_size + 16));  // K0 reads <= 8 B past the end
     RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.segs), std::max<size_t>(p.segs.size() * sizeof(RjSegDev), 16)));
     RJ_HIP(hipMalloc(reinterpret_cast<void **>(&r.ds), std::max<size_t>(p.ds.size() * sizeof(RjDsBlock), 16)));
@@ -198,7 +202,7 @@ int Decoder::StreamsToDevice(Stream *const *streams, int n) {
       if (!p.ptabs.empty())
         RJ_HIP(hipMemcpy(r.ptabs, p.ptabs.data(), p.ptabs.size() * sizeof(RjHuffDev), hipMemcpyHostToDevice));
     }
-    s->resident = r;
+    r.generation = s->generation();
   }
   return kOk;
 }
@@ -206,6 +210,17 @@ int Decoder::StreamsToDevice(Stream *const *streams, int n) {
 int Decoder::ParseOnDevice(Stream *const *streams, const uint8_t *const *data, const size_t *len, int n) {
   std::lock_guard<std::mutex> lock(mu_);
   if (streams == nullptr || data == nullptr || len == nullptr || n < 0) return kInvalidParameter;
+  const int st = ParseOnDeviceImpl(streams, data, len, n);
+  // Whatever ended the call (a header that failed to parse, a HIP error), no stream is left
+  // half-parsed: a stream whose header walk deferred its marker scan gets the host scan.
+  for (int i = 0; i < n; i++) {
+    Stream *s = streams[i];
+    if (s != nullptr && s->scan_pending() && data[i] != nullptr) s->Parse(data[i], uint32_t(len[i]));
+  }
+  return st;
+}
+
+int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *data, const size_t *len, int n) {
   RJ_HIP(hipSetDevice(device_));
   const auto t0 = std::chrono::steady_clock::now();
   // ---- host: headers only (O(header) per stream) ----
@@ -368,6 +383,40 @@ int Decoder::ParseOnDevice(Stream *const *streams, const uint8_t *const *data, c
   return kOk;
 }
 
+int Decoder::PtrDevice(const void *p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  for (const PtrRange &r : ptr_cache_)
+    if (a >= r.lo && a < r.hi) return r.device;
+  int dev = -1;  // host memory unless HIP says device / managed
+  uintptr_t lo = a, hi = a + 1;
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) == hipSuccess) {
+    if (at.type == hipMemoryTypeDevice) dev = at.device;
+    else if (at.type == hipMemoryTypeManaged || at.isManaged) dev = device_;  // kernels write it in place
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, const_cast<void *>(p)) == hipSuccess && size) {
+      lo = reinterpret_cast<uintptr_t>(base);
+      hi = lo + size;
+    } else {
+      (void)hipGetLastError();
+    }
+  } else {
+    (void)hipGetLastError();  // pageable host memory
+  }
+  if (dev >= 0 && dev != device_) {  // another GPU: copies go peer to peer (xGMI) where allowed
+    if (peer_enabled_.size() <= size_t(dev)) peer_enabled_.resize(size_t(dev) + 1, 0);
+    if (!peer_enabled_[dev]) {
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, device_, dev) == hipSuccess && can) (void)hipDeviceEnablePeerAccess(dev, 0);
+      (void)hipGetLastError();  // already enabled, or no peer path: hipMemcpy2DAsync stages it
+      peer_enabled_[dev] = 1;
+    }
+  }
+  ptr_cache_.push_back({lo, hi, dev});
+  return dev;
+}
+
 int Decoder::Decode(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
   std::lock_guard<std::mutex> lock(mu_);
   if (streams == nullptr || params == nullptr || dst == nullptr || n < 0) return kInvalidParameter;
@@ -397,7 +446,18 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   for (int i = 0; i < n; i++) {
     const DecodePlan &p = streams[i]->plan();
     if (p.status != 0) return p.status;
+    if (streams[i]->scan_pending()) return kBadJpeg;  // header-only parse never completed
   }
+  // ---- destinations on another device or in host memory: decoded into staging, then copied
+  // (the allocation lookup is cached per call by address range) ----
+  ptr_cache_.clear();
+  routes_.clear();
+  std::vector<uint8_t> &routed = sc_.routed;
+  routed.assign(n, 0);
+  for (int i = 0; i < n; i++)
+    for (int c = 0; c < 4; c++)
+      if (dst[i].channel[c] != nullptr && PtrDevice(dst[i].channel[c]) != device_) routed[i] = 1;
+  uint64_t route_bytes = 0;
 
   const auto t_dedupe = std::chrono::steady_clock::now();
   // ---- table de-duplication ----
@@ -558,9 +618,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     const int css = in.css;
     const int32_t pw = d.out_w, ph = d.out_h, top = d.top, left = d.left;
     auto need = [&](int c) { return o.channel[c] != nullptr; };
+    uint32_t ext_rows[4] = {}, ext_bytes[4] = {};  // what the call writes per channel (routing)
     auto job = [&](uint32_t kind, uint32_t sel, int dc, int32_t rows, uint32_t bytes, uint32_t pitch, int32_t r0,
                    int32_t b0) {
       if (rows <= 0 || bytes == 0) return;
+      ext_rows[dc] = std::max(ext_rows[dc], uint32_t(rows));
+      ext_bytes[dc] = std::max(ext_bytes[dc], bytes);
       RjJobDev j;
       std::memset(&j, 0, sizeof(j));
       j.image = uint32_t(i);
@@ -632,6 +695,14 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         break;
       default:
         break;  // reference: unknown format writes nothing and succeeds
+    }
+    if (routed[i]) {
+      for (int c = 0; c < 4; c++) {
+        if (ext_rows[c] == 0 || o.channel[c] == nullptr) continue;
+        routes_.push_back(RouteCopy{uint32_t(i), uint32_t(c), ext_rows[c], ext_bytes[c], o.pitch[c], route_bytes,
+                                    o.channel[c]});
+        route_bytes += AlignUp(uint64_t(ext_rows[c] - 1) * o.pitch[c] + ext_bytes[c], 256);
+      }
     }
     // fast path: drop the general jobs again and count fused strips instead
     if (path_policy_ == 0 && FusedEligible(in, p, fmt, roi, o)) {
@@ -943,6 +1014,19 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   epoch_ = (epoch_ + 1) & 0x0FFFFFFFu;
   if (epoch_ == 0) epoch_ = 1;
   RJ_CHECK(d_planes_.Ensure(std::max<uint64_t>(plane_bytes, 256)));
+  if (!routes_.empty()) {  // routed images write device-local staging at the caller's pitch
+    RJ_CHECK(d_route_.Ensure(route_bytes));
+    uint8_t *rb = d_route_.as<uint8_t>();
+    for (const RouteCopy &rc : routes_) imgs[rc.image].dst[rc.chan] = rb + rc.off;
+    for (RjJobDev &j : jobs) {
+      if (!routed[j.image]) continue;
+      for (const RouteCopy &rc : routes_)
+        if (rc.image == j.image && rc.user == j.dst) {
+          j.dst = rb + rc.off;
+          break;
+        }
+    }
+  }
   uint8_t *h = h_stage_.data();
   uint8_t *dbase = d_desc_.as<uint8_t>();
   for (int i = 0; i < n; i++) {
@@ -1288,6 +1372,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (profiling_) RJ_HIP(hipEventRecord(ev_[4], stream_));
   RJ_HIP(LaunchOutputJobs(stream_, d_imgs, d_jobs, int(jobs.size()), rows_total, d_planes_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[5], stream_));
+  for (const RouteCopy &rc : routes_)  // to the caller's device / host memory
+    RJ_HIP(hipMemcpy2DAsync(rc.user, rc.pitch, d_route_.as<uint8_t>() + rc.off, rc.pitch, rc.row_bytes, rc.rows,
+                            hipMemcpyDefault, stream_));
   RJ_HIP(hipStreamSynchronize(stream_));
   if (prog_images && prog_pipe) {  // a refinement wave that gave up waiting (never expected)
     uint32_t err = 0;
@@ -1345,6 +1432,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   timings_.coef_bytes = coef_blocks * 128;  // dense-equivalent; the sparse bytes are data-dependent
   timings_.output_bytes = out_bytes;
   timings_.fused_images = fused_images;
+  timings_.routed_images = 0;
+  for (int i = 0; i < n; i++) timings_.routed_images += routed[i];
   timings_.prog_images = prog_images;
   timings_.prog_intervals = pival_total;
   timings_.prog_levels = prog_levels;

@@ -62,6 +62,27 @@ class Decoder {
 
  private:
   int DecodeLocked(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
+  int ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *data, const size_t *len, int n);
+  // Device of the allocation holding p (hipPointerGetAttributes, cached per call by address
+  // range); -1: host memory (pinned or pageable).
+  int PtrDevice(const void *p);
+
+  // Destinations that do not live on this handle's device (another GPU, host memory): the
+  // image is decoded into device-local staging at the caller's pitch, then copied to where
+  // the caller's pointer lives (hipMemcpy2DAsync; peer copies go over xGMI) -- SURVEY.md 8e.
+  struct PtrRange {
+    uintptr_t lo, hi;
+    int device;
+  };
+  std::vector<PtrRange> ptr_cache_;
+  struct RouteCopy {
+    uint32_t image, chan, rows, row_bytes, pitch;
+    uint64_t off;  // staging offset
+    void *user;
+  };
+  std::vector<RouteCopy> routes_;
+  std::vector<int> peer_enabled_;
+  DeviceBuffer d_route_;
 
   RocJpegBackend backend_;
   int device_;
@@ -92,7 +113,7 @@ class Decoder {
     std::vector<RjJobDev> jobs;
     std::vector<uint64_t> stage_off;
     std::vector<uint32_t> tab_of, row_prefix, grow_prefix, seg_lane0, lane_seg, bucket_pos, seg_pos;
-    std::vector<uint8_t> is_fused, row_group;
+    std::vector<uint8_t> is_fused, row_group, routed;
     std::vector<uint2> row_list;
     std::vector<uint32_t> prow_prefix, pgrow_prefix, prog_lanes, prog_bucket;  // progressive images
     std::vector<RjFoldJob> fold_jobs;

@@ -1,0 +1,138 @@
+"""Multi-GPU batched decode: the per-image work table, LPT shards, one broadcast.
+
+The reference decodes on one device per handle (src/rocjpeg_api.cpp:107-120); its batched call
+(src/rocjpeg_decoder.cpp:196-292) is what every rank runs here, on its own shard.  The flow, one
+process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI):
+
+  rank 0   build_work_table()   header walk of every image (C-ABI rocJpegAmdBuildWorkTable)
+           assign_shards()      greedy LPT on the decode-cost estimate (rocJpegAmdAssignShards)
+  all      broadcast_table()    ONE broadcast of the 64-byte records (the only collective)
+  rank r   shard_of(table, r)   its images; it parses them from the shared bitstream blob and
+                                calls rocJpegDecodeBatched on them
+
+No bitstream, pixel or pointer crosses ranks: `stream_offset` is an offset into a blob every
+rank can read (a dataset file on the node), and each rank's output lands on its own GPU
+(`dest_device`).  The records are the ctypes/numpy mirror of RocJpegAmdWorkItem
+(include/rocjpeg_amd.h).
+"""
+import ctypes
+
+import numpy as np
+
+from . import Status, lib
+
+WORK_ITEM_DTYPE = np.dtype([
+    ("stream_offset", "<u8"), ("stream_bytes", "<u4"), ("ecs_bytes", "<u4"),
+    ("width", "<u4"), ("height", "<u4"), ("subsampling", "<i4"), ("restart_intervals", "<u4"),
+    ("flags", "<u4"), ("shard", "<i4"), ("dest_device", "<i4"), ("index", "<u4"),
+    ("cost", "<u8"), ("reserved", "<u8"),
+])
+assert WORK_ITEM_DTYPE.itemsize == 64
+
+WORK_PROGRESSIVE = 1
+WORK_BAD = 2
+WORK_UNSUPPORTED = 4
+
+
+def _u8_pointer(blob):
+    """(ctypes pointer, keep-alive) for a bytes-like or uint8 ndarray blob (no copy for arrays)."""
+    if isinstance(blob, np.ndarray):
+        if blob.dtype != np.uint8 or not blob.flags["C_CONTIGUOUS"]:
+            raise ValueError("blob must be a contiguous uint8 array")
+        return ctypes.c_void_p(blob.ctypes.data), blob
+    buf = np.frombuffer(blob, dtype=np.uint8)
+    return ctypes.c_void_p(buf.ctypes.data), buf
+
+
+def build_work_table(blob, offsets, sizes, base_offset=0):
+    """One record per image of `blob` (images at `offsets`, `sizes` bytes).  `base_offset` is
+    added to every stream_offset (the blob is one part of a larger logical blob)."""
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    sizes = np.ascontiguousarray(sizes, dtype=np.uint32)
+    n = len(offsets)
+    if len(sizes) != n:
+        raise ValueError("offsets and sizes differ in length")
+    table = np.zeros(n, dtype=WORK_ITEM_DTYPE)
+    if n == 0:
+        return table
+    ptr, keep = _u8_pointer(blob)
+    st = lib().rocJpegAmdBuildWorkTable(ptr, offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                        sizes.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n,
+                                        ctypes.c_void_p(table.ctypes.data))
+    del keep
+    if st != 0:
+        raise RuntimeError(f"rocJpegAmdBuildWorkTable: {Status(st)!r}")
+    if base_offset:
+        table["stream_offset"] += np.uint64(base_offset)
+    return table
+
+
+def concat_tables(tables):
+    """Join per-part tables into one batch table (index = position in the batch)."""
+    t = np.concatenate(tables) if tables else np.zeros(0, dtype=WORK_ITEM_DTYPE)
+    t["index"] = np.arange(len(t), dtype=np.uint32)
+    return t
+
+
+def assign_shards(table, num_shards, shard_devices=None):
+    """Greedy LPT in place (shard, dest_device); returns each shard's summed cost."""
+    n = len(table)
+    cost = np.zeros(num_shards, dtype=np.uint64)
+    devs = None
+    if shard_devices is not None:
+        devs = (ctypes.c_int * num_shards)(*[int(d) for d in shard_devices])
+    st = lib().rocJpegAmdAssignShards(ctypes.c_void_p(table.ctypes.data) if n else None, n, int(num_shards), devs,
+                                      cost.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    if st != 0:
+        raise RuntimeError(f"rocJpegAmdAssignShards: {Status(st)!r}")
+    return cost
+
+
+def imbalance(shard_cost):
+    """max / mean - 1 of the shards' assigned cost."""
+    c = np.asarray(shard_cost, dtype=np.float64)
+    return float(c.max() / c.mean() - 1.0) if len(c) and c.mean() > 0 else 0.0
+
+
+def broadcast_table(table, src=0, device=None):
+    """The one collective of the path: rank `src` sends its table (a length, then the records as
+    bytes), every rank returns the same table.  `device`: where the tensors live for the backend
+    (a CUDA device for nccl/RCCL, cpu for gloo)."""
+    import torch
+    import torch.distributed as dist
+    dev = device if device is not None else torch.device("cpu")
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return table
+    rank = dist.get_rank()
+    n = torch.tensor([len(table) if rank == src else 0], dtype=torch.int64, device=dev)
+    dist.broadcast(n, src=src)
+    nbytes = int(n.item()) * WORK_ITEM_DTYPE.itemsize
+    if rank == src:
+        payload = torch.from_numpy(np.ascontiguousarray(table).view(np.uint8).copy()).to(dev)
+    else:
+        payload = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    if nbytes:
+        dist.broadcast(payload, src=src)
+    return payload.cpu().numpy().view(WORK_ITEM_DTYPE).copy()
+
+
+def shard_of(table, rank):
+    """This rank's records, in batch order."""
+    return table[table["shard"] == rank]
+
+
+class Blob:
+    """A logical bitstream blob made of parts (e.g. one dataset file per generator rank, each
+    memory-mapped): global offset -> bytes."""
+
+    def __init__(self, parts):
+        self.parts = list(parts)
+        self.bases = np.cumsum([0] + [len(p) for p in self.parts])[:-1].astype(np.uint64)
+
+    def part_base(self, k):
+        return int(self.bases[k])
+
+    def get(self, offset, size):
+        k = int(np.searchsorted(self.bases, np.uint64(offset), side="right")) - 1
+        o = int(offset) - int(self.bases[k])
+        return bytes(self.parts[k][o:o + int(size)])

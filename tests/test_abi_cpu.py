@@ -134,3 +134,42 @@ def test_create_without_gpu_fails_cleanly():
     assert st in (R.Status.EXECUTION_FAILED, R.Status.NOT_INITIALIZED)
     if h:
         R.lib().rocJpegDestroy(h)
+
+
+# ---- binary drop-in: the reference header and ours give identical layouts and signatures ----
+_REF_API = "/root/reference/api"
+_ABI_GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "abi_layout_reference.json")
+
+
+def _abi_probe(include_dir, tmp_path):
+    """Compile tests/c/abi_probe.c against the rocjpeg.h in `include_dir`: once -c with the
+    signature checks (incompatible pointer types are errors), once linked and run for the
+    layout JSON."""
+    import json
+    import subprocess
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "abi_probe.c")
+    flags = ["-std=c11", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", f"-I{include_dir}"]
+    subprocess.run(["gcc", *flags, "-c", "-DABI_SIGNATURES", "-Werror=incompatible-pointer-types", src,
+                    "-o", str(tmp_path / "sig.o")], check=True, capture_output=True)
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", *flags, src, "-o", str(exe)], check=True, capture_output=True)
+    return json.loads(subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout)
+
+
+def test_abi_layout_matches_reference_golden(tmp_path):
+    """include/rocjpeg.h vs the layout the reference header produced (committed fixture, so the
+    check runs where /root/reference is absent)."""
+    import json
+    ours = _abi_probe(INCLUDE, tmp_path)
+    assert ours == json.load(open(_ABI_GOLDEN))
+
+
+@pytest.mark.skipif(not os.path.isfile(os.path.join(_REF_API, "rocjpeg.h")), reason="reference header absent")
+def test_abi_layout_matches_reference_header(tmp_path):
+    """Both headers compiled side by side (api/rocjpeg.h:46-343): same sizeof / offsetof / enum
+    values, and every entry point type-checks against the same signature."""
+    (tmp_path / "ref").mkdir()
+    (tmp_path / "ours").mkdir()
+    ref = _abi_probe(_REF_API, tmp_path / "ref")
+    ours = _abi_probe(INCLUDE, tmp_path / "ours")
+    assert ours == ref

@@ -1,0 +1,127 @@
+"""Batch-level behaviour on the GPU:
+  * a full C2-size call (1024 x 1080p 4:2:0, DRI one MCU row) under the default pipelined
+    layout, every image compared with the oracle on the device;
+  * rocJpegAmdStreamParseDevice with a corrupt header in the batch: no stream is
+    left half-parsed, the good streams decode exactly;
+  * destinations that are not on the handle's device (pinned and pageable host memory) are
+    routed through staging and land byte-identical (SURVEY.md 8e destination routing)."""
+import io
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import rocjpeg_amd as R
+from tests import oracle_lib as O
+from tests.gpu_util import channel_shapes, torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = O.ROOT
+
+
+@pytest.fixture(scope="module")
+def dec():
+    torch()
+    d = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    yield d
+    d.close()
+
+
+def _c2_images(count, seed0=1234):
+    """The bench's C2 generator (seeded 1080p crops of the mug image + N(0,2) noise, Pillow q90
+    4:2:0, restart interval = one MCU row), threaded."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    bench._init_gen()
+    with ThreadPoolExecutor(16) as ex:
+        return list(ex.map(bench._make_jpeg, [(s, bench.WORKLOADS["c2"]["gen"]) for s in range(seed0, seed0 + count)]))
+
+
+def test_c2_1024_default_pipelined_layout(dec):
+    t = torch()
+    distinct, copies = 256, 4
+    datas = _c2_images(distinct)
+    with ThreadPoolExecutor(16) as ex:  # the oracle call releases the GIL
+        want = list(ex.map(lambda d: O.oracle_decode(d, int(R.OutputFormat.RGB), [(1080, 5760)]), datas))
+    assert all(st == 0 for st, _ in want)
+    streams = [R.JpegStream(datas[i % distinct]) for i in range(distinct * copies)]
+    dec.streams_to_device(streams)
+    out = t.full((len(streams), 1080, 5760), 0xA5, dtype=t.uint8, device="cuda")
+    imgs = [R.make_image([out[i].data_ptr()], [5760]) for i in range(len(streams))]
+    dec.set_profiling(True)
+    st = dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs)
+    tm = dec.last_timings()
+    dec.set_profiling(False)
+    assert st == 0, R.error_name(st)
+    assert tm["images"] == 1024 and tm["intervals"] == 1024 * 68
+    assert tm["pipe_groups"] == 2 and tm["split_intervals"] == 0  # the layout the bench runs
+    ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
+    bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
+    assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
+
+
+def _fixture(name):
+    ent = next(f for f in O.manifest() if f["name"] == name)
+    return O.fixture_bytes(ent)
+
+
+def test_parse_device_corrupt_header_leaves_no_pending_stream(dec):
+    t = torch()
+    good = [_fixture("p420_q90_ri_256x128"), _fixture("p444_q95_ri_128x128")]
+    bad = bytearray(good[0])
+    i = bad.index(b"\xff\xc0")
+    bad[i + 4:i + 6] = b"\x00\x01"  # SOF0 length 1: the header walk fails
+    st, streams = dec.parse_device(good + [bytes(bad)])
+    assert st == R.Status.BAD_JPEG
+    for s, d in zip(streams[:2], good):
+        nc, css, w, h = dec.image_info(s)
+        shapes = channel_shapes(R.OutputFormat.RGB, css, w, h)
+        buf = t.zeros(shapes[0], dtype=t.uint8, device="cuda")
+        assert dec.decode(s, R.decode_params(R.OutputFormat.RGB), R.make_image([buf.data_ptr()], [shapes[0][1]])) == 0
+        ost, want = O.oracle_decode(d, int(R.OutputFormat.RGB), shapes)
+        assert ost == 0 and np.array_equal(buf.cpu().numpy(), want[0])
+    # the stream whose header failed is not decodable
+    buf = t.zeros((128, 768), dtype=t.uint8, device="cuda")
+    assert dec.decode(streams[2], R.decode_params(R.OutputFormat.RGB), R.make_image([buf.data_ptr()], [768])) != 0
+
+
+@pytest.mark.parametrize("fmt", [R.OutputFormat.RGB, R.OutputFormat.YUV_PLANAR, R.OutputFormat.NATIVE])
+@pytest.mark.parametrize("where", ["pinned", "pageable", "mixed"])
+def test_host_destinations_are_routed(dec, fmt, where):
+    t = torch()
+    names = ["p420_q90_ri_256x128", "p422_q90_ri_192x96", "p444_q95_ri_128x128", "p420_q90_odd_97x65",
+             "p420_prog_128x96"]
+    datas = [_fixture(n) for n in names]
+    streams = [R.JpegStream(d) for d in datas]
+    bufs, imgs, shapes = [], [], []
+    for k, s in enumerate(streams):
+        nc, css, w, h = dec.image_info(s)
+        shp = channel_shapes(fmt, css, w, h, rgb_pitch_pad=16 if fmt == R.OutputFormat.RGB else 0)
+        shapes.append(shp)
+        host = where == "pinned" or (where == "mixed" and k % 2 == 0)
+        if where == "pageable" or (where == "mixed" and k % 2 == 1 and k != 3):
+            bb = [np.full(sh, 0xA5, np.uint8) for sh in shp]
+            ptrs = [b.ctypes.data for b in bb]
+        elif host:
+            bb = [t.full(sh, 0xA5, dtype=t.uint8).pin_memory() for sh in shp]
+            ptrs = [b.data_ptr() for b in bb]
+        else:  # device (k == 3 in the mixed batch)
+            bb = [t.full(sh, 0xA5, dtype=t.uint8, device="cuda") for sh in shp]
+            ptrs = [b.data_ptr() for b in bb]
+        bufs.append(bb)
+        imgs.append(R.make_image(ptrs, [sh[1] for sh in shp]))
+    dec.set_profiling(True)
+    st = dec.decode_batched(streams, R.decode_params(fmt), imgs)
+    tm = dec.last_timings()
+    dec.set_profiling(False)
+    assert st == 0, R.error_name(st)
+    assert tm["routed_images"] == (4 if where == "mixed" else 5)
+    for d, bb, shp in zip(datas, bufs, shapes):
+        ost, want = O.oracle_decode(d, int(fmt), shp)
+        assert ost == 0
+        for b, w_ in zip(bb, want):
+            got = b if isinstance(b, np.ndarray) else b.cpu().numpy()
+            assert np.array_equal(got, w_)
