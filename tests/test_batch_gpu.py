@@ -73,7 +73,7 @@ def test_parse_device_corrupt_header_leaves_no_pending_stream(dec):
     good = [_fixture("p420_q90_ri_256x128"), _fixture("p444_q95_ri_128x128")]
     bad = bytearray(good[0])
     i = bad.index(b"\xff\xc0")
-    bad[i + 4:i + 6] = b"\x00\x01"  # SOF0 length 1: the header walk fails
+    bad[i + 2:i + 4] = b"\x00\x01"  # SOF0 segment length 1: the header walk fails
     st, streams = dec.parse_device(good + [bytes(bad)])
     assert st == R.Status.BAD_JPEG
     for s, d in zip(streams[:2], good):
