@@ -95,7 +95,8 @@ typedef struct {
   uint64_t prog_kernel_bytes[3];
   /* images whose destination was not on the handle's device (another GPU or host memory):
      decoded into device-local staging, then copied where the caller's pointers live */
-  uint32_t routed_images, reserved0;
+  uint32_t routed_images;
+  uint32_t lean_k1;          /* 1: K1 ran the lean row-interval kernel (rj_huff.hip, raw entries) */
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);

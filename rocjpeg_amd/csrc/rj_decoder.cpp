@@ -144,6 +144,7 @@ int Decoder::Initialize() {
   if (const char *g = getenv("RJ_PIPE_GROUPS")) pipe_groups_ = std::max(1, std::min(kMaxPipe, atoi(g)));
   if (const char *m = getenv("RJ_PIPE_MIN")) pipe_min_ = uint32_t(std::max(1, atoi(m)));
   if (const char *o = getenv("RJ_SORT_LANES")) sort_lanes_ = atoi(o) != 0;
+  if (const char *l = getenv("RJ_LEAN")) lean_enabled_ = atoi(l) != 0;
   for (auto &q : pstream_) RJ_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
   for (auto &e : pev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : pk1_) RJ_HIP(hipEventCreate(&e));
@@ -464,8 +465,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   std::vector<uint32_t> &tab_of = sc_.tab_of;
   tab_of.resize(n);
   std::vector<const RjTableSet *> tabs;
+  std::vector<Stream *> &owner_stream = sc_.owner_stream;  // stream whose tables tabs[idx] are
   {
     std::vector<const DecodePlan *> owner;  // plan whose derived tables tabs[idx] points at
+    owner_stream.clear();
     std::unordered_map<uint64_t, std::vector<uint32_t>> seen;
     uint32_t last = UINT32_MAX;  // batches are usually one encoder's output: try the last hit first
     for (int i = 0; i < n; i++) {
@@ -485,6 +488,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
           idx = uint32_t(tabs.size());
           tabs.push_back(&p.tables);
           owner.push_back(&p);
+          owner_stream.push_back(streams[i]);
           cands.push_back(idx);
         }
       }
@@ -961,6 +965,20 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   }
   const uint32_t lanes_dev = lanes_all - lanes_wg;
 
+  // ---- lean K1 (rj_huff.hip): when every baseline image of the call is a "row" image (each
+  // restart interval inside one MCU row) and no interval is split, K1 writes raw entries and K2
+  // restores the DC predictions ----
+  bool lean = lean_enabled_ && !any_split && seg_total > 0;
+  for (int i = 0; i < n && lean; i++) {
+    const DecodePlan &p = streams[i]->plan();
+    if (p.progressive) continue;
+    const uint32_t ri = streams[i]->info().restart_interval;
+    lean = ri > 0 && p.mcux % ri == 0 && p.nblk_mcu <= RJ_MAX_BLK_MCU;
+  }
+  if (lean)
+    for (int i = 0; i < n; i++) imgs[i].dc_diff = streams[i]->plan().progressive ? 0u : 1u;
+  timings_.lean_k1 = lean ? 1u : 0u;
+
   // ---- one pinned staging blob, uploaded in two parts: A (descriptors, tables, non-resident
   // bitstreams) before K0; B (K1 lane order, K2 row lists) after K0 is launched -- the lane
   // sort and row classes below are host work that then runs while K0 executes. ----
@@ -976,7 +994,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t off_pgrows = AlignUp(off_prows + n * sizeof(uint32_t), 256);
   const uint64_t off_plane = AlignUp(off_pgrows + n * sizeof(uint32_t), 256);
   const uint64_t off_fold = AlignUp(off_plane + prog_lanes.size() * sizeof(uint32_t), 256);
-  const uint64_t off_stage = AlignUp(off_fold + fold_jobs.size() * sizeof(RjFoldJob), 256);
+  const uint64_t off_lean = AlignUp(off_fold + fold_jobs.size() * sizeof(RjFoldJob), 256);
+  const uint64_t off_stage = AlignUp(off_lean + (lean ? tabs.size() * sizeof(RjLeanTables) : 0), 256);
   const uint64_t blob_a = AlignUp(off_stage + stage_bytes, 256);
   const uint64_t n_lane_seg = any_split ? lane_seg.size() : (sorted ? seg_total : 0);
   const uint64_t off_lane_seg = blob_a;
@@ -1067,6 +1086,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   }
   std::memcpy(h + off_imgs, imgs.data(), n * sizeof(RjImageDev));
   for (size_t t = 0; t < tabs.size(); t++) std::memcpy(h + off_tabs + t * sizeof(RjTableSet), tabs[t], sizeof(RjTableSet));
+  if (lean)
+    for (size_t t = 0; t < tabs.size(); t++)
+      std::memcpy(h + off_lean + t * sizeof(RjLeanTables), owner_stream[t]->LeanTables(), sizeof(RjLeanTables));
+  const RjLeanTables *d_lean = reinterpret_cast<const RjLeanTables *>(dbase + off_lean);
   if (!jobs.empty()) std::memcpy(h + off_jobs, jobs.data(), jobs.size() * sizeof(RjJobDev));
   std::memcpy(h + off_rows, row_prefix.data(), n * sizeof(uint32_t));
   std::memcpy(h + off_grows, grow_prefix.data(), n * sizeof(uint32_t));
@@ -1330,8 +1353,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0 and upload B done
     if (getenv("RJ_DEBUG_PIPE_SERIAL")) {  // development: each class's K1 alone, one after another
       for (int g = 0; g < ngroups; g++) {
-        RJ_HIP(LaunchEntropyLanes(stream_, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g],
-                                  d_destuff_.as<uint8_t>(), d_tabs, cbuf, epoch_));
+        if (lean)
+          RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g],
+                                 d_destuff_.as<uint8_t>(), d_tabs, d_lean, cbuf));
+        else
+          RJ_HIP(LaunchEntropyLanes(stream_, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g],
+                                    d_destuff_.as<uint8_t>(), d_tabs, cbuf, epoch_));
         if (profiling_) RJ_HIP(hipEventRecord(pk1_[g], stream_));
       }
     }
@@ -1339,8 +1366,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       hipStream_t st = g == ngroups - 1 ? stream_ : pstream_[g];
       if (st != stream_) RJ_HIP(hipStreamWaitEvent(st, pev_[kMaxPipe - 1], 0));
       if (profiling_) RJ_HIP(hipEventRecord(k1s_[g], st));
-      RJ_HIP(LaunchEntropyLanes(st, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g], d_destuff_.as<uint8_t>(),
-                                d_tabs, cbuf, epoch_));
+      if (lean)
+        RJ_HIP(LaunchHuffLanes(st, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g], d_destuff_.as<uint8_t>(),
+                               d_tabs, d_lean, cbuf));
+      else
+        RJ_HIP(LaunchEntropyLanes(st, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g], d_destuff_.as<uint8_t>(),
+                                  d_tabs, cbuf, epoch_));
       if (profiling_) RJ_HIP(hipEventRecord(pk1_[g], st));
       RJ_HIP(hipEventRecord(kev_[g], st));
       for (int q = 0; q < g; q++) RJ_HIP(hipStreamWaitEvent(st, kev_[q], 0));  // rows spanning classes
@@ -1359,10 +1390,16 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
     for (int g = 0; g + 1 < ngroups; g++) RJ_HIP(hipStreamWaitEvent(stream_, pev_[g], 0));
   } else {
-    for (int stage = 0; stage < 3; stage++) {
-      RJ_HIP(LaunchEntropy(stream_, stage, d_imgs, n, lanes_wg, lanes_dev, seg_total, d_destuff_.as<uint8_t>(),
-                           d_tabs, cbuf, epoch_));
-      if (profiling_ && stage < 2) RJ_HIP(hipEventRecord(ev_[6 + stage], stream_));
+    if (lean) {  // no split interval: one pass, no resolution / serial stages
+      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, seg_total, d_destuff_.as<uint8_t>(), d_tabs, d_lean, cbuf));
+      if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
+      if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
+    } else {
+      for (int stage = 0; stage < 3; stage++) {
+        RJ_HIP(LaunchEntropy(stream_, stage, d_imgs, n, lanes_wg, lanes_dev, seg_total, d_destuff_.as<uint8_t>(),
+                             d_tabs, cbuf, epoch_));
+        if (profiling_ && stage < 2) RJ_HIP(hipEventRecord(ev_[6 + stage], stream_));
+      }
     }
     if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
     RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr));
@@ -1420,6 +1457,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   }
 #ifdef RJ_EXP_STAMPS
   if (getenv("RJ_DEBUG_STAMPS")) DumpRowStamps();
+#endif
+#ifdef RJ_HL_STAMPS
+  if (getenv("RJ_DEBUG_STAMPS") && lean) DumpHuffStamps();
 #endif
 
   timings_.images = uint32_t(n);

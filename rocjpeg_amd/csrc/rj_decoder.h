@@ -100,6 +100,7 @@ class Decoder {
   int pipe_groups_ = 2;            // env RJ_PIPE_GROUPS (1 = sequential)
   uint32_t pipe_min_ = 2048;       // env RJ_PIPE_MIN: fewest intervals worth pipelining
   bool sort_lanes_ = true;         // env RJ_SORT_LANES=0: K1 lanes in interval order
+  bool lean_enabled_ = true;       // env RJ_LEAN=0: never the lean K1 (rj_huff.hip)
   hipStream_t pstream_[kMaxPipe - 1] = {};
   hipEvent_t pev_[kMaxPipe] = {};
   hipEvent_t pk1_[kMaxPipe] = {};
@@ -117,6 +118,7 @@ class Decoder {
     std::vector<uint2> row_list;
     std::vector<uint32_t> prow_prefix, pgrow_prefix, prog_lanes, prog_bucket;  // progressive images
     std::vector<RjFoldJob> fold_jobs;
+    std::vector<Stream *> owner_stream;
   } sc_;
   hipEvent_t prog_ev_[3] = {};  // profiling: K1p start, K1p end (dense K2 start), dense K2 end
   std::vector<hipEvent_t> prog_lev_ev_;  // development (RJ_DEBUG_PROG): per-level K1p spans

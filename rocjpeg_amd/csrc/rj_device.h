@@ -181,6 +181,32 @@ struct RjTableSet {
   uint16_t qz[4][64];  // zigzag (DQT) order, as stored by the parser (rocjpeg_parser.cpp:239)
 };
 
+// ---- lean K1 (rj_huff.hip): "row" images, whose every restart interval lies inside one MCU
+// row, are decoded into raw entries and K2 restores the DC predictions ----
+// One 32-bit table entry per code prefix; every field the symbol step needs is in it:
+//   [4:0]  (32 - n) & 31, n = code bits + extra bits (the bit-field offset of the extra bits)
+//   [12:8] n                       [13] the symbol writes an entry (DC; AC coefficient)
+//   [19:16] s (extra bits)         [27:21] R: zigzag run (DC 0; AC r; ZRL 15; EOB 63 -> k >= 64)
+//   bit 31: code longer than the first level: [7:0] = AC second-level subtable, 0xFF = search
+// First levels: DC 10 bits, AC 11 bits; AC codes of 12..16 bits: up to RJ_HL_SUBS subtables of
+// 32 entries (the next 5 bits) per table.
+#define RJ_HL_DC_BITS 10
+#define RJ_HL_AC_BITS 11
+#define RJ_HL_SUBS 8
+#define RJ_HL_AC_WORDS ((1 << RJ_HL_AC_BITS) + RJ_HL_SUBS * 32)
+#define RJ_HL_DC_WORDS (1 << RJ_HL_DC_BITS)
+#define RJ_HL_ESC 0x80000000u
+struct RjLeanTables {  // LDS image: AC0, AC1 (first level + subtables), DC0, DC1
+  uint32_t ac[2][RJ_HL_AC_WORDS];
+  uint32_t dc[2][RJ_HL_DC_WORDS];
+};
+// Raw entry (lean K1 -> K2): [14:0] the symbol's extra bits, [19:16] s, [27:21] zigzag position
+// (0 = the block's DC, which holds the DC *difference*; 64..78 only on corrupt data: position 63;
+// 127 = end of stream), bit 28: zero block (libjpeg's insufficient-data / missing-marker blocks:
+// every coefficient 0, DC absolute).
+#define RJ_RE_TERM (127u << 21)
+#define RJ_RE_ZERO ((1u << 28))
+
 // Output jobs of the general (two-stage) path: one per written channel.
 enum RjJobKind : uint32_t {
   RJ_JOB_COPY = 0,      // CopyChannel: surface plane bytes, dst pitch bytes per row
@@ -270,6 +296,7 @@ struct RjImageDev {
   uint64_t destuff_off;  // into the destuffed buffer
   uint64_t ent_off;      // in entries (sparse coefficients), group-aligned
   uint32_t ri_mcus;      // MCUs per restart interval (0: one interval)
+  uint32_t dc_diff;      // 1: lean K1 raw entries (DC differences; K2 restores the predictions)
   uint32_t chunk_prefix; // exclusive prefix of K1 chunks over the batch (unpadded)
   // component planes (general path)
   uint64_t plane_off[4];

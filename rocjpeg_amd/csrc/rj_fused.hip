@@ -117,6 +117,14 @@ struct Nav {
 // <= 64 entries.  Entries are consumed row by row from the window; the ordinal of an entry's
 // block is the number of block starts at or before it, so rows need no alignment to blocks.
 // cbits: component of each block within the MCU (2 bits each), for the DC corrections.
+// libjpeg HUFF_EXTEND of a raw entry (lean K1): the s extra bits as a signed value (s = 0 -> 0)
+__device__ __forceinline__ int raw_value(uint32_t e) {
+  const uint32_t s = (e >> 16) & 15u, raw = e & 0x7FFFu;
+  const uint32_t half = (1u << s) >> 1;
+  return raw < half ? int(raw) - int(2 * half - 1) : int(raw);
+}
+
+template <bool kRaw>
 __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefBuf &coefs,
                                              const uint32_t *__restrict__ ent, uint32_t lane, uint32_t nb,
                                              uint32_t drop, uint32_t nblk, uint32_t cbits, EntWin &win, Nav &nv,
@@ -139,22 +147,25 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
       win.load(ent, nv.cur(), lane);
     }
     const uint32_t piece = min(need - done, nv.bleft);  // blocks taken from this piece
-    const bool fix_dc = (nv.dcd[0] | nv.dcd[1] | nv.dcd[2]) != 0;
+    const bool fix_dc = !kRaw && (nv.dcd[0] | nv.dcd[1] | nv.dcd[2]) != 0;
     uint32_t seen = 0;                                  // block starts before the current row
     bool found = false;
     for (uint32_t guard = 0; !found && guard < (1u << 20); guard++) {  // bounded even on a corrupt stream
 #pragma unroll
       for (int r = 0; r < RJ_WIN_ROWS; r++) {
         const uint32_t e = win.w[r];
-        const uint32_t p = (e >> 16) & 127u;
+        // kRaw: zigzag position at [27:21] (64..78 on corrupt data = position 63), else [22:16]
+        uint32_t p = kRaw ? (e >> 21) & 127u : (e >> 16) & 127u;
+        if (kRaw) p = p == 127u ? p : min(p, 63u);
         const bool st = p == 0 || p == 127;
         const uint64_t m = __ballot(st);
         const uint32_t below = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
         const uint32_t ord = seen + below + (st ? 1u : 0u) - 1u;
         const uint32_t blk = done + ord;  // block index counted from the first dropped one
         if (ord < piece && p < 64u && blk >= drop) {
-          int v = int16_t(e & 0xFFFFu);
-          if (fix_dc && p == 0) {
+          int v = kRaw ? raw_value(e) : int(int16_t(e & 0xFFFFu));
+          if (kRaw && (e & RJ_RE_ZERO)) v = -32768;  // zero block: marked for the DC restore
+          if (!kRaw && fix_dc && p == 0) {
             const uint32_t bi = (blk - drop) % nblk;  // strips start at an MCU boundary
             const uint32_t cc = (cbits >> (2 * bi)) & 3u;
             v += cc == 0 ? nv.dcd[0] : (cc == 1 ? nv.dcd[1] : nv.dcd[2]);
@@ -175,6 +186,48 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
     done += piece;
     nv.bleft -= piece;
   }
+}
+
+// Inclusive prefix sum over the wave's 64 lanes (DPP: row shifts, then row broadcasts).
+__device__ __forceinline__ int wave_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
+// DC prediction of a strip of raw-entry blocks (lean K1 wrote differences; T.81 F.2.1.3.1):
+// lane = block of the strip (MCU order), its component c.  Per component an inclusive scan of
+// the differences over the strip, plus the running predictor `carry` of the previous strips of
+// the row; a restart interval starting inside the strip (every ri MCUs) resets it there.  Zero
+// blocks (marked -32768) are absolute 0 (libjpeg's insufficient data / missing marker: every
+// later block of the interval is one too).  Writes the absolute DC back into the LDS block.
+__device__ __forceinline__ void restore_dc(uint8_t *s_buf, uint32_t tid, uint32_t nb, uint32_t nblk, uint32_t c,
+                                           uint32_t mx0, uint32_t mcu_row0, uint32_t ri, int (&carry)[3]) {
+  int16_t *dcp = reinterpret_cast<int16_t *>(s_buf + tid * RJ_BLK_STRIDE);
+  const int d = tid < nb ? int(*dcp) : 0;
+  const bool zero = d == -32768;
+  const int dd = zero ? 0 : d;
+  // the last interval start at or before this block's MCU, as a lane (-1: before the strip)
+  const uint32_t m = mcu_row0 + mx0 + tid / nblk;
+  const uint32_t mstart = m - m % ri;
+  const int rlane = mstart >= mcu_row0 + mx0 ? int((mstart - mcu_row0 - mx0) * nblk) : -1;
+  int pred = 0;
+#pragma unroll
+  for (uint32_t cc = 0; cc < 3; cc++) {
+    const int sc = wave_scan(c == cc ? dd : 0);
+    // value of the scan just before the reset lane (0 if the reset is at lane 0)
+    const int before = __shfl(sc, rlane > 0 ? rlane - 1 : 0);
+    const int mine = rlane < 0 ? carry[cc] + sc : sc - (rlane > 0 ? before : 0);
+    if (c == cc) pred = mine;
+    // the next strip starts from the last block's predictor
+    const int last = __builtin_amdgcn_readlane(mine, int(nb - 1));
+    carry[cc] = last;
+  }
+  if (tid < nb) *dcp = int16_t(zero ? 0 : pred);
 }
 
 // Two sign-magnitude int16 (bit 15 = negative) -> two's complement, per half (packed ops).
@@ -287,6 +340,9 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
   for (uint32_t k = tid; k < ncomp * 64; k += 64) s_q[k >> 6][k & 63] = ts->qz[im.comp_tq[k >> 6] & 3][k & 63];
 
   const uint32_t mcux = U(im.mcux);
+  const bool dc_diff = !kDense && U(im.dc_diff) != 0;  // raw entries: restore_dc per strip
+  const uint32_t ri_dc = U(im.ri_mcus ? im.ri_mcus : mcux);
+  int carry[3] = {0, 0, 0};
   const uint32_t strips_x = (mcux + S - 1) / S;
   const uint32_t *ent = coefs.ent;
   uint32_t cbits = 0;  // component of each block within the MCU
@@ -344,11 +400,16 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
     if constexpr (kDense) {
       if (has_blk) load_dense_block(im, coefs.dense, lane_blk, mx0, my, inter, s_buf + tid * RJ_BLK_STRIDE);
     } else {
-      parse_blocks(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf);
+      if (dc_diff) parse_blocks<true>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf);
+      else parse_blocks<false>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf);
       drop = 0;
       if (sx + 1 < strips_x && nv.bleft) win.load(ent, nv.cur(), tid);  // next strip's window: lands behind B and C
     }
     __syncthreads();
+    if (!kDense && dc_diff) {
+      restore_dc(s_buf, tid, nb, nblk, lane_blk >> 12, mx0, my * mcux, ri_dc, carry);
+      __syncthreads();
+    }
 
     RJ_STAMP(tb);
     RJ_STAMP_ADD(0, tb - ta);

@@ -1,0 +1,320 @@
+// rj_huff.hip -- lean K1: baseline Huffman decode of "row" images (every restart interval
+// inside one MCU row), one lane per interval (T.81 F.2.2, libjpeg jdhuff.c semantics).
+//
+// The reference hands this step to VCN (src/rocjpeg_vaapi_decoder.cpp:677-689).  At ~1 wave per
+// SIMD (a C2 batch has 68 intervals per image) the serial symbol chain is issue-bound, so the
+// step keeps only what the bit position depends on:
+//   * one 32-bit table entry per code prefix carries every field the step uses (rj_device.h
+//     RjLeanTables): bit count, extra-bit width, run, whether it writes an entry;
+//   * the step writes the *raw* symbol (extra bits + size + zigzag position): sign extension
+//     and the DC prediction move to K2 (rj_fused.hip), which sees 64 blocks at once and needs
+//     a handful of instructions per strip for them;
+//   * bits: the two stream words holding the bit position in registers, the next one read one
+//     step ahead from the lane's LDS ring; a 32-bit peek is one v_alignbit_b32 (q = -pos);
+//   * block / MCU bookkeeping: the block index inside the MCU selects the tables through a
+//     2-bit-per-block pattern.
+// Everything else (ring refills from HBM, stage flushes, libjpeg's insufficient-data and
+// missing-marker rules) happens at wave-uniform phase boundaries every RJ_HL_PHASE symbols, and
+// the per-lane activity / end-of-data selects only in the phases where some lane may finish.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#include "rj_device.h"
+#include "rj_kernels.h"
+#include "rj_math.h"
+
+namespace rj {
+
+#define RJ_HL_WG 256
+#define RJ_HL_CHUNKS 8                      // 16-B chunks in a lane's bit ring
+#define RJ_HL_WORDS (RJ_HL_CHUNKS * 4)      // 32 words
+#define RJ_HL_STAGE 16                      // staged entries per lane
+#define RJ_HL_GROUP 8                       // flushed in 32-B groups: < 8 pending at a phase start
+#define RJ_HL_PHASE 8                       // symbols per phase (<= 8 words: 31 bits per symbol)
+// LDS byte offsets of the four tables (RjLeanTables order)
+#define RJ_HL_AC_BYTES (RJ_HL_AC_WORDS * 4)
+#define RJ_HL_DC0 (2 * RJ_HL_AC_BYTES)
+#define RJ_HL_LUT_WORDS (2 * RJ_HL_AC_WORDS + 2 * RJ_HL_DC_WORDS)
+
+__device__ const uint4 rj_hl_zero[2] = {};
+
+#ifdef RJ_HL_STAMPS  // diagnostic build: cycles in the symbol steps / the phase ends, summed over waves
+__device__ unsigned long long rj_hl_stamp[8];
+#define RJ_HL_COUNT_ESC st_esc++
+#else
+#define RJ_HL_COUNT_ESC
+#endif
+
+// word w of the lane's column of a lane-interleaved LDS array ([w][lane]: conflict-free)
+struct HCol {
+  uint32_t *base;
+  __device__ __forceinline__ uint32_t &operator[](uint32_t w) const { return base[w * RJ_HL_WG]; }
+};
+
+__device__ __forceinline__ void hl_put(const HCol &ring, uint32_t slot, const uint4 &v) {
+  const uint32_t w0 = __builtin_bswap32(v.x), w1 = __builtin_bswap32(v.y);
+  const uint32_t w2 = __builtin_bswap32(v.z), w3 = __builtin_bswap32(v.w);
+  ring[4 * slot] = w0;
+  ring[4 * slot + 1] = w1;
+  ring[4 * slot + 2] = w2;
+  ring[4 * slot + 3] = w3;
+}
+
+// the 32-B group of staged entries [from, from + 8) (from a multiple of 8) to HBM
+__device__ __forceinline__ void hl_flush(const HCol &stage, uint32_t from, uint32_t *dst) {
+  uint32_t w[RJ_HL_GROUP];
+  const uint32_t s0 = from & (RJ_HL_STAGE - 1);
+#pragma unroll
+  for (int q = 0; q < RJ_HL_GROUP; q++) w[q] = stage[s0 + q];
+  uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+  gp(d4)[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  gp(d4)[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+// Codes the first level does not resolve (rare): AC second level, or libjpeg's canonical
+// search (jpeg_huff_decode) on the table in HBM, repacked into the entry format.
+__device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool isdc, uint32_t acbase,
+                                           const uint32_t *s_lut, const RjTableSet *ts, uint32_t ids) {
+  const uint32_t sub = e & 0xFFu;
+  const RjHuffDev *t = isdc ? &ts->dc[ids & 1u] : &ts->ac[(ids >> 1) & 1u];
+  if (!isdc && sub < RJ_HL_SUBS)
+    return s_lut[(acbase >> 2) + (1u << RJ_HL_AC_BITS) + sub * 32u + ((peek >> (32 - RJ_HL_AC_BITS - 5)) & 31u)];
+  const uint32_t p16 = peek >> 16;
+  uint32_t len = 17, sym = 0;  // bad code: 17 bits, symbol 0 (libjpeg JWRN_HUFF_BAD_CODE)
+#pragma unroll 1
+  for (uint32_t l = 1; l <= 16; l++)
+    if (p16 < t->maxcode16[l]) {
+      len = l;
+      sym = t->vals[((p16 >> (16 - l)) + t->valoff[l]) & 255];
+      break;
+    }
+  const uint32_t s = sym & 15u, r = sym >> 4;
+  const uint32_t R = isdc ? 0u : (s ? r : (r == 15 ? 15u : 63u));
+  const uint32_t emit = (isdc || s) ? 1u : 0u;
+  const uint32_t n = len + s;
+  return ((32u - n) & 31u) | (n << 8) | (emit << 13) | (s << 16) | (R << 21);
+}
+
+// One symbol step.  SAFE: per-lane activity (blocks_left) and libjpeg's insufficient-data rule.
+#define RJ_HL_STEP(SAFE)                                                                                  \
+  do {                                                                                                    \
+    const uint32_t peek = __builtin_amdgcn_alignbit(wa, wb, q);                                           \
+    uint32_t e = s_lut[(tb >> 2) + (peek >> tsh)];                                                        \
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(e >= RJ_HL_ESC) != 0, 0)) {                          \
+      RJ_HL_COUNT_ESC;                                                                                    \
+      if (e >= RJ_HL_ESC) e = hl_escape(e, peek, tsh != 21u, acb, s_lut, tset, pat >> b);                 \
+    }                                                                                                     \
+    const uint32_t raw = __builtin_amdgcn_ubfe(peek, e, e >> 16);                                         \
+    uint32_t entry = ((e & 0x0FEF0000u) | raw) + (k << 21);                                               \
+    uint32_t emit = (e >> 13) & 1u;                                                                       \
+    const uint32_t qold = q;                                                                              \
+    q -= (e >> 8) & 31u;                                                                                  \
+    uint32_t kn = k + ((e >> 21) & 127u) + 1u;                                                            \
+    if (SAFE) {                                                                                           \
+      entry = skip ? RJ_RE_ZERO : entry; /* libjpeg: the rest of the interval is zero blocks */          \
+      emit = skip ? 1u : emit;                                                                            \
+      kn = skip ? 64u : kn;                                                                               \
+      emit = blocks_left > 0 ? emit : 0u;                                                                 \
+    }                                                                                                     \
+    stage[ne & (RJ_HL_STAGE - 1)] = entry; /* a non-emitted write lands in the next free slot */          \
+    ne += emit;                                                                                           \
+    {                                                                                                     \
+      const bool adv = (qold ^ q) > 31u; /* the bit position entered the next word */                   \
+      wa = adv ? wb : wa;                                                                                 \
+      wb = adv ? wc : wb;                                                                                 \
+      rr += adv ? 1u : 0u;                                                                                \
+      wc = ring[rr & (RJ_HL_WORDS - 1)];                                                                  \
+    }                                                                                                     \
+    const bool bend = kn >= 64u;                                                                          \
+    k = bend ? 0u : kn;                                                                                   \
+    const uint32_t bn = b + 2u == nb2 ? 0u : b + 2u;                                                      \
+    if (SAFE) {                                                                                           \
+      const bool act = blocks_left > 0;                                                                   \
+      blocks_left -= (bend && act) ? 1u : 0u;                                                             \
+      skip = skip || (bend && bn == 0u && (0u - q) > nbits);                                              \
+    } else {                                                                                              \
+      blocks_left -= bend ? 1u : 0u;                                                                      \
+    }                                                                                                     \
+    b = bend ? bn : b;                                                                                    \
+    /* next symbol's table: the new block's DC table, or the current block's AC table */                 \
+    const uint32_t ids = pat >> b;                                                                        \
+    acb = bend ? ((ids >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES) : acb;                                      \
+    const uint32_t dcb = RJ_HL_DC0 + ((ids & 1u) << (RJ_HL_DC_BITS + 2));                                 \
+    tb = bend ? dcb : acb;                                                                                \
+    tsh = bend ? uint32_t(32 - RJ_HL_DC_BITS) : uint32_t(32 - RJ_HL_AC_BITS);                            \
+  } while (0)
+
+// Lane `g` of [lane0, lane0 + nlanes): the interval rj_lane_seg(g), decoded whole.
+__global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0,
+                                                      uint32_t nlanes, const uint8_t *__restrict__ destuffed,
+                                                      const RjTableSet *__restrict__ tabsets,
+                                                      const RjLeanTables *__restrict__ lean, RjCoefBuf coefs) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_HL_WORDS][RJ_HL_WG];
+  __shared__ __attribute__((aligned(16))) uint32_t s_stage[RJ_HL_STAGE][RJ_HL_WG];
+  __shared__ __attribute__((aligned(16))) uint32_t s_lut[RJ_HL_LUT_WORDS];
+  __shared__ uint32_t s_T, s_ne;
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) s_ne = 0;
+  const uint32_t g = lane0 + blockIdx.x * RJ_HL_WG + tid;
+  bool pending = g < lane0 + nlanes;
+  uint32_t gseg = 0;
+  if (pending) {
+    gseg = rj_lane_seg(coefs, g);
+    pending = gseg != 0xFFFFFFFFu;
+  }
+  int i = 0;
+  if (pending) i = upper_index(nimg, gseg, [&](int qq) { return imgs[qq].seg_prefix; });
+  const RjImageDev &im = imgs[i];
+  const uint32_t my_ts = im.tabset;
+  // one pass per distinct table set among the workgroup's lanes (normally exactly one)
+  while (__syncthreads_or(pending)) {
+    if (tid == 0) s_T = 0xFFFFFFFFu;
+    __syncthreads();
+    if (pending) atomicMin(&s_T, my_ts);
+    __syncthreads();
+    const uint32_t T = s_T;
+    {
+      const uint4 *src = reinterpret_cast<const uint4 *>(lean + T);
+      uint4 *d4 = reinterpret_cast<uint4 *>(s_lut);
+      for (uint32_t w = tid; w < RJ_HL_LUT_WORDS / 4; w += RJ_HL_WG) d4[w] = gp(src)[w];
+    }
+    __syncthreads();
+    if (!(pending && my_ts == T)) continue;
+    pending = false;
+    const uint32_t seg = gseg - im.seg_prefix;
+    const RjSegDev sg = gp(im.segs)[seg];
+    const uint32_t nblk = im.nblk_mcu;
+    uint32_t pat = 0;  // per block b: bit 2b its DC table, bit 2b + 1 its AC table
+    for (uint32_t bb = 0; bb < nblk; bb++) {
+      const uint32_t cc = im.blk_comp[bb] & 3;
+      pat |= ((im.comp_td[cc] & 1u) | ((im.comp_ta[cc] & 1u) << 1)) << (2 * bb);
+    }
+    const uint32_t nb2 = 2 * nblk;
+    const uint32_t nbytes = sg.dst_len;
+    const uint32_t nbits = nbytes * 8u;
+    const uint32_t blocks = sg.mcu_count * nblk;
+    const uint4 *src = reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off);
+    uint32_t *ent = coefs.ent + im.ent_off + sg.ent_off;
+    const uint64_t ent_abs = im.ent_off + sg.ent_off;
+    RjPiece *piece = coefs.piece + rj_seg_lane0(coefs, gseg);
+    const RjTableSet *tset = tabsets + T;  // canonical search (escape path)
+    const HCol ring{&s_ring[0][tid]}, stage{&s_stage[0][tid]};
+
+    const uint32_t nchunks = (nbytes + 15) / 16;
+    for (uint32_t c = 0; c < RJ_HL_CHUNKS; c++) hl_put(ring, c, *gp(c < nchunks ? src + c : rj_hl_zero));
+    uint32_t cm = RJ_HL_CHUNKS;  // chunks committed (past the data: zero chunks)
+    uint32_t q = 0;               // -(bits consumed)
+    uint32_t wa = ring[0], wb = ring[1], wc = ring[2];
+    // q = 0 is bit 0: alignbit(wa, wb, 0) would return wb, so the window starts one word back
+    // (words -1, 0; j = (pos - 1) >> 5): wa is a dummy word whose bits are never returned
+    wc = wb;
+    wb = wa;
+    wa = 0;
+    uint32_t rr = 1;  // ring index of wc
+    uint32_t ne = 0, fl = 0;
+    bool skip = (sg.flags & RJ_SEG_MISSING) != 0;
+    uint32_t blocks_left = blocks;
+    uint32_t b = 0, k = 0;
+    uint32_t acb = ((pat >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES);
+    uint32_t tb = RJ_HL_DC0 + ((pat & 1u) << (RJ_HL_DC_BITS + 2));
+    uint32_t tsh = 32 - RJ_HL_DC_BITS;
+    // Ring refills travel two phases ahead (HBM / MALL latency under this scattered pattern is
+    // longer than a phase): the loop body is two phases, each with its own in-flight register set
+    // (a register copy of a pending load would wait for it at once).
+    uint32_t na = 0, nb = 0;  // chunks in flight in set a / set b
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0, b0 = a0, b1 = a0;
+#ifdef RJ_HL_STAMPS
+    uint64_t st_steps = 0, st_end = 0, st_fast = 0, st_safe = 0, st_esc = 0;
+#define RJ_HL_T0 const uint64_t t0 = __builtin_amdgcn_s_memtime()
+#define RJ_HL_T1(fast)                                  \
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();     \
+  st_steps += t1 - t0;                                  \
+  if (fast) st_fast++;                                  \
+  else st_safe++
+#define RJ_HL_T2 st_end += __builtin_amdgcn_s_memtime() - t1
+#else
+#define RJ_HL_T0
+#define RJ_HL_T1(fast)
+#define RJ_HL_T2
+#endif
+    // one phase: RJ_HL_PHASE steps, then (wave-uniform) the set issued two phases ago lands in
+    // the ring, this set is re-issued behind the other set's chunks, a full stage group leaves
+#define RJ_HL_ONE_PHASE(P0, P1, NP, NOTHER)                                                              \
+  {                                                                                                   \
+    RJ_HL_T0;                                                                                         \
+    /* no lane can finish its blocks or reach its data's end in this phase: the lean body */          \
+    const bool fast = __builtin_amdgcn_ballot_w64(                                                    \
+                          !(blocks_left >= RJ_HL_PHASE && !skip && (0u - q) + RJ_HL_PHASE * 31u < nbits)) == 0; \
+    if (fast) {                                                                                       \
+      _Pragma("unroll") for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(false);             \
+    } else {                                                                                          \
+      _Pragma("unroll") for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(true);              \
+    }                                                                                                 \
+    RJ_HL_T1(fast);                                                                                   \
+    if (NP > 0) hl_put(ring, cm & (RJ_HL_CHUNKS - 1), P0);                                            \
+    if (NP > 1) hl_put(ring, (cm + 1) & (RJ_HL_CHUNKS - 1), P1);                                      \
+    cm += NP;                                                                                         \
+    wc = ring[rr & (RJ_HL_WORDS - 1)]; /* may predate the commit */                                   \
+    /* rr - 2 = the word in wa; chunks wholly below it are free (the first step of an interval     \
+       always advances, so rr >= 2 here); the other set's chunks are live */                          \
+    const uint32_t live = cm + NOTHER - ((rr - 2) >> 2);                                              \
+    NP = min(RJ_HL_CHUNKS - live, 2u);                                                                \
+    const uint32_t ci = cm + NOTHER;                                                                  \
+    P0 = *gp(ci < nchunks ? src + ci : rj_hl_zero);                                                   \
+    P1 = *gp(ci + 1 < nchunks ? src + ci + 1 : rj_hl_zero + 1);                                       \
+    if (ne - fl >= RJ_HL_GROUP) { /* < 16 pending: one group leaves, < 8 stay */                      \
+      hl_flush(stage, fl, ent + fl);                                                                  \
+      fl += RJ_HL_GROUP;                                                                              \
+    }                                                                                                 \
+    RJ_HL_T2;                                                                                         \
+  }
+    while (__builtin_amdgcn_ballot_w64(blocks_left > 0) != 0) {
+      RJ_HL_ONE_PHASE(a0, a1, na, nb);
+      if (__builtin_amdgcn_ballot_w64(blocks_left > 0) == 0) break;
+      RJ_HL_ONE_PHASE(b0, b1, nb, na);
+    }
+#ifdef RJ_HL_STAMPS
+    if ((tid & 63) == 0) {
+      atomicAdd(&rj_hl_stamp[0], (unsigned long long)st_steps);
+      atomicAdd(&rj_hl_stamp[1], (unsigned long long)st_end);
+      atomicAdd(&rj_hl_stamp[2], (unsigned long long)st_fast);
+      atomicAdd(&rj_hl_stamp[3], (unsigned long long)st_safe);
+      atomicAdd(&rj_hl_stamp[4], 1ull);
+      atomicAdd(&rj_hl_stamp[5], (unsigned long long)st_esc);
+    }
+#endif
+    stage[ne & (RJ_HL_STAGE - 1)] = RJ_RE_TERM;
+    while (fl < ne + 1) {  // [fl, ne]: at most 16 entries, the terminator included
+      hl_flush(stage, fl, ent + fl);
+      fl += RJ_HL_GROUP;
+    }
+    *gp(piece) = RjPiece{ent_abs, 0u, blocks, 1u, {0, 0, 0}};
+    if (coefs.count) atomicAdd(&s_ne, ne + 1);
+  }
+  if (tid == 0 && coefs.count != nullptr && s_ne != 0) atomicAdd(coefs.count, (unsigned long long)s_ne);
+}
+
+#ifdef RJ_HL_STAMPS
+void DumpHuffStamps() {
+  unsigned long long h[8];
+  (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(rj_hl_stamp), sizeof(h));
+  const double w = h[4] ? double(h[4]) : 1.0;
+  const double ph = double(h[2] + h[3]) ? double(h[2] + h[3]) : 1.0;
+  fprintf(stderr, "[rj k_huff] waves %llu: per wave %.0f phases (%.0f safe), %.0f escape steps; cycles per phase: steps %.0f, end %.0f\n",
+          h[4], ph / w, h[3] / w, h[5] / w, h[0] / ph, h[1] / ph);
+  unsigned long long z[8] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(rj_hl_stamp), z, sizeof(z));
+}
+#endif
+
+hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
+                           const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
+                           RjCoefBuf coefs) {
+  if (nlanes == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_huff, dim3((nlanes + RJ_HL_WG - 1) / RJ_HL_WG), dim3(RJ_HL_WG), 0, st, imgs, nimg, lane0, nlanes,
+                     destuffed, tabsets, lean, coefs);
+  return hipGetLastError();
+}
+
+}  // namespace rj

@@ -22,6 +22,12 @@ hipError_t LaunchEntropy(hipStream_t st, int stage, const RjImageDev *imgs, int 
 hipError_t LaunchEntropyLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                               const uint8_t *destuffed, const RjTableSet *tabsets, RjCoefBuf coefs, uint32_t epoch);
 
+// Lean K1 (rj_huff.hip): lanes [lane0, lane0 + nlanes), one whole interval each, raw entries;
+// only for calls whose every baseline image is a row image and no interval is split.
+hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
+                           const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
+                           RjCoefBuf coefs);
+
 // K2b (general path): every output format / ROI of rocjpeg_decoder.cpp:143-180 from the planes.
 hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobDev *jobs, int njobs, uint32_t total_rows,
                             const uint8_t *planes);
@@ -66,6 +72,9 @@ hipError_t LaunchScan(hipStream_t st, const RjScanJob *jobs, uint32_t njobs, con
 
 #ifdef RJ_EXP_STAMPS
 void DumpRowStamps();
+#endif
+#ifdef RJ_HL_STAMPS
+void DumpHuffStamps();
 #endif
 
 }  // namespace rj

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <vector>
 
 #include "rj_common.h"
 
@@ -38,6 +39,47 @@ uint64_t Fnv1a(uint64_t h, const void *p, size_t n) {
 }
 
 }  // namespace
+
+// Lean K1 entry of a resolved code (rj_device.h RjLeanTables).  libjpeg semantics: DC symbol =
+// difference category s; AC symbol (r, s): s != 0 a coefficient after r zeros, (15, 0) ZRL, any
+// other (r, 0) ends the block (decode_mcu: `if (r != 15) break`).
+static uint32_t LeanEntry(uint32_t len, uint32_t sym, bool is_dc) {
+  const uint32_t s = sym & 15u, r = sym >> 4;
+  const uint32_t R = is_dc ? 0u : (s ? r : (r == 15 ? 15u : 63u));
+  const uint32_t emit = (is_dc || s) ? 1u : 0u;
+  const uint32_t n = len + s;
+  return ((32u - n) & 31u) | (n << 8) | (emit << 13) | (s << 16) | (R << 21);
+}
+
+void BuildLeanTable(const uint8_t bits[16], const uint8_t *vals, bool is_dc, uint32_t *first, uint32_t *subs) {
+  const int B = is_dc ? RJ_HL_DC_BITS : RJ_HL_AC_BITS;
+  const uint32_t bad = LeanEntry(17, 0, is_dc);  // libjpeg: a bad code is 17 bits of symbol 0
+  for (int e = 0; e < (1 << B); e++) first[e] = bad;
+  if (subs)
+    for (int e = 0; e < RJ_HL_SUBS * 32; e++) subs[e] = bad;
+  int nsub = 0;
+  std::vector<int> sub_of(size_t(1) << B, -1);
+  int k = 0, code = 0;
+  for (int l = 1; l <= 16; l++) {
+    for (int i = 0; i < bits[l - 1]; i++, k++, code++) {
+      const uint32_t ent = LeanEntry(uint32_t(l), vals[k], is_dc);
+      if (l <= B) {
+        for (int f = 0; f < (1 << (B - l)); f++) first[(code << (B - l)) | f] = ent;
+        continue;
+      }
+      const int prefix = code >> (l - B);
+      if (sub_of[prefix] < 0) {
+        sub_of[prefix] = (!is_dc && subs && nsub < RJ_HL_SUBS) ? nsub++ : RJ_HL_SUBS;
+        first[prefix] = RJ_HL_ESC | (sub_of[prefix] < RJ_HL_SUBS ? uint32_t(sub_of[prefix]) : 0xFFu);
+      }
+      if (sub_of[prefix] < RJ_HL_SUBS) {  // the next 16 - B = 5 bits
+        const int rest = code & ((1 << (l - B)) - 1);
+        for (int f = 0; f < (1 << (16 - l)); f++) subs[sub_of[prefix] * 32 + ((rest << (16 - l)) | f)] = ent;
+      }
+    }
+    code <<= 1;
+  }
+}
 
 bool BuildHuffman(const uint8_t bits[16], const uint8_t *vals, bool is_dc, RjHuffDev *t) {
   std::memset(t, 0, sizeof(*t));
@@ -95,6 +137,7 @@ bool Stream::Parse(const uint8_t *d, uint32_t n, bool defer_scan) {
   std::lock_guard<std::mutex> lock(mu_);  // rocjpeg_parser.cpp:44
   ReleaseResident();
   generation_++;
+  lean_.reset();
   info_ = StreamInfo();
   plan_ = DecodePlan();
   plan_.status = -3;
@@ -430,6 +473,18 @@ void Stream::CompleteFromDevice(uint32_t ecs_size, const RjSegDev *segs, uint32_
   p.entries = ent;
   p.nchunks = nch;
   scan_pending_ = false;
+}
+
+const RjLeanTables *Stream::LeanTables() {
+  if (!lean_) {
+    auto t = std::make_unique<RjLeanTables>();
+    for (int id = 0; id < 2; id++) {
+      BuildLeanTable(info_.ht[id].dc_bits, info_.ht[id].dc_vals, true, t->dc[id], nullptr);
+      BuildLeanTable(info_.ht[id].ac_bits, info_.ht[id].ac_vals, false, t->ac[id], t->ac[id] + (1 << RJ_HL_AC_BITS));
+    }
+    lean_ = std::move(t);
+  }
+  return lean_.get();
 }
 
 void Stream::ReleaseResident() {

@@ -104,6 +104,8 @@ class Stream {
   } resident;
   void ReleaseResident();
   ~Stream() { ReleaseResident(); }
+  // lean K1 tables (rj_huff.hip) of this stream's DHTs, built on first use (callers hold mutex())
+  const RjLeanTables *LeanTables();
 
  private:
   void BuildPlan();
@@ -114,6 +116,7 @@ class Stream {
   void BuildProgressivePlan(const uint8_t *data);
   StreamInfo info_;
   DecodePlan plan_;
+  std::unique_ptr<RjLeanTables> lean_;
   uint64_t generation_ = 0;
   std::mutex mu_;
 };
@@ -123,6 +126,10 @@ int ImageInfo(const StreamInfo &s, uint8_t *num_components, int *subsampling, ui
 
 // True when the frame header ahead of the first SOS is SOF2 (progressive Huffman).
 bool IsProgressiveStream(const uint8_t *data, uint32_t size);
+
+// Canonical Huffman table -> lean K1 first level (2^RJ_HL_DC_BITS or 2^RJ_HL_AC_BITS entries)
+// and, for AC, RJ_HL_SUBS second-level subtables (subs); the table must be valid (BuildHuffman).
+void BuildLeanTable(const uint8_t bits[16], const uint8_t *vals, bool is_dc, uint32_t *first, uint32_t *subs);
 
 // Canonical Huffman table -> RjHuffDev; false for an invalid table.
 bool BuildHuffman(const uint8_t bits[16], const uint8_t *vals, bool is_dc, RjHuffDev *out);
