@@ -145,6 +145,9 @@ int Decoder::Initialize() {
   if (const char *m = getenv("RJ_PIPE_MIN")) pipe_min_ = uint32_t(std::max(1, atoi(m)));
   if (const char *o = getenv("RJ_SORT_LANES")) sort_lanes_ = atoi(o) != 0;
   if (const char *l = getenv("RJ_LEAN")) lean_enabled_ = atoi(l) != 0;
+  if (const char *sk = getenv("RJ_STREAM_K2")) stream_enabled_ = atoi(sk) != 0;
+  if (const char *sw = getenv("RJ_STREAM_WG")) stream_wg_per_cu_ = std::max(1, std::min(16, atoi(sw)));
+  cu_count_ = std::max(1, prop.multiProcessorCount);
   for (auto &q : pstream_) RJ_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
   for (auto &e : pev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : pk1_) RJ_HIP(hipEventCreate(&e));
@@ -548,6 +551,14 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     std::memcpy(d.blk_dx, p.blk_dx, RJ_MAX_BLK_MCU);
     std::memcpy(d.blk_dy, p.blk_dy, RJ_MAX_BLK_MCU);
     d.tabset = tab_of[i];
+    {  // the int32 IDCT is exact while |coefficient x quantiser| < 2^14 (rj_math.h)
+      uint32_t qmax = 1;
+      for (int c = 0; c < in.ncomp; c++) {
+        const uint16_t *qz = p.tables.qz[d.comp_tq[c] & 3];
+        for (int k = 0; k < 64; k++) qmax = std::max<uint32_t>(qmax, qz[k]);
+      }
+      d.idct_thr = 16383u / qmax;
+    }
     d.nseg = uint32_t(p.segs.size());
     d.seg_prefix = seg_total;
     seg_total += d.nseg;
@@ -995,7 +1006,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t off_plane = AlignUp(off_pgrows + n * sizeof(uint32_t), 256);
   const uint64_t off_fold = AlignUp(off_plane + prog_lanes.size() * sizeof(uint32_t), 256);
   const uint64_t off_lean = AlignUp(off_fold + fold_jobs.size() * sizeof(RjFoldJob), 256);
-  const uint64_t off_stage = AlignUp(off_lean + (lean ? tabs.size() * sizeof(RjLeanTables) : 0), 256);
+  const uint64_t off_wide = AlignUp(off_lean + (lean ? tabs.size() * sizeof(RjLeanTables) : 0), 256);
+  const uint64_t off_stage = AlignUp(off_wide + kWideSites * sizeof(uint32_t), 256);
   const uint64_t blob_a = AlignUp(off_stage + stage_bytes, 256);
   const uint64_t n_lane_seg = any_split ? lane_seg.size() : (sorted ? seg_total : 0);
   const uint64_t off_lane_seg = blob_a;
@@ -1033,6 +1045,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   epoch_ = (epoch_ + 1) & 0x0FFFFFFFu;
   if (epoch_ == 0) epoch_ = 1;
   RJ_CHECK(d_planes_.Ensure(std::max<uint64_t>(plane_bytes, 256)));
+  // K2 fix-up lists (rows outside the int32 IDCT's exact domain): one slice per K2 launch, the
+  // counters zeroed in upload A; capacity = every K2 launch's rows together
+  RJ_CHECK(d_wide_.Ensure((uint64_t(fused_rows) + general_rows + pfused_rows + pgeneral_rows + seg_total + 1) *
+                          sizeof(uint2)));
   if (!routes_.empty()) {  // routed images write device-local staging at the caller's pitch
     RJ_CHECK(d_route_.Ensure(route_bytes));
     uint8_t *rb = d_route_.as<uint8_t>();
@@ -1104,6 +1120,18 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const RjJobDev *d_jobs = reinterpret_cast<const RjJobDev *>(dbase + off_jobs);
   const uint2 *d_row_list = reinterpret_cast<const uint2 *>(dbase + off_row_list);
   const uint32_t *d_lane_seg = reinterpret_cast<const uint32_t *>(dbase + off_lane_seg);
+  std::memset(h + off_wide, 0, kWideSites * sizeof(uint32_t));
+  uint32_t *const d_wide_cnt = reinterpret_cast<uint32_t *>(dbase + off_wide);
+  uint64_t wide_used = 0;
+  int wide_site = 0;
+  // the next K2 launch's fix-up list: its counter and `rows` slots
+  auto wide = [&](uint32_t rows, uint32_t *&cnt, uint2 *&list) {
+    cnt = d_wide_cnt + std::min(wide_site++, kWideSites - 1);
+    list = d_wide_.as<uint2>() + wide_used;
+    wide_used += rows;
+  };
+  uint32_t *wcnt = nullptr;
+  uint2 *wlist = nullptr;
 
   const auto t_k0 = std::chrono::steady_clock::now();
   if (profiling_) RJ_HIP(hipEventRecord(ev_[0], stream_));
@@ -1216,10 +1244,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       if (dbg_lev) RJ_HIP(hipEventRecord(prog_lev_ev_[L + 1], stream_));
     }
     if (profiling_) RJ_HIP(hipEventRecord(prog_ev_[1], stream_));
+    wide(pfused_rows, wcnt, wlist);
     RJ_HIP(LaunchRowsDense(stream_, false, d_imgs, n, reinterpret_cast<const uint32_t *>(dbase + off_prows), pfused_rows,
-                           cbuf, d_tabs, nullptr));
+                           cbuf, d_tabs, nullptr, wcnt, wlist));
+    wide(pgeneral_rows, wcnt, wlist);
     RJ_HIP(LaunchRowsDense(stream_, true, d_imgs, n, reinterpret_cast<const uint32_t *>(dbase + off_pgrows),
-                           pgeneral_rows, cbuf, d_tabs, d_planes_.as<uint8_t>()));
+                           pgeneral_rows, cbuf, d_tabs, d_planes_.as<uint8_t>(), wcnt, wlist));
     if (profiling_) RJ_HIP(hipEventRecord(prog_ev_[2], stream_));
   }
   if (profiling_) RJ_HIP(hipEventRecord(ev_[2], stream_));
@@ -1349,7 +1379,42 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
             ms(t_host0, t_dedupe), ms(t_dedupe, t_layout), ms(t_layout, t_lanes), ms(t_lanes, t_k0),
             ms(t_k0, t_end));
   }
-  if (ngroups > 1) {
+  // ---- streaming K2 (rj_fused.hip k_rows_stream): every interval one MCU row, every image
+  // fused, lean K1 -- one K1 launch over all lanes publishes each interval when its entries are
+  // out, persistent K2 workgroups on a second stream start each row as soon as its interval is
+  // published, and a cleanup pass after K1 takes the rows a bounded wait deferred ----
+  const bool stream_k2 = stream_enabled_ && lean && ngroups > 1 && rows_from_lanes && fused_images > 0 &&
+                         fused_images == uint32_t(n) - prog_images;
+  timings_.k2_stream = stream_k2 ? 1u : 0u;
+  if (stream_k2) {
+    const bool fresh = d_flags_.capacity() < uint64_t(seg_total) * 4;
+    RJ_CHECK(d_flags_.Ensure(std::max<uint64_t>(uint64_t(seg_total) * 4, 256)));
+    RJ_CHECK(d_sctl_.Ensure((uint64_t(seg_total) + 4) * 4));
+    if (fresh || epoch_ == 1)  // new memory, or the 28-bit epoch wrapped: no stale flag may match
+      RJ_HIP(hipMemsetAsync(d_flags_.as<uint32_t>(), 0, d_flags_.capacity(), stream_));
+    uint32_t *ctl = d_sctl_.as<uint32_t>();
+    RJ_HIP(hipMemsetAsync(ctl, 0, 16, stream_));
+    RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0, upload B, counters done
+    RJ_HIP(hipStreamWaitEvent(pstream_[0], pev_[kMaxPipe - 1], 0));
+    if (profiling_) RJ_HIP(hipEventRecord(k1s_[0], stream_));
+    RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, seg_total, d_destuff_.as<uint8_t>(), d_tabs, d_lean, cbuf,
+                           d_flags_.as<uint32_t>(), epoch_, ctl + 3));
+    if (profiling_) RJ_HIP(hipEventRecord(pk1_[0], stream_));
+    if (profiling_) RJ_HIP(hipEventRecord(k2s_[0], pstream_[0]));
+    const uint32_t grid = std::min<uint32_t>(seg_total, uint32_t(stream_wg_per_cu_) * uint32_t(cu_count_));
+    wide(seg_total, wcnt, wlist);
+    RJ_HIP(LaunchRowsStream(pstream_[0], true, d_imgs, n, d_lane_seg, seg_total, d_flags_.as<uint32_t>(), epoch_, ctl,
+                            ctl + 4, HuffLaneWaves(seg_total), grid, cbuf, d_tabs, wcnt, wlist));
+    if (profiling_) RJ_HIP(hipEventRecord(k2e_[0], pstream_[0]));
+    RJ_HIP(hipEventRecord(pev_[0], pstream_[0]));
+    RJ_HIP(hipStreamWaitEvent(stream_, pev_[0], 0));
+    if (profiling_) RJ_HIP(hipEventRecord(k2s_[1], stream_));
+    RJ_HIP(LaunchRowsStream(stream_, false, d_imgs, n, d_lane_seg, seg_total, d_flags_.as<uint32_t>(), epoch_, ctl,
+                            ctl + 4, HuffLaneWaves(seg_total), std::min<uint32_t>(seg_total, 16u * uint32_t(cu_count_)),
+                            cbuf, d_tabs, wcnt, wlist));
+    RJ_HIP(LaunchRowsFix(stream_, false, false, d_imgs, n, cbuf, d_tabs, nullptr, wcnt, wlist, seg_total));
+    if (profiling_) RJ_HIP(hipEventRecord(k2e_[1], stream_));
+  } else if (ngroups > 1) {
     RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0 and upload B done
     if (getenv("RJ_DEBUG_PIPE_SERIAL")) {  // development: each class's K1 alone, one after another
       for (int g = 0; g < ngroups; g++) {
@@ -1377,13 +1442,16 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       for (int q = 0; q < g; q++) RJ_HIP(hipStreamWaitEvent(st, kev_[q], 0));  // rows spanning classes
       if (profiling_) RJ_HIP(hipEventRecord(k2s_[g], st));
       if (rows_from_lanes) {
+        wide(lane_off[g + 1] - lane_off[g], wcnt, wlist);
         RJ_HIP(LaunchRowsOfLanes(st, fused_images == 0, d_imgs, n, d_lane_seg + lane_off[g],
-                                 lane_off[g + 1] - lane_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>()));
+                                 lane_off[g + 1] - lane_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>(), wcnt, wlist));
       } else {
+        wide(frow_off[g + 1] - frow_off[g], wcnt, wlist);
         RJ_HIP(LaunchRows(st, false, d_imgs, n, d_rows, d_row_list + frow_off[g], frow_off[g + 1] - frow_off[g],
-                          cbuf, d_tabs, nullptr));
+                          cbuf, d_tabs, nullptr, wcnt, wlist));
+        wide(grow_off[g + 1] - grow_off[g], wcnt, wlist);
         RJ_HIP(LaunchRows(st, true, d_imgs, n, d_grows, d_row_list + fused_rows + grow_off[g],
-                          grow_off[g + 1] - grow_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>()));
+                          grow_off[g + 1] - grow_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>(), wcnt, wlist));
       }
       if (profiling_) RJ_HIP(hipEventRecord(k2e_[g], st));
       if (st != stream_) RJ_HIP(hipEventRecord(pev_[g], st));
@@ -1402,9 +1470,11 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       }
     }
     if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
-    RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr));
+    wide(fused_rows, wcnt, wlist);
+    RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr, wcnt, wlist));
+    wide(general_rows, wcnt, wlist);
     RJ_HIP(LaunchRows(stream_, true, d_imgs, n, d_grows, nullptr, general_rows, cbuf, d_tabs,
-                      d_planes_.as<uint8_t>()));
+                      d_planes_.as<uint8_t>(), wcnt, wlist));
   }
   if (profiling_) RJ_HIP(hipEventRecord(ev_[4], stream_));
   RJ_HIP(LaunchOutputJobs(stream_, d_imgs, d_jobs, int(jobs.size()), rows_total, d_planes_.as<uint8_t>()));
@@ -1413,6 +1483,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(hipMemcpy2DAsync(rc.user, rc.pitch, d_route_.as<uint8_t>() + rc.off, rc.pitch, rc.row_bytes, rc.rows,
                             hipMemcpyDefault, stream_));
   RJ_HIP(hipStreamSynchronize(stream_));
+  if (profiling_) {
+    uint32_t wc[kWideSites];
+    RJ_HIP(hipMemcpy(wc, d_wide_cnt, sizeof(wc), hipMemcpyDeviceToHost));
+    timings_.wide_rows = 0;
+    for (int k = 0; k < kWideSites; k++) timings_.wide_rows += wc[k];
+  }
   if (prog_images && prog_pipe) {  // a refinement wave that gave up waiting (never expected)
     uint32_t err = 0;
     RJ_HIP(hipMemcpy(&err, d_pprog_.as<uint32_t>() + pival_total, 4, hipMemcpyDeviceToHost));
@@ -1484,7 +1560,25 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(hipEventElapsedTime(&ms[1], ev_[1], ev_[2]));
     RJ_HIP(hipEventElapsedTime(&ms[4], ev_[4], ev_[5]));
     RJ_HIP(hipEventElapsedTime(&timings_.total_ms, ev_[0], ev_[5]));
-    if (ngroups > 1) {  // K1 ends with the last class; K2 of the earlier classes overlaps it
+    if (stream_k2) {  // one K1 launch; K2 = the streaming pass + the cleanup pass
+      float k1 = 0, a = 0, b = 0, k12 = 0;
+      RJ_HIP(hipEventElapsedTime(&k1, k1s_[0], pk1_[0]));
+      RJ_HIP(hipEventElapsedTime(&a, k2s_[0], k2e_[0]));
+      RJ_HIP(hipEventElapsedTime(&b, k2s_[1], k2e_[1]));
+      RJ_HIP(hipEventElapsedTime(&k12, ev_[2], ev_[4]));
+      ms[2] = k1;
+      ms[3] = k12 - k1;
+      timings_.entropy_chunks_ms = k1;
+      timings_.k1_launch_ms_sum = k1;
+      timings_.k1_launches = 1;
+      timings_.k2_launch_ms_sum = a + b;
+      timings_.k2_launches = 2;
+      uint32_t ctl[2] = {0, 0};
+      RJ_HIP(hipMemcpy(ctl, d_sctl_.as<uint32_t>(), sizeof(ctl), hipMemcpyDeviceToHost));
+      timings_.k2_deferred_rows = ctl[1];
+      timings_.k2_stream_rows = std::min(ctl[0], seg_total) - ctl[1];
+      timings_.k2_stream_ms = a;
+    } else if (ngroups > 1) {  // K1 ends with the last class; K2 of the earlier classes overlaps it
       float k1 = 0, k12 = 0;
       for (int g = 0; g < ngroups; g++) {
         float t = 0;

@@ -95,12 +95,19 @@ class Decoder {
   // pipelined launch (rj_decoder.cpp): interval length classes 0..pipe_groups_-2 on pstream_,
   // the last class on stream_; pev_ joins them (no timing), pk1_ times each class's K1
   static constexpr int kMaxPipe = 4;  // = HIP's default hardware queues per process
+  static constexpr int kWideSites = 4 + 2 * kMaxPipe;  // K2 launches per call, bound (fix-up counters)
   // 2 by default: the caller's own stream (e.g. torch's) takes a hardware queue too, and two
   // streams sharing one queue serialise (measured: 4 classes sometimes double the K1 span)
   int pipe_groups_ = 2;            // env RJ_PIPE_GROUPS (1 = sequential)
   uint32_t pipe_min_ = 2048;       // env RJ_PIPE_MIN: fewest intervals worth pipelining
   bool sort_lanes_ = true;         // env RJ_SORT_LANES=0: K1 lanes in interval order
-  bool lean_enabled_ = true;       // env RJ_LEAN=0: never the lean K1 (rj_huff.hip)
+  bool lean_enabled_ = false;      // env RJ_LEAN=1: the lean K1 (rj_huff.hip), measured slower
+  bool stream_enabled_ = false;    // env RJ_STREAM_K2=1: streaming K2 (k_rows_stream), measured no faster
+  int cu_count_ = 256;
+  int stream_wg_per_cu_ = 2;       // env RJ_STREAM_WG: streaming K2 workgroups per CU (K1's LDS must still fit)
+  DeviceBuffer d_flags_;           // streaming K2: per interval, the epoch of the call that published it
+  DeviceBuffer d_sctl_;            // streaming K2: row counters + deferred row list
+  DeviceBuffer d_wide_;            // K2 fix-up lists (rows outside the int32 IDCT's domain)
   hipStream_t pstream_[kMaxPipe - 1] = {};
   hipEvent_t pev_[kMaxPipe] = {};
   hipEvent_t pk1_[kMaxPipe] = {};

@@ -188,9 +188,9 @@ struct RjTableSet {
 //   [12:8] n                       [13] the symbol writes an entry (DC; AC coefficient)
 //   [19:16] s (extra bits)         [27:21] R: zigzag run (DC 0; AC r; ZRL 15; EOB 63 -> k >= 64)
 //   bit 31: code longer than the first level: [7:0] = AC second-level subtable, 0xFF = search
-// First levels: DC 10 bits, AC 11 bits; AC codes of 12..16 bits: up to RJ_HL_SUBS subtables of
+// First levels: DC 9 bits, AC 11 bits; AC codes of 12..16 bits: up to RJ_HL_SUBS subtables of
 // 32 entries (the next 5 bits) per table.
-#define RJ_HL_DC_BITS 10
+#define RJ_HL_DC_BITS 9
 #define RJ_HL_AC_BITS 11
 #define RJ_HL_SUBS 8
 #define RJ_HL_AC_WORDS ((1 << RJ_HL_AC_BITS) + RJ_HL_SUBS * 32)
@@ -297,6 +297,7 @@ struct RjImageDev {
   uint64_t ent_off;      // in entries (sparse coefficients), group-aligned
   uint32_t ri_mcus;      // MCUs per restart interval (0: one interval)
   uint32_t dc_diff;      // 1: lean K1 raw entries (DC differences; K2 restores the predictions)
+  uint32_t idct_thr;     // |coefficient| above which the int32 IDCT may differ: (2^14 - 1) / max quantiser
   uint32_t chunk_prefix; // exclusive prefix of K1 chunks over the batch (unpadded)
   // component planes (general path)
   uint64_t plane_off[4];

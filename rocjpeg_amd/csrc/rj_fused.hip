@@ -128,7 +128,7 @@ template <bool kRaw>
 __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefBuf &coefs,
                                              const uint32_t *__restrict__ ent, uint32_t lane, uint32_t nb,
                                              uint32_t drop, uint32_t nblk, uint32_t cbits, EntWin &win, Nav &nv,
-                                             uint8_t *s_buf) {
+                                             uint8_t *s_buf, int thr, bool &bad) {
   uint32_t done = 0;
   const uint32_t need = nb + drop;
   for (uint32_t moves = 0; done < need && moves < (1u << 16); moves++) {  // bounded on corrupt pieces
@@ -162,6 +162,7 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
         const uint32_t below = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
         const uint32_t ord = seen + below + (st ? 1u : 0u) - 1u;
         const uint32_t blk = done + ord;  // block index counted from the first dropped one
+        bool oob = false;
         if (ord < piece && p < 64u && blk >= drop) {
           int v = kRaw ? raw_value(e) : int(int16_t(e & 0xFFFFu));
           if (kRaw && (e & RJ_RE_ZERO)) v = -32768;  // zero block: marked for the DC restore
@@ -170,8 +171,11 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
             const uint32_t cc = (cbits >> (2 * bi)) & 3u;
             v += cc == 0 ? nv.dcd[0] : (cc == 1 ? nv.dcd[1] : nv.dcd[2]);
           }
+          // outside the int32 IDCT's exact domain (raw DC: a difference, checked by restore_dc)
+          oob = (!kRaw || p != 0) && int16_t(v) != -32768 && abs(int(int16_t(v))) > thr;
           *reinterpret_cast<int16_t *>(s_buf + (blk - drop) * RJ_BLK_STRIDE + p * 2) = int16_t(v);
         }
+        bad = bad || __ballot(oob) != 0;
         const uint64_t hit = __ballot(st && ord == piece);  // start of the first block past the piece
         seen += __popcll(m);
         if (hit) {
@@ -205,8 +209,8 @@ __device__ __forceinline__ int wave_scan(int x) {
 // the row; a restart interval starting inside the strip (every ri MCUs) resets it there.  Zero
 // blocks (marked -32768) are absolute 0 (libjpeg's insufficient data / missing marker: every
 // later block of the interval is one too).  Writes the absolute DC back into the LDS block.
-__device__ __forceinline__ void restore_dc(uint8_t *s_buf, uint32_t tid, uint32_t nb, uint32_t nblk, uint32_t c,
-                                           uint32_t mx0, uint32_t mcu_row0, uint32_t ri, int (&carry)[3]) {
+__device__ __forceinline__ bool restore_dc(uint8_t *s_buf, uint32_t tid, uint32_t nb, uint32_t nblk, uint32_t c,
+                                           uint32_t mx0, uint32_t mcu_row0, uint32_t ri, int (&carry)[3], int thr) {
   int16_t *dcp = reinterpret_cast<int16_t *>(s_buf + tid * RJ_BLK_STRIDE);
   const int d = tid < nb ? int(*dcp) : 0;
   const bool zero = d == -32768;
@@ -227,7 +231,9 @@ __device__ __forceinline__ void restore_dc(uint8_t *s_buf, uint32_t tid, uint32_
     const int last = __builtin_amdgcn_readlane(mine, int(nb - 1));
     carry[cc] = last;
   }
-  if (tid < nb) *dcp = int16_t(zero ? 0 : pred);
+  const int16_t dc = int16_t(zero ? 0 : pred);  // libjpeg keeps the predictor wide, stores (JCOEF)
+  if (tid < nb) *dcp = dc;
+  return __ballot(tid < nb && abs(int(dc)) > thr) != 0;  // outside the int32 IDCT's exact domain
 }
 
 // Two sign-magnitude int16 (bit 15 = negative) -> two's complement, per half (packed ops).
@@ -270,40 +276,45 @@ __device__ __forceinline__ void load_dense_block(const RjImageDev &im, const uin
 //   kPlanes = true : general path, blocks into the MCU-padded component planes (K2b reads them)
 //   kDense = true  : progressive images -- blocks come from the dense coefficient buffer
 //                    (rj_prog.hip layout: zigzag, AC sign-magnitude) instead of entry streams
-template <bool kPlanes, bool kDense = false>
-__global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ imgs, int nimg,
-                                             const uint32_t *__restrict__ row_prefix,
-                                             const uint2 *__restrict__ row_list,
-                                             const uint32_t *__restrict__ row_segs,
-                                             RjCoefBuf coefs,
-                                             const RjTableSet *__restrict__ tabsets,
-                                             uint8_t *__restrict__ planes) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];  // A/B, then tiles
-  __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
-
-  RJ_STAMP(t_start);
-  const uint32_t tid = threadIdx.x;
-  int i;
-  uint32_t my;  // MCU row inside image i
+// (image i, MCU row my) of a K2 launch: from an explicit list, from the K1 lane order (every
+// interval one MCU row), or from the per-image row prefix
+__device__ __forceinline__ void row_of_block(const RjImageDev *__restrict__ imgs, int nimg,
+                                             const uint32_t *__restrict__ row_prefix, const uint2 *__restrict__ row_list,
+                                             const uint32_t *__restrict__ row_segs, uint32_t w, int &i, uint32_t &my) {
   if (row_list != nullptr) {  // pipelined launch: an explicit (image, row) list for this group
-    const uint2 e = row_list[blockIdx.x];
+    const uint2 e = row_list[w];
     i = int(U(e.x));
     my = U(e.y);
-  } else if (row_segs != nullptr) {  // pipelined, every interval one MCU row: the class's intervals
-    const uint32_t gseg = U(row_segs[blockIdx.x]);
+  } else if (row_segs != nullptr) {  // every interval one MCU row: the K1 lanes' intervals
+    const uint32_t gseg = U(row_segs[w]);
     i = __builtin_amdgcn_readfirstlane(upper_index(nimg, gseg, [&](int q) { return imgs[q].seg_prefix; }));
     my = U(gp(imgs[i].segs)[gseg - imgs[i].seg_prefix].mcu_first / imgs[i].mcux);
   } else {
-    const uint32_t row = blockIdx.x;
     int lo = 0, hi = nimg - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (row_prefix[mid] <= row) lo = mid;
+      if (row_prefix[mid] <= w) lo = mid;
       else hi = mid - 1;
     }
     i = __builtin_amdgcn_readfirstlane(lo);  // wave-uniform: image fields become scalar loads
-    my = row - row_prefix[i];
+    my = w - row_prefix[i];
   }
+}
+
+// The work of one MCU row (one wavefront), looping over the row's strips of S MCUs.
+//   kPlanes = false: fused output (rj_decoder.cpp FusedEligible images)
+//   kPlanes = true : general path, blocks into the MCU-padded component planes (K2b reads them)
+//   kDense = true  : progressive images -- blocks come from the dense coefficient buffer
+//                    (rj_prog.hip layout: zigzag, AC sign-magnitude) instead of entry streams
+//   kWide = true   : the fix-up pass (k_rows_fix): strips with coefficients outside the int32
+//                    IDCT's exact domain take the 64-bit IDCT.  Otherwise such a row is appended
+//                    to wide_list (as (image, row); wide_cnt counts) for the fix-up launch.
+template <bool kPlanes, bool kDense, bool kWide = false>
+__device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, int i, uint32_t my, RjCoefBuf coefs,
+                                         const RjTableSet *__restrict__ tabsets, uint8_t *__restrict__ planes,
+                                         uint8_t *s_buf, uint16_t (*s_q)[64], uint32_t *wide_cnt, uint2 *wide_list) {
+  RJ_STAMP(t_start);
+  const uint32_t tid = threadIdx.x;
   const RjImageDev &im = imgs[i];
   const uint32_t hmax = U(im.hmax), vmax = U(im.vmax);
   const uint32_t mcu_w = 8 * hmax, mcu_h = 8 * vmax;
@@ -341,8 +352,10 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
 
   const uint32_t mcux = U(im.mcux);
   const bool dc_diff = !kDense && U(im.dc_diff) != 0;  // raw entries: restore_dc per strip
+  const int thr = int(U(im.idct_thr));
   const uint32_t ri_dc = U(im.ri_mcus ? im.ri_mcus : mcux);
   int carry[3] = {0, 0, 0};
+  bool row_wide = false;
   const uint32_t strips_x = (mcux + S - 1) / S;
   const uint32_t *ent = coefs.ent;
   uint32_t cbits = 0;  // component of each block within the MCU
@@ -392,6 +405,7 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
     const uint32_t nb = nm * nblk;
     const bool has_blk = tid < nb;
 
+    bool wide = false;  // some coefficient of the strip needs the exact 64-bit IDCT
     // ---- A: clear the strip's LDS blocks, expand the entry stream into them ----
     __syncthreads();  // previous strip's tiles fully read
     for (uint32_t k = tid; k < nb * 8; k += 64)
@@ -400,14 +414,14 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
     if constexpr (kDense) {
       if (has_blk) load_dense_block(im, coefs.dense, lane_blk, mx0, my, inter, s_buf + tid * RJ_BLK_STRIDE);
     } else {
-      if (dc_diff) parse_blocks<true>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf);
-      else parse_blocks<false>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf);
+      if (dc_diff) parse_blocks<true>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, thr, wide);
+      else parse_blocks<false>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, thr, wide);
       drop = 0;
       if (sx + 1 < strips_x && nv.bleft) win.load(ent, nv.cur(), tid);  // next strip's window: lands behind B and C
     }
     __syncthreads();
     if (!kDense && dc_diff) {
-      restore_dc(s_buf, tid, nb, nblk, lane_blk >> 12, mx0, my * mcux, ri_dc, carry);
+      wide = restore_dc(s_buf, tid, nb, nblk, lane_blk >> 12, mx0, my * mcux, ri_dc, carry, thr) || wide;
       __syncthreads();
     }
 
@@ -416,13 +430,26 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
     // ---- B: lane-per-block IDCT in registers ----
     const uint32_t c_b = lane_blk >> 12;
     int32_t v[64];
+    const int16_t *zz = reinterpret_cast<const int16_t *>(s_buf + tid * RJ_BLK_STRIDE);
     if (has_blk)
-      dezigzag_dequant(reinterpret_cast<const uint4 *>(s_buf + tid * RJ_BLK_STRIDE),
-                       reinterpret_cast<const uint4 *>(s_q[c_b]), v);
+      dezigzag_dequant(reinterpret_cast<const uint4 *>(zz), reinterpret_cast<const uint4 *>(s_q[c_b]), v);
+    if constexpr (kDense) {  // progressive coefficients: check the dequantised values directly
+      int32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int k = 0; k < 64; k++) {
+        lo = min(lo, v[k]);
+        hi = max(hi, v[k]);
+      }
+      wide = __ballot(has_blk && (lo < -16383 || hi > 16383)) != 0;
+    }
+    row_wide = row_wide || wide;
+    if constexpr (kWide)  // pass 1 now: the tiles overwrite the LDS block below
+      if (wide && has_blk) idct_pass1_wide(zz, s_q[c_b], v);
     if constexpr (kPlanes) {
       if (has_blk) {
         uint32_t o[16];
-        idct_islow_block(v, o);
+        if (kWide && wide) idct_pass2_wrap(v, o);
+        else idct_islow_block(v, o);
         const uint32_t hc = inter ? im.comp_h[c_b] : 1, vc = inter ? im.comp_v[c_b] : 1;
         const uint32_t bx = mx0 * hc + (lane_blk & 255u), by = my * vc + ((lane_blk >> 8) & 15u);
         const uint32_t pitch = im.plane_pitch[c_b];
@@ -435,7 +462,8 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
     __syncthreads();  // every block is in registers: the staging area becomes the sample tiles
     if (has_blk) {
       uint32_t o[16];
-      idct_islow_block(v, o);
+      if (kWide && wide) idct_pass2_wrap(v, o);
+      else idct_islow_block(v, o);
       const uint32_t twc = c_b == 0 ? tw[0] : (c_b == 1 ? tw[1] : tw[2]);
       const uint32_t toc = c_b == 0 ? toff[0] : (c_b == 1 ? toff[1] : toff[2]);
       uint8_t *dst = s_buf + toc + ((lane_blk >> 8) & 15u) * 8u * twc + (lane_blk & 255u) * 8u;
@@ -553,6 +581,11 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
   RJ_STAMP(te);
   RJ_STAMP_ADD(2, te - tc);
   }  // strips
+  if constexpr (!kWide)
+    if (row_wide && tid == 0) {
+      const uint32_t k = atomicAdd(wide_cnt, 1u);
+      wide_list[k] = make_uint2(uint32_t(i), my);
+    }
 #ifdef RJ_EXP_STAMPS
   if (tid == 0)
     for (int q = 0; q < 4; q++) atomicAdd(&rj_stamp[q], (unsigned long long)acc[q]);
@@ -560,32 +593,174 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
 #endif
 }
 
+// K2: one wavefront (workgroup) per MCU row.
+template <bool kPlanes, bool kDense = false>
+__global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ imgs, int nimg,
+                                             const uint32_t *__restrict__ row_prefix,
+                                             const uint2 *__restrict__ row_list,
+                                             const uint32_t *__restrict__ row_segs,
+                                             RjCoefBuf coefs,
+                                             const RjTableSet *__restrict__ tabsets,
+                                             uint8_t *__restrict__ planes, uint32_t *wide_cnt, uint2 *wide_list) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];  // A/B, then tiles
+  __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
+  int i;
+  uint32_t my;
+  row_of_block(imgs, nimg, row_prefix, row_list, row_segs, blockIdx.x, i, my);
+  row_body<kPlanes, kDense>(imgs, i, my, coefs, tabsets, planes, s_buf, s_q, wide_cnt, wide_list);
+}
+
+// K2 fix-up: the rows a K2 launch recorded (a strip outside the int32 IDCT's exact domain --
+// corrupt data with large quantisers), decoded again with the 64-bit IDCT for those strips.
+// Launched right behind its K2 launch on the same stream; with nothing recorded every
+// workgroup reads the count and leaves.
+template <bool kPlanes, bool kDense>
+__global__ __launch_bounds__(64) void k_rows_fix(const RjImageDev *__restrict__ imgs, int nimg, RjCoefBuf coefs,
+                                                 const RjTableSet *__restrict__ tabsets, uint8_t *__restrict__ planes,
+                                                 const uint32_t *wide_cnt, const uint2 *wide_list, uint32_t cap) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];
+  __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
+  const uint32_t cnt = min(U(*wide_cnt), cap);
+  for (uint32_t r = blockIdx.x; r < cnt; r += gridDim.x) {
+    const uint2 e = wide_list[r];
+    const int i = int(U(e.x));
+    if (i >= nimg) continue;
+    __syncthreads();  // the previous row's tiles fully read
+    row_body<kPlanes, kDense, true>(imgs, i, U(e.y), coefs, tabsets, planes, s_buf, s_q, nullptr, nullptr);
+  }
+}
+
+// Streaming K2 (fused rows of a call whose every interval is one MCU row): persistent
+// workgroups take rows in K1 lane order (shortest intervals first -- the order their K1 waves
+// finish in) and start each as soon as K1 has published its interval (lean K1 `flags`, release
+// after its stores; here one relaxed poll, then an agent acquire: MI355X_MICROARCH.md, valid
+// forms).  They stop taking rows once every K1 wave is done (ctl[3] == k1_waves): the rest goes
+// to the cleanup pass (kWait = false, after K1, full occupancy), which also takes the rows a
+// bounded wait deferred -- no workgroup ever waits on work that might not be resident, so the
+// two concurrent launches cannot deadlock.
+//   ctl[0]: next row (streaming pass), ctl[1]: deferred rows, ctl[2]: cleanup counter,
+//   ctl[3]: K1 waves done; deferred: the deferred rows
+template <bool kWait>
+__global__ __launch_bounds__(64, 4) void k_rows_stream(const RjImageDev *__restrict__ imgs, int nimg,
+                                                    const uint32_t *__restrict__ row_segs, uint32_t nrows,
+                                                    const uint32_t *flags, uint32_t epoch, uint32_t *ctl,
+                                                    uint32_t *deferred, uint32_t k1_waves, RjCoefBuf coefs,
+                                                    const RjTableSet *__restrict__ tabsets, uint32_t *wide_cnt, uint2 *wide_list) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];
+  __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
+  __shared__ uint32_t s_row;
+  const uint32_t tid = threadIdx.x;
+  // cleanup: the rows the streaming pass never took, then the deferred ones
+  const uint32_t start = kWait ? 0u : min(U(__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)), nrows);
+  const uint32_t ndef = kWait ? 0u : U(__hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  for (;;) {
+    __syncthreads();  // the previous row's tiles fully read
+    if (tid == 0) {
+      uint32_t w = 0xFFFFFFFFu;
+      // streaming: no new row once K1 is done (the cleanup pass has full occupancy)
+      if (!kWait || __hip_atomic_load(ctl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k1_waves)
+        w = atomicAdd(ctl + (kWait ? 0 : 2), 1u);
+      s_row = w;
+    }
+    __syncthreads();
+    const uint32_t w = U(s_row);
+    uint32_t row;
+    if (kWait) {
+      if (w >= nrows) break;
+      row = w;
+    } else {
+      if (w < nrows - start) row = start + w;
+      else if (w - (nrows - start) < ndef) row = U(deferred[w - (nrows - start)]);
+      else break;
+    }
+    if (kWait) {
+      const uint32_t gseg = U(row_segs[row]);
+      bool ready = false;
+      for (uint32_t k = 0; k < (1u << 14); k++) {  // ~2^14 x ~1 us: far beyond any K1 span
+        if (U(__hip_atomic_load(flags + gseg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == epoch) {
+          ready = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(32);
+      }
+      if (!ready) {
+        if (tid == 0) deferred[atomicAdd(ctl + 1, 1u)] = row;
+        continue;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    int i;
+    uint32_t my;
+    row_of_block(imgs, nimg, nullptr, nullptr, row_segs, row, i, my);
+    row_body<false, false>(imgs, i, my, coefs, tabsets, nullptr, s_buf, s_q, wide_cnt, wide_list);
+  }
+}
+
+hipError_t LaunchRowsStream(hipStream_t st, bool wait, const RjImageDev *imgs, int nimg, const uint32_t *row_segs,
+                            uint32_t nrows, const uint32_t *flags, uint32_t epoch, uint32_t *ctl, uint32_t *deferred,
+                            uint32_t k1_waves, uint32_t grid, RjCoefBuf coefs, const RjTableSet *tabsets,
+                            uint32_t *wide_cnt, uint2 *wide_list) {
+  if (nrows == 0) return hipSuccess;
+  if (wait)
+    hipLaunchKernelGGL(k_rows_stream<true>, dim3(grid), dim3(64), 0, st, imgs, nimg, row_segs, nrows, flags, epoch, ctl,
+                       deferred, k1_waves, coefs, tabsets, wide_cnt, wide_list);
+  else
+    hipLaunchKernelGGL(k_rows_stream<false>, dim3(grid), dim3(64), 0, st, imgs, nimg, row_segs, nrows, flags, epoch,
+                       ctl, deferred, k1_waves, coefs, tabsets, wide_cnt, wide_list);
+  return hipGetLastError();
+}
+
+// the fix-up launch behind a K2 launch of `cap` rows (same stream, same variant)
+hipError_t LaunchRowsFix(hipStream_t st, bool to_planes, bool dense, const RjImageDev *imgs, int nimg, RjCoefBuf coefs,
+                         const RjTableSet *tabsets, uint8_t *planes, const uint32_t *wide_cnt, const uint2 *wide_list,
+                         uint32_t cap) {
+  if (cap == 0) return hipSuccess;
+  const dim3 grid(std::min<uint32_t>(cap, 256));
+  if (dense) {
+    if (to_planes)
+      hipLaunchKernelGGL((k_rows_fix<true, true>), grid, dim3(64), 0, st, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, cap);
+    else
+      hipLaunchKernelGGL((k_rows_fix<false, true>), grid, dim3(64), 0, st, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, cap);
+  } else {
+    if (to_planes)
+      hipLaunchKernelGGL((k_rows_fix<true, false>), grid, dim3(64), 0, st, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, cap);
+    else
+      hipLaunchKernelGGL((k_rows_fix<false, false>), grid, dim3(64), 0, st, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, cap);
+  }
+  return hipGetLastError();
+}
+
 hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
                       const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
-                      uint8_t *planes) {
+                      uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list) {
   if (nrows == 0) return hipSuccess;
   const uint32_t *no_segs = nullptr;
   if (to_planes)
     hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, no_segs, coefs,
-                       tabsets, planes);
+                       tabsets, planes, wide_cnt, wide_list);
   else
     hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, no_segs, coefs,
-                       tabsets, planes);
-  return hipGetLastError();
+                       tabsets, planes, wide_cnt, wide_list);
+  const hipError_t e = hipGetLastError();
+  return e != hipSuccess ? e : LaunchRowsFix(st, to_planes, false, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, nrows);
 }
 
 hipError_t LaunchRowsDense(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
-                           uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets, uint8_t *planes) {
+                           uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets, uint8_t *planes,
+                           uint32_t *wide_cnt, uint2 *wide_list) {
   if (nrows == 0) return hipSuccess;
   const uint32_t *no_segs = nullptr;
   const uint2 *no_list = nullptr;
   if (to_planes)
     hipLaunchKernelGGL((k_rows<true, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, no_list, no_segs,
-                       coefs, tabsets, planes);
+                       coefs, tabsets, planes, wide_cnt, wide_list);
   else
     hipLaunchKernelGGL((k_rows<false, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, no_list, no_segs,
-                       coefs, tabsets, planes);
-  return hipGetLastError();
+                       coefs, tabsets, planes, wide_cnt, wide_list);
+  const hipError_t e = hipGetLastError();
+  return e != hipSuccess ? e : LaunchRowsFix(st, to_planes, true, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, nrows);
 }
 
 #ifdef RJ_EXP_STAMPS
@@ -602,17 +777,18 @@ void DumpRowStamps() {
 
 hipError_t LaunchRowsOfLanes(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg,
                              const uint32_t *row_segs, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
-                             uint8_t *planes) {
+                             uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list) {
   if (nrows == 0) return hipSuccess;
   const uint32_t *no_prefix = nullptr;
   const uint2 *no_list = nullptr;
   if (to_planes)
     hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, no_prefix, no_list, row_segs, coefs,
-                       tabsets, planes);
+                       tabsets, planes, wide_cnt, wide_list);
   else
     hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, no_prefix, no_list, row_segs, coefs,
-                       tabsets, planes);
-  return hipGetLastError();
+                       tabsets, planes, wide_cnt, wide_list);
+  const hipError_t e = hipGetLastError();
+  return e != hipSuccess ? e : LaunchRowsFix(st, to_planes, false, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, nrows);
 }
 
 }  // namespace rj

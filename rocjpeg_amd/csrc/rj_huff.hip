@@ -149,12 +149,14 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
 __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0,
                                                       uint32_t nlanes, const uint8_t *__restrict__ destuffed,
                                                       const RjTableSet *__restrict__ tabsets,
-                                                      const RjLeanTables *__restrict__ lean, RjCoefBuf coefs) {
+                                                      const RjLeanTables *__restrict__ lean, RjCoefBuf coefs,
+                                                      uint32_t *flags, uint32_t epoch, uint32_t *done) {
   __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_HL_WORDS][RJ_HL_WG];
   __shared__ __attribute__((aligned(16))) uint32_t s_stage[RJ_HL_STAGE][RJ_HL_WG];
   __shared__ __attribute__((aligned(16))) uint32_t s_lut[RJ_HL_LUT_WORDS];
   __shared__ uint32_t s_T, s_ne;
   const uint32_t tid = threadIdx.x;
+  if (flags != nullptr) __builtin_amdgcn_s_setprio(2);  // the serial chains win issue over streaming K2 waves
   if (tid == 0) s_ne = 0;
   const uint32_t g = lane0 + blockIdx.x * RJ_HL_WG + tid;
   bool pending = g < lane0 + nlanes;
@@ -291,8 +293,16 @@ __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restri
     }
     *gp(piece) = RjPiece{ent_abs, 0u, blocks, 1u, {0, 0, 0}};
     if (coefs.count) atomicAdd(&s_ne, ne + 1);
+    if (flags != nullptr) {  // streaming K2: publish the interval (release after this wave's stores)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flag must not overtake the write-back
+      __hip_atomic_store(flags + gseg, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   if (tid == 0 && coefs.count != nullptr && s_ne != 0) atomicAdd(coefs.count, (unsigned long long)s_ne);
+  // streaming K2 stops taking rows once every K1 wave is here (its intervals were published above)
+  if (done != nullptr && (tid & 63) == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 #ifdef RJ_HL_STAMPS
@@ -310,10 +320,11 @@ void DumpHuffStamps() {
 
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
-                           RjCoefBuf coefs) {
+                           RjCoefBuf coefs, uint32_t *flags, uint32_t epoch, uint32_t *done) {
   if (nlanes == 0) return hipSuccess;
+  static_assert(RJ_HL_WG == 256, "HuffLaneWaves");
   hipLaunchKernelGGL(k_huff, dim3((nlanes + RJ_HL_WG - 1) / RJ_HL_WG), dim3(RJ_HL_WG), 0, st, imgs, nimg, lane0, nlanes,
-                     destuffed, tabsets, lean, coefs);
+                     destuffed, tabsets, lean, coefs, flags, epoch, done);
   return hipGetLastError();
 }
 

@@ -24,9 +24,14 @@ hipError_t LaunchEntropyLanes(hipStream_t st, const RjImageDev *imgs, int nimg, 
 
 // Lean K1 (rj_huff.hip): lanes [lane0, lane0 + nlanes), one whole interval each, raw entries;
 // only for calls whose every baseline image is a row image and no interval is split.
+// flags != null: each interval publishes flags[gseg] = epoch once its entries are visible
+// device-wide (streaming K2).
+// done != null: every wave adds 1 to *done when it has published its lanes' intervals.
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
-                           RjCoefBuf coefs);
+                           RjCoefBuf coefs, uint32_t *flags = nullptr, uint32_t epoch = 0, uint32_t *done = nullptr);
+// waves of a LaunchHuffLanes grid over n lanes
+inline uint32_t HuffLaneWaves(uint32_t nlanes) { return (nlanes + 255) / 256 * 4; }
 
 // K2b (general path): every output format / ROI of rocjpeg_decoder.cpp:143-180 from the planes.
 hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobDev *jobs, int njobs, uint32_t total_rows,
@@ -37,14 +42,29 @@ hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobD
 // the (image, MCU row) pair row_list[w]).  Sparse entries -> dequant + ISLOW IDCT
 // -> either the fused output (upsample + CSC / layout straight into the caller's buffers, only
 // for rj_decoder.cpp::FusedEligible images) or the MCU-padded component planes (to_planes).
+// wide_cnt (zero on entry) / wide_list (nrows slots): this launch's fix-up list; rows with
+// coefficients outside the int32 IDCT's exact domain are recorded there and decoded again by
+// the fix-up launch (k_rows_fix) that every K2 launcher issues behind its K2 launch.
 hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
                       const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
-                      uint8_t *planes);
+                      uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list);
 // K2 over the MCU rows of the intervals row_segs[0, nrows) (batch-global interval indices), for
 // batches whose every interval is exactly one MCU row.
 hipError_t LaunchRowsOfLanes(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg,
                              const uint32_t *row_segs, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
-                             uint8_t *planes);
+                             uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list);
+
+// Streaming K2 (rj_fused.hip k_rows_stream): persistent workgroups over the rows of a call
+// whose every interval is one MCU row, each row started once lean K1 has published its interval
+// (flags[gseg] == epoch); wait = false: the cleanup pass over the rows a bounded wait deferred.
+hipError_t LaunchRowsStream(hipStream_t st, bool wait, const RjImageDev *imgs, int nimg, const uint32_t *row_segs,
+                            uint32_t nrows, const uint32_t *flags, uint32_t epoch, uint32_t *ctl, uint32_t *deferred,
+                            uint32_t k1_waves, uint32_t grid, RjCoefBuf coefs, const RjTableSet *tabsets,
+                            uint32_t *wide_cnt, uint2 *wide_list);
+// The fix-up launch alone (the streaming K2 issues it after its cleanup pass; cap = rows).
+hipError_t LaunchRowsFix(hipStream_t st, bool to_planes, bool dense, const RjImageDev *imgs, int nimg, RjCoefBuf coefs,
+                         const RjTableSet *tabsets, uint8_t *planes, const uint32_t *wide_cnt, const uint2 *wide_list,
+                         uint32_t cap);
 
 // K1p (rj_prog.hip): progressive scans, one lane per restart interval of one scan; `lanes`
 // lists batch-global interval indices (RjImageDev.pival_prefix), grouped so every wave holds
@@ -65,7 +85,8 @@ hipError_t LaunchProgressiveFold(hipStream_t st, const RjImageDev *imgs, const R
 
 // K2 over progressive images' MCU rows: dense coefficients (RjCoefBuf.dense) instead of entries.
 hipError_t LaunchRowsDense(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
-                           uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets, uint8_t *planes);
+                           uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets, uint8_t *planes,
+                           uint32_t *wide_cnt, uint2 *wide_list);
 
 // GPU marker scan (rj_scan.hip): one wave per stream.
 hipError_t LaunchScan(hipStream_t st, const RjScanJob *jobs, uint32_t njobs, const uint8_t *arena);

@@ -174,6 +174,113 @@ __device__ __forceinline__ void idct_islow_block(int32_t (&v)[64], uint32_t (&o)
   }
 }
 
+// Exact ISLOW for coefficients outside the int32 domain above (only corrupt streams with large
+// quantisers get here; K2 detects them per strip and records the row, which the K2 fix-up
+// launch -- k_rows_fix, its own kernel, so none of this touches the common path's registers --
+// decodes again with this arithmetic for the flagged strips):
+// libjpeg jidctint.c as on LP64 (INT32/JLONG = long) with its RANGE_MASK wrap --
+// oracle/jpeg_oracle.c idct_islow.  The output needs bits 18..27 of each pass-2 sum only, and
+// pass 2 is linear with integer constants, so it is exact modulo 2^32 given the pass-1 outputs
+// modulo 2^32: pass 1 runs in 64-bit (its outputs need bits 11..42 of the sums), pass 2 in
+// wrapping 32-bit with full multiplies (v_mul_lo_u32; m24 would truncate).
+// islow_1d in wrapping 32-bit arithmetic with full multiplies (pass 2 of the wide path).
+__device__ __forceinline__ void islow_1d_wrap(const int32_t *xi, uint32_t rnd, int32_t t[8]) {
+  const uint32_t x0 = xi[0], x1 = xi[1], x2 = xi[2], x3 = xi[3], x4 = xi[4], x5 = xi[5], x6 = xi[6], x7 = xi[7];
+  uint32_t z1 = (x2 + x6) * uint32_t(RJ_FIX_0_541196100);
+  const uint32_t tmp2 = z1 - x6 * uint32_t(RJ_FIX_1_847759065);
+  const uint32_t tmp3 = z1 + x2 * uint32_t(RJ_FIX_0_765366865);
+  const uint32_t e0 = ((x0 + x4) << 13) + rnd, e1 = ((x0 - x4) << 13) + rnd;
+  const uint32_t t10 = e0 + tmp3, t13 = e0 - tmp3, t11 = e1 + tmp2, t12 = e1 - tmp2;
+  uint32_t o0 = x7, o1 = x5, o2 = x3, o3 = x1;
+  z1 = o0 + o3;
+  uint32_t z2 = o1 + o2, z3 = o0 + o2, z4 = o1 + o3;
+  const uint32_t z5 = (z3 + z4) * uint32_t(RJ_FIX_1_175875602);
+  o0 *= uint32_t(RJ_FIX_0_298631336);
+  o1 *= uint32_t(RJ_FIX_2_053119869);
+  o2 *= uint32_t(RJ_FIX_3_072711026);
+  o3 *= uint32_t(RJ_FIX_1_501321110);
+  z1 *= uint32_t(-RJ_FIX_0_899976223);
+  z2 *= uint32_t(-RJ_FIX_2_562915447);
+  z3 = z3 * uint32_t(-RJ_FIX_1_961570560) + z5;
+  z4 = z4 * uint32_t(-RJ_FIX_0_390180644) + z5;
+  o0 += z1 + z3;
+  o1 += z2 + z4;
+  o2 += z2 + z3;
+  o3 += z1 + z4;
+  t[0] = int32_t(t10 + o3);
+  t[7] = int32_t(t10 - o3);
+  t[1] = int32_t(t11 + o2);
+  t[6] = int32_t(t11 - o2);
+  t[2] = int32_t(t12 + o1);
+  t[5] = int32_t(t12 - o1);
+  t[3] = int32_t(t13 + o0);
+  t[4] = int32_t(t13 - o0);
+}
+
+// pass 1 of the wide path: 64-bit sums from the LDS block (zigzag coefficients, zigzag
+// quantisers), outputs modulo 2^32 into v (natural order) -- all pass 2 needs.
+__device__ __forceinline__ void idct_pass1_wide(const int16_t *zz, const uint16_t *qz, int32_t (&v)[64]) {
+  constexpr uint8_t kZz[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
+                               3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
+                               10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+                               21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+  auto X = [&](int nat) { return int64_t(zz[kZz[nat]]) * int64_t(qz[kZz[nat]]); };
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    int64_t z2 = X(16 + c), z3 = X(48 + c);
+    int64_t z1 = (z2 + z3) * RJ_FIX_0_541196100;
+    int64_t tmp2 = z1 - z3 * RJ_FIX_1_847759065;
+    int64_t tmp3 = z1 + z2 * RJ_FIX_0_765366865;
+    z2 = X(c);
+    z3 = X(32 + c);
+    int64_t tmp0 = (z2 + z3) * 8192, tmp1 = (z2 - z3) * 8192;
+    const int64_t t10 = tmp0 + tmp3, t13 = tmp0 - tmp3, t11 = tmp1 + tmp2, t12 = tmp1 - tmp2;
+    tmp0 = X(56 + c);
+    tmp1 = X(40 + c);
+    tmp2 = X(24 + c);
+    tmp3 = X(8 + c);
+    z1 = tmp0 + tmp3;
+    z2 = tmp1 + tmp2;
+    z3 = tmp0 + tmp2;
+    int64_t z4 = tmp1 + tmp3;
+    const int64_t z5 = (z3 + z4) * RJ_FIX_1_175875602;
+    tmp0 *= RJ_FIX_0_298631336;
+    tmp1 *= RJ_FIX_2_053119869;
+    tmp2 *= RJ_FIX_3_072711026;
+    tmp3 *= RJ_FIX_1_501321110;
+    z1 *= -RJ_FIX_0_899976223;
+    z2 *= -RJ_FIX_2_562915447;
+    z3 = z3 * -RJ_FIX_1_961570560 + z5;
+    z4 = z4 * -RJ_FIX_0_390180644 + z5;
+    tmp0 += z1 + z3;
+    tmp1 += z2 + z4;
+    tmp2 += z2 + z3;
+    tmp3 += z1 + z4;
+    const int64_t rnd = 1 << 10;
+    v[0 * 8 + c] = int32_t((t10 + tmp3 + rnd) >> 11);
+    v[7 * 8 + c] = int32_t((t10 - tmp3 + rnd) >> 11);
+    v[1 * 8 + c] = int32_t((t11 + tmp2 + rnd) >> 11);
+    v[6 * 8 + c] = int32_t((t11 - tmp2 + rnd) >> 11);
+    v[2 * 8 + c] = int32_t((t12 + tmp1 + rnd) >> 11);
+    v[5 * 8 + c] = int32_t((t12 - tmp1 + rnd) >> 11);
+    v[3 * 8 + c] = int32_t((t13 + tmp0 + rnd) >> 11);
+    v[4 * 8 + c] = int32_t((t13 - tmp0 + rnd) >> 11);
+  }
+}
+
+// pass 2 of the wide path (rows, wrapping 32-bit); output as idct_islow_block
+__device__ __forceinline__ void idct_pass2_wrap(const int32_t (&v)[64], uint32_t (&o)[16]) {
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    int32_t t[8];
+    islow_1d_wrap(v + r * 8, uint32_t(RJ_PASS2_RND), t);
+    o[2 * r] = islow_pack4(islow_limit_biased(t[0]), islow_limit_biased(t[1]), islow_limit_biased(t[2]),
+                           islow_limit_biased(t[3]));
+    o[2 * r + 1] = islow_pack4(islow_limit_biased(t[4]), islow_limit_biased(t[5]), islow_limit_biased(t[6]),
+                               islow_limit_biased(t[7]));
+  }
+}
+
 // Colour conversion of the reference (src/rocjpeg_hip_kernels.cpp:1431-1443, same in every
 // CSC kernel): BT.709-style constants, fmaf order as written there, u8 by v_cvt_pk_u8_f32.
 __device__ __forceinline__ uint32_t cvt_u8(float f) { return __builtin_amdgcn_cvt_pk_u8_f32(f, 0, 0u) & 0xFFu; }

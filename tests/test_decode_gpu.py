@@ -208,16 +208,21 @@ def test_long_interval_batch_mixed(dec):
         assert G.first_mismatch(G.to_host(bufs)[0], want[0]) is None
 
 
-@pytest.fixture(scope="module", params=[(0, 4), (1, 4), (0, 1)], ids=["auto_g4", "general_g4", "auto_g1"])
+@pytest.fixture(scope="module",
+                params=[(0, 4, {}), (1, 4, {}), (0, 1, {}), (0, 4, {"RJ_LEAN": "1"}), (0, 1, {"RJ_LEAN": "1"}),
+                        (0, 2, {"RJ_LEAN": "1", "RJ_STREAM_K2": "1"})],
+                ids=["auto_g4", "general_g4", "auto_g1", "lean_g4", "lean_g1", "lean_stream_g2"])
 def pdec(request):
     """A decoder that sorts the K1 lanes of every call with no split interval by length
     (RJ_PIPE_MIN=1) and, with 4 groups, pipelines it: interval length classes on separate
-    streams, each class's K2 rows after the K1 lanes of its class and all earlier ones."""
+    streams, each class's K2 rows after the K1 lanes of its class and all earlier ones.  The
+    lean K1 (RJ_LEAN=1, row-interval batches only) and the streaming K2 (RJ_STREAM_K2=1) are
+    opt-in variants, covered here."""
     import os
     from tests import gpu_util as G
     G.torch()
-    policy, groups = request.param
-    env = {"RJ_PIPE_MIN": "1", "RJ_PIPE_GROUPS": str(groups)}
+    policy, groups, extra = request.param
+    env = {"RJ_PIPE_MIN": "1", "RJ_PIPE_GROUPS": str(groups), **extra}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -230,6 +235,7 @@ def pdec(request):
                 os.environ[k] = v
     d.set_path_policy(policy)
     d.groups = groups
+    d.extra = extra
     d.set_profiling(True)
     yield d
     d.close()
@@ -291,6 +297,8 @@ def test_pipelined_row_aligned_batch(pdec, fmt):
     assert t["pipe_groups"] == pdec.groups
     if pdec.groups > 1:
         assert t["pipe_lane_rows"] == 1
+    assert t["lean_k1"] == (1 if pdec.extra.get("RJ_LEAN") else 0)
+    assert t["k2_stream"] == (1 if pdec.extra.get("RJ_STREAM_K2") else 0)
     for k, (d, shapes, bufs) in enumerate(zip(datas, shapes_all, bufs_all)):
         ost, want = O.oracle_decode(d, int(fmt), shapes)
         assert ost == 0

@@ -116,3 +116,56 @@ def test_fuzz_progressive_runs_and_is_deterministic(dec, seed):
     assert st1 == st2 == 0
     for a, b in zip(outs1, outs2):
         assert np.array_equal(a, b)
+
+
+def _coarse_quant_jpegs():
+    """Streams whose quantisers are all 255 (DQT maximum for 8-bit tables): once damaged, decoded
+    coefficients x quantiser leave the int32 IDCT's exact domain (|x| < 2^14, rj_math.h), which
+    K2 detects per strip and hands to the 64-bit restatement of jidctint.c.  Restart interval one
+    MCU row (the lean K1 with raw DC differences) and none (the chunked K1), four subsamplings."""
+    import io
+    from PIL import Image
+    rng = np.random.default_rng(7)
+    out = []
+    for (w, h), sub, rst in [((256, 128), 2, True), ((200, 72), 0, True), ((160, 96), 1, True),
+                             ((256, 128), 2, False), ((97, 65), 2, False)]:
+        a = np.clip(128 + 90 * np.sin(np.arange(w)[None, :, None] / 7.0) + rng.normal(0, 40, (h, w, 3)), 0, 255)
+        b = io.BytesIO()
+        kw = dict(qtables=[[255] * 64, [255] * 64], subsampling=sub)
+        if rst:
+            kw["restart_marker_blocks"] = (w + 15) // 16
+        Image.fromarray(a.astype(np.uint8)).save(b, "JPEG", **kw)
+        out.append(b.getvalue())
+    g = io.BytesIO()
+    Image.fromarray(rng.integers(0, 255, (64, 96), dtype=np.uint8)).save(g, "JPEG", qtables=[[255] * 64],
+                                                                          restart_marker_blocks=12)
+    out.append(g.getvalue())
+    return out
+
+
+def test_coarse_quant_clean_streams_stay_in_int32_domain(dec):
+    base = _coarse_quant_jpegs()
+    dec.set_profiling(True)
+    st, outs, shapes = _decode_batch(dec, base)
+    tm = dec.last_timings()
+    dec.set_profiling(False)
+    assert st == 0 and tm["wide_rows"] == 0
+    for d, o, shp in zip(base, outs, shapes):
+        ost, want = O.oracle_decode(d, int(R.OutputFormat.RGB), shp)
+        assert ost == 0 and np.array_equal(o, want[0])
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_fuzz_coarse_quant_outside_int32_domain(dec, seed):
+    base = _coarse_quant_jpegs()
+    datas = base + [damage(d, seed * 100 + k, nhits=40) for k, d in enumerate(base)]
+    dec.set_profiling(True)
+    st, outs, shapes = _decode_batch(dec, datas)
+    tm = dec.last_timings()
+    dec.set_profiling(False)
+    assert st == 0
+    assert tm["wide_rows"] > 0  # the fix-up path ran (the undamaged streams stay in the int32 domain)
+    for d, o, shp in zip(datas, outs, shapes):
+        ost, want = O.oracle_decode(d, int(R.OutputFormat.RGB), shp)
+        assert ost == 0
+        assert np.array_equal(o, want[0])

@@ -13,5 +13,5 @@ for spec in sys.argv[1:]:
     tag = spec.split(':')[0]
     d = json.loads(open(f'gpurun_out/ab/{tag}.log').read().strip().splitlines()[-1])
     k = d['roofline']['per_kernel_launch_ms_sum']
-    print(f"{tag:14s} {d['value']:10.0f} img/s  {d['ms_per_step']:7.3f} ms  K1 {k.get('k_entropy',0):6.3f}  K2 {k.get('k_rows',0):6.3f}  parity {d['parity_timed_output']}")
+    print(f"{tag:14s} {d['value']:10.0f} img/s  {d['ms_per_step']:7.3f} ms  K1 {k.get('k_entropy',0)+k.get('k_huff',0):6.3f}  K2 {k.get('k_rows',0):6.3f}  parity {d['parity_timed_output']}")
 PY
