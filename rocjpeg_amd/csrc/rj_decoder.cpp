@@ -118,6 +118,7 @@ Decoder::~Decoder() {
       if (q) (void)hipStreamDestroy(q);
     (void)hipStreamDestroy(stream_);
   }
+  if (h_wide_flag_) (void)hipHostFree(h_wide_flag_);
 }
 
 int Decoder::Initialize() {
@@ -148,6 +149,9 @@ int Decoder::Initialize() {
   if (const char *sk = getenv("RJ_STREAM_K2")) stream_enabled_ = atoi(sk) != 0;
   if (const char *sw = getenv("RJ_STREAM_WG")) stream_wg_per_cu_ = std::max(1, std::min(16, atoi(sw)));
   cu_count_ = std::max(1, prop.multiProcessorCount);
+  RJ_HIP(hipHostMalloc(reinterpret_cast<void **>(&h_wide_flag_), 64, hipHostMallocMapped | hipHostMallocCoherent));
+  RJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_wide_flag_), h_wide_flag_, 0));
+  *reinterpret_cast<volatile uint32_t *>(h_wide_flag_) = 0;
   for (auto &q : pstream_) RJ_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
   for (auto &e : pev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : pk1_) RJ_HIP(hipEventCreate(&e));
@@ -1037,6 +1041,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   cbuf.fallback = d_fallback_.as<uint32_t>();
   cbuf.count = nullptr;
   cbuf.dense = d_coef_.as<uint32_t>();
+  cbuf.wide_flag = d_wide_flag_;
   if (profiling_) {
     RJ_CHECK(d_count_.Ensure(256));
     cbuf.count = d_count_.as<unsigned long long>();
@@ -1123,12 +1128,13 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   std::memset(h + off_wide, 0, kWideSites * sizeof(uint32_t));
   uint32_t *const d_wide_cnt = reinterpret_cast<uint32_t *>(dbase + off_wide);
   uint64_t wide_used = 0;
-  int wide_site = 0;
+  wide_sites_.clear();
   // the next K2 launch's fix-up list: its counter and `rows` slots
-  auto wide = [&](uint32_t rows, uint32_t *&cnt, uint2 *&list) {
-    cnt = d_wide_cnt + std::min(wide_site++, kWideSites - 1);
+  auto wide = [&](uint32_t rows, uint32_t *&cnt, uint2 *&list, bool planes, bool dense) {
+    cnt = d_wide_cnt + std::min<int>(int(wide_sites_.size()), kWideSites - 1);
     list = d_wide_.as<uint2>() + wide_used;
     wide_used += rows;
+    if (rows) wide_sites_.push_back({planes, dense, rows, cnt, list});
   };
   uint32_t *wcnt = nullptr;
   uint2 *wlist = nullptr;
@@ -1244,10 +1250,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       if (dbg_lev) RJ_HIP(hipEventRecord(prog_lev_ev_[L + 1], stream_));
     }
     if (profiling_) RJ_HIP(hipEventRecord(prog_ev_[1], stream_));
-    wide(pfused_rows, wcnt, wlist);
+    wide(pfused_rows, wcnt, wlist, false, true);
     RJ_HIP(LaunchRowsDense(stream_, false, d_imgs, n, reinterpret_cast<const uint32_t *>(dbase + off_prows), pfused_rows,
                            cbuf, d_tabs, nullptr, wcnt, wlist));
-    wide(pgeneral_rows, wcnt, wlist);
+    wide(pgeneral_rows, wcnt, wlist, true, true);
     RJ_HIP(LaunchRowsDense(stream_, true, d_imgs, n, reinterpret_cast<const uint32_t *>(dbase + off_pgrows),
                            pgeneral_rows, cbuf, d_tabs, d_planes_.as<uint8_t>(), wcnt, wlist));
     if (profiling_) RJ_HIP(hipEventRecord(prog_ev_[2], stream_));
@@ -1402,7 +1408,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (profiling_) RJ_HIP(hipEventRecord(pk1_[0], stream_));
     if (profiling_) RJ_HIP(hipEventRecord(k2s_[0], pstream_[0]));
     const uint32_t grid = std::min<uint32_t>(seg_total, uint32_t(stream_wg_per_cu_) * uint32_t(cu_count_));
-    wide(seg_total, wcnt, wlist);
+    wide(seg_total, wcnt, wlist, false, false);
     RJ_HIP(LaunchRowsStream(pstream_[0], true, d_imgs, n, d_lane_seg, seg_total, d_flags_.as<uint32_t>(), epoch_, ctl,
                             ctl + 4, HuffLaneWaves(seg_total), grid, cbuf, d_tabs, wcnt, wlist));
     if (profiling_) RJ_HIP(hipEventRecord(k2e_[0], pstream_[0]));
@@ -1412,7 +1418,6 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(LaunchRowsStream(stream_, false, d_imgs, n, d_lane_seg, seg_total, d_flags_.as<uint32_t>(), epoch_, ctl,
                             ctl + 4, HuffLaneWaves(seg_total), std::min<uint32_t>(seg_total, 16u * uint32_t(cu_count_)),
                             cbuf, d_tabs, wcnt, wlist));
-    RJ_HIP(LaunchRowsFix(stream_, false, false, d_imgs, n, cbuf, d_tabs, nullptr, wcnt, wlist, seg_total));
     if (profiling_) RJ_HIP(hipEventRecord(k2e_[1], stream_));
   } else if (ngroups > 1) {
     RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0 and upload B done
@@ -1442,14 +1447,14 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       for (int q = 0; q < g; q++) RJ_HIP(hipStreamWaitEvent(st, kev_[q], 0));  // rows spanning classes
       if (profiling_) RJ_HIP(hipEventRecord(k2s_[g], st));
       if (rows_from_lanes) {
-        wide(lane_off[g + 1] - lane_off[g], wcnt, wlist);
+        wide(lane_off[g + 1] - lane_off[g], wcnt, wlist, fused_images == 0, false);
         RJ_HIP(LaunchRowsOfLanes(st, fused_images == 0, d_imgs, n, d_lane_seg + lane_off[g],
                                  lane_off[g + 1] - lane_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>(), wcnt, wlist));
       } else {
-        wide(frow_off[g + 1] - frow_off[g], wcnt, wlist);
+        wide(frow_off[g + 1] - frow_off[g], wcnt, wlist, false, false);
         RJ_HIP(LaunchRows(st, false, d_imgs, n, d_rows, d_row_list + frow_off[g], frow_off[g + 1] - frow_off[g],
                           cbuf, d_tabs, nullptr, wcnt, wlist));
-        wide(grow_off[g + 1] - grow_off[g], wcnt, wlist);
+        wide(grow_off[g + 1] - grow_off[g], wcnt, wlist, true, false);
         RJ_HIP(LaunchRows(st, true, d_imgs, n, d_grows, d_row_list + fused_rows + grow_off[g],
                           grow_off[g + 1] - grow_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>(), wcnt, wlist));
       }
@@ -1470,9 +1475,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       }
     }
     if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
-    wide(fused_rows, wcnt, wlist);
+    wide(fused_rows, wcnt, wlist, false, false);
     RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr, wcnt, wlist));
-    wide(general_rows, wcnt, wlist);
+    wide(general_rows, wcnt, wlist, true, false);
     RJ_HIP(LaunchRows(stream_, true, d_imgs, n, d_grows, nullptr, general_rows, cbuf, d_tabs,
                       d_planes_.as<uint8_t>(), wcnt, wlist));
   }
@@ -1483,11 +1488,22 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(hipMemcpy2DAsync(rc.user, rc.pitch, d_route_.as<uint8_t>() + rc.off, rc.pitch, rc.row_bytes, rc.rows,
                             hipMemcpyDefault, stream_));
   RJ_HIP(hipStreamSynchronize(stream_));
-  if (profiling_) {
+  timings_.wide_rows = 0;
+  if (*reinterpret_cast<volatile uint32_t *>(h_wide_flag_)) {
+    // rows outside the int32 IDCT's exact domain (corrupt data, large quantisers): decode them
+    // again in 64-bit, then redo the output jobs (general rows) and routed copies, all idempotent
+    *reinterpret_cast<volatile uint32_t *>(h_wide_flag_) = 0;
     uint32_t wc[kWideSites];
     RJ_HIP(hipMemcpy(wc, d_wide_cnt, sizeof(wc), hipMemcpyDeviceToHost));
-    timings_.wide_rows = 0;
     for (int k = 0; k < kWideSites; k++) timings_.wide_rows += wc[k];
+    for (const WideSite &ws : wide_sites_)
+      RJ_HIP(LaunchRowsFix(stream_, ws.planes, ws.dense, d_imgs, n, cbuf, d_tabs,
+                           ws.planes ? d_planes_.as<uint8_t>() : nullptr, ws.cnt, ws.list, ws.cap));
+    RJ_HIP(LaunchOutputJobs(stream_, d_imgs, d_jobs, int(jobs.size()), rows_total, d_planes_.as<uint8_t>()));
+    for (const RouteCopy &rc : routes_)
+      RJ_HIP(hipMemcpy2DAsync(rc.user, rc.pitch, d_route_.as<uint8_t>() + rc.off, rc.pitch, rc.row_bytes, rc.rows,
+                              hipMemcpyDefault, stream_));
+    RJ_HIP(hipStreamSynchronize(stream_));
   }
   if (prog_images && prog_pipe) {  // a refinement wave that gave up waiting (never expected)
     uint32_t err = 0;

@@ -108,6 +108,15 @@ class Decoder {
   DeviceBuffer d_flags_;           // streaming K2: per interval, the epoch of the call that published it
   DeviceBuffer d_sctl_;            // streaming K2: row counters + deferred row list
   DeviceBuffer d_wide_;            // K2 fix-up lists (rows outside the int32 IDCT's domain)
+  uint32_t *h_wide_flag_ = nullptr;  // host-mapped, coherent: K2 recorded a row for the fix-up
+  uint32_t *d_wide_flag_ = nullptr;
+  struct WideSite {                // one K2 launch of the current call
+    bool planes, dense;
+    uint32_t cap;
+    uint32_t *cnt;
+    uint2 *list;
+  };
+  std::vector<WideSite> wide_sites_;
   hipStream_t pstream_[kMaxPipe - 1] = {};
   hipEvent_t pev_[kMaxPipe] = {};
   hipEvent_t pk1_[kMaxPipe] = {};

@@ -73,6 +73,7 @@ struct RjCoefBuf {
   const uint32_t *seg_lane0;  // per interval: its first lane; null: identity (no interval split)
   unsigned long long *count;  // profiling: entries written, summed per workgroup (null: off)
   const uint32_t *dense;      // progressive images: dense coefficients (RjImageDev.coef_off)
+  uint32_t *wide_flag;        // host-mapped: set by K2 when it recorded a row for the fix-up
 };
 #define RJ_ENT_PER_BLOCK 64       // worst case: DC + 63 AC (each position written at most once)
 #define RJ_ENT_GROUP 16           // K1 writes entries in 64-B groups; regions are group-aligned

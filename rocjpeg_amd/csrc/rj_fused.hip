@@ -585,6 +585,8 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
     if (row_wide && tid == 0) {
       const uint32_t k = atomicAdd(wide_cnt, 1u);
       wide_list[k] = make_uint2(uint32_t(i), my);
+      // host-mapped flag: the host issues the fix-up launches after the call's kernels
+      __hip_atomic_store(coefs.wide_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 #ifdef RJ_EXP_STAMPS
   if (tid == 0)
@@ -612,8 +614,8 @@ __global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ i
 
 // K2 fix-up: the rows a K2 launch recorded (a strip outside the int32 IDCT's exact domain --
 // corrupt data with large quantisers), decoded again with the 64-bit IDCT for those strips.
-// Launched right behind its K2 launch on the same stream; with nothing recorded every
-// workgroup reads the count and leaves.
+// Issued by the host only when a K2 launch of the call raised the host-mapped flag
+// (RjCoefBuf.wide_flag), after the call's kernels -- the common path pays nothing.
 template <bool kPlanes, bool kDense>
 __global__ __launch_bounds__(64) void k_rows_fix(const RjImageDev *__restrict__ imgs, int nimg, RjCoefBuf coefs,
                                                  const RjTableSet *__restrict__ tabsets, uint8_t *__restrict__ planes,
@@ -743,8 +745,7 @@ hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, in
   else
     hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, no_segs, coefs,
                        tabsets, planes, wide_cnt, wide_list);
-  const hipError_t e = hipGetLastError();
-  return e != hipSuccess ? e : LaunchRowsFix(st, to_planes, false, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, nrows);
+  return hipGetLastError();
 }
 
 hipError_t LaunchRowsDense(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
@@ -759,8 +760,7 @@ hipError_t LaunchRowsDense(hipStream_t st, bool to_planes, const RjImageDev *img
   else
     hipLaunchKernelGGL((k_rows<false, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, no_list, no_segs,
                        coefs, tabsets, planes, wide_cnt, wide_list);
-  const hipError_t e = hipGetLastError();
-  return e != hipSuccess ? e : LaunchRowsFix(st, to_planes, true, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, nrows);
+  return hipGetLastError();
 }
 
 #ifdef RJ_EXP_STAMPS
@@ -787,8 +787,7 @@ hipError_t LaunchRowsOfLanes(hipStream_t st, bool to_planes, const RjImageDev *i
   else
     hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, no_prefix, no_list, row_segs, coefs,
                        tabsets, planes, wide_cnt, wide_list);
-  const hipError_t e = hipGetLastError();
-  return e != hipSuccess ? e : LaunchRowsFix(st, to_planes, false, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, nrows);
+  return hipGetLastError();
 }
 
 }  // namespace rj

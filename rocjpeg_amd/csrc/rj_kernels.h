@@ -43,8 +43,8 @@ hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobD
 // -> either the fused output (upsample + CSC / layout straight into the caller's buffers, only
 // for rj_decoder.cpp::FusedEligible images) or the MCU-padded component planes (to_planes).
 // wide_cnt (zero on entry) / wide_list (nrows slots): this launch's fix-up list; rows with
-// coefficients outside the int32 IDCT's exact domain are recorded there and decoded again by
-// the fix-up launch (k_rows_fix) that every K2 launcher issues behind its K2 launch.
+// coefficients outside the int32 IDCT's exact domain are recorded there (and coefs.wide_flag
+// raised) for the host to issue LaunchRowsFix after the call's kernels.
 hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
                       const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
                       uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list);
@@ -61,7 +61,7 @@ hipError_t LaunchRowsStream(hipStream_t st, bool wait, const RjImageDev *imgs, i
                             uint32_t nrows, const uint32_t *flags, uint32_t epoch, uint32_t *ctl, uint32_t *deferred,
                             uint32_t k1_waves, uint32_t grid, RjCoefBuf coefs, const RjTableSet *tabsets,
                             uint32_t *wide_cnt, uint2 *wide_list);
-// The fix-up launch alone (the streaming K2 issues it after its cleanup pass; cap = rows).
+// The fix-up launch of one K2 launch's list (same variant; cap = that launch's rows).
 hipError_t LaunchRowsFix(hipStream_t st, bool to_planes, bool dense, const RjImageDev *imgs, int nimg, RjCoefBuf coefs,
                          const RjTableSet *tabsets, uint8_t *planes, const uint32_t *wide_cnt, const uint2 *wide_list,
                          uint32_t cap);

@@ -13,8 +13,10 @@ import collections
 import csv
 import glob
 import json
+import os
 import re
 import sys
+import time
 
 root, batch = sys.argv[1], int(sys.argv[2])
 out = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json"
@@ -24,7 +26,9 @@ def group(name):
     n = name.split("(")[0].replace("void ", "").replace("rj::", "").strip()
     if n.startswith("k_entropy<false"):
         return "k_entropy"
-    if n.startswith("k_rows"):
+    if n.startswith("k_rows_fix"):
+        return "k_rows_fix"
+    if n.startswith("k_rows<"):
         return "k_rows"
     return re.sub(r"<.*", "", n)
 
@@ -42,7 +46,8 @@ for f in sorted(glob.glob(f"{root}/pass*/*counter_collection.csv")):
 calls = {}
 for (p, c), ids in disp["k_destuff"].items():
     calls[(p, c)] = len(ids)
-res = {"source": root, "batch": batch,
+res = {"source": root, "commit": os.environ.get("RJ_COMMIT", "?"), "date": time.strftime("%Y-%m-%d"),
+       "batch": batch,
        "method": "per decode call: sum over the call's dispatches of 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes)",
        "kernels": {}}
 for k in sorted(tot):
