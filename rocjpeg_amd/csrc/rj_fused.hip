@@ -301,6 +301,50 @@ __device__ __forceinline__ void row_of_block(const RjImageDev *__restrict__ imgs
   }
 }
 
+// Phase C fast path: interleaved RGB of a 3-component image over a whole strip inside the
+// image, 4-byte aligned destination -- no per-quad bounds and no format branches in the loop.
+// Lane = 4 consecutive pixels of one row (12 output bytes, one dwordx3 store); kHs / kVs:
+// chroma halved horizontally / vertically (4:2:0 both, 4:2:2 kHs, 4:4:4 neither).
+template <bool kHs, bool kVs>
+__device__ __forceinline__ void rgb_strip(const uint8_t *ty, const uint8_t *tu, const uint8_t *tv, uint32_t tw0,
+                                          uint32_t tw1, uint32_t tid, uint32_t quads_x, uint32_t rows, uint8_t *dst,
+                                          uint32_t pitch) {
+  const uint32_t qsy = 64 / quads_x, qsx = 64 - qsy * quads_x;
+  uint32_t qy = tid / quads_x, qx = tid - qy * quads_x;
+  while (qy < rows) {
+    const uint32_t x = qx * 4;
+    const uint32_t y4 = *reinterpret_cast<const uint32_t *>(ty + __umul24(qy, tw0) + x);
+    const uint32_t crow = __umul24(kVs ? (qy >> 1) : qy, tw1);
+    float u[4], v[4];
+    if constexpr (kHs) {
+      const uint32_t u2 = *reinterpret_cast<const uint16_t *>(tu + crow + (x >> 1));
+      const uint32_t v2 = *reinterpret_cast<const uint16_t *>(tv + crow + (x >> 1));
+      u[0] = u[1] = u8f(u2, 0) - 128.0f;
+      u[2] = u[3] = u8f(u2, 1) - 128.0f;
+      v[0] = v[1] = u8f(v2, 0) - 128.0f;
+      v[2] = v[3] = u8f(v2, 1) - 128.0f;
+    } else {
+      const uint32_t u4 = *reinterpret_cast<const uint32_t *>(tu + crow + x);
+      const uint32_t v4 = *reinterpret_cast<const uint32_t *>(tv + crow + x);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        u[j] = u8f(u4, j) - 128.0f;
+        v[j] = u8f(v4, j) - 128.0f;
+      }
+    }
+    uint32_t w0, w1, w2;
+    csc4(y4, u, v, w0, w1, w2);
+    const uint32_t off = __umul24(qy, pitch) + __umul24(qx, 12u);  // 32-bit: saddr store form
+    *reinterpret_cast<RJ_GLOBAL uint3 *>(gp(dst) + off) = make_uint3(w0, w1, w2);
+    qx += qsx;
+    qy += qsy;
+    if (qx >= quads_x) {
+      qx -= quads_x;
+      qy++;
+    }
+  }
+}
+
 // The work of one MCU row (one wavefront), looping over the row's strips of S MCUs.
 //   kPlanes = false: fused output (rj_decoder.cpp FusedEligible images)
 //   kPlanes = true : general path, blocks into the MCU-padded component planes (K2b reads them)
@@ -482,7 +526,17 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
   const uint32_t rows = min(mcu_h, H > py0 ? H - py0 : 0u);
 
   // destination offsets are 32-bit (the host only fuses when pitch * height < 2^31, pitch < 2^24)
-  if (fmt >= 1 && fmt <= 4) {
+  if (fmt == 3 && ncomp == 3 && al_y && wmax == strip_w && rows == mcu_h) {
+    const uint8_t *ty = s_buf + toff[0], *tu = s_buf + toff[1], *tv = s_buf + toff[2];
+    uint8_t *d = dst0 + (__umul24(py0, pitch0) + px0 * 3);
+    if (hs1) {
+      if (vs1) rgb_strip<true, true>(ty, tu, tv, tw[0], tw[1], tid, quads_x, rows, d, pitch0);
+      else rgb_strip<true, false>(ty, tu, tv, tw[0], tw[1], tid, quads_x, rows, d, pitch0);
+    } else {
+      if (vs1) rgb_strip<false, true>(ty, tu, tv, tw[0], tw[1], tid, quads_x, rows, d, pitch0);
+      else rgb_strip<false, false>(ty, tu, tv, tw[0], tw[1], tid, quads_x, rows, d, pitch0);
+    }
+  } else if (fmt >= 1 && fmt <= 4) {
     const uint32_t pitch = pitch0;
     const bool a4 = al_y;
     // lane walks quads tid, tid+64, ... of the strip (row-major) with an incremental (x, y)
