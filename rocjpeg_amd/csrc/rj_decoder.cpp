@@ -1298,15 +1298,25 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     uint32_t *ls = lane_seg.data();
     std::vector<uint32_t> &seg_pos = sc_.seg_pos;
     seg_pos.resize(seg_total);
+    rows_from_lanes = ngroups > 1 && aligned;
+    // rows from lanes: K2 row w of class g is lane lane_off[g] + w's interval, listed as
+    // (image, row) in lane order -- K2 then starts each row from its record and the interval's
+    // own piece, with no search over the images (rj_fused.hip row_body)
+    std::vector<uint2> &row_list = sc_.row_list;
+    if (rows_from_lanes) row_list.resize(seg_total);
+    uint2 *rl = rows_from_lanes ? row_list.data() : nullptr;
     uint32_t gs = 0;
-    for (int i = 0; i < n; i++)
+    for (int i = 0; i < n; i++) {
+      uint32_t r = 0;
       for (const RjSegDev &sg : streams[i]->plan().segs) {
         const uint32_t l = pos[bucket(sg.src_len)]++;
         ls[l] = gs;
+        if (rl) rl[l] = uint2{uint32_t(i), r++};
         seg_pos[gs++] = l;
       }
+    }
+    if (rl) std::memcpy(h + off_row_list, rl, uint64_t(seg_total) * sizeof(uint2));
     for (int g = 0; g <= ngroups; g++) lane_off[g] = uint32_t(uint64_t(seg_total) * g / ngroups);
-    rows_from_lanes = ngroups > 1 && aligned;
     if (ngroups > 1) {
       auto class_of = [&](uint32_t l) {  // no division in the per-interval loop
         uint8_t g = 0;
@@ -1346,9 +1356,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
           fpos[g] = frow_off[g];
           gpos[g] = fused_rows + grow_off[g];
         }
-        std::vector<uint2> &row_list = sc_.row_list;
         row_list.resize(uint64_t(fused_rows) + general_rows);
-        uint2 *rl = row_list.data();
+        rl = row_list.data();
         for (int i = 0; i < n; i++) {
           const DecodePlan &p = streams[i]->plan();
           if (p.progressive) continue;
@@ -1448,8 +1457,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       if (profiling_) RJ_HIP(hipEventRecord(k2s_[g], st));
       if (rows_from_lanes) {
         wide(lane_off[g + 1] - lane_off[g], wcnt, wlist, fused_images == 0, false);
-        RJ_HIP(LaunchRowsOfLanes(st, fused_images == 0, d_imgs, n, d_lane_seg + lane_off[g],
-                                 lane_off[g + 1] - lane_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>(), wcnt, wlist));
+        RJ_HIP(LaunchRows(st, fused_images == 0, d_imgs, n, nullptr, d_row_list + lane_off[g],
+                          lane_off[g + 1] - lane_off[g], cbuf, d_tabs, d_planes_.as<uint8_t>(), wcnt, wlist));
       } else {
         wide(frow_off[g + 1] - frow_off[g], wcnt, wlist, false, false);
         RJ_HIP(LaunchRows(st, false, d_imgs, n, d_rows, d_row_list + frow_off[g], frow_off[g + 1] - frow_off[g],

@@ -600,6 +600,9 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
                                                       const RjTableSet *__restrict__ tabsets, RjCoefBuf coefs,
                                                       uint32_t epoch) {
   static_assert(RJ_WG == RJ_K1_WG, "lane layout granule");
+#ifdef RJ_K1_PRIO
+  __builtin_amdgcn_s_setprio(RJ_K1_PRIO);  // experiment: the serial chains win issue over co-resident K2 waves
+#endif
   // lane-interleaved (LRow): 33 ring words per lane (the exact decoder's 32-word ring + mirror;
   // the chunk decoder uses 24) and RJ_STAGE staged entries per lane
   __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_XRING_WORDS + 1][RJ_WG];

@@ -30,6 +30,9 @@
 namespace rj {
 
 #define RJ_BLK_STRIDE 144  // bytes per staged block in LDS (128 + 16 pad)
+#ifndef RJ_K2_OCC
+#define RJ_K2_OCC 4  // K2 waves per SIMD the register budget is set for (128 VGPRs)
+#endif
 
 #ifdef RJ_EXP_STAMPS  // diagnostic build: cycles per K2 phase, summed over waves (rj_decoder.cpp prints)
 __device__ unsigned long long rj_stamp[8];
@@ -411,16 +414,25 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
   EntWin win;
   if constexpr (!kDense) {
     const uint32_t ri = U(im.ri_mcus);
-    nv.seg = U(ri ? (my * mcux) / ri : 0);
-    const RjSegDev sg = gp(im.segs)[nv.seg];
-    const uint32_t rel = (my * mcux - sg.mcu_first) * nblk;
-    const RjPiece *pb = coefs.piece + rj_seg_lane0(coefs, im.seg_prefix + nv.seg);
-    const uint32_t np = U(min(gp(pb)->npieces, 4096u));
-    uint32_t pj = 0;
-    while (pj + 1 < np && U(gp(pb + pj + 1)->first_blk) <= rel) pj++;
-    nv.pj = pj;
-    nv.take(pb + pj);
-    drop = U(rel - gp(pb + pj)->first_blk);
+    if (ri == mcux && coefs.seg_lane0 == nullptr) {
+      // the row is interval `my`, decoded whole by one exact K1 lane: its single piece sits at
+      // the interval's own slot and starts at the row's first block (no segment/piece walk --
+      // every load of the row's start is then one dependent step from the row record)
+      nv.seg = my;
+      nv.pj = 0;
+      nv.take(coefs.piece + U(im.seg_prefix) + my);
+    } else {
+      nv.seg = U(ri ? (my * mcux) / ri : 0);
+      const RjSegDev sg = gp(im.segs)[nv.seg];
+      const uint32_t rel = (my * mcux - sg.mcu_first) * nblk;
+      const RjPiece *pb = coefs.piece + rj_seg_lane0(coefs, im.seg_prefix + nv.seg);
+      const uint32_t np = U(min(gp(pb)->npieces, 4096u));
+      uint32_t pj = 0;
+      while (pj + 1 < np && U(gp(pb + pj + 1)->first_blk) <= rel) pj++;
+      nv.pj = pj;
+      nv.take(pb + pj);
+      drop = U(rel - gp(pb + pj)->first_blk);
+    }
     win.load(ent, nv.cur(), tid);
   }
 
@@ -451,6 +463,9 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
 
     bool wide = false;  // some coefficient of the strip needs the exact 64-bit IDCT
     // ---- A: clear the strip's LDS blocks, expand the entry stream into them ----
+#ifdef RJ_NO_WINPF
+    if (!kDense && sx > 0 && nv.bleft) win.load(ent, nv.cur(), tid);
+#endif
     __syncthreads();  // previous strip's tiles fully read
     for (uint32_t k = tid; k < nb * 8; k += 64)
       *reinterpret_cast<uint4 *>(s_buf + (k >> 3) * RJ_BLK_STRIDE + (k & 7) * 16) = make_uint4(0, 0, 0, 0);
@@ -461,7 +476,9 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
       if (dc_diff) parse_blocks<true>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, thr, wide);
       else parse_blocks<false>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, thr, wide);
       drop = 0;
+#ifndef RJ_NO_WINPF
       if (sx + 1 < strips_x && nv.bleft) win.load(ent, nv.cur(), tid);  // next strip's window: lands behind B and C
+#endif
     }
     __syncthreads();
     if (!kDense && dc_diff) {
@@ -651,7 +668,7 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
 
 // K2: one wavefront (workgroup) per MCU row.
 template <bool kPlanes, bool kDense = false>
-__global__ __launch_bounds__(64, 4) void k_rows(const RjImageDev *__restrict__ imgs, int nimg,
+__global__ __launch_bounds__(64, RJ_K2_OCC) void k_rows(const RjImageDev *__restrict__ imgs, int nimg,
                                              const uint32_t *__restrict__ row_prefix,
                                              const uint2 *__restrict__ row_list,
                                              const uint32_t *__restrict__ row_segs,

@@ -1,0 +1,13 @@
+#!/usr/bin/env bash
+# Build the working tree's library with extra compile flags as rocjpeg_amd/librocjpeg_amd_<name>.so
+# (A/B runs: RJ_LIB_PATH=$PWD/rocjpeg_amd/librocjpeg_amd_<name>.so).  Development aid.
+#   tools/build_flags.sh <name> "<flags>"
+set -e
+ROOT=$(git rev-parse --show-toplevel)
+TMP=$(mktemp -d /tmp/rjflags.XXXXXX)
+cp -r "$ROOT/rocjpeg_amd" "$ROOT/include" "$TMP/"
+rm -f "$TMP"/rocjpeg_amd/csrc/*.o "$TMP"/rocjpeg_amd/*.so
+make -C "$TMP/rocjpeg_amd" -j8 EXTRA="$2" >/dev/null
+cp "$TMP/rocjpeg_amd/librocjpeg_amd.so" "$ROOT/rocjpeg_amd/librocjpeg_amd_$1.so"
+rm -rf "$TMP"
+echo "built rocjpeg_amd/librocjpeg_amd_$1.so ($2)"

@@ -1,13 +1,13 @@
 #!/usr/bin/env bash
 # K1 counter passes (SQ sets of tools/pmc_sets_sq.txt) on a C2 bench with K1 and K2 as single
-# sequential launches (RJ_PIPE_GROUPS=1), lean (default) and old (RJ_LEAN=0) kernels.
+# sequential launches (RJ_PIPE_GROUPS=1), lean (RJ_LEAN=1) and old (default) kernels.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/pmc_k1_${1:-run}
 mkdir -p $OUT
 export RJ_PIPE_GROUPS=1
 for variant in lean old; do
-  if [ $variant = old ]; then export RJ_LEAN=0; else unset RJ_LEAN; fi
+  if [ $variant = old ]; then export RJ_LEAN=0; else export RJ_LEAN=1; fi
   i=0; mkdir -p $OUT/$variant
   while IFS= read -r counters; do
     [ -z "$counters" ] && continue
