@@ -158,6 +158,11 @@ int Decoder::Initialize() {
   for (auto &e : kev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : prog_ev_) RJ_HIP(hipEventCreate(&e));
   for (auto &e : prog_join_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  // development diagnostics, read once (never per call)
+  const char *dbg_names[] = {"RJ_DEBUG_SCAN", "RJ_DEBUG_PROG", "RJ_DEBUG_WAVES", "RJ_DEBUG_HOST",
+                             "RJ_DEBUG_PIPE_SERIAL", "RJ_DEBUG_STAMPS", "RJ_DEBUG_K1", "RJ_DEBUG_K1_PIECES"};
+  for (int k = 0; k < 8; k++)
+    if (getenv(dbg_names[k])) dbg_ |= 1u << k;
   if (const char *pp = getenv("RJ_PROG_PIPE")) prog_pipe_enabled_ = atoi(pp) != 0;
   if (const char *pw = getenv("RJ_PROG_WAVE_ALL")) prog_wave_all_ = atoi(pw) != 0;
   for (auto *arr : {k1s_, k2s_, k2e_})
@@ -365,7 +370,7 @@ int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *dat
   RJ_HIP(hipMemcpyAsync(h + off_out, d + off_out, down_end - off_out, hipMemcpyDeviceToHost, stream_));
   RJ_HIP(hipStreamSynchronize(stream_));
   const auto t2 = std::chrono::steady_clock::now();
-  if (getenv("RJ_DEBUG_SCAN"))
+  if (Dbg(kDebugScan))
     fprintf(stderr, "[rj scan] %zu streams: host headers+staging+alloc %.3f ms, upload+kernel+readback %.3f ms\n",
             size_t(np), std::chrono::duration<double, std::milli>(t1 - t0).count(),
             std::chrono::duration<double, std::milli>(t2 - t1).count());
@@ -1152,7 +1157,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(hipMemsetAsync(d_nz_.as<unsigned long long>(), 0, nz_total * 8, stream_));
     if (prec_total) RJ_HIP(hipMemsetAsync(d_prec_.as<unsigned long long>(), 0, prec_total * 8, stream_));
     const RjFoldJob *d_fold = reinterpret_cast<const RjFoldJob *>(dbase + off_fold);
-    const bool dbg_lev = profiling_ && getenv("RJ_DEBUG_PROG") != nullptr;
+    const bool dbg_lev = profiling_ && Dbg(kDebugProg);
     if (dbg_lev && prog_lev_ev_.size() < nlev + 1) {
       for (size_t q = prog_lev_ev_.size(); q < nlev + 1; q++) {
         hipEvent_t e;
@@ -1210,7 +1215,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         RJ_HIP(hipEventRecord(prog_join_[1], pstream_[0]));
       }
       unsigned long long *wstamps = nullptr;
-      if (getenv("RJ_DEBUG_WAVES")) {
+      if (Dbg(kDebugWaves)) {
         RJ_CHECK(d_wstamp_.Ensure(std::max<uint64_t>(uint64_t(wave_off[nlev] - wave_first_end) * 32, 256)));
         wstamps = d_wstamp_.as<unsigned long long>();
       }
@@ -1386,7 +1391,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
 
   const auto t_end = std::chrono::steady_clock::now();
   timings_.host_ms = std::chrono::duration<float, std::milli>(t_end - t_host0).count();
-  if (getenv("RJ_DEBUG_HOST")) {  // development: where the host planning time goes
+  if (Dbg(kDebugHost)) {  // development: where the host planning time goes
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
       return std::chrono::duration<double, std::milli>(b - a).count();
     };
@@ -1430,7 +1435,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (profiling_) RJ_HIP(hipEventRecord(k2e_[1], stream_));
   } else if (ngroups > 1) {
     RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0 and upload B done
-    if (getenv("RJ_DEBUG_PIPE_SERIAL")) {  // development: each class's K1 alone, one after another
+    if (Dbg(kDebugPipeSerial)) {  // development: each class's K1 alone, one after another
       for (int g = 0; g < ngroups; g++) {
         if (lean)
           RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g],
@@ -1441,7 +1446,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         if (profiling_) RJ_HIP(hipEventRecord(pk1_[g], stream_));
       }
     }
-    for (int g = 0; g < ngroups && !getenv("RJ_DEBUG_PIPE_SERIAL"); g++) {
+    for (int g = 0; g < ngroups && !Dbg(kDebugPipeSerial); g++) {
       hipStream_t st = g == ngroups - 1 ? stream_ : pstream_[g];
       if (st != stream_) RJ_HIP(hipStreamWaitEvent(st, pev_[kMaxPipe - 1], 0));
       if (profiling_) RJ_HIP(hipEventRecord(k1s_[g], st));
@@ -1521,7 +1526,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       RJ_ERR("progressive refinement: a producer did not report progress");
       return kExecutionFailed;
     }
-    if (getenv("RJ_DEBUG_WAVES")) {  // per scan of the batch's first image layout: wave timing
+    if (Dbg(kDebugWaves)) {  // per scan of the batch's first image layout: wave timing
       const uint32_t nw = wave_off[nlev] - wave_first_end;
       std::vector<unsigned long long> st(size_t(nw) * 4);
       RJ_HIP(hipMemcpy(st.data(), d_wstamp_.as<unsigned long long>(), st.size() * 8, hipMemcpyDeviceToHost));
@@ -1557,10 +1562,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
   }
 #ifdef RJ_EXP_STAMPS
-  if (getenv("RJ_DEBUG_STAMPS")) DumpRowStamps();
+  if (Dbg(kDebugStamps)) DumpRowStamps();
 #endif
 #ifdef RJ_HL_STAMPS
-  if (getenv("RJ_DEBUG_STAMPS") && lean) DumpHuffStamps();
+  if (Dbg(kDebugStamps) && lean) DumpHuffStamps();
 #endif
 
   timings_.images = uint32_t(n);
@@ -1611,7 +1616,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         k1 = std::max(k1, t);
       }
       RJ_HIP(hipEventElapsedTime(&k12, ev_[2], ev_[4]));
-      if (getenv("RJ_DEBUG_K1")) {
+      if (Dbg(kDebugK1)) {
         float prev = 0;
         for (int g = 0; g < ngroups; g++) {
           float t = 0;
@@ -1657,7 +1662,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         timings_.prog_kernel_ms[sp.kind] += t;
         timings_.prog_kernel_launches[sp.kind]++;
       }
-      if (getenv("RJ_DEBUG_PROG") && prog_lev_ev_.size() >= nlev + 1) {
+      if (Dbg(kDebugProg) && prog_lev_ev_.size() >= nlev + 1) {
         for (uint32_t L = 0; L < nlev; L++) {
           float t = 0;
           RJ_HIP(hipEventElapsedTime(&t, prog_lev_ev_[L], prog_lev_ev_[L + 1]));
@@ -1673,7 +1678,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     timings_.huffman_ms = ms[2];
     timings_.idct_ms = ms[3];
     timings_.output_ms = ms[4];
-    if (getenv("RJ_DEBUG_K1")) {  // development diagnostics of the chunked decode
+    if (Dbg(kDebugK1)) {  // development diagnostics of the chunked decode
       std::vector<RjChunkRes> cr(lanes_all);
       RJ_HIP(hipMemcpy(cr.data(), d_chunkres_.as<RjChunkRes>(), cr.size() * sizeof(RjChunkRes), hipMemcpyDeviceToHost));
       double sum_ov = 0, sum_it = 0;
@@ -1699,7 +1704,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
               nfail, nsync ? sum_ov / nsync : 0.0, max_ov);
       for (int h = 0; h < 8; h++) fprintf(stderr, " %u", hist[h]);
       fprintf(stderr, " | iters mean %.0f max %u\n", (nsync + ndone) ? sum_it / (nsync + ndone) : 0.0, max_it);
-      if (n == 1 && getenv("RJ_DEBUG_K1_PIECES")) {  // one image: its first interval's pieces and chunks
+      if (n == 1 && Dbg(kDebugK1Pieces)) {  // one image: its first interval's pieces and chunks
         const uint32_t l0 = seg_lane0[0], nch = rj_chunks(streams[0]->plan().segs[0].src_len);
         std::vector<RjPiece> pc(nch);
         RJ_HIP(hipMemcpy(pc.data(), d_piece_.as<RjPiece>() + l0, nch * sizeof(RjPiece), hipMemcpyDeviceToHost));

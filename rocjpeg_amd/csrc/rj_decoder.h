@@ -94,6 +94,12 @@ class Decoder {
   hipEvent_t ev_[8] = {};  // 0..5 stage boundaries, 6..7 inside K1
   // pipelined launch (rj_decoder.cpp): interval length classes 0..pipe_groups_-2 on pstream_,
   // the last class on stream_; pev_ joins them (no timing), pk1_ times each class's K1
+  enum DebugFlag : uint32_t {  // env RJ_DEBUG_* (development diagnostics), bit k = dbg_names[k]
+    kDebugScan = 1u << 0, kDebugProg = 1u << 1, kDebugWaves = 1u << 2, kDebugHost = 1u << 3,
+    kDebugPipeSerial = 1u << 4, kDebugStamps = 1u << 5, kDebugK1 = 1u << 6, kDebugK1Pieces = 1u << 7
+  };
+  uint32_t dbg_ = 0;
+  bool Dbg(uint32_t f) const { return (dbg_ & f) != 0; }
   static constexpr int kMaxPipe = 4;  // = HIP's default hardware queues per process
   static constexpr int kWideSites = 4 + 2 * kMaxPipe;  // K2 launches per call, bound (fix-up counters)
   // 2 by default: the caller's own stream (e.g. torch's) takes a hardware queue too, and two
