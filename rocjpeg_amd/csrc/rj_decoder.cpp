@@ -142,10 +142,15 @@ int Decoder::Initialize() {
   }
   RJ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   for (auto &e : ev_) RJ_HIP(hipEventCreate(&e));
-  if (const char *g = getenv("RJ_PIPE_GROUPS")) pipe_groups_ = std::max(1, std::min(kMaxPipe, atoi(g)));
+  if (const char *g = getenv("RJ_PIPE_GROUPS")) {
+    pipe_groups_ = std::max(1, std::min(kMaxPipe, atoi(g)));
+    pipe_groups_set_ = true;
+  }
   if (const char *m = getenv("RJ_PIPE_MIN")) pipe_min_ = uint32_t(std::max(1, atoi(m)));
   if (const char *o = getenv("RJ_SORT_LANES")) sort_lanes_ = atoi(o) != 0;
   if (const char *l = getenv("RJ_LEAN")) lean_enabled_ = atoi(l) != 0;
+  if (const char *l = getenv("RJ_LPT")) lpt_ = atoi(l) != 0;
+  if (const char *l = getenv("RJ_K1_SOLO")) k1_solo_lds_ = uint32_t(std::max(0, atoi(l)));
   if (const char *sk = getenv("RJ_STREAM_K2")) stream_enabled_ = atoi(sk) != 0;
   if (const char *sw = getenv("RJ_STREAM_WG")) stream_wg_per_cu_ = std::max(1, std::min(16, atoi(sw)));
   cu_count_ = std::max(1, prop.multiProcessorCount);
@@ -160,8 +165,9 @@ int Decoder::Initialize() {
   for (auto &e : prog_join_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // development diagnostics, read once (never per call)
   const char *dbg_names[] = {"RJ_DEBUG_SCAN", "RJ_DEBUG_PROG", "RJ_DEBUG_WAVES", "RJ_DEBUG_HOST",
-                             "RJ_DEBUG_PIPE_SERIAL", "RJ_DEBUG_STAMPS", "RJ_DEBUG_K1", "RJ_DEBUG_K1_PIECES"};
-  for (int k = 0; k < 8; k++)
+                             "RJ_DEBUG_PIPE_SERIAL", "RJ_DEBUG_STAMPS", "RJ_DEBUG_K1", "RJ_DEBUG_K1_PIECES",
+                             "RJ_DEBUG_NODEP"};
+  for (int k = 0; k < 9; k++)
     if (getenv(dbg_names[k])) dbg_ |= 1u << k;
   if (const char *pp = getenv("RJ_PROG_PIPE")) prog_pipe_enabled_ = atoi(pp) != 0;
   if (const char *pw = getenv("RJ_PROG_WAVE_ALL")) prog_wave_all_ = atoi(pw) != 0;
@@ -1002,9 +1008,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // ---- one pinned staging blob, uploaded in two parts: A (descriptors, tables, non-resident
   // bitstreams) before K0; B (K1 lane order, K2 row lists) after K0 is launched -- the lane
   // sort and row classes below are host work that then runs while K0 executes. ----
-  const bool sorted = !any_split && sort_lanes_ && (seg_total >= 256 || seg_total >= pipe_min_);
+  const bool sorted = !any_split && sort_lanes_ && (seg_total >= 256 || seg_total >= pipe_min_ || lean);
   int ngroups = 1;
-  if (sorted && pipe_groups_ > 1 && seg_total >= pipe_min_) ngroups = pipe_groups_;
+  // the lean K1 runs as one launch, longest intervals first (K2 after it): its workgroups then
+  // end close together, and the pipelined split did not overlap K1 with K2 in measurements
+  const int groups_wanted = (lean && !pipe_groups_set_) ? 1 : pipe_groups_;
+  if (sorted && groups_wanted > 1 && seg_total >= pipe_min_) ngroups = groups_wanted;
   const uint64_t off_imgs = 0;
   const uint64_t off_tabs = AlignUp(off_imgs + n * sizeof(RjImageDev), 256);
   const uint64_t off_jobs = AlignUp(off_tabs + tabs.size() * sizeof(RjTableSet), 256);
@@ -1279,7 +1288,11 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   bool rows_from_lanes = false;
   if (sorted) {
     constexpr uint32_t kBuckets = 4096;  // 32-B length buckets up to 128 KB
-    auto bucket = [](uint32_t len) { return std::min<uint32_t>(len >> 5, kBuckets - 1); };
+    const bool desc = lpt_ && ngroups == 1;  // one launch: longest intervals first
+    auto bucket = [desc](uint32_t len) {
+      const uint32_t b = std::min<uint32_t>(len >> 5, kBuckets - 1);
+      return desc ? kBuckets - 1 - b : b;
+    };
     std::vector<uint32_t> &pos = sc_.bucket_pos;
     pos.assign(kBuckets, 0);
     bool aligned = fused_images == uint32_t(n - int(prog_images)) || fused_images == 0;
@@ -1477,8 +1490,16 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
     for (int g = 0; g + 1 < ngroups; g++) RJ_HIP(hipStreamWaitEvent(stream_, pev_[g], 0));
   } else {
-    if (lean) {  // no split interval: one pass, no resolution / serial stages
-      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, seg_total, d_destuff_.as<uint8_t>(), d_tabs, d_lean, cbuf));
+    if (lean && Dbg(kDebugNoDep)) {  // timing experiment: K1 beside K2, no dependency (wrong output)
+      RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));
+      RJ_HIP(hipStreamWaitEvent(pstream_[0], pev_[kMaxPipe - 1], 0));
+      RJ_HIP(LaunchHuffLanes(pstream_[0], d_imgs, n, 0u, seg_total, d_destuff_.as<uint8_t>(), d_tabs, d_lean, cbuf));
+      RJ_HIP(hipEventRecord(pev_[0], pstream_[0]));
+      if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
+      if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
+    } else if (lean) {  // no split interval: one pass, no resolution / serial stages
+      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, seg_total, d_destuff_.as<uint8_t>(), d_tabs, d_lean, cbuf,
+                             nullptr, 0u, nullptr, k1_solo_lds_));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
     } else {
@@ -1495,6 +1516,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(LaunchRows(stream_, true, d_imgs, n, d_grows, nullptr, general_rows, cbuf, d_tabs,
                       d_planes_.as<uint8_t>(), wcnt, wlist));
   }
+  if (lean && ngroups == 1 && Dbg(kDebugNoDep)) RJ_HIP(hipStreamWaitEvent(stream_, pev_[0], 0));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[4], stream_));
   RJ_HIP(LaunchOutputJobs(stream_, d_imgs, d_jobs, int(jobs.size()), rows_total, d_planes_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[5], stream_));
@@ -1619,10 +1641,13 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       if (Dbg(kDebugK1)) {
         float prev = 0;
         for (int g = 0; g < ngroups; g++) {
-          float t = 0;
+          float t = 0, t1s = 0, t2s = 0, t2e = 0;
           RJ_HIP(hipEventElapsedTime(&t, ev_[2], pk1_[g]));
-          fprintf(stderr, "[rj] class %d: %u lanes, max %u B, K1 end %.3f ms (+%.3f)\n", g,
-                  lane_off[g + 1] - lane_off[g], class_max[g], t, t - prev);
+          RJ_HIP(hipEventElapsedTime(&t1s, ev_[2], k1s_[g]));
+          RJ_HIP(hipEventElapsedTime(&t2s, ev_[2], k2s_[g]));
+          RJ_HIP(hipEventElapsedTime(&t2e, ev_[2], k2e_[g]));
+          fprintf(stderr, "[rj] class %d: %u lanes, max %u B, K1 %.3f..%.3f ms (+%.3f), K2 %.3f..%.3f ms\n", g,
+                  lane_off[g + 1] - lane_off[g], class_max[g], t1s, t, t - prev, t2s, t2e);
           prev = t;
         }
       }

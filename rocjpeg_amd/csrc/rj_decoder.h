@@ -96,7 +96,8 @@ class Decoder {
   // the last class on stream_; pev_ joins them (no timing), pk1_ times each class's K1
   enum DebugFlag : uint32_t {  // env RJ_DEBUG_* (development diagnostics), bit k = dbg_names[k]
     kDebugScan = 1u << 0, kDebugProg = 1u << 1, kDebugWaves = 1u << 2, kDebugHost = 1u << 3,
-    kDebugPipeSerial = 1u << 4, kDebugStamps = 1u << 5, kDebugK1 = 1u << 6, kDebugK1Pieces = 1u << 7
+    kDebugPipeSerial = 1u << 4, kDebugStamps = 1u << 5, kDebugK1 = 1u << 6, kDebugK1Pieces = 1u << 7,
+    kDebugNoDep = 1u << 8
   };
   uint32_t dbg_ = 0;
   bool Dbg(uint32_t f) const { return (dbg_ & f) != 0; }
@@ -104,10 +105,16 @@ class Decoder {
   static constexpr int kWideSites = 4 + 2 * kMaxPipe;  // K2 launches per call, bound (fix-up counters)
   // 2 by default: the caller's own stream (e.g. torch's) takes a hardware queue too, and two
   // streams sharing one queue serialise (measured: 4 classes sometimes double the K1 span)
-  int pipe_groups_ = 2;            // env RJ_PIPE_GROUPS (1 = sequential)
+  int pipe_groups_ = 2;            // env RJ_PIPE_GROUPS (1 = sequential); the lean K1 defaults to 1
+  bool pipe_groups_set_ = false;
   uint32_t pipe_min_ = 2048;       // env RJ_PIPE_MIN: fewest intervals worth pipelining
   bool sort_lanes_ = true;         // env RJ_SORT_LANES=0: K1 lanes in interval order
-  bool lean_enabled_ = false;      // env RJ_LEAN=1: the lean K1 (rj_huff.hip), measured slower
+  bool lpt_ = true;                 // env RJ_LPT=0: one K1 launch takes the shortest intervals first
+  // env RJ_K1_SOLO=<bytes>: extra dynamic LDS per lean K1 workgroup, so that one fits per CU: the
+  // workgroups past the first round (LPT order: the shortest) then wait for the CUs that finish
+  // first instead of doubling up on a CU beside a long-interval workgroup
+  uint32_t k1_solo_lds_ = 16384;
+  bool lean_enabled_ = true;       // env RJ_LEAN=0: the exact K1 (rj_entropy.hip) for row images too
   bool stream_enabled_ = false;    // env RJ_STREAM_K2=1: streaming K2 (k_rows_stream), measured no faster
   int cu_count_ = 256;
   int stream_wg_per_cu_ = 2;       // env RJ_STREAM_WG: streaming K2 workgroups per CU (K1's LDS must still fit)

@@ -26,11 +26,14 @@
 
 namespace rj {
 
-#define RJ_HL_WG 256
+#define RJ_HL_DEC 256                       // decoder lanes per workgroup
+#define RJ_HL_WG (2 * RJ_HL_DEC)            // + one mover wave per decoder wave
 #define RJ_HL_CHUNKS 8                      // 16-B chunks in a lane's bit ring
 #define RJ_HL_WORDS (RJ_HL_CHUNKS * 4)      // 32 words
-#define RJ_HL_STAGE 16                      // staged entries per lane
+#ifndef RJ_HL_GROUP
 #define RJ_HL_GROUP 8                       // flushed in 32-B groups: < 8 pending at a phase start
+#endif
+#define RJ_HL_STAGE (2 * RJ_HL_GROUP)       // staged entries per lane
 #define RJ_HL_PHASE 8                       // symbols per phase (<= 8 words: 31 bits per symbol)
 // LDS byte offsets of the four tables (RjLeanTables order)
 #define RJ_HL_AC_BYTES (RJ_HL_AC_WORDS * 4)
@@ -38,6 +41,19 @@ namespace rj {
 #define RJ_HL_LUT_WORDS (2 * RJ_HL_AC_WORDS + 2 * RJ_HL_DC_WORDS)
 
 __device__ const uint4 rj_hl_zero[2] = {};
+
+// timing experiments only (results are wrong): RJ_HL_X_NOSTORE drops the in-loop entry flushes,
+// RJ_HL_X_NOLOAD refills the ring from the lane's first chunks (cache hits)
+#ifdef RJ_HL_X_NOSTORE
+#define RJ_HL_X_FLUSH(x)
+#else
+#define RJ_HL_X_FLUSH(x) x
+#endif
+#ifdef RJ_HL_X_NOLOAD
+#define RJ_HL_X_LOADIDX(p) (src + ((p) - src) % 2)
+#else
+#define RJ_HL_X_LOADIDX(p) (p)
+#endif
 
 #ifdef RJ_HL_STAMPS  // diagnostic build: cycles in the symbol steps / the phase ends, summed over waves
 __device__ unsigned long long rj_hl_stamp[8];
@@ -49,7 +65,7 @@ __device__ unsigned long long rj_hl_stamp[8];
 // word w of the lane's column of a lane-interleaved LDS array ([w][lane]: conflict-free)
 struct HCol {
   uint32_t *base;
-  __device__ __forceinline__ uint32_t &operator[](uint32_t w) const { return base[w * RJ_HL_WG]; }
+  __device__ __forceinline__ uint32_t &operator[](uint32_t w) const { return base[w * RJ_HL_DEC]; }
 };
 
 __device__ __forceinline__ void hl_put(const HCol &ring, uint32_t slot, const uint4 &v) {
@@ -68,8 +84,16 @@ __device__ __forceinline__ void hl_flush(const HCol &stage, uint32_t from, uint3
 #pragma unroll
   for (int q = 0; q < RJ_HL_GROUP; q++) w[q] = stage[s0 + q];
   uint4 *d4 = reinterpret_cast<uint4 *>(dst);
-  gp(d4)[0] = make_uint4(w[0], w[1], w[2], w[3]);
-  gp(d4)[1] = make_uint4(w[4], w[5], w[6], w[7]);
+#pragma unroll
+  for (int q = 0; q < RJ_HL_GROUP / 4; q++) {
+    const uint4 v = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+#ifdef RJ_HL_X_NT
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<RJ_GLOBAL u32x4 *>(gp(d4) + q));
+#else
+    gp(d4)[q] = v;
+#endif
+  }
 }
 
 // Codes the first level does not resolve (rare): AC second level, or libjpeg's canonical
@@ -145,20 +169,39 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
     tsh = bend ? uint32_t(32 - RJ_HL_DC_BITS) : uint32_t(32 - RJ_HL_AC_BITS);                            \
   } while (0)
 
-// Lane `g` of [lane0, lane0 + nlanes): the interval rj_lane_seg(g), decoded whole.
+// LDS lane columns shared by a decoder lane and its mover lane: plain LDS words whose order of
+// execution is the program order of each wave (the LDS pipeline serves a wave's requests in
+// order), read / written as volatile so that the compiler keeps that order too.
+// (explicitly in the LDS address space: a volatile generic pointer becomes a system-coherent
+// flat access, which waits for every outstanding store of the wave)
+typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t *p) { return *(const lds_vu32 *)(p); }
+__device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) { *(lds_vu32 *)(p) = v; }
+#define RJ_HL_FIN 0xFFFFFFFFu  // decoder -> mover: the lane's decode is over
+
+// Workgroup = RJ_HL_DEC decoder lanes (waves 0..3) + one mover wave per decoder wave (4..7).
+// Lane `g` of [lane0, lane0 + nlanes): the interval rj_lane_seg(g), decoded whole by decoder
+// lane g % RJ_HL_DEC; mover lane g % RJ_HL_DEC + RJ_HL_DEC keeps that lane's bit ring filled.
+// The decoder never waits on vector memory: its only VMEM operations are the entry flushes
+// (fire and forget), so no store latency couples into its symbol chain (vmcnt counts loads and
+// stores in one queue -- a decoder that also issued its ring loads waited for its older stores).
 __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0,
                                                       uint32_t nlanes, const uint8_t *__restrict__ destuffed,
                                                       const RjTableSet *__restrict__ tabsets,
                                                       const RjLeanTables *__restrict__ lean, RjCoefBuf coefs,
                                                       uint32_t *flags, uint32_t epoch, uint32_t *done) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_HL_WORDS][RJ_HL_WG];
-  __shared__ __attribute__((aligned(16))) uint32_t s_stage[RJ_HL_STAGE][RJ_HL_WG];
+  __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_HL_WORDS][RJ_HL_DEC];
+  __shared__ __attribute__((aligned(16))) uint32_t s_stage[RJ_HL_STAGE][RJ_HL_DEC];
   __shared__ __attribute__((aligned(16))) uint32_t s_lut[RJ_HL_LUT_WORDS];
+  __shared__ uint32_t s_dec[RJ_HL_DEC];  // decoder -> mover: ring words fully consumed (RJ_HL_FIN: done)
+  __shared__ uint32_t s_mov[RJ_HL_DEC];  // mover -> decoder: 16-B chunks committed to the ring
   __shared__ uint32_t s_T, s_ne;
   const uint32_t tid = threadIdx.x;
-  if (flags != nullptr) __builtin_amdgcn_s_setprio(2);  // the serial chains win issue over streaming K2 waves
+  const bool mover = tid >= RJ_HL_DEC;
+  const uint32_t L = mover ? tid - RJ_HL_DEC : tid;  // the decoder lane (LDS column)
+  if (flags != nullptr && !mover) __builtin_amdgcn_s_setprio(2);  // the serial chains win issue over streaming K2 waves
   if (tid == 0) s_ne = 0;
-  const uint32_t g = lane0 + blockIdx.x * RJ_HL_WG + tid;
+  const uint32_t g = lane0 + blockIdx.x * RJ_HL_DEC + L;
   bool pending = g < lane0 + nlanes;
   uint32_t gseg = 0;
   if (pending) {
@@ -174,6 +217,10 @@ __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restri
     if (tid == 0) s_T = 0xFFFFFFFFu;
     __syncthreads();
     if (pending) atomicMin(&s_T, my_ts);
+    if (!mover) {
+      s_dec[L] = 0;
+      s_mov[L] = 0;
+    }
     __syncthreads();
     const uint32_t T = s_T;
     {
@@ -186,6 +233,46 @@ __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restri
     pending = false;
     const uint32_t seg = gseg - im.seg_prefix;
     const RjSegDev sg = gp(im.segs)[seg];
+    const uint32_t nbytes = sg.dst_len;
+    const uint4 *src = reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off);
+    const uint32_t nchunks = (nbytes + 15) / 16;
+    const HCol ring{&s_ring[0][L]};
+
+    if (mover) {
+      // ---- mover: keep the ring's free chunk slots filled (past the data: zero chunks, the
+      // zero bits libjpeg inserts), up to 4 chunks per round; a round's loads are committed at
+      // the start of the next round, so each round waits for loads issued one round earlier ----
+      uint32_t cm = 0, na = 0;
+      uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, p2 = p0, p3 = p0;
+      for (;;) {
+        const uint32_t rd = lds_ld(&s_dec[L]);
+        if (na > 0) {
+          hl_put(ring, cm & (RJ_HL_CHUNKS - 1), p0);
+          if (na > 1) hl_put(ring, (cm + 1) & (RJ_HL_CHUNKS - 1), p1);
+          if (na > 2) hl_put(ring, (cm + 2) & (RJ_HL_CHUNKS - 1), p2);
+          if (na > 3) hl_put(ring, (cm + 3) & (RJ_HL_CHUNKS - 1), p3);
+          cm += na;
+          lds_st(&s_mov[L], cm);  // after the ring words (same wave, in order)
+          na = 0;
+        }
+        const bool fin = rd == RJ_HL_FIN;
+        // chunk slots below the decoder's oldest live word are free
+        const uint32_t live = fin ? RJ_HL_CHUNKS : cm - (rd >> 2);
+        const uint32_t n = min(RJ_HL_CHUNKS - live, 4u);
+        if (n > 0) {
+          p0 = *gp(cm < nchunks ? src + cm : rj_hl_zero);
+          if (n > 1) p1 = *gp(cm + 1 < nchunks ? src + cm + 1 : rj_hl_zero);
+          if (n > 2) p2 = *gp(cm + 2 < nchunks ? src + cm + 2 : rj_hl_zero);
+          if (n > 3) p3 = *gp(cm + 3 < nchunks ? src + cm + 3 : rj_hl_zero);
+          na = n;
+        }
+        if (__builtin_amdgcn_ballot_w64(!fin) == 0) break;
+        if (__builtin_amdgcn_ballot_w64(n > 0) == 0) __builtin_amdgcn_s_sleep(4);
+      }
+      continue;
+    }
+
+    // ---- decoder ----
     const uint32_t nblk = im.nblk_mcu;
     uint32_t pat = 0;  // per block b: bit 2b its DC table, bit 2b + 1 its AC table
     for (uint32_t bb = 0; bb < nblk; bb++) {
@@ -193,26 +280,28 @@ __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restri
       pat |= ((im.comp_td[cc] & 1u) | ((im.comp_ta[cc] & 1u) << 1)) << (2 * bb);
     }
     const uint32_t nb2 = 2 * nblk;
-    const uint32_t nbytes = sg.dst_len;
     const uint32_t nbits = nbytes * 8u;
     const uint32_t blocks = sg.mcu_count * nblk;
-    const uint4 *src = reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off);
     uint32_t *ent = coefs.ent + im.ent_off + sg.ent_off;
     const uint64_t ent_abs = im.ent_off + sg.ent_off;
     RjPiece *piece = coefs.piece + rj_seg_lane0(coefs, gseg);
     const RjTableSet *tset = tabsets + T;  // canonical search (escape path)
-    const HCol ring{&s_ring[0][tid]}, stage{&s_stage[0][tid]};
-
-    const uint32_t nchunks = (nbytes + 15) / 16;
-    for (uint32_t c = 0; c < RJ_HL_CHUNKS; c++) hl_put(ring, c, *gp(c < nchunks ? src + c : rj_hl_zero));
-    uint32_t cm = RJ_HL_CHUNKS;  // chunks committed (past the data: zero chunks)
+    const HCol stage{&s_stage[0][L]};
+    // a phase reads ring words up to rr + 8 (8 symbols of <= 31 bits, the last one's read-ahead)
+#define RJ_HL_WAIT_RING(upto)                                                                     \
+  {                                                                                               \
+    uint32_t cmv = lds_ld(&s_mov[L]);                                                             \
+    while (__builtin_amdgcn_ballot_w64(4u * cmv < (upto)) != 0) {                                 \
+      __builtin_amdgcn_s_sleep(2);                                                                \
+      cmv = lds_ld(&s_mov[L]);                                                                    \
+    }                                                                                             \
+    asm volatile("" ::: "memory");                                                                \
+  }
+    RJ_HL_WAIT_RING(10u);
     uint32_t q = 0;               // -(bits consumed)
-    uint32_t wa = ring[0], wb = ring[1], wc = ring[2];
     // q = 0 is bit 0: alignbit(wa, wb, 0) would return wb, so the window starts one word back
     // (words -1, 0; j = (pos - 1) >> 5): wa is a dummy word whose bits are never returned
-    wc = wb;
-    wb = wa;
-    wa = 0;
+    uint32_t wa = 0, wb = ring[0], wc = ring[1];
     uint32_t rr = 1;  // ring index of wc
     uint32_t ne = 0, fl = 0;
     bool skip = (sg.flags & RJ_SEG_MISSING) != 0;
@@ -221,11 +310,6 @@ __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restri
     uint32_t acb = ((pat >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES);
     uint32_t tb = RJ_HL_DC0 + ((pat & 1u) << (RJ_HL_DC_BITS + 2));
     uint32_t tsh = 32 - RJ_HL_DC_BITS;
-    // Ring refills travel two phases ahead (HBM / MALL latency under this scattered pattern is
-    // longer than a phase): the loop body is two phases, each with its own in-flight register set
-    // (a register copy of a pending load would wait for it at once).
-    uint32_t na = 0, nb = 0;  // chunks in flight in set a / set b
-    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0, b0 = a0, b1 = a0;
 #ifdef RJ_HL_STAMPS
     uint64_t st_steps = 0, st_end = 0, st_fast = 0, st_safe = 0, st_esc = 0;
 #define RJ_HL_T0 const uint64_t t0 = __builtin_amdgcn_s_memtime()
@@ -240,42 +324,31 @@ __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restri
 #define RJ_HL_T1(fast)
 #define RJ_HL_T2
 #endif
-    // one phase: RJ_HL_PHASE steps, then (wave-uniform) the set issued two phases ago lands in
-    // the ring, this set is re-issued behind the other set's chunks, a full stage group leaves
-#define RJ_HL_ONE_PHASE(P0, P1, NP, NOTHER)                                                              \
-  {                                                                                                   \
-    RJ_HL_T0;                                                                                         \
-    /* no lane can finish its blocks or reach its data's end in this phase: the lean body */          \
-    const bool fast = __builtin_amdgcn_ballot_w64(                                                    \
-                          !(blocks_left >= RJ_HL_PHASE && !skip && (0u - q) + RJ_HL_PHASE * 31u < nbits)) == 0; \
-    if (fast) {                                                                                       \
-      _Pragma("unroll") for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(false);             \
-    } else {                                                                                          \
-      _Pragma("unroll") for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(true);              \
-    }                                                                                                 \
-    RJ_HL_T1(fast);                                                                                   \
-    if (NP > 0) hl_put(ring, cm & (RJ_HL_CHUNKS - 1), P0);                                            \
-    if (NP > 1) hl_put(ring, (cm + 1) & (RJ_HL_CHUNKS - 1), P1);                                      \
-    cm += NP;                                                                                         \
-    wc = ring[rr & (RJ_HL_WORDS - 1)]; /* may predate the commit */                                   \
-    /* rr - 2 = the word in wa; chunks wholly below it are free (the first step of an interval     \
-       always advances, so rr >= 2 here); the other set's chunks are live */                          \
-    const uint32_t live = cm + NOTHER - ((rr - 2) >> 2);                                              \
-    NP = min(RJ_HL_CHUNKS - live, 2u);                                                                \
-    const uint32_t ci = cm + NOTHER;                                                                  \
-    P0 = *gp(ci < nchunks ? src + ci : rj_hl_zero);                                                   \
-    P1 = *gp(ci + 1 < nchunks ? src + ci + 1 : rj_hl_zero + 1);                                       \
-    if (ne - fl >= RJ_HL_GROUP) { /* < 16 pending: one group leaves, < 8 stay */                      \
-      hl_flush(stage, fl, ent + fl);                                                                  \
-      fl += RJ_HL_GROUP;                                                                              \
-    }                                                                                                 \
-    RJ_HL_T2;                                                                                         \
-  }
     while (__builtin_amdgcn_ballot_w64(blocks_left > 0) != 0) {
-      RJ_HL_ONE_PHASE(a0, a1, na, nb);
-      if (__builtin_amdgcn_ballot_w64(blocks_left > 0) == 0) break;
-      RJ_HL_ONE_PHASE(b0, b1, nb, na);
+      RJ_HL_T0;
+      // no lane can finish its blocks or reach its data's end in this phase: the lean body
+      const bool fast = __builtin_amdgcn_ballot_w64(
+                            !(blocks_left >= RJ_HL_PHASE && !skip && (0u - q) + RJ_HL_PHASE * 31u < nbits)) == 0;
+      if (fast) {
+#pragma unroll
+        for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(false);
+      } else {
+#pragma unroll
+        for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(true);
+      }
+      RJ_HL_T1(fast);
+      // ---- phase end: words below rr - 2 (the one in wa) are free for the mover; a full stage
+      // group leaves (< 8 stay pending); wait until the next phase's words are in the ring ----
+      lds_st(&s_dec[L], rr - 2u);
+      if (ne - fl >= RJ_HL_GROUP) {
+        RJ_HL_X_FLUSH(hl_flush(stage, fl, ent + fl));
+        fl += RJ_HL_GROUP;
+      }
+      RJ_HL_WAIT_RING(rr + 9u);
+      wc = ring[rr & (RJ_HL_WORDS - 1)];  // the last step's read-ahead may predate the commit
+      RJ_HL_T2;
     }
+    lds_st(&s_dec[L], RJ_HL_FIN);
 #ifdef RJ_HL_STAMPS
     if ((tid & 63) == 0) {
       atomicAdd(&rj_hl_stamp[0], (unsigned long long)st_steps);
@@ -301,8 +374,8 @@ __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restri
     }
   }
   if (tid == 0 && coefs.count != nullptr && s_ne != 0) atomicAdd(coefs.count, (unsigned long long)s_ne);
-  // streaming K2 stops taking rows once every K1 wave is here (its intervals were published above)
-  if (done != nullptr && (tid & 63) == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // streaming K2 stops taking rows once every K1 decoder wave is here (its intervals were published above)
+  if (done != nullptr && !mover && (tid & 63) == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 #ifdef RJ_HL_STAMPS
@@ -320,10 +393,10 @@ void DumpHuffStamps() {
 
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
-                           RjCoefBuf coefs, uint32_t *flags, uint32_t epoch, uint32_t *done) {
+                           RjCoefBuf coefs, uint32_t *flags, uint32_t epoch, uint32_t *done, uint32_t extra_lds) {
   if (nlanes == 0) return hipSuccess;
-  static_assert(RJ_HL_WG == 256, "HuffLaneWaves");
-  hipLaunchKernelGGL(k_huff, dim3((nlanes + RJ_HL_WG - 1) / RJ_HL_WG), dim3(RJ_HL_WG), 0, st, imgs, nimg, lane0, nlanes,
+  static_assert(RJ_HL_DEC == 256, "HuffLaneWaves");
+  hipLaunchKernelGGL(k_huff, dim3((nlanes + RJ_HL_DEC - 1) / RJ_HL_DEC), dim3(RJ_HL_WG), extra_lds, st, imgs, nimg, lane0, nlanes,
                      destuffed, tabsets, lean, coefs, flags, epoch, done);
   return hipGetLastError();
 }

@@ -29,7 +29,8 @@ hipError_t LaunchEntropyLanes(hipStream_t st, const RjImageDev *imgs, int nimg, 
 // done != null: every wave adds 1 to *done when it has published its lanes' intervals.
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
-                           RjCoefBuf coefs, uint32_t *flags = nullptr, uint32_t epoch = 0, uint32_t *done = nullptr);
+                           RjCoefBuf coefs, uint32_t *flags = nullptr, uint32_t epoch = 0, uint32_t *done = nullptr,
+                           uint32_t extra_lds = 0);
 // waves of a LaunchHuffLanes grid over n lanes
 inline uint32_t HuffLaneWaves(uint32_t nlanes) { return (nlanes + 255) / 256 * 4; }
 

@@ -1,6 +1,6 @@
 """Batch-level behaviour on the GPU:
-  * a full C2-size call (1024 x 1080p 4:2:0, DRI one MCU row) under the default pipelined
-    layout, every image compared with the oracle on the device;
+  * a full C2-size call (1024 x 1080p 4:2:0, DRI one MCU row) under the default layout (lean
+    K1, longest intervals first), every image compared with the oracle on the device;
   * rocJpegAmdStreamParseDevice with a corrupt header in the batch: no stream is
     left half-parsed, the good streams decode exactly;
   * destinations that are not on the handle's device (pinned and pageable host memory) are
@@ -57,7 +57,8 @@ def test_c2_1024_default_pipelined_layout(dec):
     dec.set_profiling(False)
     assert st == 0, R.error_name(st)
     assert tm["images"] == 1024 and tm["intervals"] == 1024 * 68
-    assert tm["pipe_groups"] == 2 and tm["split_intervals"] == 0  # the layout the bench runs
+    # the layout the bench runs: lean K1, one launch, longest intervals first
+    assert tm["lean_k1"] == 1 and tm["pipe_groups"] == 1 and tm["split_intervals"] == 0
     ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
     bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
     assert not bad, f"{len(bad)} images differ, first {bad[:8]}"

@@ -209,15 +209,18 @@ def test_long_interval_batch_mixed(dec):
 
 
 @pytest.fixture(scope="module",
-                params=[(0, 4, {}), (1, 4, {}), (0, 1, {}), (0, 4, {"RJ_LEAN": "1"}), (0, 1, {"RJ_LEAN": "1"}),
-                        (0, 2, {"RJ_LEAN": "1", "RJ_STREAM_K2": "1"})],
-                ids=["auto_g4", "general_g4", "auto_g1", "lean_g4", "lean_g1", "lean_stream_g2"])
+                params=[(0, 4, {"RJ_LEAN": "0"}), (1, 4, {"RJ_LEAN": "0"}), (0, 1, {"RJ_LEAN": "0"}), (0, 4, {}),
+                        (0, 1, {}), (1, 1, {}), (0, 1, {"RJ_LPT": "0", "RJ_K1_SOLO": "0"}),
+                        (0, 2, {"RJ_STREAM_K2": "1"})],
+                ids=["exact_g4", "exact_general_g4", "exact_g1", "lean_g4", "lean_g1", "lean_general_g1",
+                     "lean_g1_short_first", "lean_stream_g2"])
 def pdec(request):
     """A decoder that sorts the K1 lanes of every call with no split interval by length
     (RJ_PIPE_MIN=1) and, with 4 groups, pipelines it: interval length classes on separate
     streams, each class's K2 rows after the K1 lanes of its class and all earlier ones.  The
-    lean K1 (RJ_LEAN=1, row-interval batches only) and the streaming K2 (RJ_STREAM_K2=1) are
-    opt-in variants, covered here."""
+    lean K1 (the default for row-interval batches: one launch, longest intervals first, one
+    workgroup per CU; RJ_LEAN=0 takes the exact K1) and the streaming K2 (RJ_STREAM_K2=1) are
+    covered here."""
     import os
     from tests import gpu_util as G
     G.torch()
@@ -297,7 +300,7 @@ def test_pipelined_row_aligned_batch(pdec, fmt):
     assert t["pipe_groups"] == pdec.groups
     if pdec.groups > 1:
         assert t["pipe_lane_rows"] == 1
-    assert t["lean_k1"] == (1 if pdec.extra.get("RJ_LEAN") else 0)
+    assert t["lean_k1"] == (0 if pdec.extra.get("RJ_LEAN") == "0" else 1)
     assert t["k2_stream"] == (1 if pdec.extra.get("RJ_STREAM_K2") else 0)
     for k, (d, shapes, bufs) in enumerate(zip(datas, shapes_all, bufs_all)):
         ost, want = O.oracle_decode(d, int(fmt), shapes)
