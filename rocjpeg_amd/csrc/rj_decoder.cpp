@@ -166,8 +166,8 @@ int Decoder::Initialize() {
   // development diagnostics, read once (never per call)
   const char *dbg_names[] = {"RJ_DEBUG_SCAN", "RJ_DEBUG_PROG", "RJ_DEBUG_WAVES", "RJ_DEBUG_HOST",
                              "RJ_DEBUG_PIPE_SERIAL", "RJ_DEBUG_STAMPS", "RJ_DEBUG_K1", "RJ_DEBUG_K1_PIECES",
-                             "RJ_DEBUG_NODEP"};
-  for (int k = 0; k < 9; k++)
+                             "RJ_DEBUG_NODEP", "RJ_TEST_PROG_GIVEUP"};
+  for (int k = 0; k < 10; k++)
     if (getenv(dbg_names[k])) dbg_ |= 1u << k;
   if (const char *pp = getenv("RJ_PROG_PIPE")) prog_pipe_enabled_ = atoi(pp) != 0;
   if (const char *pw = getenv("RJ_PROG_WAVE_ALL")) prog_wave_all_ = atoi(pw) != 0;
@@ -1232,7 +1232,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       RJ_HIP(LaunchProgressiveWave(stream_, d_imgs, n, d_plane + wave_first_end, wave_off[nlev] - wave_first_end,
                                    d_destuff_.as<uint8_t>(), d_coef_.as<uint32_t>(), d_nz_.as<unsigned long long>(),
                                    d_prec_.as<unsigned long long>(), d_pprog_.as<uint32_t>(), pival_total, wstamps,
-                                   prog_wave_all ? 0u : RJ_WAVE_FIRST_DONE));
+                                   (prog_wave_all ? 0u : RJ_WAVE_FIRST_DONE) |
+                                       (Dbg(kTestProgGiveUp) ? RJ_WAVE_TEST_GIVEUP : 0u)));
       RJ_HIP(pk_end(stream_, 1, wave_off[nlev] - wave_first_end));
       if (side) RJ_HIP(hipStreamWaitEvent(stream_, prog_join_[1], 0));
       RJ_HIP(pk_begin(stream_));
@@ -1286,9 +1287,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   uint32_t lane_off[kMaxPipe + 1] = {}, frow_off[kMaxPipe + 1] = {}, grow_off[kMaxPipe + 1] = {};
   uint32_t class_max[kMaxPipe] = {};  // longest interval (bytes) of each class
   bool rows_from_lanes = false;
+  bool lane_rows = false;  // every interval is one MCU row and every row takes the same K2 path
+  bool lanes_desc = false;  // lane order: longest interval first
   if (sorted) {
     constexpr uint32_t kBuckets = 4096;  // 32-B length buckets up to 128 KB
     const bool desc = lpt_ && ngroups == 1;  // one launch: longest intervals first
+    lanes_desc = desc;
     auto bucket = [desc](uint32_t len) {
       const uint32_t b = std::min<uint32_t>(len >> 5, kBuckets - 1);
       return desc ? kBuckets - 1 - b : b;
@@ -1316,6 +1320,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     uint32_t *ls = lane_seg.data();
     std::vector<uint32_t> &seg_pos = sc_.seg_pos;
     seg_pos.resize(seg_total);
+    lane_rows = aligned;
     rows_from_lanes = ngroups > 1 && aligned;
     // rows from lanes: K2 row w of class g is lane lane_off[g] + w's interval, listed as
     // (image, row) in lane order -- K2 then starts each row from its record and the interval's
@@ -1416,7 +1421,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // fused, lean K1 -- one K1 launch over all lanes publishes each interval when its entries are
   // out, persistent K2 workgroups on a second stream start each row as soon as its interval is
   // published, and a cleanup pass after K1 takes the rows a bounded wait deferred ----
-  const bool stream_k2 = stream_enabled_ && lean && ngroups > 1 && rows_from_lanes && fused_images > 0 &&
+  const bool stream_k2 = stream_enabled_ && lean && lane_rows && fused_images > 0 &&
                          fused_images == uint32_t(n) - prog_images;
   timings_.k2_stream = stream_k2 ? 1u : 0u;
   if (stream_k2) {
@@ -1431,20 +1436,20 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(hipStreamWaitEvent(pstream_[0], pev_[kMaxPipe - 1], 0));
     if (profiling_) RJ_HIP(hipEventRecord(k1s_[0], stream_));
     RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, seg_total, d_destuff_.as<uint8_t>(), d_tabs, d_lean, cbuf,
-                           d_flags_.as<uint32_t>(), epoch_, ctl + 3));
+                           d_flags_.as<uint32_t>(), epoch_, ctl + 3, k1_solo_lds_));
     if (profiling_) RJ_HIP(hipEventRecord(pk1_[0], stream_));
     if (profiling_) RJ_HIP(hipEventRecord(k2s_[0], pstream_[0]));
     const uint32_t grid = std::min<uint32_t>(seg_total, uint32_t(stream_wg_per_cu_) * uint32_t(cu_count_));
     wide(seg_total, wcnt, wlist, false, false);
     RJ_HIP(LaunchRowsStream(pstream_[0], true, d_imgs, n, d_lane_seg, seg_total, d_flags_.as<uint32_t>(), epoch_, ctl,
-                            ctl + 4, HuffLaneWaves(seg_total), grid, cbuf, d_tabs, wcnt, wlist));
+                            ctl + 4, HuffLaneWaves(seg_total), grid, cbuf, d_tabs, wcnt, wlist, lanes_desc ? 1u : 0u));
     if (profiling_) RJ_HIP(hipEventRecord(k2e_[0], pstream_[0]));
     RJ_HIP(hipEventRecord(pev_[0], pstream_[0]));
     RJ_HIP(hipStreamWaitEvent(stream_, pev_[0], 0));
     if (profiling_) RJ_HIP(hipEventRecord(k2s_[1], stream_));
     RJ_HIP(LaunchRowsStream(stream_, false, d_imgs, n, d_lane_seg, seg_total, d_flags_.as<uint32_t>(), epoch_, ctl,
                             ctl + 4, HuffLaneWaves(seg_total), std::min<uint32_t>(seg_total, 16u * uint32_t(cu_count_)),
-                            cbuf, d_tabs, wcnt, wlist));
+                            cbuf, d_tabs, wcnt, wlist, lanes_desc ? 1u : 0u));
     if (profiling_) RJ_HIP(hipEventRecord(k2e_[1], stream_));
   } else if (ngroups > 1) {
     RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0 and upload B done

@@ -97,7 +97,7 @@ class Decoder {
   enum DebugFlag : uint32_t {  // env RJ_DEBUG_* (development diagnostics), bit k = dbg_names[k]
     kDebugScan = 1u << 0, kDebugProg = 1u << 1, kDebugWaves = 1u << 2, kDebugHost = 1u << 3,
     kDebugPipeSerial = 1u << 4, kDebugStamps = 1u << 5, kDebugK1 = 1u << 6, kDebugK1Pieces = 1u << 7,
-    kDebugNoDep = 1u << 8
+    kDebugNoDep = 1u << 8, kTestProgGiveUp = 1u << 9
   };
   uint32_t dbg_ = 0;
   bool Dbg(uint32_t f) const { return (dbg_ & f) != 0; }

@@ -262,6 +262,7 @@ struct RjProgScanDev {
 };
 #define RJ_PROG_DONE 0xFFFFFFFFu  // interval progress: finished
 #define RJ_WAVE_FIRST_DONE 1u      // k_prog_wave flag: first scans decoded before the grid (no waits on them)
+#define RJ_WAVE_TEST_GIVEUP 2u     // k_prog_wave flag (tests): every producer wait gives up after a few polls
 #define RJ_FOLD_ALL 0xFFFFFFFFu   // k_prog_fold level: every level (after a pipelined launch)
 // AC refinement record of one unit (block): 32 B, written once by the decoding lane
 struct RjRefineRec {

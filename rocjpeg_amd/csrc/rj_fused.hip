@@ -79,7 +79,9 @@ __device__ __forceinline__ void store_bytes(uint8_t *d, uint32_t n, const uint32
 // Entry-stream window of one wave: w[r] = ent[base + r * 64 + lane] (coalesced rows).  The
 // loads of the next strip's window are issued as soon as its start is known (end of phase A)
 // and complete behind the IDCT and output phases.
+#ifndef RJ_WIN_ROWS
 #define RJ_WIN_ROWS 8
+#endif
 struct EntWin {
   uint32_t w[RJ_WIN_ROWS];
   uint32_t base_lo, base_hi;
@@ -293,7 +295,15 @@ __device__ __forceinline__ void row_of_block(const RjImageDev *__restrict__ imgs
     i = __builtin_amdgcn_readfirstlane(upper_index(nimg, gseg, [&](int q) { return imgs[q].seg_prefix; }));
     my = U(gp(imgs[i].segs)[gseg - imgs[i].seg_prefix].mcu_first / imgs[i].mcux);
   } else {
+    // interpolation guess (exact for a batch of equal image heights: two independent loads),
+    // then a binary search on the side it missed
+    const uint32_t nrows = gridDim.x;
+    int g = int(min(uint64_t(w) * uint64_t(nimg) / max(nrows, 1u), uint64_t(nimg - 1)));
+    const uint32_t pg = row_prefix[g], pg1 = g + 1 < nimg ? row_prefix[g + 1] : 0xFFFFFFFFu;
     int lo = 0, hi = nimg - 1;
+    if (pg <= w && w < pg1) lo = hi = g;
+    else if (pg > w) hi = g - 1;
+    else lo = g + 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
       if (row_prefix[mid] <= w) lo = mid;
@@ -302,6 +312,27 @@ __device__ __forceinline__ void row_of_block(const RjImageDev *__restrict__ imgs
     i = __builtin_amdgcn_readfirstlane(lo);  // wave-uniform: image fields become scalar loads
     my = w - row_prefix[i];
   }
+}
+
+// 4 pixels -> 12 bytes RGB with packed fp32 (v_pk_fma_f32: two fmas per instruction, each
+// rounded exactly as v_fma_f32), pixels (0,1) and (2,3) in the two halves.  Same arithmetic and
+// packing order as csc4.  u01 / v01: chroma (as float minus 128) of pixels 0..1 / 2..3 when
+// they share it (kHs), else the per-pixel values are passed in pairs.
+typedef float rj_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void csc4_pk(uint32_t y4, rj_f2 ua, rj_f2 ub, rj_f2 va, rj_f2 vb, uint32_t &d0,
+                                        uint32_t &d1, uint32_t &d2) {
+  const rj_f2 ya = {u8f(y4, 0), u8f(y4, 1)}, yb = {u8f(y4, 2), u8f(y4, 3)};
+  const rj_f2 kr = {1.5748f, 1.5748f}, kgu = {-0.1873f, -0.1873f}, kgv = {-0.4681f, -0.4681f}, kb = {1.8556f, 1.8556f};
+  const rj_f2 ra = __builtin_elementwise_fma(kr, va, ya), rb = __builtin_elementwise_fma(kr, vb, yb);
+  const rj_f2 ga = __builtin_elementwise_fma(kgv, va, __builtin_elementwise_fma(kgu, ua, ya));
+  const rj_f2 gb = __builtin_elementwise_fma(kgv, vb, __builtin_elementwise_fma(kgu, ub, yb));
+  const rj_f2 ba = __builtin_elementwise_fma(kb, ua, ya), bb = __builtin_elementwise_fma(kb, ub, yb);
+  d0 = __builtin_amdgcn_cvt_pk_u8_f32(ra.y, 3, __builtin_amdgcn_cvt_pk_u8_f32(ba.x, 2,
+       __builtin_amdgcn_cvt_pk_u8_f32(ga.x, 1, __builtin_amdgcn_cvt_pk_u8_f32(ra.x, 0, 0u))));
+  d1 = __builtin_amdgcn_cvt_pk_u8_f32(gb.x, 3, __builtin_amdgcn_cvt_pk_u8_f32(rb.x, 2,
+       __builtin_amdgcn_cvt_pk_u8_f32(ba.y, 1, __builtin_amdgcn_cvt_pk_u8_f32(ga.y, 0, 0u))));
+  d2 = __builtin_amdgcn_cvt_pk_u8_f32(bb.y, 3, __builtin_amdgcn_cvt_pk_u8_f32(gb.y, 2,
+       __builtin_amdgcn_cvt_pk_u8_f32(rb.y, 1, __builtin_amdgcn_cvt_pk_u8_f32(bb.x, 0, 0u))));
 }
 
 // Phase C fast path: interleaved RGB of a 3-component image over a whole strip inside the
@@ -318,25 +349,26 @@ __device__ __forceinline__ void rgb_strip(const uint8_t *ty, const uint8_t *tu, 
     const uint32_t x = qx * 4;
     const uint32_t y4 = *reinterpret_cast<const uint32_t *>(ty + __umul24(qy, tw0) + x);
     const uint32_t crow = __umul24(kVs ? (qy >> 1) : qy, tw1);
-    float u[4], v[4];
+    const rj_f2 m128 = {128.0f, 128.0f};
+    rj_f2 ua, ub, va, vb;
     if constexpr (kHs) {
       const uint32_t u2 = *reinterpret_cast<const uint16_t *>(tu + crow + (x >> 1));
       const uint32_t v2 = *reinterpret_cast<const uint16_t *>(tv + crow + (x >> 1));
-      u[0] = u[1] = u8f(u2, 0) - 128.0f;
-      u[2] = u[3] = u8f(u2, 1) - 128.0f;
-      v[0] = v[1] = u8f(v2, 0) - 128.0f;
-      v[2] = v[3] = u8f(v2, 1) - 128.0f;
+      const rj_f2 uu = rj_f2{u8f(u2, 0), u8f(u2, 1)} - m128, vv = rj_f2{u8f(v2, 0), u8f(v2, 1)} - m128;
+      ua = rj_f2{uu.x, uu.x};
+      ub = rj_f2{uu.y, uu.y};
+      va = rj_f2{vv.x, vv.x};
+      vb = rj_f2{vv.y, vv.y};
     } else {
       const uint32_t u4 = *reinterpret_cast<const uint32_t *>(tu + crow + x);
       const uint32_t v4 = *reinterpret_cast<const uint32_t *>(tv + crow + x);
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        u[j] = u8f(u4, j) - 128.0f;
-        v[j] = u8f(v4, j) - 128.0f;
-      }
+      ua = rj_f2{u8f(u4, 0), u8f(u4, 1)} - m128;
+      ub = rj_f2{u8f(u4, 2), u8f(u4, 3)} - m128;
+      va = rj_f2{u8f(v4, 0), u8f(v4, 1)} - m128;
+      vb = rj_f2{u8f(v4, 2), u8f(v4, 3)} - m128;
     }
     uint32_t w0, w1, w2;
-    csc4(y4, u, v, w0, w1, w2);
+    csc4_pk(y4, ua, ub, va, vb, w0, w1, w2);
     const uint32_t off = __umul24(qy, pitch) + __umul24(qx, 12u);  // 32-bit: saddr store form
     *reinterpret_cast<RJ_GLOBAL uint3 *>(gp(dst) + off) = make_uint3(w0, w1, w2);
     qx += qsx;
@@ -718,7 +750,8 @@ __global__ __launch_bounds__(64, 4) void k_rows_stream(const RjImageDev *__restr
                                                     const uint32_t *__restrict__ row_segs, uint32_t nrows,
                                                     const uint32_t *flags, uint32_t epoch, uint32_t *ctl,
                                                     uint32_t *deferred, uint32_t k1_waves, RjCoefBuf coefs,
-                                                    const RjTableSet *__restrict__ tabsets, uint32_t *wide_cnt, uint2 *wide_list) {
+                                                    const RjTableSet *__restrict__ tabsets, uint32_t *wide_cnt, uint2 *wide_list,
+                                                    uint32_t reverse) {
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];
   __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
   __shared__ uint32_t s_row;
@@ -746,8 +779,10 @@ __global__ __launch_bounds__(64, 4) void k_rows_stream(const RjImageDev *__restr
       else if (w - (nrows - start) < ndef) row = U(deferred[w - (nrows - start)]);
       else break;
     }
+    // rows in the order K1 finishes them: reverse lane order when K1 took the longest first
+    const uint32_t phys = reverse ? nrows - 1 - row : row;
     if (kWait) {
-      const uint32_t gseg = U(row_segs[row]);
+      const uint32_t gseg = U(row_segs[phys]);
       bool ready = false;
       for (uint32_t k = 0; k < (1u << 14); k++) {  // ~2^14 x ~1 us: far beyond any K1 span
         if (U(__hip_atomic_load(flags + gseg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == epoch) {
@@ -766,7 +801,7 @@ __global__ __launch_bounds__(64, 4) void k_rows_stream(const RjImageDev *__restr
     }
     int i;
     uint32_t my;
-    row_of_block(imgs, nimg, nullptr, nullptr, row_segs, row, i, my);
+    row_of_block(imgs, nimg, nullptr, nullptr, row_segs, phys, i, my);
     row_body<false, false>(imgs, i, my, coefs, tabsets, nullptr, s_buf, s_q, wide_cnt, wide_list);
   }
 }
@@ -774,14 +809,14 @@ __global__ __launch_bounds__(64, 4) void k_rows_stream(const RjImageDev *__restr
 hipError_t LaunchRowsStream(hipStream_t st, bool wait, const RjImageDev *imgs, int nimg, const uint32_t *row_segs,
                             uint32_t nrows, const uint32_t *flags, uint32_t epoch, uint32_t *ctl, uint32_t *deferred,
                             uint32_t k1_waves, uint32_t grid, RjCoefBuf coefs, const RjTableSet *tabsets,
-                            uint32_t *wide_cnt, uint2 *wide_list) {
+                            uint32_t *wide_cnt, uint2 *wide_list, uint32_t reverse) {
   if (nrows == 0) return hipSuccess;
   if (wait)
     hipLaunchKernelGGL(k_rows_stream<true>, dim3(grid), dim3(64), 0, st, imgs, nimg, row_segs, nrows, flags, epoch, ctl,
-                       deferred, k1_waves, coefs, tabsets, wide_cnt, wide_list);
+                       deferred, k1_waves, coefs, tabsets, wide_cnt, wide_list, reverse);
   else
     hipLaunchKernelGGL(k_rows_stream<false>, dim3(grid), dim3(64), 0, st, imgs, nimg, row_segs, nrows, flags, epoch,
-                       ctl, deferred, k1_waves, coefs, tabsets, wide_cnt, wide_list);
+                       ctl, deferred, k1_waves, coefs, tabsets, wide_cnt, wide_list, reverse);
   return hipGetLastError();
 }
 

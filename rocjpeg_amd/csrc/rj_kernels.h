@@ -61,7 +61,7 @@ hipError_t LaunchRowsOfLanes(hipStream_t st, bool to_planes, const RjImageDev *i
 hipError_t LaunchRowsStream(hipStream_t st, bool wait, const RjImageDev *imgs, int nimg, const uint32_t *row_segs,
                             uint32_t nrows, const uint32_t *flags, uint32_t epoch, uint32_t *ctl, uint32_t *deferred,
                             uint32_t k1_waves, uint32_t grid, RjCoefBuf coefs, const RjTableSet *tabsets,
-                            uint32_t *wide_cnt, uint2 *wide_list);
+                            uint32_t *wide_cnt, uint2 *wide_list, uint32_t reverse = 0);
 // The fix-up launch of one K2 launch's list (same variant; cap = that launch's rows).
 hipError_t LaunchRowsFix(hipStream_t st, bool to_planes, bool dense, const RjImageDev *imgs, int nimg, RjCoefBuf coefs,
                          const RjTableSet *tabsets, uint8_t *planes, const uint32_t *wide_cnt, const uint2 *wide_list,

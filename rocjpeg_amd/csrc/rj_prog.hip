@@ -713,7 +713,10 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
       uint32_t &sn = q == 0 ? seen_n0 : (q == 1 ? seen_n1 : seen_n2);
       for (uint32_t j = j0; j <= j1; j++) {
         const uint32_t s0 = pri ? j * pri : 0u;
-        const uint32_t need = hi - s0;  // units of producer interval j (capped by its DONE)
+        // units of producer interval j (capped by its DONE); the test hook waits for a count
+        // no producer reaches, so that the give-up path runs
+        const uint32_t need = (flags & RJ_WAVE_TEST_GIVEUP) ? 0xFFFFFFFEu : hi - s0;
+        const uint32_t spin_max = (flags & RJ_WAVE_TEST_GIVEUP) ? 16u : (1u << 23);
         if (j == sj && need <= sn) continue;
         uint32_t *pp = progress + im.pival_prefix + pival0 + j;
         // relaxed polls (an acquire load would invalidate the L2 on every poll), then one acquire
@@ -721,7 +724,7 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
         // the host turns the flag into EXECUTION_FAILED
         uint32_t got = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (uint32_t spin = 0; got < need; spin++) {
-          if (spin >= (1u << 23)) {
+          if (spin >= spin_max) {
             if (threadIdx.x == 0) __hip_atomic_store(progress_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
           }

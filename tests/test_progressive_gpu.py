@@ -282,3 +282,54 @@ def test_progressive_1080p_batch_one_call(dec):
     ref = t.from_numpy(want[0]).to("cuda")
     bad = [k for k, bufs in enumerate(bufs_all) if not t.equal(bufs[0], ref)]
     assert not bad, bad[:8]
+
+
+def test_progressive_producer_wait_give_up_is_clean():
+    """A refinement wave whose producers never report progress gives up after its bounded wait
+    and the call returns ROCJPEG_STATUS_EXECUTION_FAILED -- no hang, no fault.  Forced with the
+    test hook RJ_TEST_PROG_GIVEUP (k_prog_wave waits for a count no producer reaches, with a
+    short poll budget).  The same handle still decodes baseline streams exactly afterwards, and a
+    handle without the hook decodes the progressive streams exactly."""
+    import os
+    from tests import gpu_util as G
+    G.torch()
+    env = {"RJ_TEST_PROG_GIVEUP": "1", "RJ_PROG_WAVE_ALL": "1"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        d = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    good = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    try:
+        def batch(dec, datas):
+            streams = [R.JpegStream(x) for x in datas]
+            bufs_all, imgs, shapes_all = [], [], []
+            for s in streams:
+                nc, css, w, h = dec.image_info(s)
+                shapes = G.channel_shapes(R.OutputFormat.RGB, css, w, h)
+                bufs, img = G.gpu_buffers(shapes)
+                bufs_all.append(bufs)
+                imgs.append(img)
+                shapes_all.append(shapes)
+            st = dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs)
+            return st, shapes_all, bufs_all
+
+        prog = [O.fixture_bytes(e) for e in PIPELINED]
+        st, _, _ = batch(d, prog)
+        assert st == R.Status.EXECUTION_FAILED, R.error_name(st)
+        base = [O.fixture_bytes(e) for e in BASE[:4]]
+        for dec, datas in ((d, base), (good, prog)):
+            st, shapes_all, bufs_all = batch(dec, datas)
+            assert st == 0, R.error_name(st)
+            for x, shapes, bufs in zip(datas, shapes_all, bufs_all):
+                ost, want = O.oracle_decode(x, int(R.OutputFormat.RGB), shapes)
+                assert ost == 0
+                assert G.first_mismatch(G.to_host(bufs)[0], want[0]) is None
+    finally:
+        d.close()
+        good.close()
