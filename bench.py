@@ -334,8 +334,9 @@ def kernel_table(t, n):
     """(summed launch ms per call, launches per call, units (images) per launch) per kernel of
     a profiled pass; the pipelined K1/K2 launches each take an equal share of the intervals."""
     kern = {}
-    if t["k1_launches"]:
-        kern["k_entropy"] = (t["k1_launch_ms_sum"], t["k1_launches"], n / t["k1_launches"])
+    if t["k1_launches"]:  # lean K1 (row images) is k_huff, the chunk-lane K1 k_entropy
+        k1 = "k_huff" if t["lean_k1"] else "k_entropy"
+        kern[k1] = (t["k1_launch_ms_sum"], t["k1_launches"], n / t["k1_launches"])
     if t["k2_launches"]:
         kern["k_rows"] = (t["k2_launch_ms_sum"], t["k2_launches"], n / t["k2_launches"])
     kern["k_destuff"] = (t["destuff_ms"], 1, n)
@@ -366,7 +367,7 @@ def roofline(t, n, workload, per_image_bytes):
         r["traffic"], r["traffic_source"] = tr
     # intermediate-inclusive figures (what the kernels actually move through HBM by design)
     entb = t["entry_bytes"]
-    if dom == "k_entropy" and t["k1_launches"]:
+    if dom in ("k_entropy", "k_huff") and t["k1_launches"]:
         b = (t["ecs_bytes"] + entb) / t["k1_launches"]
         r["achieved_incl_intermediates"] = round(b / (avg_ms * 1e-3) / 1e9, 2)
     if "k_rows" in kern:

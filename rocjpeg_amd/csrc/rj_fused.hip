@@ -339,16 +339,20 @@ __device__ __forceinline__ void csc4_pk(uint32_t y4, rj_f2 ua, rj_f2 ub, rj_f2 v
 // image, 4-byte aligned destination -- no per-quad bounds and no format branches in the loop.
 // Lane = 4 consecutive pixels of one row (12 output bytes, one dwordx3 store); kHs / kVs:
 // chroma halved horizontally / vertically (4:2:0 both, 4:2:2 kHs, 4:4:4 neither).
+// kVs: a lane takes the 4 x 2 pixels of two rows that share one chroma row (the chroma is read
+// and converted once for both), so qy counts row pairs.
 template <bool kHs, bool kVs>
 __device__ __forceinline__ void rgb_strip(const uint8_t *ty, const uint8_t *tu, const uint8_t *tv, uint32_t tw0,
                                           uint32_t tw1, uint32_t tid, uint32_t quads_x, uint32_t rows, uint8_t *dst,
                                           uint32_t pitch) {
   const uint32_t qsy = 64 / quads_x, qsx = 64 - qsy * quads_x;
   uint32_t qy = tid / quads_x, qx = tid - qy * quads_x;
-  while (qy < rows) {
+  const uint32_t nq = kVs ? rows >> 1 : rows;  // kVs: rows is even (an MCU row of 16)
+  while (qy < nq) {
     const uint32_t x = qx * 4;
-    const uint32_t y4 = *reinterpret_cast<const uint32_t *>(ty + __umul24(qy, tw0) + x);
-    const uint32_t crow = __umul24(kVs ? (qy >> 1) : qy, tw1);
+    const uint32_t yrow = kVs ? 2 * qy : qy;
+    const uint32_t y4 = *reinterpret_cast<const uint32_t *>(ty + __umul24(yrow, tw0) + x);
+    const uint32_t crow = __umul24(qy, tw1);
     const rj_f2 m128 = {128.0f, 128.0f};
     rj_f2 ua, ub, va, vb;
     if constexpr (kHs) {
@@ -369,8 +373,13 @@ __device__ __forceinline__ void rgb_strip(const uint8_t *ty, const uint8_t *tu, 
     }
     uint32_t w0, w1, w2;
     csc4_pk(y4, ua, ub, va, vb, w0, w1, w2);
-    const uint32_t off = __umul24(qy, pitch) + __umul24(qx, 12u);  // 32-bit: saddr store form
+    const uint32_t off = __umul24(yrow, pitch) + __umul24(qx, 12u);  // 32-bit: saddr store form
     *reinterpret_cast<RJ_GLOBAL uint3 *>(gp(dst) + off) = make_uint3(w0, w1, w2);
+    if constexpr (kVs) {  // the second row of the pair, same chroma
+      const uint32_t y4b = *reinterpret_cast<const uint32_t *>(ty + __umul24(yrow + 1, tw0) + x);
+      csc4_pk(y4b, ua, ub, va, vb, w0, w1, w2);
+      *reinterpret_cast<RJ_GLOBAL uint3 *>(gp(dst) + (off + pitch)) = make_uint3(w0, w1, w2);
+    }
     qx += qsx;
     qy += qsy;
     if (qx >= quads_x) {
