@@ -104,6 +104,8 @@ typedef struct {
   /* MCU rows with coefficients outside the int32 IDCT's exact domain (|coef x quant| >= 2^14:
      corrupt data with large quantisers), decoded again by the K2 fix-up launch in 64-bit */
   uint32_t wide_rows;
+  /* lean K1 split launch: intervals decoded by a head and a tail lane (rj_huff.hip) */
+  uint32_t lean_split;
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);

@@ -152,6 +152,7 @@ int Decoder::Initialize() {
   if (const char *l = getenv("RJ_LPT")) lpt_ = atoi(l) != 0;
   if (const char *l = getenv("RJ_K1_SOLO")) k1_solo_lds_ = uint32_t(std::max(0, atoi(l)));
   if (const char *sk = getenv("RJ_STREAM_K2")) stream_enabled_ = atoi(sk) != 0;
+  if (const char *sp = getenv("RJ_SPLIT")) split_enabled_ = atoi(sp) != 0;
   if (const char *sw = getenv("RJ_STREAM_WG")) stream_wg_per_cu_ = std::max(1, std::min(16, atoi(sw)));
   cu_count_ = std::max(1, prop.multiProcessorCount);
   RJ_HIP(hipHostMalloc(reinterpret_cast<void **>(&h_wide_flag_), 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -1027,7 +1028,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t off_wide = AlignUp(off_lean + (lean ? tabs.size() * sizeof(RjLeanTables) : 0), 256);
   const uint64_t off_stage = AlignUp(off_wide + kWideSites * sizeof(uint32_t), 256);
   const uint64_t blob_a = AlignUp(off_stage + stage_bytes, 256);
-  const uint64_t n_lane_seg = any_split ? lane_seg.size() : (sorted ? seg_total : 0);
+  // (a lean launch may split intervals: head + tail lanes, up to 2 per interval + one wave of padding)
+  const uint64_t n_lane_seg = any_split ? lane_seg.size() : (sorted ? (lean ? 2ull * seg_total + 64 : seg_total) : 0);
   const uint64_t off_lane_seg = blob_a;
   const uint64_t off_seg_lane0 = AlignUp(off_lane_seg + n_lane_seg * 4, 256);
   const uint64_t off_row_list = AlignUp(off_seg_lane0 + uint64_t(seg_lane0.size()) * 4, 256);
@@ -1056,6 +1058,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   cbuf.count = nullptr;
   cbuf.dense = d_coef_.as<uint32_t>();
   cbuf.wide_flag = d_wide_flag_;
+  cbuf.piece_shift = 0;
   if (profiling_) {
     RJ_CHECK(d_count_.Ensure(256));
     cbuf.count = d_count_.as<unsigned long long>();
@@ -1329,10 +1332,15 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (rows_from_lanes) row_list.resize(seg_total);
     uint2 *rl = rows_from_lanes ? row_list.data() : nullptr;
     uint32_t gs = 0;
+    std::vector<uint2> &seg_len = sc_.seg_len;
+    if (lean) seg_len.resize(seg_total);
     for (int i = 0; i < n; i++) {
       uint32_t r = 0;
+      const uint32_t nblk_i = streams[i]->plan().nblk_mcu;
       for (const RjSegDev &sg : streams[i]->plan().segs) {
         const uint32_t l = pos[bucket(sg.src_len)]++;
+        if (lean)
+          seg_len[gs] = uint2{(sg.flags & RJ_SEG_MISSING) ? 0u : sg.dst_len, sg.mcu_count * nblk_i};
         ls[l] = gs;
         if (rl) rl[l] = uint2{uint32_t(i), r++};
         seg_pos[gs++] = l;
@@ -1392,20 +1400,62 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       }
     }
   }
+  // ---- lean split launch (rj_huff.hip): while the call has fewer intervals than two decoder
+  // waves per SIMD can hold, the longest intervals get a head lane and a tail lane (which
+  // starts at rj_split_byte and is joined where the two decoders' MCU starts meet) ----
+  uint32_t nsplit = 0, nl_split = 0;
+  RjHuffSplit hsplit{0, 0};
+  if (lean && sorted && lanes_desc && ngroups == 1 && !any_split && split_enabled_ && !stream_enabled_ &&
+      !Dbg(kDebugNoDep)) {
+    const int64_t waves = int64_t(cu_count_) * (RJ_HL_SPLIT_DEC / 64);  // one round of the split grid
+    const int64_t kmax = 64 * waves - int64_t(seg_total);
+    uint64_t cap = 0;
+    while (int64_t(nsplit) < kmax && nsplit < seg_total) {
+      const uint2 sl = sc_.seg_len[lane_seg[nsplit]];
+      if (sl.x < RJ_SPLIT_MIN_BYTES) break;  // lanes are sorted longest first
+      cap = std::max<uint64_t>(cap, rj_group(8ull * (sl.x - rj_split_byte(sl.x)) + sl.y +
+                                             uint64_t(RJ_MAX_BLK_MCU) * RJ_ENT_PER_BLOCK + 1));
+      nsplit++;
+    }
+    if (nsplit > 0) {
+      const uint32_t wsplit = (nsplit + 31) / 32;
+      nl_split = wsplit * 64 + (seg_total - nsplit);
+      std::vector<uint32_t> &l2 = sc_.lane_split;
+      l2.assign(nl_split, UINT32_MAX);
+      for (uint32_t j = 0; j < nsplit; j++) {
+        l2[(j / 32) * 64 + (j % 32)] = lane_seg[j] | RJ_LANE_HEAD;
+        l2[(j / 32) * 64 + 32 + (j % 32)] = lane_seg[j] | RJ_LANE_TAIL;
+      }
+      std::memcpy(l2.data() + uint64_t(wsplit) * 64, lane_seg.data() + nsplit, uint64_t(seg_total - nsplit) * 4);
+      hsplit.ent = AlignUp(ent_total, RJ_ENT_GROUP);
+      hsplit.cap = cap;
+      RJ_CHECK(d_entries_.Ensure((hsplit.ent + uint64_t(wsplit) * 32 * cap + RJ_ENT_SLACK) * 4));
+      RJ_CHECK(d_piece_.Ensure(2ull * seg_total * sizeof(RjPiece)));
+      cbuf.ent = d_entries_.as<uint32_t>();
+      cbuf.piece = d_piece_.as<RjPiece>();
+      cbuf.piece_shift = 1;  // interval s: pieces 2s (head) and 2s + 1 (tail)
+    }
+  }
+  timings_.lean_split = nsplit;
   if (any_split) {
     std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(lane_seg.size()) * 4);
     std::memcpy(h + off_seg_lane0, seg_lane0.data(), uint64_t(seg_lane0.size()) * 4);
     cbuf.lane_seg = d_lane_seg;
     cbuf.seg_lane0 = reinterpret_cast<const uint32_t *>(dbase + off_seg_lane0);
   } else if (sorted) {  // lanes in length order; pieces stay at the interval's own slot
-    std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(seg_total) * 4);
+    if (nsplit) std::memcpy(h + off_lane_seg, sc_.lane_split.data(), uint64_t(nl_split) * 4);
+    else std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(seg_total) * 4);
     cbuf.lane_seg = d_lane_seg;
     cbuf.seg_lane0 = nullptr;
   } else {  // identity layout
     cbuf.lane_seg = nullptr;
     cbuf.seg_lane0 = nullptr;
   }
-  if (blob > blob_a) RJ_HIP(hipMemcpyAsync(dbase + blob_a, h + blob_a, blob - blob_a, hipMemcpyHostToDevice, stream_));
+  // part B: everything up to the row lists, or only the lane list actually used
+  const uint64_t blob_b = (!any_split && sorted && ngroups == 1)
+                              ? std::min<uint64_t>(blob, AlignUp(off_lane_seg + uint64_t(nsplit ? nl_split : seg_total) * 4, 256))
+                              : blob;
+  if (blob_b > blob_a) RJ_HIP(hipMemcpyAsync(dbase + blob_a, h + blob_a, blob_b - blob_a, hipMemcpyHostToDevice, stream_));
 
   const auto t_end = std::chrono::steady_clock::now();
   timings_.host_ms = std::chrono::duration<float, std::milli>(t_end - t_host0).count();
@@ -1503,8 +1553,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
     } else if (lean) {  // no split interval: one pass, no resolution / serial stages
-      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, seg_total, d_destuff_.as<uint8_t>(), d_tabs, d_lean, cbuf,
-                             nullptr, 0u, nullptr, k1_solo_lds_));
+      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, nsplit ? nl_split : seg_total, d_destuff_.as<uint8_t>(), d_tabs,
+                             d_lean, cbuf, nullptr, 0u, nullptr, k1_solo_lds_, nsplit ? &hsplit : nullptr));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
     } else {
@@ -1595,6 +1645,19 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (Dbg(kDebugStamps) && lean) DumpHuffStamps();
 #endif
 
+  if (nsplit && n == 1 && Dbg(kDebugK1Pieces)) {  // development: every interval's pieces (split launch)
+    std::vector<RjPiece> pc(2ull * seg_total);
+    RJ_HIP(hipMemcpy(pc.data(), d_piece_.as<RjPiece>(), pc.size() * sizeof(RjPiece), hipMemcpyDeviceToHost));
+    for (uint32_t q = 0; q < seg_total; q++) {
+      const RjPiece &a = pc[2 * q], &t = pc[2 * q + 1];
+      const RjSegDev &sg = streams[0]->plan().segs[q];
+      fprintf(stderr, "[K1 split] seg %u dst_len %u flags %u: npieces %u head n %u", q, sg.dst_len, sg.flags, a.npieces,
+              a.nblk);
+      if (a.npieces == 2) fprintf(stderr, " | tail first %u n %u skip %u ent+%llu", t.first_blk, t.nblk, t.npieces,
+                                  (unsigned long long)(t.ent - hsplit.ent));
+      fprintf(stderr, "\n");
+    }
+  }
   timings_.images = uint32_t(n);
   timings_.intervals = seg_total;
   timings_.chunks = lanes_all;

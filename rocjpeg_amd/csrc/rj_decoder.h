@@ -115,6 +115,7 @@ class Decoder {
   // first instead of doubling up on a CU beside a long-interval workgroup
   uint32_t k1_solo_lds_ = 16384;
   bool lean_enabled_ = true;       // env RJ_LEAN=0: the exact K1 (rj_entropy.hip) for row images too
+  bool split_enabled_ = false;     // env RJ_SPLIT=1: lean K1 head + tail lanes (rj_huff.hip; measured slower)
   bool stream_enabled_ = false;    // env RJ_STREAM_K2=1: streaming K2 (k_rows_stream), measured no faster
   int cu_count_ = 256;
   int stream_wg_per_cu_ = 2;       // env RJ_STREAM_WG: streaming K2 workgroups per CU (K1's LDS must still fit)
@@ -142,7 +143,8 @@ class Decoder {
     std::vector<RjImageDev> imgs;
     std::vector<RjJobDev> jobs;
     std::vector<uint64_t> stage_off;
-    std::vector<uint32_t> tab_of, row_prefix, grow_prefix, seg_lane0, lane_seg, bucket_pos, seg_pos;
+    std::vector<uint32_t> tab_of, row_prefix, grow_prefix, seg_lane0, lane_seg, bucket_pos, seg_pos, lane_split;
+    std::vector<uint2> seg_len;  // per interval: destuffed bytes, blocks (lean split planning)
     std::vector<uint8_t> is_fused, row_group, routed;
     std::vector<uint2> row_list;
     std::vector<uint32_t> prow_prefix, pgrow_prefix, prog_lanes, prog_bucket;  // progressive images

@@ -36,7 +36,8 @@ __host__ __device__ inline uint32_t rj_fused_strip_mcus(uint32_t hmax, uint32_t 
 struct RjPiece {
   uint64_t ent;
   uint32_t first_blk, nblk;
-  uint32_t npieces;  // valid in the interval's first piece
+  uint32_t npieces;  // in the interval's first piece; in a later piece of a lean split interval:
+                     // the blocks of the stream at `ent` that precede the piece (its skip)
   int32_t dcd[3];
 };
 // chunk-start record (speculative lanes): block start at bit `pos` of the interval, block
@@ -74,6 +75,18 @@ struct RjCoefBuf {
   unsigned long long *count;  // profiling: entries written, summed per workgroup (null: off)
   const uint32_t *dense;      // progressive images: dense coefficients (RjImageDev.coef_off)
   uint32_t *wide_flag;        // host-mapped: set by K2 when it recorded a row for the fix-up
+  uint32_t piece_shift;       // identity layout: interval s's pieces start at s << piece_shift
+};
+// Lean K1 split launch (rj_huff.hip): an interval decoded by a head lane from its start and a
+// tail lane from rj_split_byte(dst_len); lane_seg entries carry the role in their top bits.
+#define RJ_LANE_HEAD 0x40000000u
+#define RJ_LANE_TAIL 0x80000000u
+#define RJ_HL_SPLIT_DEC 512          // decoder lanes per workgroup of the split launch
+#define RJ_SPLIT_MIN_BYTES 1024u     // shorter intervals stay whole
+__host__ __device__ inline uint32_t rj_split_byte(uint32_t dst_len) { return (dst_len * 29u / 64u) & ~15u; }
+struct RjHuffSplit {
+  uint64_t ent;  // first entry of the tail lanes' regions (pair p at ent + p * cap)
+  uint64_t cap;  // entries per tail region
 };
 #define RJ_ENT_PER_BLOCK 64       // worst case: DC + 63 AC (each position written at most once)
 #define RJ_ENT_GROUP 16           // K1 writes entries in 64-B groups; regions are group-aligned

@@ -101,6 +101,7 @@ struct Nav {
   uint32_t bleft;           // blocks left in the current piece
   uint32_t seg, pj;         // interval (image-relative) and piece within it
   int32_t dcd[3];           // DC correction of the current piece, per component
+  uint32_t skip;            // blocks at cur() to pass over before the piece (lean split tails)
   __device__ __forceinline__ uint64_t cur() const { return uint64_t(cur_hi) << 32 | cur_lo; }
   __device__ __forceinline__ void set_cur(uint64_t v) {
     cur_lo = U(uint32_t(v));
@@ -113,6 +114,7 @@ struct Nav {
     dcd[0] = int32_t(U(uint32_t(p.dcd[0])));
     dcd[1] = int32_t(U(uint32_t(p.dcd[1])));
     dcd[2] = int32_t(U(uint32_t(p.dcd[2])));
+    skip = 0;
   }
 };
 
@@ -129,7 +131,7 @@ __device__ __forceinline__ int raw_value(uint32_t e) {
   return raw < half ? int(raw) - int(2 * half - 1) : int(raw);
 }
 
-template <bool kRaw>
+template <bool kRaw, bool kSplit>
 __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefBuf &coefs,
                                              const uint32_t *__restrict__ ent, uint32_t lane, uint32_t nb,
                                              uint32_t drop, uint32_t nblk, uint32_t cbits, EntWin &win, Nav &nv,
@@ -139,19 +141,22 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
   for (uint32_t moves = 0; done < need && moves < (1u << 16); moves++) {  // bounded on corrupt pieces
     if (nv.bleft == 0) {  // next piece, or the first piece of the next interval (synchronous reload)
       if (nv.seg >= im.nseg) break;
-      const RjPiece *pb = coefs.piece + rj_seg_lane0(coefs, im.seg_prefix + nv.seg);
+      const RjPiece *pb = coefs.piece + rj_seg_lane0_k<kSplit>(coefs, im.seg_prefix + nv.seg);
       if (nv.pj + 1 < gp(pb)->npieces) {
         nv.pj++;
       } else {
         nv.seg++;
         nv.pj = 0;
         if (nv.seg >= im.nseg) break;
-        pb = coefs.piece + rj_seg_lane0(coefs, im.seg_prefix + nv.seg);
+        pb = coefs.piece + rj_seg_lane0_k<kSplit>(coefs, im.seg_prefix + nv.seg);
       }
       nv.take(pb + nv.pj);
+      if (kRaw && kSplit && nv.pj > 0) nv.skip = U(gp(pb + nv.pj)->npieces);  // a split interval's tail
       win.load(ent, nv.cur(), lane);
     }
-    const uint32_t piece = min(need - done, nv.bleft);  // blocks taken from this piece
+    // a split tail's piece starts after `skip` blocks of its stream: pass over them first
+    const bool pass = kSplit && nv.skip != 0;
+    const uint32_t piece = pass ? nv.skip : min(need - done, nv.bleft);  // blocks taken from this piece
     const bool fix_dc = !kRaw && (nv.dcd[0] | nv.dcd[1] | nv.dcd[2]) != 0;
     uint32_t seen = 0;                                  // block starts before the current row
     bool found = false;
@@ -168,7 +173,12 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
         const uint32_t ord = seen + below + (st ? 1u : 0u) - 1u;
         const uint32_t blk = done + ord;  // block index counted from the first dropped one
         bool oob = false;
-        if (ord < piece && p < 64u && blk >= drop) {
+        // a split interval's tail piece may end early (its lane stopped at libjpeg's
+        // insufficient-data point): the piece's remaining blocks are zero blocks, and nothing
+        // after its terminator belongs to the stream
+        const uint64_t term = (kRaw && kSplit) ? __ballot(p == 127 && ord < piece) : 0ull;
+        const int tl = term ? __ffsll((long long)term) - 1 : 64;
+        if (!pass && ord < piece && p < 64u && blk >= drop && int(lane) < tl) {
           int v = kRaw ? raw_value(e) : int(int16_t(e & 0xFFFFu));
           if (kRaw && (e & RJ_RE_ZERO)) v = -32768;  // zero block: marked for the DC restore
           if (!kRaw && fix_dc && p == 0) {
@@ -181,6 +191,14 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
           *reinterpret_cast<int16_t *>(s_buf + (blk - drop) * RJ_BLK_STRIDE + p * 2) = int16_t(v);
         }
         bad = bad || __ballot(oob) != 0;
+        if (term) {
+          const uint32_t t_ord = pass ? piece : __builtin_amdgcn_readlane(ord, tl);
+          for (uint32_t z = t_ord + lane; z < piece; z += 64)
+            if (done + z >= drop) *reinterpret_cast<int16_t *>(s_buf + (done + z - drop) * RJ_BLK_STRIDE) = int16_t(-32768);
+          nv.set_cur((uint64_t(win.base_hi) << 32 | win.base_lo) + uint32_t(r) * 64u + uint32_t(tl));
+          found = true;
+          break;
+        }
         const uint64_t hit = __ballot(st && ord == piece);  // start of the first block past the piece
         seen += __popcll(m);
         if (hit) {
@@ -192,8 +210,13 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
       }
       if (!found) win.load(ent, (uint64_t(win.base_hi) << 32 | win.base_lo) + RJ_WIN_ROWS * 64u, lane);
     }
-    done += piece;
-    nv.bleft -= piece;
+    if (pass) {
+      nv.skip = 0;
+      win.load(ent, nv.cur(), lane);  // the piece proper starts mid-window
+    } else {
+      done += piece;
+      nv.bleft -= piece;
+    }
   }
 }
 
@@ -397,7 +420,7 @@ __device__ __forceinline__ void rgb_strip(const uint8_t *ty, const uint8_t *tu, 
 //   kWide = true   : the fix-up pass (k_rows_fix): strips with coefficients outside the int32
 //                    IDCT's exact domain take the 64-bit IDCT.  Otherwise such a row is appended
 //                    to wide_list (as (image, row); wide_cnt counts) for the fix-up launch.
-template <bool kPlanes, bool kDense, bool kWide = false>
+template <bool kPlanes, bool kDense, bool kWide = false, bool kSplit = false>
 __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, int i, uint32_t my, RjCoefBuf coefs,
                                          const RjTableSet *__restrict__ tabsets, uint8_t *__restrict__ planes,
                                          uint8_t *s_buf, uint16_t (*s_q)[64], uint32_t *wide_cnt, uint2 *wide_list) {
@@ -461,12 +484,12 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
       // every load of the row's start is then one dependent step from the row record)
       nv.seg = my;
       nv.pj = 0;
-      nv.take(coefs.piece + U(im.seg_prefix) + my);
+      nv.take(coefs.piece + rj_seg_lane0_k<kSplit>(coefs, U(im.seg_prefix) + my));
     } else {
       nv.seg = U(ri ? (my * mcux) / ri : 0);
       const RjSegDev sg = gp(im.segs)[nv.seg];
       const uint32_t rel = (my * mcux - sg.mcu_first) * nblk;
-      const RjPiece *pb = coefs.piece + rj_seg_lane0(coefs, im.seg_prefix + nv.seg);
+      const RjPiece *pb = coefs.piece + rj_seg_lane0_k<kSplit>(coefs, im.seg_prefix + nv.seg);
       const uint32_t np = U(min(gp(pb)->npieces, 4096u));
       uint32_t pj = 0;
       while (pj + 1 < np && U(gp(pb + pj + 1)->first_blk) <= rel) pj++;
@@ -514,8 +537,8 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
     if constexpr (kDense) {
       if (has_blk) load_dense_block(im, coefs.dense, lane_blk, mx0, my, inter, s_buf + tid * RJ_BLK_STRIDE);
     } else {
-      if (dc_diff) parse_blocks<true>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, thr, wide);
-      else parse_blocks<false>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, thr, wide);
+      if (dc_diff) parse_blocks<true, kSplit>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, thr, wide);
+      else parse_blocks<false, false>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, thr, wide);
       drop = 0;
 #ifndef RJ_NO_WINPF
       if (sx + 1 < strips_x && nv.bleft) win.load(ent, nv.cur(), tid);  // next strip's window: lands behind B and C
@@ -708,7 +731,7 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
 }
 
 // K2: one wavefront (workgroup) per MCU row.
-template <bool kPlanes, bool kDense = false>
+template <bool kPlanes, bool kDense = false, bool kSplit = false>
 __global__ __launch_bounds__(64, RJ_K2_OCC) void k_rows(const RjImageDev *__restrict__ imgs, int nimg,
                                              const uint32_t *__restrict__ row_prefix,
                                              const uint2 *__restrict__ row_list,
@@ -721,14 +744,14 @@ __global__ __launch_bounds__(64, RJ_K2_OCC) void k_rows(const RjImageDev *__rest
   int i;
   uint32_t my;
   row_of_block(imgs, nimg, row_prefix, row_list, row_segs, blockIdx.x, i, my);
-  row_body<kPlanes, kDense>(imgs, i, my, coefs, tabsets, planes, s_buf, s_q, wide_cnt, wide_list);
+  row_body<kPlanes, kDense, false, kSplit>(imgs, i, my, coefs, tabsets, planes, s_buf, s_q, wide_cnt, wide_list);
 }
 
 // K2 fix-up: the rows a K2 launch recorded (a strip outside the int32 IDCT's exact domain --
 // corrupt data with large quantisers), decoded again with the 64-bit IDCT for those strips.
 // Issued by the host only when a K2 launch of the call raised the host-mapped flag
 // (RjCoefBuf.wide_flag), after the call's kernels -- the common path pays nothing.
-template <bool kPlanes, bool kDense>
+template <bool kPlanes, bool kDense, bool kSplit = false>
 __global__ __launch_bounds__(64) void k_rows_fix(const RjImageDev *__restrict__ imgs, int nimg, RjCoefBuf coefs,
                                                  const RjTableSet *__restrict__ tabsets, uint8_t *__restrict__ planes,
                                                  const uint32_t *wide_cnt, const uint2 *wide_list, uint32_t cap) {
@@ -740,7 +763,7 @@ __global__ __launch_bounds__(64) void k_rows_fix(const RjImageDev *__restrict__ 
     const int i = int(U(e.x));
     if (i >= nimg) continue;
     __syncthreads();  // the previous row's tiles fully read
-    row_body<kPlanes, kDense, true>(imgs, i, U(e.y), coefs, tabsets, planes, s_buf, s_q, nullptr, nullptr);
+    row_body<kPlanes, kDense, true, kSplit>(imgs, i, U(e.y), coefs, tabsets, planes, s_buf, s_q, nullptr, nullptr);
   }
 }
 
@@ -829,7 +852,8 @@ hipError_t LaunchRowsStream(hipStream_t st, bool wait, const RjImageDev *imgs, i
   return hipGetLastError();
 }
 
-// the fix-up launch behind a K2 launch of `cap` rows (same stream, same variant)
+// the fix-up launch behind a K2 launch of `cap` rows (same stream, same variant; a lean split
+// launch's pieces, coefs.piece_shift = 1, take the split-aware instances)
 hipError_t LaunchRowsFix(hipStream_t st, bool to_planes, bool dense, const RjImageDev *imgs, int nimg, RjCoefBuf coefs,
                          const RjTableSet *tabsets, uint8_t *planes, const uint32_t *wide_cnt, const uint2 *wide_list,
                          uint32_t cap) {
@@ -840,6 +864,11 @@ hipError_t LaunchRowsFix(hipStream_t st, bool to_planes, bool dense, const RjIma
       hipLaunchKernelGGL((k_rows_fix<true, true>), grid, dim3(64), 0, st, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, cap);
     else
       hipLaunchKernelGGL((k_rows_fix<false, true>), grid, dim3(64), 0, st, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, cap);
+  } else if (coefs.piece_shift != 0) {
+    if (to_planes)
+      hipLaunchKernelGGL((k_rows_fix<true, false, true>), grid, dim3(64), 0, st, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, cap);
+    else
+      hipLaunchKernelGGL((k_rows_fix<false, false, true>), grid, dim3(64), 0, st, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, cap);
   } else {
     if (to_planes)
       hipLaunchKernelGGL((k_rows_fix<true, false>), grid, dim3(64), 0, st, imgs, nimg, coefs, tabsets, planes, wide_cnt, wide_list, cap);
@@ -854,12 +883,20 @@ hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, in
                       uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list) {
   if (nrows == 0) return hipSuccess;
   const uint32_t *no_segs = nullptr;
-  if (to_planes)
+  if (coefs.piece_shift != 0) {  // lean split launch: pieces with skips / early terminators
+    if (to_planes)
+      hipLaunchKernelGGL((k_rows<true, false, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list,
+                         no_segs, coefs, tabsets, planes, wide_cnt, wide_list);
+    else
+      hipLaunchKernelGGL((k_rows<false, false, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list,
+                         no_segs, coefs, tabsets, planes, wide_cnt, wide_list);
+  } else if (to_planes) {
     hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, no_segs, coefs,
                        tabsets, planes, wide_cnt, wide_list);
-  else
+  } else {
     hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, no_segs, coefs,
                        tabsets, planes, wide_cnt, wide_list);
+  }
   return hipGetLastError();
 }
 

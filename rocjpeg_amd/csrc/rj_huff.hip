@@ -26,19 +26,16 @@
 
 namespace rj {
 
-#define RJ_HL_DEC 256                       // decoder lanes per workgroup
-#define RJ_HL_WG (2 * RJ_HL_DEC)            // + one mover wave per decoder wave
 #define RJ_HL_CHUNKS 8                      // 16-B chunks in a lane's bit ring
 #define RJ_HL_WORDS (RJ_HL_CHUNKS * 4)      // 32 words
-#ifndef RJ_HL_GROUP
-#define RJ_HL_GROUP 8                       // flushed in 32-B groups: < 8 pending at a phase start
-#endif
-#define RJ_HL_STAGE (2 * RJ_HL_GROUP)       // staged entries per lane
 #define RJ_HL_PHASE 8                       // symbols per phase (<= 8 words: 31 bits per symbol)
 // LDS byte offsets of the four tables (RjLeanTables order)
 #define RJ_HL_AC_BYTES (RJ_HL_AC_WORDS * 4)
 #define RJ_HL_DC0 (2 * RJ_HL_AC_BYTES)
 #define RJ_HL_LUT_WORDS (2 * RJ_HL_AC_WORDS + 2 * RJ_HL_DC_WORDS)
+// Split launch (rj_kernels.h LaunchHuffLanes): MCU-start records kept by a tail lane
+#define RJ_HL_REC 48
+#define RJ_HL_REC_LIMIT 65280u              // records are 16-bit bit positions past the split
 
 __device__ const uint4 rj_hl_zero[2] = {};
 
@@ -62,13 +59,15 @@ __device__ unsigned long long rj_hl_stamp[8];
 #define RJ_HL_COUNT_ESC
 #endif
 
-// word w of the lane's column of a lane-interleaved LDS array ([w][lane]: conflict-free)
+// word w of the lane's column of a lane-interleaved LDS array ([w][lane], S lanes: conflict-free)
+template <int S>
 struct HCol {
   uint32_t *base;
-  __device__ __forceinline__ uint32_t &operator[](uint32_t w) const { return base[w * RJ_HL_DEC]; }
+  __device__ __forceinline__ uint32_t &operator[](uint32_t w) const { return base[w * S]; }
 };
 
-__device__ __forceinline__ void hl_put(const HCol &ring, uint32_t slot, const uint4 &v) {
+template <int S>
+__device__ __forceinline__ void hl_put(const HCol<S> &ring, uint32_t slot, const uint4 &v) {
   const uint32_t w0 = __builtin_bswap32(v.x), w1 = __builtin_bswap32(v.y);
   const uint32_t w2 = __builtin_bswap32(v.z), w3 = __builtin_bswap32(v.w);
   ring[4 * slot] = w0;
@@ -77,15 +76,16 @@ __device__ __forceinline__ void hl_put(const HCol &ring, uint32_t slot, const ui
   ring[4 * slot + 3] = w3;
 }
 
-// the 32-B group of staged entries [from, from + 8) (from a multiple of 8) to HBM
-__device__ __forceinline__ void hl_flush(const HCol &stage, uint32_t from, uint32_t *dst) {
-  uint32_t w[RJ_HL_GROUP];
-  const uint32_t s0 = from & (RJ_HL_STAGE - 1);
+// the group of G staged entries [from, from + G) (from a multiple of G; the stage holds 2G) to HBM
+template <int S, int G>
+__device__ __forceinline__ void hl_flush(const HCol<S> &stage, uint32_t from, uint32_t *dst) {
+  uint32_t w[G];
+  const uint32_t s0 = from & (2 * G - 1);
 #pragma unroll
-  for (int q = 0; q < RJ_HL_GROUP; q++) w[q] = stage[s0 + q];
+  for (int q = 0; q < G; q++) w[q] = stage[s0 + q];
   uint4 *d4 = reinterpret_cast<uint4 *>(dst);
 #pragma unroll
-  for (int q = 0; q < RJ_HL_GROUP / 4; q++) {
+  for (int q = 0; q < G / 4; q++) {
     const uint4 v = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 #ifdef RJ_HL_X_NT
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -121,7 +121,9 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
 }
 
 // One symbol step.  SAFE: per-lane activity (blocks_left) and libjpeg's insufficient-data rule.
-#define RJ_HL_STEP(SAFE)                                                                                  \
+// SYNC (split launch): the lane notes where its last MCU started (mpos, mleft), and a tail lane
+// records its MCU starts (recs, nr; head lanes keep nr = RJ_HL_REC and write a scratch slot).
+#define RJ_HL_STEP(SAFE, SYNC)                                                                                  \
   do {                                                                                                    \
     const uint32_t peek = __builtin_amdgcn_alignbit(wa, wb, q);                                           \
     uint32_t e = s_lut[(tb >> 2) + (peek >> tsh)];                                                        \
@@ -141,7 +143,7 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
       kn = skip ? 64u : kn;                                                                               \
       emit = blocks_left > 0 ? emit : 0u;                                                                 \
     }                                                                                                     \
-    stage[ne & (RJ_HL_STAGE - 1)] = entry; /* a non-emitted write lands in the next free slot */          \
+    stage[ne & (kStage - 1)] = entry; /* a non-emitted write lands in the next free slot */                \
     ne += emit;                                                                                           \
     {                                                                                                     \
       const bool adv = (qold ^ q) > 31u; /* the bit position entered the next word */                   \
@@ -157,8 +159,17 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
       const bool act = blocks_left > 0;                                                                   \
       blocks_left -= (bend && act) ? 1u : 0u;                                                             \
       skip = skip || (bend && bn == 0u && (0u - q) > nbits);                                              \
+      if (kSplit) blocks_left = (skip && tail) ? 0u : blocks_left; /* K2 zero-fills a short tail */       \
     } else {                                                                                              \
       blocks_left -= bend ? 1u : 0u;                                                                      \
+    }                                                                                                     \
+    if (SYNC) {                                                                                           \
+      const bool ms = bend && bn == 0u; /* the next symbol starts an MCU */                              \
+      mpos = ms ? (0u - q) : mpos;                                                                        \
+      mleft = ms ? blocks_left : mleft;                                                                   \
+      mseen = mseen || ms;                                                                                \
+      recs[min(nr, uint32_t(RJ_HL_REC)) * kPairs] = uint16_t(0u - q);                                     \
+      nr += (ms && nr < RJ_HL_REC) ? 1u : 0u;                                                             \
     }                                                                                                     \
     b = bend ? bn : b;                                                                                    \
     /* next symbol's table: the new block's DC table, or the current block's AC table */                 \
@@ -179,35 +190,56 @@ __device__ __forceinline__ uint32_t lds_ld(const uint32_t *p) { return *(const l
 __device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) { *(lds_vu32 *)(p) = v; }
 #define RJ_HL_FIN 0xFFFFFFFFu  // decoder -> mover: the lane's decode is over
 
-// Workgroup = RJ_HL_DEC decoder lanes (waves 0..3) + one mover wave per decoder wave (4..7).
-// Lane `g` of [lane0, lane0 + nlanes): the interval rj_lane_seg(g), decoded whole by decoder
-// lane g % RJ_HL_DEC; mover lane g % RJ_HL_DEC + RJ_HL_DEC keeps that lane's bit ring filled.
-// The decoder never waits on vector memory: its only VMEM operations are the entry flushes
-// (fire and forget), so no store latency couples into its symbol chain (vmcnt counts loads and
-// stores in one queue -- a decoder that also issued its ring loads waited for its older stores).
-__global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0,
-                                                      uint32_t nlanes, const uint8_t *__restrict__ destuffed,
-                                                      const RjTableSet *__restrict__ tabsets,
-                                                      const RjLeanTables *__restrict__ lean, RjCoefBuf coefs,
-                                                      uint32_t *flags, uint32_t epoch, uint32_t *done) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_HL_WORDS][RJ_HL_DEC];
-  __shared__ __attribute__((aligned(16))) uint32_t s_stage[RJ_HL_STAGE][RJ_HL_DEC];
+// Workgroup = DEC decoder lanes + one mover wave per decoder wave.  Lane `g` of
+// [lane0, lane0 + nlanes): the interval rj_lane_seg(g), decoded by decoder lane g % DEC; mover
+// lane g % DEC + DEC keeps that lane's bit ring filled.  The decoder never waits on vector
+// memory: its only VMEM operations are the entry flushes (fire and forget), so no store latency
+// couples into its symbol chain (vmcnt counts loads and stores in one queue -- a decoder that also
+// issued its ring loads waited for its older stores).
+//
+// kSplit (DEC = 512, one workgroup per CU, two decoder waves per SIMD): an interval listed with
+// RJ_LANE_HEAD at lane l < 32 of a wave also has a tail lane at l + 32 (RJ_LANE_TAIL), which
+// decodes speculatively from the split byte rj_split_byte(dst_len) as if an MCU started there,
+// recording the bit positions of its first RJ_HL_REC MCU starts past the split.  The
+// head decodes from the interval start; past the split it compares each MCU start with the
+// tail's records.  Huffman codes resynchronise: at the first equal MCU start both decoders are in
+// the same state, so the head stops there and the interval becomes two pieces -- the head's
+// blocks before that MCU, and the tail's blocks after its first (record + 1) MCUs (the skip, in
+// the tail piece's npieces field; lean raw entries carry DC differences, so no DC correction is
+// needed).  With no equal MCU start the head decodes the whole interval.  A tail that reaches libjpeg's insufficient-data point stops: K2 zero-fills
+// the piece's missing blocks exactly as libjpeg's zero blocks.
+template <int DEC, int GROUP, bool kSplit>
+__global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
+    const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0, uint32_t nlanes, const uint8_t *__restrict__ destuffed,
+    const RjTableSet *__restrict__ tabsets, const RjLeanTables *__restrict__ lean, RjCoefBuf coefs, uint32_t *flags,
+    uint32_t epoch, uint32_t *done, RjHuffSplit split) {
+  constexpr uint32_t kStage = 2 * GROUP;
+  constexpr uint32_t kPairs = kSplit ? DEC / 2 : 1;
+  __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_HL_WORDS][DEC];
+  __shared__ __attribute__((aligned(16))) uint32_t s_stage[kStage][DEC];
   __shared__ __attribute__((aligned(16))) uint32_t s_lut[RJ_HL_LUT_WORDS];
-  __shared__ uint32_t s_dec[RJ_HL_DEC];  // decoder -> mover: ring words fully consumed (RJ_HL_FIN: done)
-  __shared__ uint32_t s_mov[RJ_HL_DEC];  // mover -> decoder: 16-B chunks committed to the ring
+  __shared__ uint32_t s_dec[DEC];  // decoder -> mover: ring words fully consumed (RJ_HL_FIN: done)
+  __shared__ uint32_t s_mov[DEC];  // mover -> decoder: 16-B chunks committed to the ring
+  __shared__ uint16_t s_rec[kSplit ? RJ_HL_REC + 1 : 1][kPairs];  // tail lanes' MCU-start records (+ scratch)
+  __shared__ uint32_t s_nrec[kPairs];  // records published by the tail (bit 31: no more will come)
   __shared__ uint32_t s_T, s_ne;
   const uint32_t tid = threadIdx.x;
-  const bool mover = tid >= RJ_HL_DEC;
-  const uint32_t L = mover ? tid - RJ_HL_DEC : tid;  // the decoder lane (LDS column)
+  const bool mover = tid >= uint32_t(DEC);
+  const uint32_t L = mover ? tid - DEC : tid;  // the decoder lane (LDS column)
   if (flags != nullptr && !mover) __builtin_amdgcn_s_setprio(2);  // the serial chains win issue over streaming K2 waves
   if (tid == 0) s_ne = 0;
-  const uint32_t g = lane0 + blockIdx.x * RJ_HL_DEC + L;
+  const uint32_t g = lane0 + blockIdx.x * DEC + L;
   bool pending = g < lane0 + nlanes;
-  uint32_t gseg = 0;
+  uint32_t gseg = 0, role = 0;
   if (pending) {
-    gseg = rj_lane_seg(coefs, g);
-    pending = gseg != 0xFFFFFFFFu;
+    const uint32_t e = rj_lane_seg(coefs, g);
+    pending = e != 0xFFFFFFFFu;
+    gseg = kSplit ? e & ~(RJ_LANE_HEAD | RJ_LANE_TAIL) : e;
+    role = kSplit ? e & (RJ_LANE_HEAD | RJ_LANE_TAIL) : 0u;
   }
+  const bool head = kSplit && role == RJ_LANE_HEAD;
+  const bool tail = kSplit && role == RJ_LANE_TAIL;
+  const uint32_t pair = (L >> 6) * 32u + (L & 31u);  // a head lane and its tail share the record column
   int i = 0;
   if (pending) i = upper_index(nimg, gseg, [&](int qq) { return imgs[qq].seg_prefix; });
   const RjImageDev &im = imgs[i];
@@ -226,17 +258,19 @@ __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restri
     {
       const uint4 *src = reinterpret_cast<const uint4 *>(lean + T);
       uint4 *d4 = reinterpret_cast<uint4 *>(s_lut);
-      for (uint32_t w = tid; w < RJ_HL_LUT_WORDS / 4; w += RJ_HL_WG) d4[w] = gp(src)[w];
+      for (uint32_t w = tid; w < RJ_HL_LUT_WORDS / 4; w += 2 * DEC) d4[w] = gp(src)[w];
     }
     __syncthreads();
     if (!(pending && my_ts == T)) continue;
     pending = false;
     const uint32_t seg = gseg - im.seg_prefix;
     const RjSegDev sg = gp(im.segs)[seg];
-    const uint32_t nbytes = sg.dst_len;
-    const uint4 *src = reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off);
+    // split intervals: the tail's bytes start at the split byte
+    const uint32_t sp_byte = (head || tail) ? rj_split_byte(sg.dst_len) : 0u;
+    const uint32_t nbytes = tail ? sg.dst_len - sp_byte : sg.dst_len;
+    const uint4 *src = reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off + (tail ? sp_byte : 0u));
     const uint32_t nchunks = (nbytes + 15) / 16;
-    const HCol ring{&s_ring[0][L]};
+    const HCol<DEC> ring{&s_ring[0][L]};
 
     if (mover) {
       // ---- mover: keep the ring's free chunk slots filled (past the data: zero chunks, the
@@ -282,12 +316,23 @@ __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restri
     const uint32_t nb2 = 2 * nblk;
     const uint32_t nbits = nbytes * 8u;
     const uint32_t blocks = sg.mcu_count * nblk;
-    uint32_t *ent = coefs.ent + im.ent_off + sg.ent_off;
-    const uint64_t ent_abs = im.ent_off + sg.ent_off;
-    RjPiece *piece = coefs.piece + rj_seg_lane0(coefs, gseg);
+    // entry regions: the interval's own; a tail lane writes its pair's slot of the split region
+    const uint64_t tail_abs = kSplit ? split.ent + uint64_t((g >> 6) * 32u + (g & 31u)) * split.cap : 0u;
+    const uint64_t ent_abs = tail ? tail_abs : im.ent_off + sg.ent_off;
+    uint32_t *ent = coefs.ent + ent_abs;
+    RjPiece *piece = coefs.piece + rj_seg_lane0_k<kSplit>(coefs, gseg);
     const RjTableSet *tset = tabsets + T;  // canonical search (escape path)
-    const HCol stage{&s_stage[0][L]};
+    const HCol<DEC> stage{&s_stage[0][L]};
+    // split state: records (tail), the last MCU start seen (head), the head's scan over the records
+    uint16_t *const recs = &s_rec[0][kSplit ? pair : 0u];
+    uint32_t nr = tail ? 0u : uint32_t(RJ_HL_REC);
+    uint32_t mpos = 0, mleft = 0, jrec = 0, blk_head = 0, skip_tail = 0;
+    bool mseen = false, synced = false, checking = head;
+    const uint32_t sp_bits = sp_byte * 8u;
+    if (tail) lds_st(&s_nrec[pair], 0u);
     // a phase reads ring words up to rr + 8 (8 symbols of <= 31 bits, the last one's read-ahead)
+// (avail: ring words known to be committed; the decoder re-reads the mover's count only when a
+// lane's next phase could read past them)
 #define RJ_HL_WAIT_RING(upto)                                                                     \
   {                                                                                               \
     uint32_t cmv = lds_ld(&s_mov[L]);                                                             \
@@ -295,8 +340,10 @@ __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restri
       __builtin_amdgcn_s_sleep(2);                                                                \
       cmv = lds_ld(&s_mov[L]);                                                                    \
     }                                                                                             \
+    avail = 4u * cmv;                                                                             \
     asm volatile("" ::: "memory");                                                                \
   }
+    uint32_t avail = 0;
     RJ_HL_WAIT_RING(10u);
     uint32_t q = 0;               // -(bits consumed)
     // q = 0 is bit 0: alignbit(wa, wb, 0) would return wb, so the window starts one word back
@@ -325,27 +372,68 @@ __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restri
 #define RJ_HL_T2
 #endif
     while (__builtin_amdgcn_ballot_w64(blocks_left > 0) != 0) {
+      if (blocks_left == 0) continue;  // finished lanes sit out the rest of the wave's phases
       RJ_HL_T0;
-      // no lane can finish its blocks or reach its data's end in this phase: the lean body
-      const bool fast = __builtin_amdgcn_ballot_w64(
-                            !(blocks_left >= RJ_HL_PHASE && !skip && (0u - q) + RJ_HL_PHASE * 31u < nbits)) == 0;
-      if (fast) {
+      // no live lane can finish its blocks or reach its data's end in this phase: the lean body
+      const bool safe = __builtin_amdgcn_ballot_w64(
+                            !(blocks_left >= RJ_HL_PHASE && !skip && (0u - q) + RJ_HL_PHASE * 31u < nbits)) != 0;
+      // split: a tail still recording, or a head that may pass an MCU start beyond the split
+      const bool sync = kSplit && __builtin_amdgcn_ballot_w64(
+                                      nr < RJ_HL_REC || (checking && (0u - q) + RJ_HL_PHASE * 31u >= sp_bits)) != 0;
+      if (!safe && !sync) {
 #pragma unroll
-        for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(false);
+        for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(false, false);
+      } else if (!safe) {
+#pragma unroll
+        for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(false, kSplit);
       } else {
 #pragma unroll
-        for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(true);
+        for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(true, kSplit);
       }
-      RJ_HL_T1(fast);
+      RJ_HL_T1(!safe);
       // ---- phase end: words below rr - 2 (the one in wa) are free for the mover; a full stage
-      // group leaves (< 8 stay pending); wait until the next phase's words are in the ring ----
+      // group leaves (< GROUP stay pending); wait until the next phase's words are in the ring ----
       lds_st(&s_dec[L], rr - 2u);
-      if (ne - fl >= RJ_HL_GROUP) {
-        RJ_HL_X_FLUSH(hl_flush(stage, fl, ent + fl));
-        fl += RJ_HL_GROUP;
+      if (ne - fl >= GROUP) {
+        RJ_HL_X_FLUSH((hl_flush<DEC, GROUP>(stage, fl, ent + fl)));
+        fl += GROUP;
       }
-      RJ_HL_WAIT_RING(rr + 9u);
-      wc = ring[rr & (RJ_HL_WORDS - 1)];  // the last step's read-ahead may predate the commit
+      if (kSplit) {
+        if (tail) {  // publish the records (16-bit positions: the next phase must stay below 2^16)
+          if ((0u - q) >= RJ_HL_REC_LIMIT) nr = RJ_HL_REC;
+          lds_st(&s_nrec[pair], nr | ((nr >= RJ_HL_REC || blocks_left == 0) ? 0x80000000u : 0u));
+        }
+        if (checking && mseen && mpos >= sp_bits) {
+          // head: is its last MCU start one of the tail's?  (records are in position order)
+          const uint32_t rel = mpos - sp_bits;
+          const uint32_t pub = lds_ld(&s_nrec[pair]);
+          const uint32_t nrec = pub & 0xFFFFu;
+          uint32_t r = 0;
+          while (jrec < nrec) {
+            r = *(const __attribute__((address_space(3))) volatile uint16_t *)(&recs[jrec * kPairs]);
+            if (r >= rel) break;
+            jrec++;
+          }
+          if (jrec < nrec && r == rel) {
+            synced = true;  // same state from here on: the rest is the tail's
+            checking = false;
+            blk_head = blocks - mleft;
+            skip_tail = (jrec + 1) * nblk;  // record j: after the tail's first j + 1 MCUs
+            blocks_left = 0;
+          } else if (jrec >= nrec && (pub >> 31) != 0) {
+            checking = false;  // no record left to meet: the head decodes the whole interval
+          }
+        }
+        mseen = false;
+      }
+#ifdef RJ_HL_EAGER_RING
+      if (true) {
+#else
+      if (__builtin_amdgcn_ballot_w64(avail < rr + 9u) != 0) {
+#endif
+        RJ_HL_WAIT_RING(rr + 9u);
+        wc = ring[rr & (RJ_HL_WORDS - 1)];  // the last step's read-ahead may predate the commit
+      }
       RJ_HL_T2;
     }
     lds_st(&s_dec[L], RJ_HL_FIN);
@@ -359,12 +447,19 @@ __global__ __launch_bounds__(RJ_HL_WG, 2) void k_huff(const RjImageDev *__restri
       atomicAdd(&rj_hl_stamp[5], (unsigned long long)st_esc);
     }
 #endif
-    stage[ne & (RJ_HL_STAGE - 1)] = RJ_RE_TERM;
-    while (fl < ne + 1) {  // [fl, ne]: at most 16 entries, the terminator included
-      hl_flush(stage, fl, ent + fl);
-      fl += RJ_HL_GROUP;
+    stage[ne & (kStage - 1)] = RJ_RE_TERM;
+    while (fl < ne + 1) {  // [fl, ne]: at most 2 GROUP entries, the terminator included
+      hl_flush<DEC, GROUP>(stage, fl, ent + fl);
+      fl += GROUP;
     }
-    *gp(piece) = RjPiece{ent_abs, 0u, blocks, 1u, {0, 0, 0}};
+    if (!tail) {
+      if (synced) {
+        gp(piece)[0] = RjPiece{ent_abs, 0u, blk_head, 2u, {0, 0, 0}};
+        gp(piece)[1] = RjPiece{tail_abs, blk_head, blocks - blk_head, skip_tail, {0, 0, 0}};  // npieces: skip
+      } else {
+        *gp(piece) = RjPiece{ent_abs, 0u, blocks, 1u, {0, 0, 0}};
+      }
+    }
     if (coefs.count) atomicAdd(&s_ne, ne + 1);
     if (flags != nullptr) {  // streaming K2: publish the interval (release after this wave's stores)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -393,11 +488,18 @@ void DumpHuffStamps() {
 
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
-                           RjCoefBuf coefs, uint32_t *flags, uint32_t epoch, uint32_t *done, uint32_t extra_lds) {
+                           RjCoefBuf coefs, uint32_t *flags, uint32_t epoch, uint32_t *done, uint32_t extra_lds,
+                           const RjHuffSplit *split) {
   if (nlanes == 0) return hipSuccess;
-  static_assert(RJ_HL_DEC == 256, "HuffLaneWaves");
-  hipLaunchKernelGGL(k_huff, dim3((nlanes + RJ_HL_DEC - 1) / RJ_HL_DEC), dim3(RJ_HL_WG), extra_lds, st, imgs, nimg, lane0, nlanes,
-                     destuffed, tabsets, lean, coefs, flags, epoch, done);
+  static_assert(RJ_HL_SPLIT_DEC == 512, "HuffLaneWaves / the split lane layout");
+  if (split != nullptr) {  // one workgroup per CU: the LUT is shared by 512 decoder lanes
+    hipLaunchKernelGGL((k_huff<RJ_HL_SPLIT_DEC, 8, true>), dim3((nlanes + RJ_HL_SPLIT_DEC - 1) / RJ_HL_SPLIT_DEC),
+                       dim3(2 * RJ_HL_SPLIT_DEC), 0, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs,
+                       nullptr, 0u, nullptr, *split);
+  } else {
+    hipLaunchKernelGGL((k_huff<256, 8, false>), dim3((nlanes + 255) / 256), dim3(512), extra_lds, st, imgs, nimg, lane0,
+                       nlanes, destuffed, tabsets, lean, coefs, flags, epoch, done, RjHuffSplit{0, 0});
+  }
   return hipGetLastError();
 }
 

@@ -52,7 +52,12 @@ __device__ __forceinline__ uint32_t rj_lane_seg(const RjCoefBuf &c, uint32_t lan
   return c.lane_seg ? *gp(c.lane_seg + lane) : lane;
 }
 __device__ __forceinline__ uint32_t rj_seg_lane0(const RjCoefBuf &c, uint32_t seg) {
-  return c.seg_lane0 ? *gp(c.seg_lane0 + seg) : seg;
+  return c.seg_lane0 ? *gp(c.seg_lane0 + seg) : seg << c.piece_shift;
+}
+// the same where the kernel instance knows the layout (kSplit: a lean split launch, piece_shift 1)
+template <bool kSplit>
+__device__ __forceinline__ uint32_t rj_seg_lane0_k(const RjCoefBuf &c, uint32_t seg) {
+  return c.seg_lane0 ? *gp(c.seg_lane0 + seg) : (kSplit ? seg << 1 : seg);
 }
 
 // index of the last entry with prefix <= key (prefix[0] == 0, monotone)
