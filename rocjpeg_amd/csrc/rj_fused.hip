@@ -220,17 +220,6 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
   }
 }
 
-// Inclusive prefix sum over the wave's 64 lanes (DPP: row shifts, then row broadcasts).
-__device__ __forceinline__ int wave_scan(int x) {
-  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
-  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
-  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
-  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
-  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
-  return x;
-}
-
 // DC prediction of a strip of raw-entry blocks (lean K1 wrote differences; T.81 F.2.1.3.1):
 // lane = block of the strip (MCU order), its component c.  Per component an inclusive scan of
 // the differences over the strip, plus the running predictor `carry` of the previous strips of

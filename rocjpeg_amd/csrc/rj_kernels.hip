@@ -24,14 +24,10 @@ namespace rj {
 // ---------------------------------------------------------------------------------------
 // helpers
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v, uint32_t lane, uint32_t &total) {
-  uint32_t x = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(x, off, 64);
-    if (lane >= uint32_t(off)) x += y;
-  }
-  total = __shfl(x, 63, 64);
+// exclusive prefix sum over the wave (DPP scan, no LDS round trips); total: the wave's sum
+__device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v, uint32_t &total) {
+  const uint32_t x = uint32_t(wave_scan(int(v)));
+  total = __builtin_amdgcn_readlane(x, 63);
   return x - v;
 }
 
@@ -74,6 +70,30 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
   for (int c = 0; c < kIt; c++) {
     const uint32_t base = uint32_t(c) * 256u;
     if (base >= len) break;  // wave-uniform
+    // fast path: a whole chunk with no FF byte (and no FF in front of it) keeps every byte --
+    // aligned dword stores: dword j of the output gets lane j-1's top bytes and lane j's low ones
+    {
+      const uint32_t t = ~w[c];
+      const bool ff = ((t - 0x01010101u) & ~t & 0x80808080u) != 0;  // some byte == 0xFF
+      if (base + 256u <= len && prev_byte != 0xFFu && __builtin_amdgcn_ballot_w64(ff) == 0) {
+        const uint32_t wc = w[c];
+        const uint32_t m = uint32_t(reinterpret_cast<uintptr_t>(dst) + out) & 3u;  // wave-uniform
+        uint8_t *D = dst + out - m;  // 4-B aligned
+        if (m == 0) {
+          *gp(reinterpret_cast<uint32_t *>(D) + lane) = wc;
+        } else {
+          const uint32_t e = __builtin_amdgcn_alignbyte(wc, wave_prev(wc), 4u - m);
+          if (lane > 0) *gp(reinterpret_cast<uint32_t *>(D) + lane) = e;
+          if (lane == 0)
+            for (uint32_t k = 0; k < 4u - m; k++) gp(D)[m + k] = uint8_t(wc >> (8 * k));
+          if (lane == 63)
+            for (uint32_t k = 4u - m; k < 4u; k++) gp(D)[256u + k - (4u - m)] = uint8_t(wc >> (8 * k));
+        }
+        out += 256u;
+        prev_byte = __builtin_amdgcn_readlane(wc, 63) >> 24;
+        continue;
+      }
+    }
     const uint32_t p = base + 4 * lane;
     uint32_t b[4];
 #pragma unroll
@@ -81,9 +101,9 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
     // the byte after this chunk: the next chunk's first byte, or the one behind the block
     uint32_t nb_next = after;
     if (c + 1 < kIt && base + 256 < len) nb_next = __builtin_amdgcn_readfirstlane(w[c + 1]) & 255u;
-    uint32_t prev = __shfl_up(b[3], 1, 64);
+    uint32_t prev = wave_prev(b[3]);
     if (lane == 0) prev = prev_byte;
-    uint32_t next = __shfl_down(b[0], 1, 64);
+    uint32_t next = wave_next(b[0]);
     if (lane == 63) next = nb_next;
     uint32_t keep = 0;
 #pragma unroll
@@ -95,12 +115,12 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
       keep |= (drop ? 0u : 1u) << k;
     }
     uint32_t total;
-    uint32_t o = wave_exclusive_scan(__popc(keep), lane, total) + out;
+    uint32_t o = wave_exclusive_scan(__popc(keep), total) + out;
 #pragma unroll
     for (int k = 0; k < 4; k++)
       if (keep & (1u << k)) gp(dst)[o++] = uint8_t(b[k]);
     out += total;
-    prev_byte = __shfl(b[3], 63, 64);
+    prev_byte = __builtin_amdgcn_readlane(b[3], 63);
   }
   // last block: zero the interval's slack after the data (>= 16 B, rj_stream.cpp BuildPlan):
   // K1 reads whole 16-B chunks and must see zero bits past the end, as libjpeg inserts

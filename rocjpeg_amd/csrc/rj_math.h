@@ -60,6 +60,24 @@ __device__ __forceinline__ uint32_t rj_seg_lane0_k(const RjCoefBuf &c, uint32_t 
   return c.seg_lane0 ? *gp(c.seg_lane0 + seg) : (kSplit ? seg << 1 : seg);
 }
 
+// Inclusive prefix sum over the wave's 64 lanes (DPP: row shifts, then row broadcasts; gfx9).
+__device__ __forceinline__ int wave_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+// lane l gets lane l - 1's x (lane 0: 0) / lane l + 1's x (lane 63: 0): DPP wave_shr:1 / wave_shl:1
+__device__ __forceinline__ uint32_t wave_prev(uint32_t x) {
+  return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ uint32_t wave_next(uint32_t x) {
+  return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x130, 0xF, 0xF, false));
+}
+
 // index of the last entry with prefix <= key (prefix[0] == 0, monotone)
 template <typename F>
 __device__ __forceinline__ int upper_index(int n, uint32_t key, F prefix_of) {
