@@ -40,6 +40,45 @@ def _c2_images(count, seed0=1234):
         return list(ex.map(bench._make_jpeg, [(s, bench.WORKLOADS["c2"]["gen"]) for s in range(seed0, seed0 + count)]))
 
 
+@pytest.fixture(scope="module")
+def split_dec():
+    """A handle with the lean split launch on (RJ_SPLIT=1, read at handle creation)."""
+    torch()
+    old = os.environ.get("RJ_SPLIT")
+    os.environ["RJ_SPLIT"] = "1"
+    try:
+        d = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    finally:
+        if old is None:
+            del os.environ["RJ_SPLIT"]
+        else:
+            os.environ["RJ_SPLIT"] = old
+    yield d
+    d.close()
+
+
+def test_c2_1024_split_launch(split_dec):
+    """The C2 call with the lean split launch: the longest 61,440 intervals decoded by head +
+    tail lanes (one workgroup of 1024 threads per CU), every image equal to the oracle."""
+    t = torch()
+    distinct, copies = 64, 16
+    datas = _c2_images(distinct, seed0=4321)
+    with ThreadPoolExecutor(16) as ex:
+        want = list(ex.map(lambda d: O.oracle_decode(d, int(R.OutputFormat.RGB), [(1080, 5760)]), datas))
+    streams = [R.JpegStream(datas[i % distinct]) for i in range(distinct * copies)]
+    out = t.full((len(streams), 1080, 5760), 0xA5, dtype=t.uint8, device="cuda")
+    imgs = [R.make_image([out[i].data_ptr()], [5760]) for i in range(len(streams))]
+    split_dec.set_profiling(True)
+    st = split_dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs)
+    tm = split_dec.last_timings()
+    split_dec.set_profiling(False)
+    assert st == 0, R.error_name(st)
+    assert tm["lean_k1"] == 1 and tm["lean_split"] > 0
+    ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
+    bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
+    assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
+
+
 def test_c2_1024_default_pipelined_layout(dec):
     t = torch()
     distinct, copies = 256, 4
