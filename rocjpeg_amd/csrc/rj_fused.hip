@@ -237,11 +237,14 @@ __device__ __forceinline__ bool restore_dc(uint8_t *s_buf, uint32_t tid, uint32_
   const uint32_t mstart = m - m % ri;
   const int rlane = mstart >= mcu_row0 + mx0 ? int((mstart - mcu_row0 - mx0) * nblk) : -1;
   int pred = 0;
+  // an interval starting inside the strip past its first lane (a restart interval shorter than
+  // the strip) needs the scan value in front of it; with row intervals none does
+  const bool mid = __ballot(tid < nb && rlane > 0) != 0;
 #pragma unroll
   for (uint32_t cc = 0; cc < 3; cc++) {
     const int sc = wave_scan(c == cc ? dd : 0);
     // value of the scan just before the reset lane (0 if the reset is at lane 0)
-    const int before = __shfl(sc, rlane > 0 ? rlane - 1 : 0);
+    const int before = mid ? __shfl(sc, rlane > 0 ? rlane - 1 : 0) : 0;
     const int mine = rlane < 0 ? carry[cc] + sc : sc - (rlane > 0 ? before : 0);
     if (c == cc) pred = mine;
     // the next strip starts from the last block's predictor

@@ -28,7 +28,9 @@ namespace rj {
 
 #define RJ_HL_CHUNKS 8                      // 16-B chunks in a lane's bit ring
 #define RJ_HL_WORDS (RJ_HL_CHUNKS * 4)      // 32 words
-#define RJ_HL_PHASE 8                       // symbols per phase (<= 8 words: 31 bits per symbol)
+#ifndef RJ_HL_PHASE
+#define RJ_HL_PHASE 8                       // symbols per phase of the whole-interval launch
+#endif
 // LDS byte offsets of the four tables (RjLeanTables order)
 #define RJ_HL_AC_BYTES (RJ_HL_AC_WORDS * 4)
 #define RJ_HL_DC0 (2 * RJ_HL_AC_BYTES)
@@ -208,7 +210,7 @@ __device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) { *(lds_vu32 *)(
 // the tail piece's npieces field; lean raw entries carry DC differences, so no DC correction is
 // needed).  With no equal MCU start the head decodes the whole interval.  A tail that reaches libjpeg's insufficient-data point stops: K2 zero-fills
 // the piece's missing blocks exactly as libjpeg's zero blocks.
-template <int DEC, int GROUP, bool kSplit>
+template <int DEC, int GROUP, bool kSplit, int PHASE>
 __global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
     const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0, uint32_t nlanes, const uint8_t *__restrict__ destuffed,
     const RjTableSet *__restrict__ tabsets, const RjLeanTables *__restrict__ lean, RjCoefBuf coefs, uint32_t *flags,
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
     asm volatile("" ::: "memory");                                                                \
   }
     uint32_t avail = 0;
-    RJ_HL_WAIT_RING(10u);
+    RJ_HL_WAIT_RING(uint32_t(PHASE) + 2u);  // words 0 .. PHASE + 1 (a phase reads up to rr + PHASE)
     uint32_t q = 0;               // -(bits consumed)
     // q = 0 is bit 0: alignbit(wa, wb, 0) would return wb, so the window starts one word back
     // (words -1, 0; j = (pos - 1) >> 5): wa is a dummy word whose bits are never returned
@@ -376,19 +378,19 @@ __global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
       RJ_HL_T0;
       // no live lane can finish its blocks or reach its data's end in this phase: the lean body
       const bool safe = __builtin_amdgcn_ballot_w64(
-                            !(blocks_left >= RJ_HL_PHASE && !skip && (0u - q) + RJ_HL_PHASE * 31u < nbits)) != 0;
+                            !(blocks_left >= PHASE && !skip && (0u - q) + PHASE * 31u < nbits)) != 0;
       // split: a tail still recording, or a head that may pass an MCU start beyond the split
       const bool sync = kSplit && __builtin_amdgcn_ballot_w64(
-                                      nr < RJ_HL_REC || (checking && (0u - q) + RJ_HL_PHASE * 31u >= sp_bits)) != 0;
+                                      nr < RJ_HL_REC || (checking && (0u - q) + PHASE * 31u >= sp_bits)) != 0;
       if (!safe && !sync) {
 #pragma unroll
-        for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(false, false);
+        for (uint32_t s_ = 0; s_ < PHASE; s_++) RJ_HL_STEP(false, false);
       } else if (!safe) {
 #pragma unroll
-        for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(false, kSplit);
+        for (uint32_t s_ = 0; s_ < PHASE; s_++) RJ_HL_STEP(false, kSplit);
       } else {
 #pragma unroll
-        for (uint32_t s_ = 0; s_ < RJ_HL_PHASE; s_++) RJ_HL_STEP(true, kSplit);
+        for (uint32_t s_ = 0; s_ < PHASE; s_++) RJ_HL_STEP(true, kSplit);
       }
       RJ_HL_T1(!safe);
       // ---- phase end: words below rr - 2 (the one in wa) are free for the mover; a full stage
@@ -429,9 +431,9 @@ __global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
 #ifdef RJ_HL_EAGER_RING
       if (true) {
 #else
-      if (__builtin_amdgcn_ballot_w64(avail < rr + 9u) != 0) {
+      if (__builtin_amdgcn_ballot_w64(avail < rr + PHASE + 1u) != 0) {
 #endif
-        RJ_HL_WAIT_RING(rr + 9u);
+        RJ_HL_WAIT_RING(rr + PHASE + 1u);
         wc = ring[rr & (RJ_HL_WORDS - 1)];  // the last step's read-ahead may predate the commit
       }
       RJ_HL_T2;
@@ -493,11 +495,11 @@ hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uin
   if (nlanes == 0) return hipSuccess;
   static_assert(RJ_HL_SPLIT_DEC == 512, "HuffLaneWaves / the split lane layout");
   if (split != nullptr) {  // one workgroup per CU: the LUT is shared by 512 decoder lanes
-    hipLaunchKernelGGL((k_huff<RJ_HL_SPLIT_DEC, 8, true>), dim3((nlanes + RJ_HL_SPLIT_DEC - 1) / RJ_HL_SPLIT_DEC),
+    hipLaunchKernelGGL((k_huff<RJ_HL_SPLIT_DEC, 8, true, 8>), dim3((nlanes + RJ_HL_SPLIT_DEC - 1) / RJ_HL_SPLIT_DEC),
                        dim3(2 * RJ_HL_SPLIT_DEC), 0, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs,
                        nullptr, 0u, nullptr, *split);
   } else {
-    hipLaunchKernelGGL((k_huff<256, 8, false>), dim3((nlanes + 255) / 256), dim3(512), extra_lds, st, imgs, nimg, lane0,
+    hipLaunchKernelGGL((k_huff<256, RJ_HL_PHASE, false, RJ_HL_PHASE>), dim3((nlanes + 255) / 256), dim3(512), extra_lds, st, imgs, nimg, lane0,
                        nlanes, destuffed, tabsets, lean, coefs, flags, epoch, done, RjHuffSplit{0, 0});
   }
   return hipGetLastError();
