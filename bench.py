@@ -444,7 +444,7 @@ def main():
     gen_pool.join()
     t_gen = time.perf_counter() - t_gen
     turbo = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the CPU comparator: N = 1 only
         turbo = TurboBaseline(mine[0], mine[1], mine[2], cores)
 
     import torch
