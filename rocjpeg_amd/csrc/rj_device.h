@@ -214,7 +214,8 @@ struct RjLeanTables {  // LDS image: AC0, AC1 (first level + subtables), DC0, DC
   uint32_t ac[2][RJ_HL_AC_WORDS];
   uint32_t dc[2][RJ_HL_DC_WORDS];
 };
-// Raw entry (lean K1 -> K2): [14:0] the symbol's extra bits, [19:16] s, [27:21] zigzag position
+// Raw entry (lean K1 -> K2): [15:0] the symbol's code and extra bits, right-aligned (its low s
+// bits are the extra bits), [19:16] s, [27:21] zigzag position
 // (0 = the block's DC, which holds the DC *difference*; 64..78 only on corrupt data: position 63;
 // 127 = end of stream), bit 28: zero block (libjpeg's insufficient-data / missing-marker blocks:
 // every coefficient 0, DC absolute).

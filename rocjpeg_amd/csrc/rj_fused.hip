@@ -126,7 +126,7 @@ struct Nav {
 // cbits: component of each block within the MCU (2 bits each), for the DC corrections.
 // libjpeg HUFF_EXTEND of a raw entry (lean K1): the s extra bits as a signed value (s = 0 -> 0)
 __device__ __forceinline__ int raw_value(uint32_t e) {
-  const uint32_t s = (e >> 16) & 15u, raw = e & 0x7FFFu;
+  const uint32_t s = (e >> 16) & 15u, raw = __builtin_amdgcn_ubfe(e, 0u, s);  // K1 keeps the code bits above
   const uint32_t half = (1u << s) >> 1;
   return raw < half ? int(raw) - int(2 * half - 1) : int(raw);
 }

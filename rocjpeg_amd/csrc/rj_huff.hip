@@ -133,8 +133,10 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
       RJ_HL_COUNT_ESC;                                                                                    \
       if (e >= RJ_HL_ESC) e = hl_escape(e, peek, tsh != 21u, acb, s_lut, tset, pat >> b);                 \
     }                                                                                                     \
-    const uint32_t raw = __builtin_amdgcn_ubfe(peek, e, e >> 16);                                         \
-    uint32_t entry = ((e & 0x0FEF0000u) | raw) + (k << 21);                                               \
+    /* the symbol's n bits right-aligned (code, then its s extra bits: K2 keeps the low s) */           \
+    const uint32_t raw = peek >> (e & 31u);                                                               \
+    uint32_t entry = __builtin_amdgcn_perm(e, raw, 0x07060100u); /* raw's low half, e's fields above */ \
+    entry += k << 21;                                                                                     \
     uint32_t emit = (e >> 13) & 1u;                                                                       \
     const uint32_t qold = q;                                                                              \
     q -= (e >> 8) & 31u;                                                                                  \
