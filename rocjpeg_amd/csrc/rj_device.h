@@ -95,14 +95,19 @@ struct RjHuffSplit {
 #define RJ_MAX_RECORDS 64         // chunk-start records per speculative chunk
 #define RJ_RECORD_EVERY 8         // one record every 8th block start of a chunk's head
 
-// Chunking of an interval of `bytes` raw entropy-coded bytes: about RJ_CHUNK_BYTES per lane;
-// intervals below two chunks are decoded by one lane with the exact serial semantics.
+// Chunking of an interval of `bytes` raw entropy-coded bytes: intervals shorter than
+// RJ_SPLIT_BYTES are decoded by one lane with the exact serial semantics (so a call whose
+// restart intervals are MCU rows keeps the lean K1); longer ones get about RJ_CHUNK_BYTES per
+// lane (3 KB measured best for restart-less 1080p: 81k -> 118k images/s over 8 KB chunks; the
+// resynchronisation costs ~1,000 bits per chunk boundary).
 #ifndef RJ_CHUNK_BYTES
-#define RJ_CHUNK_BYTES 8192u
+#define RJ_CHUNK_BYTES 3072u
 #endif
+#define RJ_SPLIT_BYTES 12288u
 #define RJ_OVERLAP_CHUNKS 3u      // a lane may decode this many chunk lengths past its own end
 #define RJ_CHUNK_ENT_PER_BYTE 4u  // region budget of a chunk lane (typical ~1.7); overflow -> serial path
 __host__ __device__ inline uint32_t rj_chunks(uint32_t bytes) {
+  if (bytes < RJ_SPLIT_BYTES) return 1u;
   const uint32_t n = (bytes + RJ_CHUNK_BYTES / 2) / RJ_CHUNK_BYTES;
   return n < 2 ? 1u : (n > 4096 ? 4096u : n);
 }

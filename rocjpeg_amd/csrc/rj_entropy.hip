@@ -3,7 +3,7 @@
 // The reference hands this step to VCN (src/rocjpeg_vaapi_decoder.cpp:677-689).  Here every
 // restart interval is decoded by one or more lanes:
 //
-//   * short intervals (< 2 chunks of RJ_CHUNK_BYTES): one lane, exact serial semantics --
+//   * short intervals (< RJ_SPLIT_BYTES): one lane, exact serial semantics --
 //     libjpeg's "insufficient data" rule (the MCU that runs past the data is decoded with zero
 //     bits, the rest of the interval is zero) and missing-RST intervals;
 //   * long intervals (long DRI, or no DRI at all -- every reference fixture): one lane per
