@@ -93,7 +93,9 @@ struct RjHuffSplit {
 #define RJ_ENT_TERM (127u << 16)  // end-of-stream marker
 #define RJ_ENT_SLACK 1024         // entries of read slack after the last region (K2 reads 512-entry windows)
 #define RJ_MAX_RECORDS 64         // chunk-start records per speculative chunk
+#ifndef RJ_RECORD_EVERY
 #define RJ_RECORD_EVERY 8         // one record every 8th block start of a chunk's head
+#endif
 
 // Chunking of an interval of `bytes` raw entropy-coded bytes: intervals shorter than
 // RJ_SPLIT_BYTES are decoded by one lane with the exact serial semantics (so a call whose
