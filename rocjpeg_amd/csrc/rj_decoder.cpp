@@ -569,10 +569,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     d.tabset = tab_of[i];
     {  // the int32 IDCT is exact while |coefficient x quantiser| < 2^14 (rj_math.h)
       uint32_t qmax = 1;
-      for (int c = 0; c < in.ncomp; c++) {
-        const uint16_t *qz = p.tables.qz[d.comp_tq[c] & 3];
-        for (int k = 0; k < 64; k++) qmax = std::max<uint32_t>(qmax, qz[k]);
-      }
+      for (int c = 0; c < in.ncomp; c++) qmax = std::max<uint32_t>(qmax, p.qmax[d.comp_tq[c] & 3]);
       d.idct_thr = 16383u / qmax;
     }
     d.nseg = uint32_t(p.segs.size());

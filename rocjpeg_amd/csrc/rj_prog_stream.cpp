@@ -461,8 +461,13 @@ void Stream::BuildProgressivePlan(const uint8_t *d) {
   // quant tables: component c's latched table in slot c (RjImageDev.comp_tq[c] = c); the
   // de-duplication key is those tables (no Huffman tables in the set: ht_loaded = 0, 0)
   std::memset(p.table_key, 0, sizeof(p.table_key));
-  for (int q = 0; q < 4; q++)
-    for (int k = 0; k < 64; k++) p.tables.qz[q][k] = q < s.ncomp ? p.pqlat[q][k] : 0;
+  for (int q = 0; q < 4; q++) {
+    p.qmax[q] = 1;
+    for (int k = 0; k < 64; k++) {
+      p.tables.qz[q][k] = q < s.ncomp ? p.pqlat[q][k] : 0;
+      p.qmax[q] = std::max<uint16_t>(p.qmax[q], p.tables.qz[q][k]);
+    }
+  }
   std::memcpy(p.table_key + 2 + sizeof(s.ht), p.pqlat, size_t(s.ncomp) * 64);
   p.table_hash = Fnv1a(1469598103934665603ull, p.table_key, sizeof(p.table_key));
 

@@ -344,8 +344,13 @@ bool Stream::BuildPlanHeader() {
         if (s.scomp[c].td == t || s.scomp[c].ta == t) { p.status = -3; return false; }
     }
   }
-  for (int q = 0; q < 4; q++)
-    for (int k = 0; k < 64; k++) p.tables.qz[q][k] = s.qt_zz[q][k];
+  for (int q = 0; q < 4; q++) {
+    p.qmax[q] = 1;
+    for (int k = 0; k < 64; k++) {
+      p.tables.qz[q][k] = s.qt_zz[q][k];
+      p.qmax[q] = std::max<uint16_t>(p.qmax[q], s.qt_zz[q][k]);
+    }
+  }
   {
     static_assert(sizeof(s.ht) == 2 * (16 + 12 + 16 + 162), "raw DHT layout");
     uint8_t *kp = p.table_key;

@@ -53,6 +53,7 @@ struct DecodePlan {
   uint64_t entries = 0;            // sparse-coefficient entries reserved (worst case)
   uint32_t nchunks = 0;            // K1 lanes (chunks) over all intervals
   RjTableSet tables;               // derived tables
+  uint16_t qmax[4] = {1, 1, 1, 1}; // largest entry of each quant table slot (the IDCT's exact domain)
   // De-duplication key: the raw DHT/DQT content the derived tables are a function of (the
   // batch planner compares these ~670 B instead of the 14.5 KB RjTableSet) and its hash.
   static constexpr size_t kTableKeyBytes = 2 + 2 * (16 + 12 + 16 + 162) + 4 * 64;
