@@ -551,7 +551,7 @@ def main():
             "huffman_detail": {"intervals": t["intervals"], "chunks": t["chunks"],
                                "split_intervals": t["split_intervals"], "serial_fallbacks": t["serial_fallbacks"],
                                "entry_bytes_per_image": round(t["entry_bytes"] / n), "lean_k1": t["lean_k1"],
-                               "lean_split": t["lean_split"],
+                               "lean_split": t["lean_split"], "k0_fused": t["k0_fused"],
                                "k2_stream": t["k2_stream"], "k2_stream_rows": t["k2_stream_rows"],
                                "k2_deferred_rows": t["k2_deferred_rows"], "k2_stream_ms": round(t["k2_stream_ms"], 4)},
             "end_to_end_algorithmic_GBps": round(imgs_total * per_img / elapsed / 1e9, 2),

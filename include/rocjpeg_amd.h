@@ -106,6 +106,8 @@ typedef struct {
   uint32_t wide_rows;
   /* lean K1 split launch: intervals decoded by a head and a tail lane (rj_huff.hip) */
   uint32_t lean_split;
+  /* 1: no K0 pass -- the lean K1 movers destuffed the raw bitstreams themselves (rj_huff.hip) */
+  uint32_t k0_fused;
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);

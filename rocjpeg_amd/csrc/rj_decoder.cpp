@@ -153,6 +153,7 @@ int Decoder::Initialize() {
   if (const char *l = getenv("RJ_K1_SOLO")) k1_solo_lds_ = uint32_t(std::max(0, atoi(l)));
   if (const char *sk = getenv("RJ_STREAM_K2")) stream_enabled_ = atoi(sk) != 0;
   if (const char *sp = getenv("RJ_SPLIT")) split_enabled_ = atoi(sp) != 0;
+  if (const char *fd = getenv("RJ_FUSE_DESTUFF")) fuse_destuff_ = atoi(fd) != 0;
   if (const char *sw = getenv("RJ_STREAM_WG")) stream_wg_per_cu_ = std::max(1, std::min(16, atoi(sw)));
   cu_count_ = std::max(1, prop.multiProcessorCount);
   RJ_HIP(hipHostMalloc(reinterpret_cast<void **>(&h_wide_flag_), 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -1158,7 +1159,11 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   RJ_HIP(hipMemcpyAsync(dbase, h, blob_a, hipMemcpyHostToDevice, stream_));
   if (cbuf.count) RJ_HIP(hipMemsetAsync(cbuf.count, 0, sizeof(unsigned long long), stream_));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
-  RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>()));
+  // lean-only calls: the K1 movers destuff the raw ECS themselves (rj_huff.hip), no K0 pass
+  const bool raw_k1 = lean && fuse_destuff_ && prog_images == 0 && !split_enabled_;
+  timings_.k0_fused = raw_k1 ? 1u : 0u;
+  if (!raw_k1) RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>()));
+  const uint8_t *k1_src = raw_k1 ? nullptr : d_destuff_.as<uint8_t>();
   if (prog_images) {  // progressive images: K1p level by level, then their K2 rows (dense)
     const uint32_t *d_plane = reinterpret_cast<const uint32_t *>(dbase + off_plane);
     if (profiling_) RJ_HIP(hipEventRecord(prog_ev_[0], stream_));
@@ -1293,23 +1298,16 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     constexpr uint32_t kBuckets = 4096;  // 32-B length buckets up to 128 KB
     const bool desc = lpt_ && ngroups == 1;  // one launch: longest intervals first
     lanes_desc = desc;
-    auto bucket = [desc](uint32_t len) {
-      const uint32_t b = std::min<uint32_t>(len >> 5, kBuckets - 1);
-      return desc ? kBuckets - 1 - b : b;
-    };
+    static_assert(kBuckets == 4096, "DecodePlan::seg_bucket (FinishSegs)");
+    auto bucket = [desc](uint32_t b) { return desc ? kBuckets - 1 - b : b; };
     std::vector<uint32_t> &pos = sc_.bucket_pos;
     pos.assign(kBuckets, 0);
     bool aligned = fused_images == uint32_t(n - int(prog_images)) || fused_images == 0;
     for (int i = 0; i < n; i++) {
       const DecodePlan &p = streams[i]->plan();
       if (p.progressive) continue;  // no K1 intervals, no rows in these launches
-      aligned = aligned && p.segs.size() == p.mcuy;
-      uint32_t m = 0;
-      for (const RjSegDev &sg : p.segs) {
-        pos[bucket(sg.src_len)]++;
-        aligned = aligned && sg.mcu_first == m && sg.mcu_count == p.mcux;
-        m += p.mcux;
-      }
+      aligned = aligned && p.rows_aligned;
+      for (const uint16_t b : p.seg_bucket) pos[bucket(b)]++;
     }
     for (uint32_t b = 0, cum = 0; b < kBuckets; b++) {
       const uint32_t c = pos[b];
@@ -1318,8 +1316,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
     lane_seg.resize(seg_total);  // built in cached memory, copied into the pinned blob below
     uint32_t *ls = lane_seg.data();
-    std::vector<uint32_t> &seg_pos = sc_.seg_pos;
-    seg_pos.resize(seg_total);
+    std::vector<uint32_t> &seg_pos = sc_.seg_pos;  // pipelined launch: each interval's lane
+    if (ngroups > 1) seg_pos.resize(seg_total);
     lane_rows = aligned;
     rows_from_lanes = ngroups > 1 && aligned;
     // rows from lanes: K2 row w of class g is lane lane_off[g] + w's interval, listed as
@@ -1329,18 +1327,28 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (rows_from_lanes) row_list.resize(seg_total);
     uint2 *rl = rows_from_lanes ? row_list.data() : nullptr;
     uint32_t gs = 0;
-    std::vector<uint2> &seg_len = sc_.seg_len;
-    if (lean) seg_len.resize(seg_total);
+    std::vector<uint2> &seg_len = sc_.seg_len;  // the split launch's planning only
+    const bool want_len = lean && split_enabled_;
+    if (want_len) seg_len.resize(seg_total);
+    const bool want_pos = ngroups > 1;
     for (int i = 0; i < n; i++) {
-      uint32_t r = 0;
-      const uint32_t nblk_i = streams[i]->plan().nblk_mcu;
-      for (const RjSegDev &sg : streams[i]->plan().segs) {
-        const uint32_t l = pos[bucket(sg.src_len)]++;
-        if (lean)
-          seg_len[gs] = uint2{(sg.flags & RJ_SEG_MISSING) ? 0u : sg.dst_len, sg.mcu_count * nblk_i};
-        ls[l] = gs;
-        if (rl) rl[l] = uint2{uint32_t(i), r++};
-        seg_pos[gs++] = l;
+      const DecodePlan &p = streams[i]->plan();
+      if (want_len || rl != nullptr || want_pos) {
+        uint32_t r = 0;
+        const uint32_t nblk_i = p.nblk_mcu;
+        for (size_t q = 0; q < p.segs.size(); q++) {
+          const uint32_t l = pos[bucket(p.seg_bucket[q])]++;
+          if (want_len) {
+            const RjSegDev &sg = p.segs[q];
+            seg_len[gs] = uint2{(sg.flags & RJ_SEG_MISSING) ? 0u : sg.dst_len, sg.mcu_count * nblk_i};
+          }
+          ls[l] = gs;
+          if (rl) rl[l] = uint2{uint32_t(i), r++};
+          if (want_pos) seg_pos[gs] = l;
+          gs++;
+        }
+      } else {  // one launch, no split planning: the lane order only
+        for (const uint16_t b : p.seg_bucket) ls[pos[bucket(b)]++] = gs++;
       }
     }
     if (rl) std::memcpy(h + off_row_list, rl, uint64_t(seg_total) * sizeof(uint2));
@@ -1482,7 +1490,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0, upload B, counters done
     RJ_HIP(hipStreamWaitEvent(pstream_[0], pev_[kMaxPipe - 1], 0));
     if (profiling_) RJ_HIP(hipEventRecord(k1s_[0], stream_));
-    RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, seg_total, d_destuff_.as<uint8_t>(), d_tabs, d_lean, cbuf,
+    RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, seg_total, k1_src, d_tabs, d_lean, cbuf,
                            d_flags_.as<uint32_t>(), epoch_, ctl + 3, k1_solo_lds_));
     if (profiling_) RJ_HIP(hipEventRecord(pk1_[0], stream_));
     if (profiling_) RJ_HIP(hipEventRecord(k2s_[0], pstream_[0]));
@@ -1504,7 +1512,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       for (int g = 0; g < ngroups; g++) {
         if (lean)
           RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g],
-                                 d_destuff_.as<uint8_t>(), d_tabs, d_lean, cbuf));
+                                 k1_src, d_tabs, d_lean, cbuf));
         else
           RJ_HIP(LaunchEntropyLanes(stream_, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g],
                                     d_destuff_.as<uint8_t>(), d_tabs, cbuf, epoch_));
@@ -1516,7 +1524,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       if (st != stream_) RJ_HIP(hipStreamWaitEvent(st, pev_[kMaxPipe - 1], 0));
       if (profiling_) RJ_HIP(hipEventRecord(k1s_[g], st));
       if (lean)
-        RJ_HIP(LaunchHuffLanes(st, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g], d_destuff_.as<uint8_t>(),
+        RJ_HIP(LaunchHuffLanes(st, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g], k1_src,
                                d_tabs, d_lean, cbuf));
       else
         RJ_HIP(LaunchEntropyLanes(st, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g], d_destuff_.as<uint8_t>(),
@@ -1545,12 +1553,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (lean && Dbg(kDebugNoDep)) {  // timing experiment: K1 beside K2, no dependency (wrong output)
       RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));
       RJ_HIP(hipStreamWaitEvent(pstream_[0], pev_[kMaxPipe - 1], 0));
-      RJ_HIP(LaunchHuffLanes(pstream_[0], d_imgs, n, 0u, seg_total, d_destuff_.as<uint8_t>(), d_tabs, d_lean, cbuf));
+      RJ_HIP(LaunchHuffLanes(pstream_[0], d_imgs, n, 0u, seg_total, k1_src, d_tabs, d_lean, cbuf));
       RJ_HIP(hipEventRecord(pev_[0], pstream_[0]));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
     } else if (lean) {  // no split interval: one pass, no resolution / serial stages
-      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, nsplit ? nl_split : seg_total, d_destuff_.as<uint8_t>(), d_tabs,
+      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, nsplit ? nl_split : seg_total, k1_src, d_tabs,
                              d_lean, cbuf, nullptr, 0u, nullptr, k1_solo_lds_, nsplit ? &hsplit : nullptr));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));

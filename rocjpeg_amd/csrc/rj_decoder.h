@@ -115,6 +115,7 @@ class Decoder {
   // first instead of doubling up on a CU beside a long-interval workgroup
   uint32_t k1_solo_lds_ = 16384;
   bool lean_enabled_ = true;       // env RJ_LEAN=0: the exact K1 (rj_entropy.hip) for row images too
+  bool fuse_destuff_ = false;      // env RJ_FUSE_DESTUFF=1: lean-only calls without K0, the K1 movers destuff (measured slower)
   bool split_enabled_ = false;     // env RJ_SPLIT=1: lean K1 head + tail lanes (rj_huff.hip; measured slower)
   bool stream_enabled_ = false;    // env RJ_STREAM_K2=1: streaming K2 (k_rows_stream), measured no faster
   int cu_count_ = 256;

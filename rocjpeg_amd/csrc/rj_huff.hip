@@ -98,6 +98,61 @@ __device__ __forceinline__ void hl_flush(const HCol<S> &stage, uint32_t from, ui
   }
 }
 
+// Raw-ECS movers (LaunchHuffLanes with destuffed == nullptr: K0 skipped).  Byte x of an
+// interval's raw range [0, slen) is byte (a0 + x) of the dword array dw; dword indices are
+// clamped to dlast, the dword holding byte slen + 3 (the marker / slack behind the data).
+// K0's rule (rj_kernels.hip k_destuff): byte i is dropped when (b[i] == 00 && b[i-1] == FF) or
+// (b[i] == FF && b[i+1] == FF), with b[-1] = 0 and no byte behind the range.
+struct HlRaw {
+  const RJ_GLOBAL uint32_t *dw;
+  uint32_t a0, dlast, slen;
+  __device__ __forceinline__ uint32_t ld(uint32_t j) const { return dw[min(j, dlast)]; }
+};
+
+// one 16-B chunk of destuffed bytes from raw byte rpos on (prev: the raw byte before rpos);
+// zero bytes past the data.  The slow path of the raw mover: chunks with an FF byte, the last
+// partial chunk.
+__device__ __forceinline__ uint4 hl_destuff_chunk(const HlRaw &R, uint32_t &rpos, uint32_t &prev) {
+  uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0, o = 0;
+  while (o < 16u && rpos < R.slen) {
+    const uint32_t j = (R.a0 + rpos) >> 2, sh = (R.a0 + rpos) & 3u;
+    uint32_t d[9], w[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) d[k] = R.ld(j + k);
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+    w[8] = d[8] >> (8u * sh);  // byte 32 (lookahead only)
+    uint32_t used = 0;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+      const uint32_t x = (w[i >> 2] >> (8 * (i & 3))) & 255u;
+      const uint32_t nx = (w[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 255u;
+      if (o < 16u && rpos + uint32_t(i) < R.slen) {
+        const bool nxv = rpos + uint32_t(i) + 1u < R.slen;
+        const bool drop = (x == 0u && prev == 0xFFu) || (x == 0xFFu && nxv && nx == 0xFFu);
+        if (!drop) {
+          const uint32_t v = x << (8u * (o & 3u));
+          const uint32_t wi = o >> 2;
+          o0 |= wi == 0 ? v : 0u;
+          o1 |= wi == 1 ? v : 0u;
+          o2 |= wi == 2 ? v : 0u;
+          o3 |= wi == 3 ? v : 0u;
+          o++;
+        }
+        prev = x;
+        used = uint32_t(i) + 1u;
+      }
+    }
+    rpos += used;
+  }
+  return make_uint4(o0, o1, o2, o3);
+}
+
+__device__ __forceinline__ bool hl_has_ff(uint32_t w) {
+  const uint32_t t = ~w;
+  return ((t - 0x01010101u) & ~t & 0x80808080u) != 0;
+}
+
 // Codes the first level does not resolve (rare): AC second level, or libjpeg's canonical
 // search (jpeg_huff_decode) on the table in HBM, repacked into the entry format.
 __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool isdc, uint32_t acbase,
@@ -276,6 +331,66 @@ __global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
     const uint32_t nchunks = (nbytes + 15) / 16;
     const HCol<DEC> ring{&s_ring[0][L]};
 
+    if (!kSplit && mover && destuffed == nullptr) {  // (the split launch keeps K0)
+      // ---- raw mover: the same ring protocol, destuffing the raw ECS on the way.  Chunks
+      // without an FF byte are the common case: their loads are issued a round ahead assuming
+      // every chunk before them is one too (raw offset = 16 per chunk); the first chunk that is
+      // not goes through hl_destuff_chunk, and the round's later chunks are loaded again ----
+      const uintptr_t ba = reinterpret_cast<uintptr_t>(im.ecs + sg.src_off);
+      const HlRaw R{gp(reinterpret_cast<const uint32_t *>(ba & ~uintptr_t(3))),
+                    uint32_t(ba & 3u), (uint32_t(ba & 3u) + sg.src_len + 3u) >> 2, sg.src_len};
+      uint32_t cm = 0, na = 0, rpos = 0, prev = 0;
+      uint32_t pw[4][5];
+      for (;;) {
+        const uint32_t rd = lds_ld(&s_dec[L]);
+        if (na > 0) {
+          bool good = true;  // every chunk so far was a fast one: window j starts at rpos
+#pragma unroll
+          for (uint32_t j = 0; j < 4; j++) {
+            if (j < na && good) {
+              const uint32_t sh = (R.a0 + rpos) & 3u;
+              const uint32_t w0 = __builtin_amdgcn_alignbyte(pw[j][1], pw[j][0], sh);
+              const uint32_t w1 = __builtin_amdgcn_alignbyte(pw[j][2], pw[j][1], sh);
+              const uint32_t w2 = __builtin_amdgcn_alignbyte(pw[j][3], pw[j][2], sh);
+              const uint32_t w3 = __builtin_amdgcn_alignbyte(pw[j][4], pw[j][3], sh);
+              uint4 c;
+              if (rpos >= R.slen) {
+                c = make_uint4(0, 0, 0, 0);  // past the data: the zero bits libjpeg inserts
+              } else if (rpos + 16u <= R.slen && prev != 0xFFu && !hl_has_ff(w0) && !hl_has_ff(w1) &&
+                         !hl_has_ff(w2) && !hl_has_ff(w3)) {
+                c = make_uint4(w0, w1, w2, w3);
+                rpos += 16u;
+                prev = w3 >> 24;
+              } else {
+                c = hl_destuff_chunk(R, rpos, prev);
+                good = false;
+              }
+              hl_put(ring, (cm + j) & (RJ_HL_CHUNKS - 1), c);
+              if (!good) na = j + 1;  // the round's later windows are stale
+            }
+          }
+          cm += na;
+          lds_st(&s_mov[L], cm);  // after the ring words (same wave, in order)
+          na = 0;
+        }
+        const bool fin = rd == RJ_HL_FIN;
+        const uint32_t live = fin ? RJ_HL_CHUNKS : cm - (rd >> 2);
+        const uint32_t n = min(RJ_HL_CHUNKS - live, 4u);
+        if (n > 0 && rpos < R.slen) {
+          const uint32_t j0 = (R.a0 + rpos) >> 2;
+#pragma unroll
+          for (uint32_t j = 0; j < 4; j++)
+            if (j < n) {
+#pragma unroll
+              for (uint32_t k = 0; k < 5; k++) pw[j][k] = R.ld(j0 + 4u * j + k);
+            }
+        }
+        na = n;
+        if (__builtin_amdgcn_ballot_w64(!fin) == 0) break;
+        if (__builtin_amdgcn_ballot_w64(n > 0) == 0) __builtin_amdgcn_s_sleep(4);
+      }
+      continue;
+    }
     if (mover) {
       // ---- mover: keep the ring's free chunk slots filled (past the data: zero chunks, the
       // zero bits libjpeg inserts), up to 4 chunks per round; a round's loads are committed at

@@ -459,6 +459,20 @@ void Stream::BuildIntervals() {
   }
   p.destuff_bytes = dst;
   p.entries = ent;
+  FinishSegs(p);
+}
+
+void FinishSegs(DecodePlan &p) {
+  p.seg_bucket.resize(p.segs.size());
+  bool aligned = p.segs.size() == p.mcuy;
+  uint32_t m = 0;
+  for (size_t q = 0; q < p.segs.size(); q++) {
+    const RjSegDev &sg = p.segs[q];
+    p.seg_bucket[q] = uint16_t(std::min<uint32_t>(sg.src_len >> 5, 4095u));
+    aligned = aligned && sg.mcu_first == m && sg.mcu_count == p.mcux;
+    m += p.mcux;
+  }
+  p.rows_aligned = aligned;
 }
 
 void Stream::CompleteFromDevice(uint32_t ecs_size, const RjSegDev *segs, uint32_t nsegs, const RjDsBlock *ds,
@@ -477,6 +491,7 @@ void Stream::CompleteFromDevice(uint32_t ecs_size, const RjSegDev *segs, uint32_
   p.destuff_bytes = dst;
   p.entries = ent;
   p.nchunks = nch;
+  FinishSegs(p);
   scan_pending_ = false;
 }
 

@@ -48,6 +48,11 @@ struct DecodePlan {
   uint8_t comp_blk0[4] = {};
   uint32_t wblk[4] = {}, hblk[4] = {};
   std::vector<RjSegDev> segs;      // one per restart interval
+  // batch planner caches (FinishSegs): per interval its 32-B length bucket (the K1 lane sort
+  // reads 2 B per interval instead of the 48-B descriptor), and whether every interval is
+  // exactly one MCU row
+  std::vector<uint16_t> seg_bucket;
+  bool rows_aligned = false;
   std::vector<RjDsBlock> ds;       // K0 blocks over all intervals
   uint64_t destuff_bytes = 0;      // destuffed buffer size incl. per-interval alignment
   uint64_t entries = 0;            // sparse-coefficient entries reserved (worst case)
@@ -75,6 +80,8 @@ struct DecodePlan {
   uint8_t pqlat[3][64] = {};       // each component's latched quant table (zigzag order)
   std::vector<uint32_t> pscan_src; // per scan: absolute stream offsets of its data [begin, end)
 };
+
+void FinishSegs(DecodePlan &p);
 
 class Stream {
  public:
