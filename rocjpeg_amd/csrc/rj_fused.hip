@@ -389,10 +389,16 @@ __device__ __forceinline__ void rgb_strip(const uint8_t *ty, const uint8_t *tu, 
     uint32_t w0, w1, w2;
     csc4_pk(y4, ua, ub, va, vb, w0, w1, w2);
     const uint32_t off = __umul24(yrow, pitch) + __umul24(qx, 12u);  // 32-bit: saddr store form
+#ifdef RJ_EXP_NOSTORE  // timing experiment (wrong output): no pixel stores
+    if (w0 == 0x12345679u && w1 == 0x9abcdef1u)
+#endif
     *reinterpret_cast<RJ_GLOBAL uint3 *>(gp(dst) + off) = make_uint3(w0, w1, w2);
     if constexpr (kVs) {  // the second row of the pair, same chroma
       const uint32_t y4b = *reinterpret_cast<const uint32_t *>(ty + __umul24(yrow + 1, tw0) + x);
       csc4_pk(y4b, ua, ub, va, vb, w0, w1, w2);
+#ifdef RJ_EXP_NOSTORE
+      if (w0 == 0x12345679u && w1 == 0x9abcdef1u)
+#endif
       *reinterpret_cast<RJ_GLOBAL uint3 *>(gp(dst) + (off + pitch)) = make_uint3(w0, w1, w2);
     }
     qx += qsx;
