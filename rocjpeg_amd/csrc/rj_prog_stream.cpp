@@ -569,6 +569,8 @@ void Stream::BuildProgressivePlan(const uint8_t *d) {
   p.prec_words = rec;
   if (rec >= (1ull << 32)) p.status = -4;  // record offsets are 32-bit
   p.segs.clear();
+  p.seg_bucket.clear();
+  p.rows_aligned = false;
   p.entries = 0;
   p.nchunks = 0;
 }
