@@ -146,6 +146,36 @@ def test_batch_mixed_progressive_and_baseline(dec, fmt, resident):
             assert G.first_mismatch(g, w) is None, (k, c, G.first_mismatch(g, w))
 
 
+def test_batch_after_reparse_swaps_stream_kinds(dec):
+    """Stream handles re-parsed with the other kind of data (baseline -> progressive and
+    progressive -> baseline, rocJpegStreamParse on a used handle) decode like fresh ones in one
+    batch: nothing cached by the earlier parse (interval tables, the lane sort's length buckets,
+    resident copies) survives into the new plan."""
+    from tests import gpu_util as G
+    fmt = R.OutputFormat.RGB
+    prog = [O.fixture_bytes(e) for e in PIPELINED][:3]
+    base = [O.fixture_bytes(e) for e in BASE[:3]]
+    streams = [R.JpegStream(d) for d in base + prog]
+    dec.streams_to_device(streams)
+    datas = prog + base  # every handle now holds the other kind
+    for s, d in zip(streams, datas):
+        s.parse(d)
+    shapes_all, bufs_all, imgs = [], [], []
+    for s in streams:
+        nc, css, w, h = dec.image_info(s)
+        shapes = G.channel_shapes(fmt, css, w, h)
+        bufs, img = G.gpu_buffers(shapes)
+        shapes_all.append(shapes)
+        bufs_all.append(bufs)
+        imgs.append(img)
+    assert dec.decode_batched(streams, R.decode_params(fmt), imgs) == 0
+    for k, (d, shapes, bufs) in enumerate(zip(datas, shapes_all, bufs_all)):
+        ost, want = O.oracle_decode(d, int(fmt), shapes)
+        assert ost == 0
+        for c, (g, w) in enumerate(zip(G.to_host(bufs), want)):
+            assert G.first_mismatch(g, w) is None, (k, c, G.first_mismatch(g, w))
+
+
 def test_progressive_timings(dec):
     from tests import gpu_util as G
     data = O.fixture_bytes(next(f for f in PROG if f["name"] == "pp420_q90_1920x1080"))
