@@ -153,6 +153,8 @@ int Decoder::Initialize() {
   if (const char *l = getenv("RJ_K1_SOLO")) k1_solo_lds_ = uint32_t(std::max(0, atoi(l)));
   if (const char *sk = getenv("RJ_STREAM_K2")) stream_enabled_ = atoi(sk) != 0;
   if (const char *sp = getenv("RJ_SPLIT")) split_enabled_ = atoi(sp) != 0;
+  if (const char *so = getenv("RJ_SPLIT_OUTLIERS")) outlier_split_ = atoi(so) != 0;
+  if (const char *sf = getenv("RJ_SPLIT_OUTLIER_FRAC")) outlier_frac_ = atof(sf);
   if (const char *fd = getenv("RJ_FUSE_DESTUFF")) fuse_destuff_ = atoi(fd) != 0;
   if (const char *sw = getenv("RJ_STREAM_WG")) stream_wg_per_cu_ = std::max(1, std::min(16, atoi(sw)));
   cu_count_ = std::max(1, prop.multiProcessorCount);
@@ -1160,7 +1162,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (cbuf.count) RJ_HIP(hipMemsetAsync(cbuf.count, 0, sizeof(unsigned long long), stream_));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
   // lean-only calls: the K1 movers destuff the raw ECS themselves (rj_huff.hip), no K0 pass
-  const bool raw_k1 = lean && fuse_destuff_ && prog_images == 0 && !split_enabled_;
+  const bool raw_k1 = lean && fuse_destuff_ && prog_images == 0 && !split_enabled_ && !outlier_split_;
   timings_.k0_fused = raw_k1 ? 1u : 0u;
   if (!raw_k1) RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>()));
   const uint8_t *k1_src = raw_k1 ? nullptr : d_destuff_.as<uint8_t>();
@@ -1410,18 +1412,52 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // starts at rj_split_byte and is joined where the two decoders' MCU starts meet) ----
   uint32_t nsplit = 0, nl_split = 0;
   RjHuffSplit hsplit{0, 0};
-  if (lean && sorted && lanes_desc && ngroups == 1 && !any_split && split_enabled_ && !stream_enabled_ &&
-      !Dbg(kDebugNoDep)) {
+  // Outlier mode (the default; RJ_SPLIT_OUTLIERS=0 turns it off, RJ_SPLIT=1 replaces it): only
+  // the intervals longer than 9/16 of the longest one split -- the longest chain then drops to
+  // ~9/16 of it -- in a launch that keeps one decoder wave per SIMD; skipped when more than
+  // outlier_frac_ of the intervals would split (near-uniform lengths, e.g. C2: splitting nearly
+  // everything is slower).  C4's mixed resolutions: 42,376 of 75,350 split, +12 %.
+  const bool outlier_mode = !split_enabled_ && outlier_split_;
+  if (lean && sorted && lanes_desc && ngroups == 1 && !any_split && (split_enabled_ || outlier_mode) &&
+      !stream_enabled_ && !Dbg(kDebugNoDep) && seg_total > 0) {
     const int64_t waves = int64_t(cu_count_) * (RJ_HL_SPLIT_DEC / 64);  // one round of the split grid
     const int64_t kmax = 64 * waves - int64_t(seg_total);
+    uint64_t lim = 0;
+    if (outlier_mode) {
+      // count the outliers on the cached 32-B length buckets first; the descriptors' exact
+      // lengths are gathered only when the call does split
+      std::vector<uint16_t> &gb = sc_.seg_bkt;
+      gb.resize(seg_total);
+      uint32_t g = 0;
+      for (int i = 0; i < n; i++)
+        for (const uint16_t b : streams[i]->plan().seg_bucket) gb[g++] = b;
+      const uint32_t blim = uint32_t(gb[lane_seg[0]]) * 9 / 16;
+      uint32_t cnt = 0;
+      while (cnt < seg_total && gb[lane_seg[cnt]] > blim) cnt++;
+      if (cnt == 0 || double(cnt) > outlier_frac_ * double(seg_total)) {
+        lim = UINT64_MAX;  // nothing to split
+      } else {
+        std::vector<uint2> &sl = sc_.seg_len;
+        sl.resize(seg_total);
+        g = 0;
+        for (int i = 0; i < n; i++) {
+          const DecodePlan &p = streams[i]->plan();
+          for (const RjSegDev &sg : p.segs)
+            sl[g++] = uint2{(sg.flags & RJ_SEG_MISSING) ? 0u : sg.dst_len, sg.mcu_count * p.nblk_mcu};
+        }
+        lim = uint64_t(sl[lane_seg[0]].x) * 9 / 16;
+      }
+    }
     uint64_t cap = 0;
-    while (int64_t(nsplit) < kmax && nsplit < seg_total) {
+    while (int64_t(nsplit) < kmax && nsplit < seg_total && lim != UINT64_MAX) {
       const uint2 sl = sc_.seg_len[lane_seg[nsplit]];
       if (sl.x < RJ_SPLIT_MIN_BYTES) break;  // lanes are sorted longest first
+      if (outlier_mode && sl.x <= lim) break;
       cap = std::max<uint64_t>(cap, rj_group(8ull * (sl.x - rj_split_byte(sl.x)) + sl.y +
                                              uint64_t(RJ_MAX_BLK_MCU) * RJ_ENT_PER_BLOCK + 1));
       nsplit++;
     }
+    if (outlier_mode && double(nsplit) > outlier_frac_ * double(seg_total)) nsplit = 0;
     if (nsplit > 0) {
       const uint32_t wsplit = (nsplit + 31) / 32;
       nl_split = wsplit * 64 + (seg_total - nsplit);
@@ -1559,7 +1595,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
     } else if (lean) {  // no split interval: one pass, no resolution / serial stages
       RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, nsplit ? nl_split : seg_total, k1_src, d_tabs,
-                             d_lean, cbuf, nullptr, 0u, nullptr, k1_solo_lds_, nsplit ? &hsplit : nullptr));
+                             d_lean, cbuf, nullptr, 0u, nullptr, k1_solo_lds_, nsplit ? &hsplit : nullptr,
+                             outlier_mode));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
     } else {

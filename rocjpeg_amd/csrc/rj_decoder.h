@@ -115,7 +115,10 @@ class Decoder {
   // first instead of doubling up on a CU beside a long-interval workgroup
   uint32_t k1_solo_lds_ = 16384;
   bool lean_enabled_ = true;       // env RJ_LEAN=0: the exact K1 (rj_entropy.hip) for row images too
-  bool fuse_destuff_ = false;      // env RJ_FUSE_DESTUFF=1: lean-only calls without K0, the K1 movers destuff (measured slower)
+  bool fuse_destuff_ = false;      // env RJ_FUSE_DESTUFF=1 (with RJ_SPLIT_OUTLIERS=0): lean-only calls without K0, the K1 movers destuff (measured slower)
+  bool outlier_split_ = true;      // env RJ_SPLIT_OUTLIERS=0: never split the outlier intervals (one decoder wave per SIMD)
+  double outlier_frac_ = 0.7;      // env RJ_SPLIT_OUTLIER_FRAC: at most this share of the intervals split in that mode
+                                   // (C4's mix: 56 % above 9/16 of the longest; C2's near-uniform rows: 84 %)
   bool split_enabled_ = false;     // env RJ_SPLIT=1: lean K1 head + tail lanes (rj_huff.hip; measured slower)
   bool stream_enabled_ = false;    // env RJ_STREAM_K2=1: streaming K2 (k_rows_stream), measured no faster
   int cu_count_ = 256;
@@ -146,6 +149,7 @@ class Decoder {
     std::vector<uint64_t> stage_off;
     std::vector<uint32_t> tab_of, row_prefix, grow_prefix, seg_lane0, lane_seg, bucket_pos, seg_pos, lane_split;
     std::vector<uint2> seg_len;  // per interval: destuffed bytes, blocks (lean split planning)
+    std::vector<uint16_t> seg_bkt;  // per interval: 32-B length bucket (outlier split planning)
     std::vector<uint8_t> is_fused, row_group, routed;
     std::vector<uint2> row_list;
     std::vector<uint32_t> prow_prefix, pgrow_prefix, prog_lanes, prog_bucket;  // progressive images

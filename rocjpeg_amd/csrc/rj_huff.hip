@@ -227,8 +227,8 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
       mpos = ms ? (0u - q) : mpos;                                                                        \
       mleft = ms ? blocks_left : mleft;                                                                   \
       mseen = mseen || ms;                                                                                \
-      recs[min(nr, uint32_t(RJ_HL_REC)) * kPairs] = uint16_t(0u - q);                                     \
-      nr += (ms && nr < RJ_HL_REC) ? 1u : 0u;                                                             \
+      recs[min(nr, kRec) * kPairs] = uint16_t(0u - q);                                                     \
+      nr += (ms && nr < kRec) ? 1u : 0u;                                                                  \
     }                                                                                                     \
     b = bend ? bn : b;                                                                                    \
     /* next symbol's table: the new block's DC table, or the current block's AC table */                 \
@@ -279,7 +279,10 @@ __global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
   __shared__ __attribute__((aligned(16))) uint32_t s_lut[RJ_HL_LUT_WORDS];
   __shared__ uint32_t s_dec[DEC];  // decoder -> mover: ring words fully consumed (RJ_HL_FIN: done)
   __shared__ uint32_t s_mov[DEC];  // mover -> decoder: 16-B chunks committed to the ring
-  __shared__ uint16_t s_rec[kSplit ? RJ_HL_REC + 1 : 1][kPairs];  // tail lanes' MCU-start records (+ scratch)
+  // MCU-start records per tail lane: 48, or 20 in the 256-lane instance (two workgroups per CU
+  // must fit in LDS; a head that finds no equal MCU start among them decodes the whole interval)
+  constexpr uint32_t kRec = DEC == 256 ? 20u : uint32_t(RJ_HL_REC);
+  __shared__ uint16_t s_rec[kSplit ? kRec + 1 : 1][kPairs];  // tail lanes' MCU-start records (+ scratch)
   __shared__ uint32_t s_nrec[kPairs];  // records published by the tail (bit 31: no more will come)
   __shared__ uint32_t s_T, s_ne;
   const uint32_t tid = threadIdx.x;
@@ -444,7 +447,7 @@ __global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
     const HCol<DEC> stage{&s_stage[0][L]};
     // split state: records (tail), the last MCU start seen (head), the head's scan over the records
     uint16_t *const recs = &s_rec[0][kSplit ? pair : 0u];
-    uint32_t nr = tail ? 0u : uint32_t(RJ_HL_REC);
+    uint32_t nr = tail ? 0u : kRec;
     uint32_t mpos = 0, mleft = 0, jrec = 0, blk_head = 0, skip_tail = 0;
     bool mseen = false, synced = false, checking = head;
     const uint32_t sp_bits = sp_byte * 8u;
@@ -498,7 +501,7 @@ __global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
                             !(blocks_left >= PHASE && !skip && (0u - q) + PHASE * 31u < nbits)) != 0;
       // split: a tail still recording, or a head that may pass an MCU start beyond the split
       const bool sync = kSplit && __builtin_amdgcn_ballot_w64(
-                                      nr < RJ_HL_REC || (checking && (0u - q) + PHASE * 31u >= sp_bits)) != 0;
+                                      nr < kRec || (checking && (0u - q) + PHASE * 31u >= sp_bits)) != 0;
       if (!safe && !sync) {
 #pragma unroll
         for (uint32_t s_ = 0; s_ < PHASE; s_++) RJ_HL_STEP(false, false);
@@ -519,8 +522,8 @@ __global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
       }
       if (kSplit) {
         if (tail) {  // publish the records (16-bit positions: the next phase must stay below 2^16)
-          if ((0u - q) >= RJ_HL_REC_LIMIT) nr = RJ_HL_REC;
-          lds_st(&s_nrec[pair], nr | ((nr >= RJ_HL_REC || blocks_left == 0) ? 0x80000000u : 0u));
+          if ((0u - q) >= RJ_HL_REC_LIMIT) nr = kRec;
+          lds_st(&s_nrec[pair], nr | ((nr >= kRec || blocks_left == 0) ? 0x80000000u : 0u));
         }
         if (checking && mseen && mpos >= sp_bits) {
           // head: is its last MCU start one of the tail's?  (records are in position order)
@@ -608,10 +611,13 @@ void DumpHuffStamps() {
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
                            RjCoefBuf coefs, uint32_t *flags, uint32_t epoch, uint32_t *done, uint32_t extra_lds,
-                           const RjHuffSplit *split) {
+                           const RjHuffSplit *split, bool split_one_wave) {
   if (nlanes == 0) return hipSuccess;
   static_assert(RJ_HL_SPLIT_DEC == 512, "HuffLaneWaves / the split lane layout");
-  if (split != nullptr) {  // one workgroup per CU: the LUT is shared by 512 decoder lanes
+  if (split != nullptr && split_one_wave) {  // outliers split: one decoder wave per SIMD
+    hipLaunchKernelGGL((k_huff<256, 8, true, 8>), dim3((nlanes + 255) / 256), dim3(512), 0, st, imgs, nimg, lane0,
+                       nlanes, destuffed, tabsets, lean, coefs, nullptr, 0u, nullptr, *split);
+  } else if (split != nullptr) {  // one workgroup per CU: the LUT is shared by 512 decoder lanes
     hipLaunchKernelGGL((k_huff<RJ_HL_SPLIT_DEC, 8, true, 8>), dim3((nlanes + RJ_HL_SPLIT_DEC - 1) / RJ_HL_SPLIT_DEC),
                        dim3(2 * RJ_HL_SPLIT_DEC), 0, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs,
                        nullptr, 0u, nullptr, *split);

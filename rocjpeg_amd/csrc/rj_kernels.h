@@ -30,10 +30,12 @@ hipError_t LaunchEntropyLanes(hipStream_t st, const RjImageDev *imgs, int nimg, 
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
                            RjCoefBuf coefs, uint32_t *flags = nullptr, uint32_t epoch = 0, uint32_t *done = nullptr,
-                           uint32_t extra_lds = 0, const RjHuffSplit *split = nullptr);
+                           uint32_t extra_lds = 0, const RjHuffSplit *split = nullptr, bool split_one_wave = false);
 // split != null: the split launch -- lane_seg lists per wave 32 head lanes then their 32 tail
 // lanes (RJ_LANE_HEAD / RJ_LANE_TAIL), split waves first, then whole intervals 64 per wave;
-// pieces at interval << 1 (coefs.piece_shift = 1); one 1024-thread workgroup per CU.
+// pieces at interval << 1 (coefs.piece_shift = 1); one 1024-thread workgroup per CU, or with
+// split_one_wave (only the outlier intervals split) 512-thread workgroups, two per CU: one
+// decoder wave per SIMD, as in the unsplit launch.
 // waves of a LaunchHuffLanes grid over n lanes
 inline uint32_t HuffLaneWaves(uint32_t nlanes) { return (nlanes + 255) / 256 * 4; }
 

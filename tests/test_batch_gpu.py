@@ -40,26 +40,31 @@ def _c2_images(count, seed0=1234):
         return list(ex.map(bench._make_jpeg, [(s, bench.WORKLOADS["c2"]["gen"]) for s in range(seed0, seed0 + count)]))
 
 
-@pytest.fixture(scope="module")
-def split_dec():
-    """A handle with the lean split launch on (RJ_SPLIT=1, read at handle creation)."""
+@pytest.fixture(scope="module", params=[{"RJ_SPLIT": "1"}, {"RJ_SPLIT_OUTLIERS": "1", "RJ_SPLIT_OUTLIER_FRAC": "1"}],
+                ids=["split_all", "split_outliers"])
+def split_dec(request):
+    """A handle with a lean split launch on (read at handle creation): RJ_SPLIT=1 splits every
+    long interval (one 1024-thread workgroup per CU); RJ_SPLIT_OUTLIERS=1 only those longer than
+    9/16 of the longest (512-thread workgroups, two per CU), here with no cap on their share."""
     torch()
-    old = os.environ.get("RJ_SPLIT")
-    os.environ["RJ_SPLIT"] = "1"
+    env = request.param
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         d = R.JpegDecoder(R.Backend.HARDWARE, 0)
     finally:
-        if old is None:
-            del os.environ["RJ_SPLIT"]
-        else:
-            os.environ["RJ_SPLIT"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     yield d
     d.close()
 
 
 def test_c2_1024_split_launch(split_dec):
-    """The C2 call with the lean split launch: the longest 61,440 intervals decoded by head +
-    tail lanes (one workgroup of 1024 threads per CU), every image equal to the oracle."""
+    """The C2 call with a lean split launch: the longest intervals (all of them up to the grid's
+    capacity, or the outliers) decoded by head + tail lanes, every image equal to the oracle."""
     t = torch()
     distinct, copies = 64, 16
     datas = _c2_images(distinct, seed0=4321)

@@ -212,10 +212,14 @@ def test_long_interval_batch_mixed(dec):
                 params=[(0, 4, {"RJ_LEAN": "0"}), (1, 4, {"RJ_LEAN": "0"}), (0, 1, {"RJ_LEAN": "0"}), (0, 4, {}),
                         (0, 1, {}), (1, 1, {}), (0, 1, {"RJ_LPT": "0", "RJ_K1_SOLO": "0"}),
                         (0, 2, {"RJ_STREAM_K2": "1"}), (0, 1, {"RJ_SPLIT": "1"}), (1, 1, {"RJ_SPLIT": "1"}),
-                        (0, 1, {"RJ_FUSE_DESTUFF": "1"}), (1, 1, {"RJ_FUSE_DESTUFF": "1"})],
+                        (0, 1, {"RJ_FUSE_DESTUFF": "1", "RJ_SPLIT_OUTLIERS": "0"}),
+                        (1, 1, {"RJ_FUSE_DESTUFF": "1", "RJ_SPLIT_OUTLIERS": "0"}),
+                        (0, 1, {"RJ_SPLIT_OUTLIERS": "1", "RJ_SPLIT_OUTLIER_FRAC": "1"}),
+                        (1, 1, {"RJ_SPLIT_OUTLIERS": "1", "RJ_SPLIT_OUTLIER_FRAC": "1"})],
                 ids=["exact_g4", "exact_general_g4", "exact_g1", "lean_g4", "lean_g1", "lean_general_g1",
                      "lean_g1_short_first", "lean_stream_g2", "lean_split_g1", "lean_split_general_g1",
-                     "lean_raw_movers_g1", "lean_raw_movers_general_g1"])
+                     "lean_raw_movers_g1", "lean_raw_movers_general_g1",
+                     "lean_split_outliers_g1", "lean_split_outliers_general_g1"])
 def pdec(request):
     """A decoder that sorts the K1 lanes of every call with no split interval by length
     (RJ_PIPE_MIN=1) and, with 4 groups, pipelines it: interval length classes on separate
@@ -305,7 +309,8 @@ def test_pipelined_row_aligned_batch(pdec, fmt):
         assert t["pipe_lane_rows"] == 1
     assert t["lean_k1"] == (0 if pdec.extra.get("RJ_LEAN") == "0" else 1)
     assert t["k2_stream"] == (1 if pdec.extra.get("RJ_STREAM_K2") else 0)
-    if pdec.extra.get("RJ_SPLIT") == "1":  # the 1080p intervals (and the damaged ones) are split
+    if pdec.extra.get("RJ_SPLIT") == "1" or pdec.extra.get("RJ_SPLIT_OUTLIERS") == "1":
+        # the 1080p intervals (and the damaged ones) are split (outliers: those near the longest)
         assert t["lean_split"] > 0
     assert t["k0_fused"] == (1 if pdec.extra.get("RJ_FUSE_DESTUFF") == "1" else 0)
     for k, (d, shapes, bufs) in enumerate(zip(datas, shapes_all, bufs_all)):
