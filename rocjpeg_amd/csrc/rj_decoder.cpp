@@ -155,6 +155,7 @@ int Decoder::Initialize() {
   if (const char *sp = getenv("RJ_SPLIT")) split_enabled_ = atoi(sp) != 0;
   if (const char *so = getenv("RJ_SPLIT_OUTLIERS")) outlier_split_ = atoi(so) != 0;
   if (const char *sf = getenv("RJ_SPLIT_OUTLIER_FRAC")) outlier_frac_ = atof(sf);
+  if (const char *st = getenv("RJ_SPLIT_OUTLIER_T")) outlier_t_ = std::max(0.5, std::min(1.0, atof(st)));
   if (const char *fd = getenv("RJ_FUSE_DESTUFF")) fuse_destuff_ = atoi(fd) != 0;
   if (const char *sw = getenv("RJ_STREAM_WG")) stream_wg_per_cu_ = std::max(1, std::min(16, atoi(sw)));
   cu_count_ = std::max(1, prop.multiProcessorCount);
@@ -1431,7 +1432,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       uint32_t g = 0;
       for (int i = 0; i < n; i++)
         for (const uint16_t b : streams[i]->plan().seg_bucket) gb[g++] = b;
-      const uint32_t blim = uint32_t(gb[lane_seg[0]]) * 9 / 16;
+      const uint32_t blim = uint32_t(double(gb[lane_seg[0]]) * outlier_t_);
       uint32_t cnt = 0;
       while (cnt < seg_total && gb[lane_seg[cnt]] > blim) cnt++;
       if (cnt == 0 || double(cnt) > outlier_frac_ * double(seg_total)) {
@@ -1445,7 +1446,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
           for (const RjSegDev &sg : p.segs)
             sl[g++] = uint2{(sg.flags & RJ_SEG_MISSING) ? 0u : sg.dst_len, sg.mcu_count * p.nblk_mcu};
         }
-        lim = uint64_t(sl[lane_seg[0]].x) * 9 / 16;
+        lim = uint64_t(double(sl[lane_seg[0]].x) * outlier_t_);
       }
     }
     uint64_t cap = 0;

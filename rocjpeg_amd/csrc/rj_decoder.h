@@ -117,6 +117,7 @@ class Decoder {
   bool lean_enabled_ = true;       // env RJ_LEAN=0: the exact K1 (rj_entropy.hip) for row images too
   bool fuse_destuff_ = false;      // env RJ_FUSE_DESTUFF=1 (with RJ_SPLIT_OUTLIERS=0): lean-only calls without K0, the K1 movers destuff (measured slower)
   bool outlier_split_ = true;      // env RJ_SPLIT_OUTLIERS=0: never split the outlier intervals (one decoder wave per SIMD)
+  double outlier_t_ = 9.0 / 16;    // env RJ_SPLIT_OUTLIER_T: outliers are longer than this share of the longest interval
   double outlier_frac_ = 0.7;      // env RJ_SPLIT_OUTLIER_FRAC: at most this share of the intervals split in that mode
                                    // (C4's mix: 56 % above 9/16 of the longest; C2's near-uniform rows: 84 %)
   bool split_enabled_ = false;     // env RJ_SPLIT=1: lean K1 head + tail lanes (rj_huff.hip; measured slower)
