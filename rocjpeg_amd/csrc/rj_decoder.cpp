@@ -1338,13 +1338,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       const DecodePlan &p = streams[i]->plan();
       if (want_len || rl != nullptr || want_pos) {
         uint32_t r = 0;
-        const uint32_t nblk_i = p.nblk_mcu;
         for (size_t q = 0; q < p.segs.size(); q++) {
           const uint32_t l = pos[bucket(p.seg_bucket[q])]++;
-          if (want_len) {
-            const RjSegDev &sg = p.segs[q];
-            seg_len[gs] = uint2{(sg.flags & RJ_SEG_MISSING) ? 0u : sg.dst_len, sg.mcu_count * nblk_i};
-          }
+          if (want_len) seg_len[gs] = uint2{uint32_t(p.seg_lenblk[q]), uint32_t(p.seg_lenblk[q] >> 32)};
           ls[l] = gs;
           if (rl) rl[l] = uint2{uint32_t(i), r++};
           if (want_pos) seg_pos[gs] = l;
@@ -1441,11 +1437,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         std::vector<uint2> &sl = sc_.seg_len;
         sl.resize(seg_total);
         g = 0;
-        for (int i = 0; i < n; i++) {
-          const DecodePlan &p = streams[i]->plan();
-          for (const RjSegDev &sg : p.segs)
-            sl[g++] = uint2{(sg.flags & RJ_SEG_MISSING) ? 0u : sg.dst_len, sg.mcu_count * p.nblk_mcu};
-        }
+        for (int i = 0; i < n; i++)
+          for (const uint64_t v : streams[i]->plan().seg_lenblk) sl[g++] = uint2{uint32_t(v), uint32_t(v >> 32)};
         lim = uint64_t(double(sl[lane_seg[0]].x) * outlier_t_);
       }
     }

@@ -570,6 +570,7 @@ void Stream::BuildProgressivePlan(const uint8_t *d) {
   if (rec >= (1ull << 32)) p.status = -4;  // record offsets are 32-bit
   p.segs.clear();
   p.seg_bucket.clear();
+  p.seg_lenblk.clear();
   p.rows_aligned = false;
   p.entries = 0;
   p.nchunks = 0;

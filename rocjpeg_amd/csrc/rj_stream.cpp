@@ -464,11 +464,14 @@ void Stream::BuildIntervals() {
 
 void FinishSegs(DecodePlan &p) {
   p.seg_bucket.resize(p.segs.size());
+  p.seg_lenblk.resize(p.segs.size());
   bool aligned = p.segs.size() == p.mcuy;
   uint32_t m = 0;
   for (size_t q = 0; q < p.segs.size(); q++) {
     const RjSegDev &sg = p.segs[q];
     p.seg_bucket[q] = uint16_t(std::min<uint32_t>(sg.src_len >> 5, 4095u));
+    p.seg_lenblk[q] = ((sg.flags & RJ_SEG_MISSING) ? 0u : uint64_t(sg.dst_len)) |
+                      (uint64_t(sg.mcu_count) * p.nblk_mcu << 32);
     aligned = aligned && sg.mcu_first == m && sg.mcu_count == p.mcux;
     m += p.mcux;
   }

@@ -52,6 +52,7 @@ struct DecodePlan {
   // reads 2 B per interval instead of the 48-B descriptor), and whether every interval is
   // exactly one MCU row
   std::vector<uint16_t> seg_bucket;
+  std::vector<uint64_t> seg_lenblk;  // per interval: destuffed bytes (0: missing) | blocks << 32 (split planning)
   bool rows_aligned = false;
   std::vector<RjDsBlock> ds;       // K0 blocks over all intervals
   uint64_t destuff_bytes = 0;      // destuffed buffer size incl. per-interval alignment
