@@ -51,17 +51,26 @@ static uint32_t LeanEntry(uint32_t len, uint32_t sym, bool is_dc) {
   return ((32u - n) & 31u) | (n << 8) | (emit << 13) | (s << 16) | (R << 21);
 }
 
-void BuildLeanTable(const uint8_t bits[16], const uint8_t *vals, bool is_dc, uint32_t *first, uint32_t *subs) {
+static void FillLeanBad(bool is_dc, uint32_t *first, uint32_t *subs) {
   const int B = is_dc ? RJ_HL_DC_BITS : RJ_HL_AC_BITS;
   const uint32_t bad = LeanEntry(17, 0, is_dc);  // libjpeg: a bad code is 17 bits of symbol 0
   for (int e = 0; e < (1 << B); e++) first[e] = bad;
   if (subs)
     for (int e = 0; e < RJ_HL_SUBS * 32; e++) subs[e] = bad;
+}
+
+bool BuildLeanTable(const uint8_t bits[16], const uint8_t *vals, bool is_dc, uint32_t *first, uint32_t *subs) {
+  const int B = is_dc ? RJ_HL_DC_BITS : RJ_HL_AC_BITS;
+  FillLeanBad(is_dc, first, subs);
   int nsub = 0;
   std::vector<int> sub_of(size_t(1) << B, -1);
   int k = 0, code = 0;
   for (int l = 1; l <= 16; l++) {
     for (int i = 0; i < bits[l - 1]; i++, k++, code++) {
+      if (code >= (1 << l) || k >= (is_dc ? 12 : 162)) {  // over-subscribed: no write past the tables
+        FillLeanBad(is_dc, first, subs);
+        return false;
+      }
       const uint32_t ent = LeanEntry(uint32_t(l), vals[k], is_dc);
       if (l <= B) {
         for (int f = 0; f < (1 << (B - l)); f++) first[(code << (B - l)) | f] = ent;
@@ -79,6 +88,7 @@ void BuildLeanTable(const uint8_t bits[16], const uint8_t *vals, bool is_dc, uin
     }
     code <<= 1;
   }
+  return true;
 }
 
 bool BuildHuffman(const uint8_t bits[16], const uint8_t *vals, bool is_dc, RjHuffDev *t) {
@@ -93,6 +103,7 @@ bool BuildHuffman(const uint8_t bits[16], const uint8_t *vals, bool is_dc, RjHuf
     if (nb) {
       t->valoff[l] = k - code;
       for (int i = 0; i < nb; i++, k++, code++) {
+        if (code >= (1 << l) || k >= 256) return false;  // over-subscribed: checked before any write
         const uint16_t ent = uint16_t((l << 8) | vals[k]);
         if (l <= 9) {
           const int shift = 9 - l;
@@ -336,9 +347,12 @@ bool Stream::BuildPlanHeader() {
     if (td >= 2 || ta >= 2 || !s.ht_loaded[td] || !s.ht_loaded[ta] || !s.qt_loaded[tq]) { p.status = -3; return false; }
   }
   for (int t = 0; t < 2; t++) {
+    p.ht_valid[t] = 0;
     if (!s.ht_loaded[t]) continue;
-    if (!BuildHuffman(s.ht[t].dc_bits, s.ht[t].dc_vals, true, &p.tables.dc[t]) ||
-        !BuildHuffman(s.ht[t].ac_bits, s.ht[t].ac_vals, false, &p.tables.ac[t])) {
+    if (BuildHuffman(s.ht[t].dc_bits, s.ht[t].dc_vals, true, &p.tables.dc[t]) &&
+        BuildHuffman(s.ht[t].ac_bits, s.ht[t].ac_vals, false, &p.tables.ac[t])) {
+      p.ht_valid[t] = 1;
+    } else {
       // only fatal when the scan actually uses this table
       for (int c = 0; c < nc; c++)
         if (s.scomp[c].td == t || s.scomp[c].ta == t) { p.status = -3; return false; }
@@ -502,8 +516,14 @@ const RjLeanTables *Stream::LeanTables() {
   if (!lean_) {
     auto t = std::make_unique<RjLeanTables>();
     for (int id = 0; id < 2; id++) {
-      BuildLeanTable(info_.ht[id].dc_bits, info_.ht[id].dc_vals, true, t->dc[id], nullptr);
-      BuildLeanTable(info_.ht[id].ac_bits, info_.ht[id].ac_vals, false, t->ac[id], t->ac[id] + (1 << RJ_HL_AC_BITS));
+      // only slots BuildPlanHeader accepted; an unused, invalid slot stays all 'bad' entries
+      uint32_t *ac_subs = t->ac[id] + (1 << RJ_HL_AC_BITS);
+      if (!plan_.ht_valid[id] ||
+          !BuildLeanTable(info_.ht[id].dc_bits, info_.ht[id].dc_vals, true, t->dc[id], nullptr))
+        FillLeanBad(true, t->dc[id], nullptr);
+      if (!plan_.ht_valid[id] ||
+          !BuildLeanTable(info_.ht[id].ac_bits, info_.ht[id].ac_vals, false, t->ac[id], ac_subs))
+        FillLeanBad(false, t->ac[id], ac_subs);
     }
     lean_ = std::move(t);
   }

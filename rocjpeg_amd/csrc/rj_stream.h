@@ -59,6 +59,7 @@ struct DecodePlan {
   uint64_t entries = 0;            // sparse-coefficient entries reserved (worst case)
   uint32_t nchunks = 0;            // K1 lanes (chunks) over all intervals
   RjTableSet tables;               // derived tables
+  uint8_t ht_valid[2] = {};        // DHT slot loaded and both its tables valid (BuildHuffman)
   uint16_t qmax[4] = {1, 1, 1, 1}; // largest entry of each quant table slot (the IDCT's exact domain)
   // De-duplication key: the raw DHT/DQT content the derived tables are a function of (the
   // batch planner compares these ~670 B instead of the 14.5 KB RjTableSet) and its hash.
@@ -137,8 +138,9 @@ int ImageInfo(const StreamInfo &s, uint8_t *num_components, int *subsampling, ui
 bool IsProgressiveStream(const uint8_t *data, uint32_t size);
 
 // Canonical Huffman table -> lean K1 first level (2^RJ_HL_DC_BITS or 2^RJ_HL_AC_BITS entries)
-// and, for AC, RJ_HL_SUBS second-level subtables (subs); the table must be valid (BuildHuffman).
-void BuildLeanTable(const uint8_t bits[16], const uint8_t *vals, bool is_dc, uint32_t *first, uint32_t *subs);
+// and, for AC, RJ_HL_SUBS second-level subtables (subs).  An over-subscribed table is refused
+// before any entry is written (false; first/subs then hold only 'bad' entries).
+bool BuildLeanTable(const uint8_t bits[16], const uint8_t *vals, bool is_dc, uint32_t *first, uint32_t *subs);
 
 // Canonical Huffman table -> RjHuffDev; false for an invalid table.
 bool BuildHuffman(const uint8_t bits[16], const uint8_t *vals, bool is_dc, RjHuffDev *out);

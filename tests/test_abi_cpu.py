@@ -173,3 +173,43 @@ def test_abi_layout_matches_reference_header(tmp_path):
     ref = _abi_probe(_REF_API, tmp_path / "ref")
     ours = _abi_probe(INCLUDE, tmp_path / "ours")
     assert ours == ref
+
+
+# ---- hardening: crafted Huffman tables (rj_stream.cpp BuildLeanTable/BuildHuffman) ----
+def oversubscribed_unused_slot_stream():
+    """A gray row-interval fixture with an extra DHT that defines slot 1, which its scan does not
+    use: DC with 12 codes of length 1, AC with 162 codes of length 2 (both over-subscribed).
+    libjpeg builds derived tables only for the scan's slots (jdhuff.c start_pass_huff_decoder),
+    so the stream is valid and decodes as the original."""
+    import struct
+    d = O.fixture_bytes(next(f for f in O.manifest() if f["name"] == "p400_q85_ri_96x72"))
+    seg = bytes([0x01, 12] + [0] * 15) + bytes(range(12)) + bytes([0x11, 0, 162] + [0] * 14) + bytes(range(162))
+    return d[:2] + b"\xff\xc4" + struct.pack(">H", len(seg) + 2) + seg + d[2:]
+
+
+def test_oversubscribed_tables_are_refused_without_writes(tmp_path):
+    """Host parse + lean-table build of the crafted stream under AddressSanitizer (host code only:
+    tests/c/huff_tables_asan.cpp links rj_stream.cpp, no GPU call).  Before the fix the lean
+    builder wrote past its 512-word DC table."""
+    import subprocess
+    csrc = os.path.join(O.ROOT, "rocjpeg_amd", "csrc")
+    exe = tmp_path / "huff_asan"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address", "-D__HIP_PLATFORM_AMD__",
+                    "-I/opt/rocm/include", f"-I{csrc}", f"-I{INCLUDE}",
+                    os.path.join(O.ROOT, "tests", "c", "huff_tables_asan.cpp"),
+                    os.path.join(csrc, "rj_stream.cpp"), os.path.join(csrc, "rj_prog_stream.cpp"),
+                    "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib", "-o", str(exe)],
+                   check=True, capture_output=True)
+    bad = tmp_path / "bad.jpg"
+    bad.write_bytes(oversubscribed_unused_slot_stream())
+    r = subprocess.run([str(exe), str(bad)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "status=0 valid=10" in r.stdout  # decodable; slot 0 valid, slot 1 refused
+    # the same bad slot used by the scan: the stream is refused at decode planning
+    used = bytearray(oversubscribed_unused_slot_stream())
+    j = used.index(b"\xff\xda")
+    used[j + 6] = 0x11  # scan component 0 -> DC/AC table 1
+    bad.write_bytes(bytes(used))
+    r = subprocess.run([str(exe), str(bad)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "status=-3 valid=10" in r.stdout
