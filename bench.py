@@ -314,13 +314,21 @@ class BatchRun:
         return last
 
     def parity(self, idx):
-        """Images `idx` of the current outputs (the last timed step's) vs the CPU oracle."""
+        """Images `idx` of the current outputs (the last timed step's) vs the CPU oracle (the
+        oracle calls release the GIL: 16 threads)."""
+        from concurrent.futures import ThreadPoolExecutor
         from tests import oracle_lib as O
+        with ThreadPoolExecutor(16) as ex:
+            wants = list(ex.map(lambda q: O.oracle_decode(self.datas[q], int(self.fmt), self.shapes[q]), idx))
         ok = True
-        for q in idx:
-            ost, want = O.oracle_decode(self.datas[q], int(self.fmt), self.shapes[q])
+        for q, (ost, want) in zip(idx, wants):
             ok = ok and ost == 0 and all(np.array_equal(v.cpu().numpy(), w_) for v, w_ in zip(self.views[q], want))
         return bool(ok)
+
+
+def parity_sample(n, k=16):
+    """k image indices spread over a batch of n (first and last included)."""
+    return sorted({int(round(i * (n - 1) / max(1, k - 1))) for i in range(k)}) if n else []
 
     def close(self):
         import torch
@@ -396,7 +404,8 @@ def run_extra(name, dec, pool_path, steps, warmup, dev):
     rf = roofline(t, b.n, name, per_img)
     res = {"value": round(b.n * steps / el, 2), "unit": "images/s", "ms_per_step": round(el / steps * 1e3, 3),
            "steps": steps, "warmup": warmup, "workload": WORKLOADS[name]["workload"].format(batch=b.n),
-           "output_format": WORKLOADS[name]["fmt"], "parity_sample": b.parity([0, b.n - 1]),
+           "output_format": WORKLOADS[name]["fmt"], "parity_sample": b.parity(parity_sample(b.n)),
+           "parity_sample_images": len(parity_sample(b.n)),
            "roofline": {k: rf[k] for k in ("kernel", "achieved", "frac", "avg_launch_ms", "launches_per_step")},
            "per_kernel_launch_ms_sum": rf["per_kernel_launch_ms_sum"], "host_ms": round(t["host_ms"], 3),
            "split_intervals": t["split_intervals"], "serial_fallbacks": t["serial_fallbacks"]}
@@ -495,7 +504,7 @@ def main():
 
     elapsed = run.timed(args.steps, args.warmup, world, cdev)
     # parity of the timed run's own output (the last step's), before anything else writes it
-    parity = run.parity(sorted({0, n // 2, n - 1}))
+    parity = run.parity(parity_sample(n))
     imgs = torch.tensor([n], dtype=torch.int64, device=cdev)
     if world > 1:
         dist.all_reduce(imgs)
@@ -559,6 +568,7 @@ def main():
             "parse_images_per_s": {"host_1_thread": round(parse_host_rate, 1),
                                    "gpu_marker_scan": round(n / run.parse_s, 1)},
             "parity_timed_output": parity,
+            "parity_timed_output_images": len(parity_sample(n)),
             "work_table": {"images": int(len(table)), "bytes": int(table.nbytes), "build_ms": round(t_build * 1e3, 2),
                            "build_and_broadcast_ms": round(t_tab * 1e3, 2),
                            "lpt_imbalance": round(S.imbalance(shard_cost), 5),

@@ -1009,12 +1009,29 @@ int oj_decode(const uint8_t *data, size_t len, int fmt, int16_t cl, int16_t ct, 
   decode_all_coefs(data, pl, co);
   planes_from_coefs(pl, co, pb);
   free(co);
+  const uint8_t *planes[3] = {0, 0, 0};
+  int32_t pw3[3] = {0, 0, 0}, ph3[3] = {0, 0, 0};
+  for (int c = 0; c < pl->nc && c < 3; c++) {
+    planes[c] = pb + pl->plane_off[c];
+    pw3[c] = pl->wblk[c] * 8;
+    ph3[c] = pl->hblk[c] * 8;
+  }
+  st = oj_output_stage(planes, pw3, ph3, css, W, H, fmt, cl, ct, cr, cbm, ch, pitch);
+  free(pb);
+  free(pl);
+  return st;
+}
+
+int oj_output_stage(const uint8_t *const planes[3], const int32_t plane_w[3], const int32_t plane_h[3], int css,
+                    int W, int H, int fmt, int16_t cl, int16_t ct, int16_t cr, int16_t cbm, uint8_t *ch[4],
+                    const uint32_t pitch[4]) {
+  if (!ch || !pitch || !planes) return ST_INVALID;
   planes_t P;
   memset(&P, 0, sizeof(P));
-  for (int c = 0; c < pl->nc && c < 3; c++) {
-    P.pl[c] = pb + pl->plane_off[c];
-    P.pw[c] = pl->wblk[c] * 8;
-    P.ph[c] = pl->hblk[c] * 8;
+  for (int c = 0; c < 3; c++) {
+    P.pl[c] = planes[c];
+    P.pw[c] = plane_w[c];
+    P.ph[c] = plane_h[c];
   }
   /* ROI (rocjpeg_decoder.cpp:124-141); gfx950 VCN has no ROI decode, so offsets apply */
   uint32_t roi_w = (uint32_t)((int)cr - (int)cl), roi_h = (uint32_t)((int)cbm - (int)ct);
@@ -1026,7 +1043,6 @@ int oj_decode(const uint8_t *data, size_t len, int fmt, int16_t cl, int16_t ct, 
   for (int k = 0; k < 3; k++)
     if ((fmt == OUT_YUV_PLANAR || fmt == OUT_RGB_PLANAR || fmt == OUT_RGB || fmt == OUT_Y) &&
         (k == 0 || fmt == OUT_RGB_PLANAR || (fmt == OUT_YUV_PLANAR && css != CSS_400)) && !ch[k]) {
-      free(pb); free(pl);
       return ST_INVALID; /* the reference would dereference NULL here */
     }
   #define COPY(SP, CHAN, ROWS, TOPR, LOFF, DI)                                          \
@@ -1128,7 +1144,5 @@ int oj_decode(const uint8_t *data, size_t len, int fmt, int16_t cl, int16_t ct, 
       break;
   }
   #undef COPY
-  free(pb);
-  free(pl);
   return ST_OK;
 }

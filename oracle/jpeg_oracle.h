@@ -70,6 +70,15 @@ int oj_decode(const uint8_t *data, size_t len, int output_format,
               int16_t crop_left, int16_t crop_top, int16_t crop_right, int16_t crop_bottom,
               uint8_t *channel[4], const uint32_t pitch[4]);
 
+/* The output stage alone (src/rocjpeg_decoder.cpp:124-180, 372-636 over the VCN surface model)
+ * on given component planes: planes[c] is plane_w[c] x plane_h[c] bytes (the decoded, MCU-padded
+ * planes; reads past them clamp to the edge); css is the parser's ChromaSubsampling, W x H the
+ * picture size.  oj_decode = decode + this.  Lets the tests pin the output stage against the
+ * reference's own kernels on arbitrary planes. */
+int oj_output_stage(const uint8_t *const planes[3], const int32_t plane_w[3], const int32_t plane_h[3], int css,
+                    int W, int H, int output_format, int16_t crop_left, int16_t crop_top, int16_t crop_right,
+                    int16_t crop_bottom, uint8_t *channel[4], const uint32_t pitch[4]);
+
 /* One pixel of the reference colour conversion (rocjpeg_hip_kernels.cpp:1431-1443). */
 void oj_csc_pixel(uint8_t y, uint8_t u, uint8_t v, uint8_t rgb[3]);
 void oj_csc_bulk(const uint8_t *y, const uint8_t *u, const uint8_t *v, size_t n, uint8_t *rgb);

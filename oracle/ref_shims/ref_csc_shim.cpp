@@ -24,6 +24,21 @@ void ref_yuyv_to_rgb(void *st, uint32_t w, uint32_t h, uint8_t *dst, uint32_t dp
 void ref_yuv400_to_rgb(void *st, uint32_t w, uint32_t h, uint8_t *dst, uint32_t dp, const uint8_t *src, uint32_t p) {
   ColorConvertYUV400ToRGB(S(st), w, h, dst, dp, src, p);
 }
+void ref_yuv444_to_rgb_planar(void *st, uint32_t w, uint32_t h, uint8_t *r, uint8_t *g, uint8_t *b, uint32_t dp,
+                              const uint8_t *base, uint32_t p, uint32_t uoff, uint32_t voff) {
+  ColorConvertYUV444ToRGBPlanar(S(st), w, h, r, g, b, dp, base, p, uoff, voff);
+}
+void ref_yuv440_to_rgb_planar(void *st, uint32_t w, uint32_t h, uint8_t *r, uint8_t *g, uint8_t *b, uint32_t dp,
+                              const uint8_t *base, uint32_t p, uint32_t uoff, uint32_t voff) {
+  ColorConvertYUV440ToRGBPlanar(S(st), w, h, r, g, b, dp, base, p, uoff, voff);
+}
+void ref_yuyv_to_rgb_planar(void *st, uint32_t w, uint32_t h, uint8_t *r, uint8_t *g, uint8_t *b, uint32_t dp,
+                            const uint8_t *src, uint32_t p) { ColorConvertYUYVToRGBPlanar(S(st), w, h, r, g, b, dp, src, p); }
+void ref_yuv400_to_rgb_planar(void *st, uint32_t w, uint32_t h, uint8_t *r, uint8_t *g, uint8_t *b, uint32_t dp,
+                              const uint8_t *src, uint32_t p) { ColorConvertYUV400ToRGBPlanar(S(st), w, h, r, g, b, dp, src, p); }
+void ref_yuyv_extract_y(void *st, uint32_t w, uint32_t h, uint8_t *y, uint32_t yp, const uint8_t *src, uint32_t p) {
+  ExtractYFromPackedYUYV(S(st), w, h, y, yp, src, p);
+}
 void ref_uv_to_planar(void *st, uint32_t w, uint32_t h, uint8_t *u, uint8_t *v, uint32_t dp, const uint8_t *uv, uint32_t p) {
   ConvertInterleavedUVToPlanarUV(S(st), w, h, u, v, dp, uv, p);
 }

@@ -29,15 +29,16 @@ def dec():
     d.close()
 
 
-def _c2_images(count, seed0=1234):
-    """The bench's C2 generator (seeded 1080p crops of the mug image + N(0,2) noise, Pillow q90
-    4:2:0, restart interval = one MCU row), threaded."""
+def _c2_images(count, seed0=1234, workload="c2"):
+    """The bench's generator (seeded crops of the mug image + N(0,2) noise, Pillow q90, restart
+    interval = one MCU row; C2: 1080p 4:2:0, C4: 640x480..3840x2160 by seed), threaded."""
     import sys
     sys.path.insert(0, ROOT)
     import bench
     bench._init_gen()
+    gen = bench.WORKLOADS[workload]["gen"]
     with ThreadPoolExecutor(16) as ex:
-        return list(ex.map(bench._make_jpeg, [(s, bench.WORKLOADS["c2"]["gen"]) for s in range(seed0, seed0 + count)]))
+        return list(ex.map(bench._make_jpeg, [(s, gen) for s in range(seed0, seed0 + count)]))
 
 
 @pytest.fixture(scope="module", params=[{"RJ_SPLIT": "1"}, {"RJ_SPLIT_OUTLIERS": "1", "RJ_SPLIT_OUTLIER_FRAC": "1"}],
@@ -106,6 +107,53 @@ def test_c2_1024_default_pipelined_layout(dec):
     ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
     bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
     assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
+
+
+def test_c4_1024_default_outlier_split(dec):
+    """BASELINE config C4 on one GPU (the per-rank shard of the 8-GPU config): 1024 mixed-resolution
+    4:2:0 images (640x480 ... 3840x2160, RI = one MCU row; 256 distinct x 4) in one
+    rocJpegDecodeBatched call under the DEFAULT handle settings.  This is the one config whose
+    default layout splits outlier intervals (the 3840-wide rows: head + tail lanes, rj_huff.hip);
+    every image is compared with the oracle on the device.  Reference path:
+    src/rocjpeg_decoder.cpp:196-292 (DecodeBatched)."""
+    t = torch()
+    distinct, copies = 256, 4
+    datas = _c2_images(distinct, seed0=1234, workload="c4")
+    with ThreadPoolExecutor(16) as ex:
+        want = list(ex.map(lambda d: O.oracle_decode(d, int(R.OutputFormat.RGB), [_rgb_shape(d)]), datas))
+    assert all(st == 0 for st, _ in want)
+    sizes = {(w_[0].shape[1] // 3, w_[0].shape[0]) for _, w_ in want}
+    assert sizes == {(640, 480), (1280, 720), (1920, 1080), (2560, 1440), (3840, 2160)}
+    streams = [R.JpegStream(datas[i % distinct]) for i in range(distinct * copies)]
+    dec.streams_to_device(streams)
+    nbytes = [want[i % distinct][1][0].size for i in range(len(streams))]
+    out = t.full((sum(nbytes),), 0xA5, dtype=t.uint8, device="cuda")
+    views, imgs, off = [], [], 0
+    for i, nb in enumerate(nbytes):
+        h, p = want[i % distinct][1][0].shape
+        views.append(out[off:off + nb].view(h, p))
+        imgs.append(R.make_image([views[-1].data_ptr()], [p]))
+        off += nb
+    dec.set_profiling(True)
+    st = dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs)
+    tm = dec.last_timings()
+    dec.set_profiling(False)
+    assert st == 0, R.error_name(st)
+    assert tm["images"] == 1024 and tm["lean_k1"] == 1
+    assert tm["lean_split"] > 0, "the default C4 layout splits its outlier intervals"
+    bad = []
+    for j in range(distinct):
+        ref = t.from_numpy(want[j][1][0]).to("cuda")
+        bad += [i for i in range(j, len(streams), distinct) if not t.equal(views[i], ref)]
+    assert not bad, f"{len(bad)} images differ, first {sorted(bad)[:8]}"
+
+
+def _rgb_shape(data):
+    """(rows, pitch) of the RGB destination, from the SOF0 header."""
+    i = data.index(b"\xff\xc0")
+    h = (data[i + 5] << 8) | data[i + 6]
+    w = (data[i + 7] << 8) | data[i + 8]
+    return (h, 3 * w)
 
 
 def _fixture(name):

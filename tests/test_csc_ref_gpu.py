@@ -1,7 +1,8 @@
-"""Pins the oracle's colour conversion against the reference's OWN HIP kernels
+"""Pins the oracle's per-pixel colour conversion against the reference's OWN HIP kernels
 (src/rocjpeg_hip_kernels.cpp compiled unmodified for gfx950 into oracle/_ref/librefcsc.so):
-every (Y, U, V) triple, i.e. all 16.7 M inputs, through ColorConvertYUV444ToRGB, plus the
-4:2:0 / 4:2:2 / 4:0:0 / 4:4:0 kernels on random planes."""
+every (Y, U, V) triple, i.e. all 16.7 M inputs, through ColorConvertYUV444ToRGB, and the NV12
+kernel's nearest chroma on random planes.  The whole output stage (all 13 kernels a gfx950
+device reaches, every format, CSS and ROI rule) is pinned in tests/test_output_stage_ref_gpu.py."""
 import ctypes
 import os
 
