@@ -231,6 +231,11 @@ def pmc_traffic(kernel, batch, launches, workload="c2"):
 
 
 # ------------------------------------------------------------------ one batch on the GPU
+def parity_sample(n, k=16):
+    """k image indices spread over a batch of n (first and last included)."""
+    return sorted({int(round(i * (n - 1) / max(1, k - 1))) for i in range(k)}) if n else []
+
+
 class BatchRun:
     """A rank's batch: streams parsed on the GPU (rocJpegAmdStreamParseDevice, resident), the
     destinations in one HBM arena sized as the reference samples size them
@@ -325,10 +330,6 @@ class BatchRun:
             ok = ok and ost == 0 and all(np.array_equal(v.cpu().numpy(), w_) for v, w_ in zip(self.views[q], want))
         return bool(ok)
 
-
-def parity_sample(n, k=16):
-    """k image indices spread over a batch of n (first and last included)."""
-    return sorted({int(round(i * (n - 1) / max(1, k - 1))) for i in range(k)}) if n else []
 
     def close(self):
         import torch
@@ -560,9 +561,7 @@ def main():
             "huffman_detail": {"intervals": t["intervals"], "chunks": t["chunks"],
                                "split_intervals": t["split_intervals"], "serial_fallbacks": t["serial_fallbacks"],
                                "entry_bytes_per_image": round(t["entry_bytes"] / n), "lean_k1": t["lean_k1"],
-                               "lean_split": t["lean_split"], "k0_fused": t["k0_fused"],
-                               "k2_stream": t["k2_stream"], "k2_stream_rows": t["k2_stream_rows"],
-                               "k2_deferred_rows": t["k2_deferred_rows"], "k2_stream_ms": round(t["k2_stream_ms"], 4)},
+                               "lean_split": t["lean_split"]},
             "end_to_end_algorithmic_GBps": round(imgs_total * per_img / elapsed / 1e9, 2),
             "host_input_images_per_s_per_gpu": round(host_rate, 1) if host_rate else None,
             "parse_images_per_s": {"host_1_thread": round(parse_host_rate, 1),

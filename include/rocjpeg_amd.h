@@ -97,17 +97,11 @@ typedef struct {
      decoded into device-local staging, then copied where the caller's pointers live */
   uint32_t routed_images;
   uint32_t lean_k1;          /* 1: K1 ran the lean row-interval kernel (rj_huff.hip, raw entries) */
-  uint32_t k2_stream;        /* 1: K2 streamed behind K1 (k_rows_stream + cleanup pass) */
-  uint32_t k2_deferred_rows; /* streaming K2: rows the bounded wait left to the cleanup pass */
-  float k2_stream_ms;        /* streaming K2 pass span (it runs beside K1) */
-  uint32_t k2_stream_rows;   /* rows the streaming pass decoded beside K1 (the rest: cleanup pass) */
   /* MCU rows with coefficients outside the int32 IDCT's exact domain (|coef x quant| >= 2^14:
      corrupt data with large quantisers), decoded again by the K2 fix-up launch in 64-bit */
   uint32_t wide_rows;
-  /* lean K1 split launch: intervals decoded by a head and a tail lane (rj_huff.hip) */
+  /* lean K1 outlier split: intervals decoded by a head and a tail lane (rj_huff.hip) */
   uint32_t lean_split;
-  /* 1: no K0 pass -- the lean K1 movers destuffed the raw bitstreams themselves (rj_huff.hip) */
-  uint32_t k0_fused;
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);

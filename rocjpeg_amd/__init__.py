@@ -101,9 +101,7 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("prog_kernel_ms", ctypes.c_float * 3), ("prog_kernel_launches", ctypes.c_uint32 * 3),
                 ("prog_kernel_bytes", ctypes.c_uint64 * 3),
                 ("routed_images", ctypes.c_uint32), ("lean_k1", ctypes.c_uint32),
-                ("k2_stream", ctypes.c_uint32), ("k2_deferred_rows", ctypes.c_uint32), ("k2_stream_ms", ctypes.c_float),
-                ("k2_stream_rows", ctypes.c_uint32), ("wide_rows", ctypes.c_uint32),
-                ("lean_split", ctypes.c_uint32), ("k0_fused", ctypes.c_uint32)]
+                ("wide_rows", ctypes.c_uint32), ("lean_split", ctypes.c_uint32)]
 
 
 class RocJpegAmdInterval(ctypes.Structure):  # include/rocjpeg_amd.h

@@ -148,16 +148,11 @@ int Decoder::Initialize() {
   }
   if (const char *m = getenv("RJ_PIPE_MIN")) pipe_min_ = uint32_t(std::max(1, atoi(m)));
   if (const char *o = getenv("RJ_SORT_LANES")) sort_lanes_ = atoi(o) != 0;
-  if (const char *l = getenv("RJ_LEAN")) lean_enabled_ = atoi(l) != 0;
   if (const char *l = getenv("RJ_LPT")) lpt_ = atoi(l) != 0;
   if (const char *l = getenv("RJ_K1_SOLO")) k1_solo_lds_ = uint32_t(std::max(0, atoi(l)));
-  if (const char *sk = getenv("RJ_STREAM_K2")) stream_enabled_ = atoi(sk) != 0;
-  if (const char *sp = getenv("RJ_SPLIT")) split_enabled_ = atoi(sp) != 0;
   if (const char *so = getenv("RJ_SPLIT_OUTLIERS")) outlier_split_ = atoi(so) != 0;
   if (const char *sf = getenv("RJ_SPLIT_OUTLIER_FRAC")) outlier_frac_ = atof(sf);
   if (const char *st = getenv("RJ_SPLIT_OUTLIER_T")) outlier_t_ = std::max(0.5, std::min(1.0, atof(st)));
-  if (const char *fd = getenv("RJ_FUSE_DESTUFF")) fuse_destuff_ = atoi(fd) != 0;
-  if (const char *sw = getenv("RJ_STREAM_WG")) stream_wg_per_cu_ = std::max(1, std::min(16, atoi(sw)));
   cu_count_ = std::max(1, prop.multiProcessorCount);
   RJ_HIP(hipHostMalloc(reinterpret_cast<void **>(&h_wide_flag_), 64, hipHostMallocMapped | hipHostMallocCoherent));
   RJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_wide_flag_), h_wide_flag_, 0));
@@ -170,9 +165,8 @@ int Decoder::Initialize() {
   for (auto &e : prog_join_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // development diagnostics, read once (never per call)
   const char *dbg_names[] = {"RJ_DEBUG_SCAN", "RJ_DEBUG_PROG", "RJ_DEBUG_WAVES", "RJ_DEBUG_HOST",
-                             "RJ_DEBUG_PIPE_SERIAL", "RJ_DEBUG_STAMPS", "RJ_DEBUG_K1", "RJ_DEBUG_K1_PIECES",
-                             "RJ_DEBUG_NODEP", "RJ_TEST_PROG_GIVEUP"};
-  for (int k = 0; k < 10; k++)
+                             "RJ_DEBUG_STAMPS", "RJ_DEBUG_K1", "RJ_DEBUG_K1_PIECES", "RJ_TEST_PROG_GIVEUP"};
+  for (int k = 0; k < 8; k++)
     if (getenv(dbg_names[k])) dbg_ |= 1u << k;
   if (const char *pp = getenv("RJ_PROG_PIPE")) prog_pipe_enabled_ = atoi(pp) != 0;
   if (const char *pw = getenv("RJ_PROG_WAVE_ALL")) prog_wave_all_ = atoi(pw) != 0;
@@ -996,7 +990,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // ---- lean K1 (rj_huff.hip): when every baseline image of the call is a "row" image (each
   // restart interval inside one MCU row) and no interval is split, K1 writes raw entries and K2
   // restores the DC predictions ----
-  bool lean = lean_enabled_ && !any_split && seg_total > 0;
+  bool lean = !any_split && seg_total > 0;
   for (int i = 0; i < n && lean; i++) {
     const DecodePlan &p = streams[i]->plan();
     if (p.progressive) continue;
@@ -1162,11 +1156,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   RJ_HIP(hipMemcpyAsync(dbase, h, blob_a, hipMemcpyHostToDevice, stream_));
   if (cbuf.count) RJ_HIP(hipMemsetAsync(cbuf.count, 0, sizeof(unsigned long long), stream_));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
-  // lean-only calls: the K1 movers destuff the raw ECS themselves (rj_huff.hip), no K0 pass
-  const bool raw_k1 = lean && fuse_destuff_ && prog_images == 0 && !split_enabled_ && !outlier_split_;
-  timings_.k0_fused = raw_k1 ? 1u : 0u;
-  if (!raw_k1) RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>()));
-  const uint8_t *k1_src = raw_k1 ? nullptr : d_destuff_.as<uint8_t>();
+  RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>()));
+  const uint8_t *k1_src = d_destuff_.as<uint8_t>();
   if (prog_images) {  // progressive images: K1p level by level, then their K2 rows (dense)
     const uint32_t *d_plane = reinterpret_cast<const uint32_t *>(dbase + off_plane);
     if (profiling_) RJ_HIP(hipEventRecord(prog_ev_[0], stream_));
@@ -1295,7 +1286,6 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   uint32_t lane_off[kMaxPipe + 1] = {}, frow_off[kMaxPipe + 1] = {}, grow_off[kMaxPipe + 1] = {};
   uint32_t class_max[kMaxPipe] = {};  // longest interval (bytes) of each class
   bool rows_from_lanes = false;
-  bool lane_rows = false;  // every interval is one MCU row and every row takes the same K2 path
   bool lanes_desc = false;  // lane order: longest interval first
   if (sorted) {
     constexpr uint32_t kBuckets = 4096;  // 32-B length buckets up to 128 KB
@@ -1321,7 +1311,6 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     uint32_t *ls = lane_seg.data();
     std::vector<uint32_t> &seg_pos = sc_.seg_pos;  // pipelined launch: each interval's lane
     if (ngroups > 1) seg_pos.resize(seg_total);
-    lane_rows = aligned;
     rows_from_lanes = ngroups > 1 && aligned;
     // rows from lanes: K2 row w of class g is lane lane_off[g] + w's interval, listed as
     // (image, row) in lane order -- K2 then starts each row from its record and the interval's
@@ -1330,17 +1319,13 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (rows_from_lanes) row_list.resize(seg_total);
     uint2 *rl = rows_from_lanes ? row_list.data() : nullptr;
     uint32_t gs = 0;
-    std::vector<uint2> &seg_len = sc_.seg_len;  // the split launch's planning only
-    const bool want_len = lean && split_enabled_;
-    if (want_len) seg_len.resize(seg_total);
     const bool want_pos = ngroups > 1;
     for (int i = 0; i < n; i++) {
       const DecodePlan &p = streams[i]->plan();
-      if (want_len || rl != nullptr || want_pos) {
+      if (rl != nullptr || want_pos) {
         uint32_t r = 0;
         for (size_t q = 0; q < p.segs.size(); q++) {
           const uint32_t l = pos[bucket(p.seg_bucket[q])]++;
-          if (want_len) seg_len[gs] = uint2{uint32_t(p.seg_lenblk[q]), uint32_t(p.seg_lenblk[q] >> 32)};
           ls[l] = gs;
           if (rl) rl[l] = uint2{uint32_t(i), r++};
           if (want_pos) seg_pos[gs] = l;
@@ -1404,23 +1389,21 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       }
     }
   }
-  // ---- lean split launch (rj_huff.hip): while the call has fewer intervals than two decoder
-  // waves per SIMD can hold, the longest intervals get a head lane and a tail lane (which
-  // starts at rj_split_byte and is joined where the two decoders' MCU starts meet) ----
+  // ---- lean outlier split (rj_huff.hip; the default, RJ_SPLIT_OUTLIERS=0 turns it off): the
+  // intervals longer than 9/16 of the longest one get a head lane and a tail lane (which starts
+  // at rj_split_byte and is joined where the two decoders' MCU starts meet) -- the longest chain
+  // then drops to ~9/16 of it -- in a launch that keeps one decoder wave per SIMD; skipped when
+  // more than outlier_frac_ of the intervals would split (near-uniform lengths, e.g. C2:
+  // splitting nearly everything is slower).  C4's mixed resolutions: 42,376 of
+  // 75,350 split, +12 %. ----
   uint32_t nsplit = 0, nl_split = 0;
   RjHuffSplit hsplit{0, 0};
-  // Outlier mode (the default; RJ_SPLIT_OUTLIERS=0 turns it off, RJ_SPLIT=1 replaces it): only
-  // the intervals longer than 9/16 of the longest one split -- the longest chain then drops to
-  // ~9/16 of it -- in a launch that keeps one decoder wave per SIMD; skipped when more than
-  // outlier_frac_ of the intervals would split (near-uniform lengths, e.g. C2: splitting nearly
-  // everything is slower).  C4's mixed resolutions: 42,376 of 75,350 split, +12 %.
-  const bool outlier_mode = !split_enabled_ && outlier_split_;
-  if (lean && sorted && lanes_desc && ngroups == 1 && !any_split && (split_enabled_ || outlier_mode) &&
-      !stream_enabled_ && !Dbg(kDebugNoDep) && seg_total > 0) {
-    const int64_t waves = int64_t(cu_count_) * (RJ_HL_SPLIT_DEC / 64);  // one round of the split grid
+  if (lean && sorted && lanes_desc && ngroups == 1 && !any_split && outlier_split_ && seg_total > 0) {
+    // one round of the split grid: two workgroups per CU of RJ_HL_SPLIT_DEC decoder lanes
+    const int64_t waves = int64_t(cu_count_) * 2 * (RJ_HL_SPLIT_DEC / 64);
     const int64_t kmax = 64 * waves - int64_t(seg_total);
     uint64_t lim = 0;
-    if (outlier_mode) {
+    {
       // count the outliers on the cached 32-B length buckets first; the descriptors' exact
       // lengths are gathered only when the call does split
       std::vector<uint16_t> &gb = sc_.seg_bkt;
@@ -1446,12 +1429,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     while (int64_t(nsplit) < kmax && nsplit < seg_total && lim != UINT64_MAX) {
       const uint2 sl = sc_.seg_len[lane_seg[nsplit]];
       if (sl.x < RJ_SPLIT_MIN_BYTES) break;  // lanes are sorted longest first
-      if (outlier_mode && sl.x <= lim) break;
+      if (sl.x <= lim) break;
       cap = std::max<uint64_t>(cap, rj_group(8ull * (sl.x - rj_split_byte(sl.x)) + sl.y +
                                              uint64_t(RJ_MAX_BLK_MCU) * RJ_ENT_PER_BLOCK + 1));
       nsplit++;
     }
-    if (outlier_mode && double(nsplit) > outlier_frac_ * double(seg_total)) nsplit = 0;
+    if (double(nsplit) > outlier_frac_ * double(seg_total)) nsplit = 0;
     if (nsplit > 0) {
       const uint32_t wsplit = (nsplit + 31) / 32;
       nl_split = wsplit * 64 + (seg_total - nsplit);
@@ -1502,54 +1485,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
             ms(t_host0, t_dedupe), ms(t_dedupe, t_layout), ms(t_layout, t_lanes), ms(t_lanes, t_k0),
             ms(t_k0, t_end));
   }
-  // ---- streaming K2 (rj_fused.hip k_rows_stream): every interval one MCU row, every image
-  // fused, lean K1 -- one K1 launch over all lanes publishes each interval when its entries are
-  // out, persistent K2 workgroups on a second stream start each row as soon as its interval is
-  // published, and a cleanup pass after K1 takes the rows a bounded wait deferred ----
-  const bool stream_k2 = stream_enabled_ && lean && lane_rows && fused_images > 0 &&
-                         fused_images == uint32_t(n) - prog_images;
-  timings_.k2_stream = stream_k2 ? 1u : 0u;
-  if (stream_k2) {
-    const bool fresh = d_flags_.capacity() < uint64_t(seg_total) * 4;
-    RJ_CHECK(d_flags_.Ensure(std::max<uint64_t>(uint64_t(seg_total) * 4, 256)));
-    RJ_CHECK(d_sctl_.Ensure((uint64_t(seg_total) + 4) * 4));
-    if (fresh || epoch_ == 1)  // new memory, or the 28-bit epoch wrapped: no stale flag may match
-      RJ_HIP(hipMemsetAsync(d_flags_.as<uint32_t>(), 0, d_flags_.capacity(), stream_));
-    uint32_t *ctl = d_sctl_.as<uint32_t>();
-    RJ_HIP(hipMemsetAsync(ctl, 0, 16, stream_));
-    RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0, upload B, counters done
-    RJ_HIP(hipStreamWaitEvent(pstream_[0], pev_[kMaxPipe - 1], 0));
-    if (profiling_) RJ_HIP(hipEventRecord(k1s_[0], stream_));
-    RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, seg_total, k1_src, d_tabs, d_lean, cbuf,
-                           d_flags_.as<uint32_t>(), epoch_, ctl + 3, k1_solo_lds_));
-    if (profiling_) RJ_HIP(hipEventRecord(pk1_[0], stream_));
-    if (profiling_) RJ_HIP(hipEventRecord(k2s_[0], pstream_[0]));
-    const uint32_t grid = std::min<uint32_t>(seg_total, uint32_t(stream_wg_per_cu_) * uint32_t(cu_count_));
-    wide(seg_total, wcnt, wlist, false, false);
-    RJ_HIP(LaunchRowsStream(pstream_[0], true, d_imgs, n, d_lane_seg, seg_total, d_flags_.as<uint32_t>(), epoch_, ctl,
-                            ctl + 4, HuffLaneWaves(seg_total), grid, cbuf, d_tabs, wcnt, wlist, lanes_desc ? 1u : 0u));
-    if (profiling_) RJ_HIP(hipEventRecord(k2e_[0], pstream_[0]));
-    RJ_HIP(hipEventRecord(pev_[0], pstream_[0]));
-    RJ_HIP(hipStreamWaitEvent(stream_, pev_[0], 0));
-    if (profiling_) RJ_HIP(hipEventRecord(k2s_[1], stream_));
-    RJ_HIP(LaunchRowsStream(stream_, false, d_imgs, n, d_lane_seg, seg_total, d_flags_.as<uint32_t>(), epoch_, ctl,
-                            ctl + 4, HuffLaneWaves(seg_total), std::min<uint32_t>(seg_total, 16u * uint32_t(cu_count_)),
-                            cbuf, d_tabs, wcnt, wlist, lanes_desc ? 1u : 0u));
-    if (profiling_) RJ_HIP(hipEventRecord(k2e_[1], stream_));
-  } else if (ngroups > 1) {
+  if (ngroups > 1) {
     RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0 and upload B done
-    if (Dbg(kDebugPipeSerial)) {  // development: each class's K1 alone, one after another
-      for (int g = 0; g < ngroups; g++) {
-        if (lean)
-          RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g],
-                                 k1_src, d_tabs, d_lean, cbuf));
-        else
-          RJ_HIP(LaunchEntropyLanes(stream_, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g],
-                                    d_destuff_.as<uint8_t>(), d_tabs, cbuf, epoch_));
-        if (profiling_) RJ_HIP(hipEventRecord(pk1_[g], stream_));
-      }
-    }
-    for (int g = 0; g < ngroups && !Dbg(kDebugPipeSerial); g++) {
+    for (int g = 0; g < ngroups; g++) {
       hipStream_t st = g == ngroups - 1 ? stream_ : pstream_[g];
       if (st != stream_) RJ_HIP(hipStreamWaitEvent(st, pev_[kMaxPipe - 1], 0));
       if (profiling_) RJ_HIP(hipEventRecord(k1s_[g], st));
@@ -1580,17 +1518,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
     for (int g = 0; g + 1 < ngroups; g++) RJ_HIP(hipStreamWaitEvent(stream_, pev_[g], 0));
   } else {
-    if (lean && Dbg(kDebugNoDep)) {  // timing experiment: K1 beside K2, no dependency (wrong output)
-      RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));
-      RJ_HIP(hipStreamWaitEvent(pstream_[0], pev_[kMaxPipe - 1], 0));
-      RJ_HIP(LaunchHuffLanes(pstream_[0], d_imgs, n, 0u, seg_total, k1_src, d_tabs, d_lean, cbuf));
-      RJ_HIP(hipEventRecord(pev_[0], pstream_[0]));
-      if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
-      if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
-    } else if (lean) {  // no split interval: one pass, no resolution / serial stages
+    if (lean) {  // no split interval: one pass, no resolution / serial stages
       RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, nsplit ? nl_split : seg_total, k1_src, d_tabs,
-                             d_lean, cbuf, nullptr, 0u, nullptr, k1_solo_lds_, nsplit ? &hsplit : nullptr,
-                             outlier_mode));
+                             d_lean, cbuf, k1_solo_lds_, nsplit ? &hsplit : nullptr));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
     } else {
@@ -1607,7 +1537,6 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(LaunchRows(stream_, true, d_imgs, n, d_grows, nullptr, general_rows, cbuf, d_tabs,
                       d_planes_.as<uint8_t>(), wcnt, wlist));
   }
-  if (lean && ngroups == 1 && Dbg(kDebugNoDep)) RJ_HIP(hipStreamWaitEvent(stream_, pev_[0], 0));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[4], stream_));
   RJ_HIP(LaunchOutputJobs(stream_, d_imgs, d_jobs, int(jobs.size()), rows_total, d_planes_.as<uint8_t>()));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[5], stream_));
@@ -1716,25 +1645,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(hipEventElapsedTime(&ms[1], ev_[1], ev_[2]));
     RJ_HIP(hipEventElapsedTime(&ms[4], ev_[4], ev_[5]));
     RJ_HIP(hipEventElapsedTime(&timings_.total_ms, ev_[0], ev_[5]));
-    if (stream_k2) {  // one K1 launch; K2 = the streaming pass + the cleanup pass
-      float k1 = 0, a = 0, b = 0, k12 = 0;
-      RJ_HIP(hipEventElapsedTime(&k1, k1s_[0], pk1_[0]));
-      RJ_HIP(hipEventElapsedTime(&a, k2s_[0], k2e_[0]));
-      RJ_HIP(hipEventElapsedTime(&b, k2s_[1], k2e_[1]));
-      RJ_HIP(hipEventElapsedTime(&k12, ev_[2], ev_[4]));
-      ms[2] = k1;
-      ms[3] = k12 - k1;
-      timings_.entropy_chunks_ms = k1;
-      timings_.k1_launch_ms_sum = k1;
-      timings_.k1_launches = 1;
-      timings_.k2_launch_ms_sum = a + b;
-      timings_.k2_launches = 2;
-      uint32_t ctl[2] = {0, 0};
-      RJ_HIP(hipMemcpy(ctl, d_sctl_.as<uint32_t>(), sizeof(ctl), hipMemcpyDeviceToHost));
-      timings_.k2_deferred_rows = ctl[1];
-      timings_.k2_stream_rows = std::min(ctl[0], seg_total) - ctl[1];
-      timings_.k2_stream_ms = a;
-    } else if (ngroups > 1) {  // K1 ends with the last class; K2 of the earlier classes overlaps it
+    if (ngroups > 1) {  // K1 ends with the last class; K2 of the earlier classes overlaps it
       float k1 = 0, k12 = 0;
       for (int g = 0; g < ngroups; g++) {
         float t = 0;

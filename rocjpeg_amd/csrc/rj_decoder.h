@@ -96,8 +96,7 @@ class Decoder {
   // the last class on stream_; pev_ joins them (no timing), pk1_ times each class's K1
   enum DebugFlag : uint32_t {  // env RJ_DEBUG_* (development diagnostics), bit k = dbg_names[k]
     kDebugScan = 1u << 0, kDebugProg = 1u << 1, kDebugWaves = 1u << 2, kDebugHost = 1u << 3,
-    kDebugPipeSerial = 1u << 4, kDebugStamps = 1u << 5, kDebugK1 = 1u << 6, kDebugK1Pieces = 1u << 7,
-    kDebugNoDep = 1u << 8, kTestProgGiveUp = 1u << 9
+    kDebugStamps = 1u << 4, kDebugK1 = 1u << 5, kDebugK1Pieces = 1u << 6, kTestProgGiveUp = 1u << 7
   };
   uint32_t dbg_ = 0;
   bool Dbg(uint32_t f) const { return (dbg_ & f) != 0; }
@@ -114,18 +113,11 @@ class Decoder {
   // workgroups past the first round (LPT order: the shortest) then wait for the CUs that finish
   // first instead of doubling up on a CU beside a long-interval workgroup
   uint32_t k1_solo_lds_ = 16384;
-  bool lean_enabled_ = true;       // env RJ_LEAN=0: the exact K1 (rj_entropy.hip) for row images too
-  bool fuse_destuff_ = false;      // env RJ_FUSE_DESTUFF=1 (with RJ_SPLIT_OUTLIERS=0): lean-only calls without K0, the K1 movers destuff (measured slower)
   bool outlier_split_ = true;      // env RJ_SPLIT_OUTLIERS=0: never split the outlier intervals (one decoder wave per SIMD)
   double outlier_t_ = 9.0 / 16;    // env RJ_SPLIT_OUTLIER_T: outliers are longer than this share of the longest interval
   double outlier_frac_ = 0.7;      // env RJ_SPLIT_OUTLIER_FRAC: at most this share of the intervals split in that mode
                                    // (C4's mix: 56 % above 9/16 of the longest; C2's near-uniform rows: 84 %)
-  bool split_enabled_ = false;     // env RJ_SPLIT=1: lean K1 head + tail lanes (rj_huff.hip; measured slower)
-  bool stream_enabled_ = false;    // env RJ_STREAM_K2=1: streaming K2 (k_rows_stream), measured no faster
   int cu_count_ = 256;
-  int stream_wg_per_cu_ = 2;       // env RJ_STREAM_WG: streaming K2 workgroups per CU (K1's LDS must still fit)
-  DeviceBuffer d_flags_;           // streaming K2: per interval, the epoch of the call that published it
-  DeviceBuffer d_sctl_;            // streaming K2: row counters + deferred row list
   DeviceBuffer d_wide_;            // K2 fix-up lists (rows outside the int32 IDCT's domain)
   uint32_t *h_wide_flag_ = nullptr;  // host-mapped, coherent: K2 recorded a row for the fix-up
   uint32_t *d_wide_flag_ = nullptr;
@@ -149,7 +141,7 @@ class Decoder {
     std::vector<RjJobDev> jobs;
     std::vector<uint64_t> stage_off;
     std::vector<uint32_t> tab_of, row_prefix, grow_prefix, seg_lane0, lane_seg, bucket_pos, seg_pos, lane_split;
-    std::vector<uint2> seg_len;  // per interval: destuffed bytes, blocks (lean split planning)
+    std::vector<uint2> seg_len;  // per interval: destuffed bytes, blocks (outlier split planning)
     std::vector<uint16_t> seg_bkt;  // per interval: 32-B length bucket (outlier split planning)
     std::vector<uint8_t> is_fused, row_group, routed;
     std::vector<uint2> row_list;

@@ -81,7 +81,7 @@ struct RjCoefBuf {
 // tail lane from rj_split_byte(dst_len); lane_seg entries carry the role in their top bits.
 #define RJ_LANE_HEAD 0x40000000u
 #define RJ_LANE_TAIL 0x80000000u
-#define RJ_HL_SPLIT_DEC 512          // decoder lanes per workgroup of the split launch
+#define RJ_HL_SPLIT_DEC 256          // decoder lanes per workgroup of the split launch (two workgroups per CU)
 #define RJ_SPLIT_MIN_BYTES 1024u     // shorter intervals stay whole
 __host__ __device__ inline uint32_t rj_split_byte(uint32_t dst_len) { return (dst_len * 29u / 64u) & ~15u; }
 struct RjHuffSplit {

@@ -296,19 +296,14 @@ __device__ __forceinline__ void load_dense_block(const RjImageDev &im, const uin
 //   kPlanes = true : general path, blocks into the MCU-padded component planes (K2b reads them)
 //   kDense = true  : progressive images -- blocks come from the dense coefficient buffer
 //                    (rj_prog.hip layout: zigzag, AC sign-magnitude) instead of entry streams
-// (image i, MCU row my) of a K2 launch: from an explicit list, from the K1 lane order (every
-// interval one MCU row), or from the per-image row prefix
+// (image i, MCU row my) of a K2 launch: from an explicit list, or from the per-image row prefix
 __device__ __forceinline__ void row_of_block(const RjImageDev *__restrict__ imgs, int nimg,
                                              const uint32_t *__restrict__ row_prefix, const uint2 *__restrict__ row_list,
-                                             const uint32_t *__restrict__ row_segs, uint32_t w, int &i, uint32_t &my) {
+                                             uint32_t w, int &i, uint32_t &my) {
   if (row_list != nullptr) {  // pipelined launch: an explicit (image, row) list for this group
     const uint2 e = row_list[w];
     i = int(U(e.x));
     my = U(e.y);
-  } else if (row_segs != nullptr) {  // every interval one MCU row: the K1 lanes' intervals
-    const uint32_t gseg = U(row_segs[w]);
-    i = __builtin_amdgcn_readfirstlane(upper_index(nimg, gseg, [&](int q) { return imgs[q].seg_prefix; }));
-    my = U(gp(imgs[i].segs)[gseg - imgs[i].seg_prefix].mcu_first / imgs[i].mcux);
   } else {
     // interpolation guess (exact for a batch of equal image heights: two independent loads),
     // then a binary search on the side it missed
@@ -389,16 +384,10 @@ __device__ __forceinline__ void rgb_strip(const uint8_t *ty, const uint8_t *tu, 
     uint32_t w0, w1, w2;
     csc4_pk(y4, ua, ub, va, vb, w0, w1, w2);
     const uint32_t off = __umul24(yrow, pitch) + __umul24(qx, 12u);  // 32-bit: saddr store form
-#ifdef RJ_EXP_NOSTORE  // timing experiment (wrong output): no pixel stores
-    if (w0 == 0x12345679u && w1 == 0x9abcdef1u)
-#endif
     *reinterpret_cast<RJ_GLOBAL uint3 *>(gp(dst) + off) = make_uint3(w0, w1, w2);
     if constexpr (kVs) {  // the second row of the pair, same chroma
       const uint32_t y4b = *reinterpret_cast<const uint32_t *>(ty + __umul24(yrow + 1, tw0) + x);
       csc4_pk(y4b, ua, ub, va, vb, w0, w1, w2);
-#ifdef RJ_EXP_NOSTORE
-      if (w0 == 0x12345679u && w1 == 0x9abcdef1u)
-#endif
       *reinterpret_cast<RJ_GLOBAL uint3 *>(gp(dst) + (off + pitch)) = make_uint3(w0, w1, w2);
     }
     qx += qsx;
@@ -525,9 +514,6 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
 
     bool wide = false;  // some coefficient of the strip needs the exact 64-bit IDCT
     // ---- A: clear the strip's LDS blocks, expand the entry stream into them ----
-#ifdef RJ_NO_WINPF
-    if (!kDense && sx > 0 && nv.bleft) win.load(ent, nv.cur(), tid);
-#endif
     __syncthreads();  // previous strip's tiles fully read
     for (uint32_t k = tid; k < nb * 8; k += 64)
       *reinterpret_cast<uint4 *>(s_buf + (k >> 3) * RJ_BLK_STRIDE + (k & 7) * 16) = make_uint4(0, 0, 0, 0);
@@ -538,9 +524,7 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
       if (dc_diff) parse_blocks<true, kSplit>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, thr, wide);
       else parse_blocks<false, false>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, thr, wide);
       drop = 0;
-#ifndef RJ_NO_WINPF
       if (sx + 1 < strips_x && nv.bleft) win.load(ent, nv.cur(), tid);  // next strip's window: lands behind B and C
-#endif
     }
     __syncthreads();
     if (!kDense && dc_diff) {
@@ -660,9 +644,6 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
         if (fmt == 3) {
           uint8_t *d = dst0 + (__umul24(py, pitch) + px * 3);
           if (n == 4 && a4) {
-#ifdef RJ_EXP_NOSTORE
-            if (w[0] == 0x12345679u && w[1] == 0x9abcdef1u)
-#endif
             *gp(reinterpret_cast<uint3 *>(d)) = make_uint3(w[0], w[1], w[2]);
           } else {
             store_bytes(d, 3 * n, w);
@@ -733,7 +714,6 @@ template <bool kPlanes, bool kDense = false, bool kSplit = false>
 __global__ __launch_bounds__(64, RJ_K2_OCC) void k_rows(const RjImageDev *__restrict__ imgs, int nimg,
                                              const uint32_t *__restrict__ row_prefix,
                                              const uint2 *__restrict__ row_list,
-                                             const uint32_t *__restrict__ row_segs,
                                              RjCoefBuf coefs,
                                              const RjTableSet *__restrict__ tabsets,
                                              uint8_t *__restrict__ planes, uint32_t *wide_cnt, uint2 *wide_list) {
@@ -741,7 +721,7 @@ __global__ __launch_bounds__(64, RJ_K2_OCC) void k_rows(const RjImageDev *__rest
   __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
   int i;
   uint32_t my;
-  row_of_block(imgs, nimg, row_prefix, row_list, row_segs, blockIdx.x, i, my);
+  row_of_block(imgs, nimg, row_prefix, row_list, blockIdx.x, i, my);
   row_body<kPlanes, kDense, false, kSplit>(imgs, i, my, coefs, tabsets, planes, s_buf, s_q, wide_cnt, wide_list);
 }
 
@@ -763,91 +743,6 @@ __global__ __launch_bounds__(64) void k_rows_fix(const RjImageDev *__restrict__ 
     __syncthreads();  // the previous row's tiles fully read
     row_body<kPlanes, kDense, true, kSplit>(imgs, i, U(e.y), coefs, tabsets, planes, s_buf, s_q, nullptr, nullptr);
   }
-}
-
-// Streaming K2 (fused rows of a call whose every interval is one MCU row): persistent
-// workgroups take rows in K1 lane order (shortest intervals first -- the order their K1 waves
-// finish in) and start each as soon as K1 has published its interval (lean K1 `flags`, release
-// after its stores; here one relaxed poll, then an agent acquire: MI355X_MICROARCH.md, valid
-// forms).  They stop taking rows once every K1 wave is done (ctl[3] == k1_waves): the rest goes
-// to the cleanup pass (kWait = false, after K1, full occupancy), which also takes the rows a
-// bounded wait deferred -- no workgroup ever waits on work that might not be resident, so the
-// two concurrent launches cannot deadlock.
-//   ctl[0]: next row (streaming pass), ctl[1]: deferred rows, ctl[2]: cleanup counter,
-//   ctl[3]: K1 waves done; deferred: the deferred rows
-template <bool kWait>
-__global__ __launch_bounds__(64, 4) void k_rows_stream(const RjImageDev *__restrict__ imgs, int nimg,
-                                                    const uint32_t *__restrict__ row_segs, uint32_t nrows,
-                                                    const uint32_t *flags, uint32_t epoch, uint32_t *ctl,
-                                                    uint32_t *deferred, uint32_t k1_waves, RjCoefBuf coefs,
-                                                    const RjTableSet *__restrict__ tabsets, uint32_t *wide_cnt, uint2 *wide_list,
-                                                    uint32_t reverse) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];
-  __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
-  __shared__ uint32_t s_row;
-  const uint32_t tid = threadIdx.x;
-  // cleanup: the rows the streaming pass never took, then the deferred ones
-  const uint32_t start = kWait ? 0u : min(U(__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)), nrows);
-  const uint32_t ndef = kWait ? 0u : U(__hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  for (;;) {
-    __syncthreads();  // the previous row's tiles fully read
-    if (tid == 0) {
-      uint32_t w = 0xFFFFFFFFu;
-      // streaming: no new row once K1 is done (the cleanup pass has full occupancy)
-      if (!kWait || __hip_atomic_load(ctl + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k1_waves)
-        w = atomicAdd(ctl + (kWait ? 0 : 2), 1u);
-      s_row = w;
-    }
-    __syncthreads();
-    const uint32_t w = U(s_row);
-    uint32_t row;
-    if (kWait) {
-      if (w >= nrows) break;
-      row = w;
-    } else {
-      if (w < nrows - start) row = start + w;
-      else if (w - (nrows - start) < ndef) row = U(deferred[w - (nrows - start)]);
-      else break;
-    }
-    // rows in the order K1 finishes them: reverse lane order when K1 took the longest first
-    const uint32_t phys = reverse ? nrows - 1 - row : row;
-    if (kWait) {
-      const uint32_t gseg = U(row_segs[phys]);
-      bool ready = false;
-      for (uint32_t k = 0; k < (1u << 14); k++) {  // ~2^14 x ~1 us: far beyond any K1 span
-        if (U(__hip_atomic_load(flags + gseg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == epoch) {
-          ready = true;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(32);
-      }
-      if (!ready) {
-        if (tid == 0) deferred[atomicAdd(ctl + 1, 1u)] = row;
-        continue;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-    int i;
-    uint32_t my;
-    row_of_block(imgs, nimg, nullptr, nullptr, row_segs, phys, i, my);
-    row_body<false, false>(imgs, i, my, coefs, tabsets, nullptr, s_buf, s_q, wide_cnt, wide_list);
-  }
-}
-
-hipError_t LaunchRowsStream(hipStream_t st, bool wait, const RjImageDev *imgs, int nimg, const uint32_t *row_segs,
-                            uint32_t nrows, const uint32_t *flags, uint32_t epoch, uint32_t *ctl, uint32_t *deferred,
-                            uint32_t k1_waves, uint32_t grid, RjCoefBuf coefs, const RjTableSet *tabsets,
-                            uint32_t *wide_cnt, uint2 *wide_list, uint32_t reverse) {
-  if (nrows == 0) return hipSuccess;
-  if (wait)
-    hipLaunchKernelGGL(k_rows_stream<true>, dim3(grid), dim3(64), 0, st, imgs, nimg, row_segs, nrows, flags, epoch, ctl,
-                       deferred, k1_waves, coefs, tabsets, wide_cnt, wide_list, reverse);
-  else
-    hipLaunchKernelGGL(k_rows_stream<false>, dim3(grid), dim3(64), 0, st, imgs, nimg, row_segs, nrows, flags, epoch,
-                       ctl, deferred, k1_waves, coefs, tabsets, wide_cnt, wide_list, reverse);
-  return hipGetLastError();
 }
 
 // the fix-up launch behind a K2 launch of `cap` rows (same stream, same variant; a lean split
@@ -880,19 +775,18 @@ hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, in
                       const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
                       uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list) {
   if (nrows == 0) return hipSuccess;
-  const uint32_t *no_segs = nullptr;
   if (coefs.piece_shift != 0) {  // lean split launch: pieces with skips / early terminators
     if (to_planes)
       hipLaunchKernelGGL((k_rows<true, false, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list,
-                         no_segs, coefs, tabsets, planes, wide_cnt, wide_list);
+                         coefs, tabsets, planes, wide_cnt, wide_list);
     else
       hipLaunchKernelGGL((k_rows<false, false, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list,
-                         no_segs, coefs, tabsets, planes, wide_cnt, wide_list);
+                         coefs, tabsets, planes, wide_cnt, wide_list);
   } else if (to_planes) {
-    hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, no_segs, coefs,
+    hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs,
                        tabsets, planes, wide_cnt, wide_list);
   } else {
-    hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, no_segs, coefs,
+    hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs,
                        tabsets, planes, wide_cnt, wide_list);
   }
   return hipGetLastError();
@@ -902,13 +796,12 @@ hipError_t LaunchRowsDense(hipStream_t st, bool to_planes, const RjImageDev *img
                            uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets, uint8_t *planes,
                            uint32_t *wide_cnt, uint2 *wide_list) {
   if (nrows == 0) return hipSuccess;
-  const uint32_t *no_segs = nullptr;
   const uint2 *no_list = nullptr;
   if (to_planes)
-    hipLaunchKernelGGL((k_rows<true, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, no_list, no_segs,
+    hipLaunchKernelGGL((k_rows<true, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, no_list,
                        coefs, tabsets, planes, wide_cnt, wide_list);
   else
-    hipLaunchKernelGGL((k_rows<false, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, no_list, no_segs,
+    hipLaunchKernelGGL((k_rows<false, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, no_list,
                        coefs, tabsets, planes, wide_cnt, wide_list);
   return hipGetLastError();
 }
@@ -924,20 +817,5 @@ void DumpRowStamps() {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(rj_stamp), z, sizeof(z));
 }
 #endif
-
-hipError_t LaunchRowsOfLanes(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg,
-                             const uint32_t *row_segs, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
-                             uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list) {
-  if (nrows == 0) return hipSuccess;
-  const uint32_t *no_prefix = nullptr;
-  const uint2 *no_list = nullptr;
-  if (to_planes)
-    hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, no_prefix, no_list, row_segs, coefs,
-                       tabsets, planes, wide_cnt, wide_list);
-  else
-    hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, no_prefix, no_list, row_segs, coefs,
-                       tabsets, planes, wide_cnt, wide_list);
-  return hipGetLastError();
-}
 
 }  // namespace rj

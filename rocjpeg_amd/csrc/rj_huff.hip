@@ -35,24 +35,13 @@ namespace rj {
 #define RJ_HL_AC_BYTES (RJ_HL_AC_WORDS * 4)
 #define RJ_HL_DC0 (2 * RJ_HL_AC_BYTES)
 #define RJ_HL_LUT_WORDS (2 * RJ_HL_AC_WORDS + 2 * RJ_HL_DC_WORDS)
-// Split launch (rj_kernels.h LaunchHuffLanes): MCU-start records kept by a tail lane
-#define RJ_HL_REC 48
+// Split launch (rj_kernels.h LaunchHuffLanes): MCU-start records kept by a tail lane (two
+// workgroups per CU must fit in LDS; a head that finds no equal MCU start among them decodes the
+// whole interval)
+#define RJ_HL_REC 20
 #define RJ_HL_REC_LIMIT 65280u              // records are 16-bit bit positions past the split
 
 __device__ const uint4 rj_hl_zero[2] = {};
-
-// timing experiments only (results are wrong): RJ_HL_X_NOSTORE drops the in-loop entry flushes,
-// RJ_HL_X_NOLOAD refills the ring from the lane's first chunks (cache hits)
-#ifdef RJ_HL_X_NOSTORE
-#define RJ_HL_X_FLUSH(x)
-#else
-#define RJ_HL_X_FLUSH(x) x
-#endif
-#ifdef RJ_HL_X_NOLOAD
-#define RJ_HL_X_LOADIDX(p) (src + ((p) - src) % 2)
-#else
-#define RJ_HL_X_LOADIDX(p) (p)
-#endif
 
 #ifdef RJ_HL_STAMPS  // diagnostic build: cycles in the symbol steps / the phase ends, summed over waves
 __device__ unsigned long long rj_hl_stamp[8];
@@ -87,70 +76,7 @@ __device__ __forceinline__ void hl_flush(const HCol<S> &stage, uint32_t from, ui
   for (int q = 0; q < G; q++) w[q] = stage[s0 + q];
   uint4 *d4 = reinterpret_cast<uint4 *>(dst);
 #pragma unroll
-  for (int q = 0; q < G / 4; q++) {
-    const uint4 v = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-#ifdef RJ_HL_X_NT
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<RJ_GLOBAL u32x4 *>(gp(d4) + q));
-#else
-    gp(d4)[q] = v;
-#endif
-  }
-}
-
-// Raw-ECS movers (LaunchHuffLanes with destuffed == nullptr: K0 skipped).  Byte x of an
-// interval's raw range [0, slen) is byte (a0 + x) of the dword array dw; dword indices are
-// clamped to dlast, the dword holding byte slen + 3 (the marker / slack behind the data).
-// K0's rule (rj_kernels.hip k_destuff): byte i is dropped when (b[i] == 00 && b[i-1] == FF) or
-// (b[i] == FF && b[i+1] == FF), with b[-1] = 0 and no byte behind the range.
-struct HlRaw {
-  const RJ_GLOBAL uint32_t *dw;
-  uint32_t a0, dlast, slen;
-  __device__ __forceinline__ uint32_t ld(uint32_t j) const { return dw[min(j, dlast)]; }
-};
-
-// one 16-B chunk of destuffed bytes from raw byte rpos on (prev: the raw byte before rpos);
-// zero bytes past the data.  The slow path of the raw mover: chunks with an FF byte, the last
-// partial chunk.
-__device__ __forceinline__ uint4 hl_destuff_chunk(const HlRaw &R, uint32_t &rpos, uint32_t &prev) {
-  uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0, o = 0;
-  while (o < 16u && rpos < R.slen) {
-    const uint32_t j = (R.a0 + rpos) >> 2, sh = (R.a0 + rpos) & 3u;
-    uint32_t d[9], w[9];
-#pragma unroll
-    for (int k = 0; k < 9; k++) d[k] = R.ld(j + k);
-#pragma unroll
-    for (int k = 0; k < 8; k++) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
-    w[8] = d[8] >> (8u * sh);  // byte 32 (lookahead only)
-    uint32_t used = 0;
-#pragma unroll
-    for (int i = 0; i < 32; i++) {
-      const uint32_t x = (w[i >> 2] >> (8 * (i & 3))) & 255u;
-      const uint32_t nx = (w[(i + 1) >> 2] >> (8 * ((i + 1) & 3))) & 255u;
-      if (o < 16u && rpos + uint32_t(i) < R.slen) {
-        const bool nxv = rpos + uint32_t(i) + 1u < R.slen;
-        const bool drop = (x == 0u && prev == 0xFFu) || (x == 0xFFu && nxv && nx == 0xFFu);
-        if (!drop) {
-          const uint32_t v = x << (8u * (o & 3u));
-          const uint32_t wi = o >> 2;
-          o0 |= wi == 0 ? v : 0u;
-          o1 |= wi == 1 ? v : 0u;
-          o2 |= wi == 2 ? v : 0u;
-          o3 |= wi == 3 ? v : 0u;
-          o++;
-        }
-        prev = x;
-        used = uint32_t(i) + 1u;
-      }
-    }
-    rpos += used;
-  }
-  return make_uint4(o0, o1, o2, o3);
-}
-
-__device__ __forceinline__ bool hl_has_ff(uint32_t w) {
-  const uint32_t t = ~w;
-  return ((t - 0x01010101u) & ~t & 0x80808080u) != 0;
+  for (int q = 0; q < G / 4; q++) gp(d4)[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 
 // Codes the first level does not resolve (rare): AC second level, or libjpeg's canonical
@@ -256,7 +182,7 @@ __device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) { *(lds_vu32 *)(
 // couples into its symbol chain (vmcnt counts loads and stores in one queue -- a decoder that also
 // issued its ring loads waited for its older stores).
 //
-// kSplit (DEC = 512, one workgroup per CU, two decoder waves per SIMD): an interval listed with
+// kSplit (the outlier intervals of a call; two workgroups per CU): an interval listed with
 // RJ_LANE_HEAD at lane l < 32 of a wave also has a tail lane at l + 32 (RJ_LANE_TAIL), which
 // decodes speculatively from the split byte rj_split_byte(dst_len) as if an MCU started there,
 // recording the bit positions of its first RJ_HL_REC MCU starts past the split.  The
@@ -268,10 +194,9 @@ __device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) { *(lds_vu32 *)(
 // needed).  With no equal MCU start the head decodes the whole interval.  A tail that reaches libjpeg's insufficient-data point stops: K2 zero-fills
 // the piece's missing blocks exactly as libjpeg's zero blocks.
 template <int DEC, int GROUP, bool kSplit, int PHASE>
-__global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
+__global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0, uint32_t nlanes, const uint8_t *__restrict__ destuffed,
-    const RjTableSet *__restrict__ tabsets, const RjLeanTables *__restrict__ lean, RjCoefBuf coefs, uint32_t *flags,
-    uint32_t epoch, uint32_t *done, RjHuffSplit split) {
+    const RjTableSet *__restrict__ tabsets, const RjLeanTables *__restrict__ lean, RjCoefBuf coefs, RjHuffSplit split) {
   constexpr uint32_t kStage = 2 * GROUP;
   constexpr uint32_t kPairs = kSplit ? DEC / 2 : 1;
   __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_HL_WORDS][DEC];
@@ -279,16 +204,13 @@ __global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
   __shared__ __attribute__((aligned(16))) uint32_t s_lut[RJ_HL_LUT_WORDS];
   __shared__ uint32_t s_dec[DEC];  // decoder -> mover: ring words fully consumed (RJ_HL_FIN: done)
   __shared__ uint32_t s_mov[DEC];  // mover -> decoder: 16-B chunks committed to the ring
-  // MCU-start records per tail lane: 48, or 20 in the 256-lane instance (two workgroups per CU
-  // must fit in LDS; a head that finds no equal MCU start among them decodes the whole interval)
-  constexpr uint32_t kRec = DEC == 256 ? 20u : uint32_t(RJ_HL_REC);
+  constexpr uint32_t kRec = RJ_HL_REC;  // MCU-start records per tail lane
   __shared__ uint16_t s_rec[kSplit ? kRec + 1 : 1][kPairs];  // tail lanes' MCU-start records (+ scratch)
   __shared__ uint32_t s_nrec[kPairs];  // records published by the tail (bit 31: no more will come)
   __shared__ uint32_t s_T, s_ne;
   const uint32_t tid = threadIdx.x;
   const bool mover = tid >= uint32_t(DEC);
   const uint32_t L = mover ? tid - DEC : tid;  // the decoder lane (LDS column)
-  if (flags != nullptr && !mover) __builtin_amdgcn_s_setprio(2);  // the serial chains win issue over streaming K2 waves
   if (tid == 0) s_ne = 0;
   const uint32_t g = lane0 + blockIdx.x * DEC + L;
   bool pending = g < lane0 + nlanes;
@@ -334,66 +256,6 @@ __global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
     const uint32_t nchunks = (nbytes + 15) / 16;
     const HCol<DEC> ring{&s_ring[0][L]};
 
-    if (!kSplit && mover && destuffed == nullptr) {  // (the split launch keeps K0)
-      // ---- raw mover: the same ring protocol, destuffing the raw ECS on the way.  Chunks
-      // without an FF byte are the common case: their loads are issued a round ahead assuming
-      // every chunk before them is one too (raw offset = 16 per chunk); the first chunk that is
-      // not goes through hl_destuff_chunk, and the round's later chunks are loaded again ----
-      const uintptr_t ba = reinterpret_cast<uintptr_t>(im.ecs + sg.src_off);
-      const HlRaw R{gp(reinterpret_cast<const uint32_t *>(ba & ~uintptr_t(3))),
-                    uint32_t(ba & 3u), (uint32_t(ba & 3u) + sg.src_len + 3u) >> 2, sg.src_len};
-      uint32_t cm = 0, na = 0, rpos = 0, prev = 0;
-      uint32_t pw[4][5];
-      for (;;) {
-        const uint32_t rd = lds_ld(&s_dec[L]);
-        if (na > 0) {
-          bool good = true;  // every chunk so far was a fast one: window j starts at rpos
-#pragma unroll
-          for (uint32_t j = 0; j < 4; j++) {
-            if (j < na && good) {
-              const uint32_t sh = (R.a0 + rpos) & 3u;
-              const uint32_t w0 = __builtin_amdgcn_alignbyte(pw[j][1], pw[j][0], sh);
-              const uint32_t w1 = __builtin_amdgcn_alignbyte(pw[j][2], pw[j][1], sh);
-              const uint32_t w2 = __builtin_amdgcn_alignbyte(pw[j][3], pw[j][2], sh);
-              const uint32_t w3 = __builtin_amdgcn_alignbyte(pw[j][4], pw[j][3], sh);
-              uint4 c;
-              if (rpos >= R.slen) {
-                c = make_uint4(0, 0, 0, 0);  // past the data: the zero bits libjpeg inserts
-              } else if (rpos + 16u <= R.slen && prev != 0xFFu && !hl_has_ff(w0) && !hl_has_ff(w1) &&
-                         !hl_has_ff(w2) && !hl_has_ff(w3)) {
-                c = make_uint4(w0, w1, w2, w3);
-                rpos += 16u;
-                prev = w3 >> 24;
-              } else {
-                c = hl_destuff_chunk(R, rpos, prev);
-                good = false;
-              }
-              hl_put(ring, (cm + j) & (RJ_HL_CHUNKS - 1), c);
-              if (!good) na = j + 1;  // the round's later windows are stale
-            }
-          }
-          cm += na;
-          lds_st(&s_mov[L], cm);  // after the ring words (same wave, in order)
-          na = 0;
-        }
-        const bool fin = rd == RJ_HL_FIN;
-        const uint32_t live = fin ? RJ_HL_CHUNKS : cm - (rd >> 2);
-        const uint32_t n = min(RJ_HL_CHUNKS - live, 4u);
-        if (n > 0 && rpos < R.slen) {
-          const uint32_t j0 = (R.a0 + rpos) >> 2;
-#pragma unroll
-          for (uint32_t j = 0; j < 4; j++)
-            if (j < n) {
-#pragma unroll
-              for (uint32_t k = 0; k < 5; k++) pw[j][k] = R.ld(j0 + 4u * j + k);
-            }
-        }
-        na = n;
-        if (__builtin_amdgcn_ballot_w64(!fin) == 0) break;
-        if (__builtin_amdgcn_ballot_w64(n > 0) == 0) __builtin_amdgcn_s_sleep(4);
-      }
-      continue;
-    }
     if (mover) {
       // ---- mover: keep the ring's free chunk slots filled (past the data: zero chunks, the
       // zero bits libjpeg inserts), up to 4 chunks per round; a round's loads are committed at
@@ -517,7 +379,7 @@ __global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
       // group leaves (< GROUP stay pending); wait until the next phase's words are in the ring ----
       lds_st(&s_dec[L], rr - 2u);
       if (ne - fl >= GROUP) {
-        RJ_HL_X_FLUSH((hl_flush<DEC, GROUP>(stage, fl, ent + fl)));
+        hl_flush<DEC, GROUP>(stage, fl, ent + fl);
         fl += GROUP;
       }
       if (kSplit) {
@@ -583,16 +445,8 @@ __global__ __launch_bounds__(2 * DEC, DEC == 256 ? 2 : 1) void k_huff(
       }
     }
     if (coefs.count) atomicAdd(&s_ne, ne + 1);
-    if (flags != nullptr) {  // streaming K2: publish the interval (release after this wave's stores)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the flag must not overtake the write-back
-      __hip_atomic_store(flags + gseg, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
   if (tid == 0 && coefs.count != nullptr && s_ne != 0) atomicAdd(coefs.count, (unsigned long long)s_ne);
-  // streaming K2 stops taking rows once every K1 decoder wave is here (its intervals were published above)
-  if (done != nullptr && !mover && (tid & 63) == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 #ifdef RJ_HL_STAMPS
@@ -610,20 +464,15 @@ void DumpHuffStamps() {
 
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
-                           RjCoefBuf coefs, uint32_t *flags, uint32_t epoch, uint32_t *done, uint32_t extra_lds,
-                           const RjHuffSplit *split, bool split_one_wave) {
+                           RjCoefBuf coefs, uint32_t extra_lds, const RjHuffSplit *split) {
   if (nlanes == 0) return hipSuccess;
-  static_assert(RJ_HL_SPLIT_DEC == 512, "HuffLaneWaves / the split lane layout");
-  if (split != nullptr && split_one_wave) {  // outliers split: one decoder wave per SIMD
-    hipLaunchKernelGGL((k_huff<256, 8, true, 8>), dim3((nlanes + 255) / 256), dim3(512), 0, st, imgs, nimg, lane0,
-                       nlanes, destuffed, tabsets, lean, coefs, nullptr, 0u, nullptr, *split);
-  } else if (split != nullptr) {  // one workgroup per CU: the LUT is shared by 512 decoder lanes
+  if (split != nullptr) {  // outliers split: one decoder wave per SIMD, two workgroups per CU
     hipLaunchKernelGGL((k_huff<RJ_HL_SPLIT_DEC, 8, true, 8>), dim3((nlanes + RJ_HL_SPLIT_DEC - 1) / RJ_HL_SPLIT_DEC),
                        dim3(2 * RJ_HL_SPLIT_DEC), 0, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs,
-                       nullptr, 0u, nullptr, *split);
+                       *split);
   } else {
-    hipLaunchKernelGGL((k_huff<256, RJ_HL_PHASE, false, RJ_HL_PHASE>), dim3((nlanes + 255) / 256), dim3(512), extra_lds, st, imgs, nimg, lane0,
-                       nlanes, destuffed, tabsets, lean, coefs, flags, epoch, done, RjHuffSplit{0, 0});
+    hipLaunchKernelGGL((k_huff<256, RJ_HL_PHASE, false, RJ_HL_PHASE>), dim3((nlanes + 255) / 256), dim3(512), extra_lds,
+                       st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs, RjHuffSplit{0, 0});
   }
   return hipGetLastError();
 }

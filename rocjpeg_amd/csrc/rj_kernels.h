@@ -24,21 +24,13 @@ hipError_t LaunchEntropyLanes(hipStream_t st, const RjImageDev *imgs, int nimg, 
 
 // Lean K1 (rj_huff.hip): lanes [lane0, lane0 + nlanes), one whole interval each, raw entries;
 // only for calls whose every baseline image is a row image and no interval is split.
-// flags != null: each interval publishes flags[gseg] = epoch once its entries are visible
-// device-wide (streaming K2).
-// done != null: every wave adds 1 to *done when it has published its lanes' intervals.
+// split != null: the outlier split launch -- lane_seg lists per wave 32 head lanes then their 32
+// tail lanes (RJ_LANE_HEAD / RJ_LANE_TAIL), split waves first, then whole intervals 64 per wave;
+// pieces at interval << 1 (coefs.piece_shift = 1); 512-thread workgroups, two per CU (one
+// decoder wave per SIMD, as in the unsplit launch).
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
-                           RjCoefBuf coefs, uint32_t *flags = nullptr, uint32_t epoch = 0, uint32_t *done = nullptr,
-                           uint32_t extra_lds = 0, const RjHuffSplit *split = nullptr, bool split_one_wave = false);
-// split != null: the split launch -- lane_seg lists per wave 32 head lanes then their 32 tail
-// lanes (RJ_LANE_HEAD / RJ_LANE_TAIL), split waves first, then whole intervals 64 per wave;
-// pieces at interval << 1 (coefs.piece_shift = 1); one 1024-thread workgroup per CU, or with
-// split_one_wave (only the outlier intervals split) 512-thread workgroups, two per CU: one
-// decoder wave per SIMD, as in the unsplit launch.
-// waves of a LaunchHuffLanes grid over n lanes
-inline uint32_t HuffLaneWaves(uint32_t nlanes) { return (nlanes + 255) / 256 * 4; }
-
+                           RjCoefBuf coefs, uint32_t extra_lds = 0, const RjHuffSplit *split = nullptr);
 // K2b (general path): every output format / ROI of rocjpeg_decoder.cpp:143-180 from the planes.
 hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobDev *jobs, int njobs, uint32_t total_rows,
                             const uint8_t *planes);
@@ -54,19 +46,6 @@ hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobD
 hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
                       const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
                       uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list);
-// K2 over the MCU rows of the intervals row_segs[0, nrows) (batch-global interval indices), for
-// batches whose every interval is exactly one MCU row.
-hipError_t LaunchRowsOfLanes(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg,
-                             const uint32_t *row_segs, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
-                             uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list);
-
-// Streaming K2 (rj_fused.hip k_rows_stream): persistent workgroups over the rows of a call
-// whose every interval is one MCU row, each row started once lean K1 has published its interval
-// (flags[gseg] == epoch); wait = false: the cleanup pass over the rows a bounded wait deferred.
-hipError_t LaunchRowsStream(hipStream_t st, bool wait, const RjImageDev *imgs, int nimg, const uint32_t *row_segs,
-                            uint32_t nrows, const uint32_t *flags, uint32_t epoch, uint32_t *ctl, uint32_t *deferred,
-                            uint32_t k1_waves, uint32_t grid, RjCoefBuf coefs, const RjTableSet *tabsets,
-                            uint32_t *wide_cnt, uint2 *wide_list, uint32_t reverse = 0);
 // The fix-up launch of one K2 launch's list (same variant; cap = that launch's rows).
 hipError_t LaunchRowsFix(hipStream_t st, bool to_planes, bool dense, const RjImageDev *imgs, int nimg, RjCoefBuf coefs,
                          const RjTableSet *tabsets, uint8_t *planes, const uint32_t *wide_cnt, const uint2 *wide_list,

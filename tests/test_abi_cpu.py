@@ -213,3 +213,20 @@ def test_oversubscribed_tables_are_refused_without_writes(tmp_path):
     r = subprocess.run([str(exe), str(bad)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "status=-3 valid=10" in r.stdout
+
+
+def test_timings_struct_matches_binding(tmp_path):
+    """The ctypes mirror of RocJpegAmdTimings (rocjpeg_amd/__init__.py) has the C layout: size and
+    the offset of every field, from a probe compiled against include/rocjpeg_amd.h."""
+    import subprocess
+    fields = [k for k, _ in R.RocJpegAmdTimings._fields_]
+    src = tmp_path / "t.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "rocjpeg_amd.h"\nint main(void) {\n'
+                   '  printf("%zu\\n", sizeof(RocJpegAmdTimings));\n' +
+                   "".join(f'  printf("%zu\\n", offsetof(RocJpegAmdTimings, {k}));\n' for k in fields) + "  return 0;\n}\n")
+    exe = tmp_path / "t"
+    subprocess.run(["gcc", "-std=c11", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", f"-I{INCLUDE}", str(src),
+                    "-o", str(exe)], check=True, capture_output=True)
+    out = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert out[0] == ctypes.sizeof(R.RocJpegAmdTimings)
+    assert out[1:] == [getattr(R.RocJpegAmdTimings, k).offset for k in fields]

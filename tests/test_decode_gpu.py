@@ -209,25 +209,18 @@ def test_long_interval_batch_mixed(dec):
 
 
 @pytest.fixture(scope="module",
-                params=[(0, 4, {"RJ_LEAN": "0"}), (1, 4, {"RJ_LEAN": "0"}), (0, 1, {"RJ_LEAN": "0"}), (0, 4, {}),
-                        (0, 1, {}), (1, 1, {}), (0, 1, {"RJ_LPT": "0", "RJ_K1_SOLO": "0"}),
-                        (0, 2, {"RJ_STREAM_K2": "1"}), (0, 1, {"RJ_SPLIT": "1"}), (1, 1, {"RJ_SPLIT": "1"}),
-                        (0, 1, {"RJ_FUSE_DESTUFF": "1", "RJ_SPLIT_OUTLIERS": "0"}),
-                        (1, 1, {"RJ_FUSE_DESTUFF": "1", "RJ_SPLIT_OUTLIERS": "0"}),
+                params=[(0, 4, {}), (1, 4, {}), (0, 1, {}), (1, 1, {}), (0, 1, {"RJ_LPT": "0", "RJ_K1_SOLO": "0"}),
                         (0, 1, {"RJ_SPLIT_OUTLIERS": "1", "RJ_SPLIT_OUTLIER_FRAC": "1"}),
                         (1, 1, {"RJ_SPLIT_OUTLIERS": "1", "RJ_SPLIT_OUTLIER_FRAC": "1"})],
-                ids=["exact_g4", "exact_general_g4", "exact_g1", "lean_g4", "lean_g1", "lean_general_g1",
-                     "lean_g1_short_first", "lean_stream_g2", "lean_split_g1", "lean_split_general_g1",
-                     "lean_raw_movers_g1", "lean_raw_movers_general_g1",
-                     "lean_split_outliers_g1", "lean_split_outliers_general_g1"])
+                ids=["g4", "general_g4", "g1", "general_g1", "g1_short_first", "split_outliers_g1",
+                     "split_outliers_general_g1"])
 def pdec(request):
     """A decoder that sorts the K1 lanes of every call with no split interval by length
     (RJ_PIPE_MIN=1) and, with 4 groups, pipelines it: interval length classes on separate
-    streams, each class's K2 rows after the K1 lanes of its class and all earlier ones.  The
-    lean K1 (the default for row-interval batches: one launch, longest intervals first, one
-    workgroup per CU; RJ_LEAN=0 takes the exact K1), the streaming K2 (RJ_STREAM_K2=1) and the
-    lean split launch (RJ_SPLIT=1: head + tail lanes per long interval, rj_huff.hip) and the raw
-    movers (RJ_FUSE_DESTUFF=1: no K0 pass, the K1 movers destuff the raw ECS) are covered here."""
+    streams, each class's K2 rows after the K1 lanes of its class and all earlier ones.  A batch
+    of row-interval images takes the lean K1 (rj_huff.hip), a batch with any other image the
+    exact K1 (rj_entropy.hip); the lean outlier split (head + tail lanes per long interval) is
+    forced on every long interval here (RJ_SPLIT_OUTLIER_FRAC=1)."""
     import os
     from tests import gpu_util as G
     G.torch()
@@ -307,12 +300,10 @@ def test_pipelined_row_aligned_batch(pdec, fmt):
     assert t["pipe_groups"] == pdec.groups
     if pdec.groups > 1:
         assert t["pipe_lane_rows"] == 1
-    assert t["lean_k1"] == (0 if pdec.extra.get("RJ_LEAN") == "0" else 1)
-    assert t["k2_stream"] == (1 if pdec.extra.get("RJ_STREAM_K2") else 0)
-    if pdec.extra.get("RJ_SPLIT") == "1" or pdec.extra.get("RJ_SPLIT_OUTLIERS") == "1":
-        # the 1080p intervals (and the damaged ones) are split (outliers: those near the longest)
+    assert t["lean_k1"] == 1
+    if pdec.extra.get("RJ_SPLIT_OUTLIERS") == "1":
+        # the 1080p intervals (and the damaged ones) near the longest are split
         assert t["lean_split"] > 0
-    assert t["k0_fused"] == (1 if pdec.extra.get("RJ_FUSE_DESTUFF") == "1" else 0)
     for k, (d, shapes, bufs) in enumerate(zip(datas, shapes_all, bufs_all)):
         ost, want = O.oracle_decode(d, int(fmt), shapes)
         assert ost == 0
