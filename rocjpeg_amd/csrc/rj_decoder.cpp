@@ -55,6 +55,14 @@ bool FusedEligible(const StreamInfo &in, const DecodePlan &p, int fmt, bool roi,
 
 }  // namespace
 
+int Decoder::HostThreads() {
+  if (const char *v = getenv("RJ_HOST_THREADS"))
+    if (atoi(v) > 0) return std::min(64, atoi(v));
+  // 8: on the GPU box (a 16-CPU share) 4-8 staging threads beat 16-32 (the copies then compete
+  // with the caller's own threads for the share; tools/host_input.py)
+  return int(std::min(8u, std::max(1u, std::thread::hardware_concurrency())));
+}
+
 int DeviceBuffer::Ensure(size_t bytes) {
   if (bytes <= cap_) return kOk;
   Release();
@@ -320,19 +328,18 @@ int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *dat
     }
   });
   RjScanJob *jobs = reinterpret_cast<RjScanJob *>(h + off_jobs);
-  {  // the bytes into the pinned staging blob: a plain copy, split over a few host threads
-    auto copy = [&](size_t k0, size_t k1) {
-      for (size_t k = k0; k < k1; k++) {
-        const Stream *s = streams[pend[k]];
-        std::memcpy(h + lay[k].src, s->info().ecs, s->info().ecs_size);
-        std::memset(h + lay[k].src + s->info().ecs_size, 0, 16);
-      }
-    };
-    const size_t nt = bytes > (32u << 20) ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency())) : 1;
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < nt; t++) th.emplace_back(copy, np * t / nt, np * (t + 1) / nt);
-    copy(0, np / nt);
-    for (auto &x : th) x.join();
+  {  // the bytes into the pinned staging blob: a plain copy over the handle's host threads
+    const int nt = bytes > (32u << 20) ? pool_.threads() : 1;
+    const size_t per = (np + size_t(nt) * 4 - 1) / (size_t(nt) * 4);
+    pool_.Run(int((np + per - 1) / per),
+              [&](int t) {
+                for (size_t k = size_t(t) * per; k < std::min(np, size_t(t + 1) * per); k++) {
+                  const Stream *s = streams[pend[k]];
+                  std::memcpy(h + lay[k].src, s->info().ecs, s->info().ecs_size);
+                  std::memset(h + lay[k].src + s->info().ecs_size, 0, 16);
+                }
+              },
+              nullptr);
   }
   for (size_t k = 0; k < np; k++) {
     const Stream *s = streams[pend[k]];
@@ -521,9 +528,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   jobs.clear();
   uint64_t destuff_total = 0, coef_blocks = 0, ent_total = 0, plane_bytes = 0, stage_bytes = 0;
   uint32_t seg_total = 0, rows_total = 0, chunk_total = 0, ds_total = 0;
-  uint64_t ecs_bytes = 0, out_bytes = 0;
-  std::vector<uint64_t> &stage_off = sc_.stage_off;
+  uint64_t ecs_bytes = 0, out_bytes = 0, ecs_stage_bytes = 0;
+  std::vector<uint64_t> &stage_off = sc_.stage_off, &ecs_off = sc_.ecs_off;
   stage_off.assign(n, UINT64_MAX);
+  ecs_off.assign(n, UINT64_MAX);
   std::vector<uint32_t> &row_prefix = sc_.row_prefix, &grow_prefix = sc_.grow_prefix;  // K2 rows: fused / general
   row_prefix.resize(n);
   grow_prefix.resize(n);
@@ -610,9 +618,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
     ecs_bytes += in.ecs_size;
     if (!(s->resident.device == device_ && s->resident.generation == s->generation())) {
+      // non-resident: its tables go with the descriptors (blob A), its bitstream into the ECS
+      // staging, which is uploaded in chunks as the host threads fill it
       stage_off[i] = stage_bytes;
-      stage_bytes += AlignUp(p.segs.size() * sizeof(RjSegDev), 256) + AlignUp(p.ds.size() * sizeof(RjDsBlock), 256) +
-                     AlignUp(in.ecs_size + 16, 256);
+      stage_bytes += AlignUp(p.segs.size() * sizeof(RjSegDev), 256) + AlignUp(p.ds.size() * sizeof(RjDsBlock), 256);
+      ecs_off[i] = ecs_stage_bytes;
+      ecs_stage_bytes += AlignUp(in.ecs_size + 16, 256);  // K0 reads <= 8 B past the end
       if (p.progressive)
         stage_bytes += AlignUp(p.pscans.size() * sizeof(RjProgScanDev), 256) +
                        AlignUp(p.pivals.size() * sizeof(RjProgIvalDev), 256) +
@@ -1081,6 +1092,19 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   }
   uint8_t *h = h_stage_.data();
   uint8_t *dbase = d_desc_.as<uint8_t>();
+  if (ecs_stage_bytes) {
+    RJ_CHECK(h_ecs_.Ensure(ecs_stage_bytes));
+    RJ_CHECK(d_ecs_.Ensure(ecs_stage_bytes));
+  }
+  uint8_t *hecs = h_ecs_.data();
+  uint8_t *decs = d_ecs_.as<uint8_t>();
+  // descriptor pointers (staged tables in blob A, staged bitstreams in the ECS staging)
+  auto staged = [&](const DecodePlan &p, uint64_t so, uint64_t &bo, uint64_t &po, uint64_t &vo, uint64_t &to) {
+    bo = so + AlignUp(p.segs.size() * sizeof(RjSegDev), 256);
+    po = bo + AlignUp(p.ds.size() * sizeof(RjDsBlock), 256);
+    vo = po + AlignUp(p.pscans.size() * sizeof(RjProgScanDev), 256);
+    to = vo + AlignUp(p.pivals.size() * sizeof(RjProgIvalDev), 256);
+  };
   for (int i = 0; i < n; i++) {
     Stream *s = streams[i];
     RjImageDev &d = imgs[i];
@@ -1088,34 +1112,89 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       d.ecs = s->resident.ecs;
       d.segs = s->resident.segs;
       d.ds = s->resident.ds;
+      if (s->plan().progressive) {
+        d.pscans = s->resident.pscans;
+        d.pivals = s->resident.pivals;
+        d.ptabs = s->resident.ptabs;
+      }
     } else {
       const DecodePlan &p = s->plan();
       const uint64_t so = off_stage + stage_off[i];
-      const uint64_t bo = so + AlignUp(p.segs.size() * sizeof(RjSegDev), 256);
-      const uint64_t eo = bo + AlignUp(p.ds.size() * sizeof(RjDsBlock), 256);
-      if (!p.ds.empty()) std::memcpy(h + bo, p.ds.data(), p.ds.size() * sizeof(RjDsBlock));
-      d.ds = reinterpret_cast<const RjDsBlock *>(dbase + bo);
-      std::memcpy(h + so, p.segs.data(), p.segs.size() * sizeof(RjSegDev));
-      std::memcpy(h + eo, s->info().ecs, s->info().ecs_size);
+      uint64_t bo, po, vo, to;
+      staged(p, so, bo, po, vo, to);
       d.segs = reinterpret_cast<const RjSegDev *>(dbase + so);
-      d.ecs = dbase + eo;
+      d.ds = reinterpret_cast<const RjDsBlock *>(dbase + bo);
+      d.ecs = decs + ecs_off[i];
       if (p.progressive) {
-        const uint64_t po = eo + AlignUp(s->info().ecs_size + 16, 256);
-        const uint64_t vo = po + AlignUp(p.pscans.size() * sizeof(RjProgScanDev), 256);
-        const uint64_t to = vo + AlignUp(p.pivals.size() * sizeof(RjProgIvalDev), 256);
-        std::memcpy(h + po, p.pscans.data(), p.pscans.size() * sizeof(RjProgScanDev));
-        std::memcpy(h + vo, p.pivals.data(), p.pivals.size() * sizeof(RjProgIvalDev));
-        if (!p.ptabs.empty()) std::memcpy(h + to, p.ptabs.data(), p.ptabs.size() * sizeof(RjHuffDev));
         d.pscans = reinterpret_cast<const RjProgScanDev *>(dbase + po);
         d.pivals = reinterpret_cast<const RjProgIvalDev *>(dbase + vo);
         d.ptabs = reinterpret_cast<const RjHuffDev *>(dbase + to);
       }
     }
-    if (stage_off[i] == UINT64_MAX && s->plan().progressive) {
-      d.pscans = s->resident.pscans;
-      d.pivals = s->resident.pivals;
-      d.ptabs = s->resident.ptabs;
+  }
+  if (profiling_) RJ_HIP(hipEventRecord(ev_[0], stream_));
+  if (stage_bytes || ecs_stage_bytes) {
+    // host threads copy the non-resident streams' tables and bitstreams into pinned memory, in
+    // chunks of consecutive images (~2 MB of bitstream each); this thread uploads the finished
+    // prefix of the staging area in DMA transfers of >= 32 MB (a 285-MB batch in 4-MB transfers
+    // ran at ~40 GB/s, in one transfer at 57), so the copies, the DMA and the next chunks'
+    // copies overlap
+    std::vector<uint32_t> &chunk_img = sc_.chunk_img;  // chunk k: images [chunk_img[k], chunk_img[k + 1])
+    chunk_img.clear();
+    constexpr uint64_t kChunkBytes = 2ull << 20, kDmaBytes = 32ull << 20;
+    uint64_t acc = 0;
+    for (int i = 0; i < n; i++) {
+      if (stage_off[i] == UINT64_MAX) continue;
+      if (chunk_img.empty() || acc >= kChunkBytes) {
+        chunk_img.push_back(uint32_t(i));
+        acc = 0;
+      }
+      acc += streams[i]->info().ecs_size;
     }
+    chunk_img.push_back(uint32_t(n));
+    const int nchunk = int(chunk_img.size()) - 1;
+    hipError_t up_err = hipSuccess;
+    uint64_t dma_lo = UINT64_MAX, dma_hi = 0;  // staged but not yet uploaded
+    pool_.Run(
+        nchunk,
+        [&](int k) {
+          for (uint32_t i = chunk_img[k]; i < chunk_img[k + 1]; i++) {
+            if (stage_off[i] == UINT64_MAX) continue;
+            const Stream *s = streams[i];
+            const DecodePlan &p = s->plan();
+            const uint64_t so = off_stage + stage_off[i];
+            uint64_t bo, po, vo, to;
+            staged(p, so, bo, po, vo, to);
+            std::memcpy(h + so, p.segs.data(), p.segs.size() * sizeof(RjSegDev));
+            if (!p.ds.empty()) std::memcpy(h + bo, p.ds.data(), p.ds.size() * sizeof(RjDsBlock));
+            if (p.progressive) {
+              std::memcpy(h + po, p.pscans.data(), p.pscans.size() * sizeof(RjProgScanDev));
+              std::memcpy(h + vo, p.pivals.data(), p.pivals.size() * sizeof(RjProgIvalDev));
+              if (!p.ptabs.empty()) std::memcpy(h + to, p.ptabs.data(), p.ptabs.size() * sizeof(RjHuffDev));
+            }
+            std::memcpy(hecs + ecs_off[i], s->info().ecs, s->info().ecs_size);
+          }
+        },
+        [&](int k) {
+          uint32_t i0 = chunk_img[k], i1 = chunk_img[k + 1];
+          while (i0 < i1 && stage_off[i0] == UINT64_MAX) i0++;
+          uint64_t lo = UINT64_MAX, hi = 0;
+          for (uint32_t i = i0; i < i1; i++)
+            if (stage_off[i] != UINT64_MAX) {
+              lo = std::min(lo, ecs_off[i]);
+              hi = std::max(hi, ecs_off[i] + streams[i]->info().ecs_size);
+            }
+          if (hi > lo) {
+            dma_lo = std::min(dma_lo, lo);
+            dma_hi = std::max(dma_hi, hi);
+          }
+          if (dma_hi > dma_lo && (dma_hi - dma_lo >= kDmaBytes || k == nchunk - 1) && up_err == hipSuccess) {
+            up_err = hipMemcpyAsync(decs + dma_lo, hecs + dma_lo, dma_hi - dma_lo, hipMemcpyHostToDevice, stream_);
+            dma_lo = UINT64_MAX;
+            dma_hi = 0;
+          }
+        });
+    RJ_HIP(up_err);
   }
   std::memcpy(h + off_imgs, imgs.data(), n * sizeof(RjImageDev));
   for (size_t t = 0; t < tabs.size(); t++) std::memcpy(h + off_tabs + t * sizeof(RjTableSet), tabs[t], sizeof(RjTableSet));
@@ -1152,7 +1231,6 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   uint2 *wlist = nullptr;
 
   const auto t_k0 = std::chrono::steady_clock::now();
-  if (profiling_) RJ_HIP(hipEventRecord(ev_[0], stream_));
   RJ_HIP(hipMemcpyAsync(dbase, h, blob_a, hipMemcpyHostToDevice, stream_));
   if (cbuf.count) RJ_HIP(hipMemsetAsync(cbuf.count, 0, sizeof(unsigned long long), stream_));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));

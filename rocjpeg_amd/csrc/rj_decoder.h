@@ -15,6 +15,7 @@
 #include "../../include/rocjpeg.h"
 #include "../../include/rocjpeg_amd.h"
 #include "rj_device.h"
+#include "rj_pool.h"
 #include "rj_stream.h"
 
 namespace rj {
@@ -139,7 +140,8 @@ class Decoder {
   struct Scratch {
     std::vector<RjImageDev> imgs;
     std::vector<RjJobDev> jobs;
-    std::vector<uint64_t> stage_off;
+    std::vector<uint64_t> stage_off, ecs_off;
+    std::vector<uint32_t> chunk_img;
     std::vector<uint32_t> tab_of, row_prefix, grow_prefix, seg_lane0, lane_seg, bucket_pos, seg_pos, lane_split;
     std::vector<uint2> seg_len;  // per interval: destuffed bytes, blocks (outlier split planning)
     std::vector<uint16_t> seg_bkt;  // per interval: 32-B length bucket (outlier split planning)
@@ -169,6 +171,12 @@ class Decoder {
   PinnedBuffer h_scan_;  // progressive: dense coefficients, nonzero masks, refinement records
   uint32_t epoch_ = 0;
   PinnedBuffer h_stage_;
+  PinnedBuffer h_ecs_;    // staged bitstreams of non-resident streams (uploaded in chunks)
+  DeviceBuffer d_ecs_;
+  // host threads of the per-call staging copies: RJ_HOST_THREADS, else up to 8 (the caller's
+  // thread counts as one)
+  HostPool pool_{HostThreads()};
+  static int HostThreads();
 };
 
 }  // namespace rj
