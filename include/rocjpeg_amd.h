@@ -143,10 +143,12 @@ typedef struct {
 #define ROCJPEG_AMD_COST_BYTE 8u        /* measured: K1 spends ~8x per ECS byte what K2 spends per pixel */
 #define ROCJPEG_AMD_COST_BYTE_PROG 120u /* progressive scans: serial refinement chains */
 
-/* Fill items[0..count) from the JPEGs at blob + offsets[i] (sizes[i] bytes each).  Returns
- * SUCCESS even when some images fail to parse (they are flagged ROCJPEG_AMD_WORK_BAD). */
-RocJpegStatus rocJpegAmdBuildWorkTable(const unsigned char *blob, const uint64_t *offsets, const uint32_t *sizes,
-                                       int count, RocJpegAmdWorkItem *items);
+/* Fill items[0..count) from the JPEGs at blob + offsets[i] (sizes[i] bytes each, inside the
+ * blob_bytes of the blob: INVALID_PARAMETER otherwise, before anything is read).  Returns
+ * SUCCESS even when some images fail to parse (they are flagged ROCJPEG_AMD_WORK_BAD);
+ * RUNTIME_ERROR when a header walk failed outside the JPEG rules (e.g. out of memory). */
+RocJpegStatus rocJpegAmdBuildWorkTable(const unsigned char *blob, uint64_t blob_bytes, const uint64_t *offsets,
+                                       const uint32_t *sizes, int count, RocJpegAmdWorkItem *items);
 
 /* Greedy LPT (longest processing time first) over `num_shards` shards: items by decreasing
  * cost, each to the shard with the least assigned cost (ties: lower shard).  Sets `shard` and

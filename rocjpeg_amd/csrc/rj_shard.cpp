@@ -8,6 +8,7 @@
 // each rank calls rocJpegDecodeBatched (src/rocjpeg_decoder.cpp:196-292 semantics) on its own
 // images.  Nothing here touches a GPU.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <queue>
 #include <thread>
@@ -59,23 +60,38 @@ void FillItem(const unsigned char *data, uint32_t size, uint32_t index, uint64_t
 
 }  // namespace
 
-RJ_EXPORT RocJpegStatus rocJpegAmdBuildWorkTable(const unsigned char *blob, const uint64_t *offsets,
-                                                 const uint32_t *sizes, int count, RocJpegAmdWorkItem *items) {
+RJ_EXPORT RocJpegStatus rocJpegAmdBuildWorkTable(const unsigned char *blob, uint64_t blob_bytes,
+                                                 const uint64_t *offsets, const uint32_t *sizes, int count,
+                                                 RocJpegAmdWorkItem *items) {
   if (count < 0 || (count > 0 && (blob == nullptr || offsets == nullptr || sizes == nullptr || items == nullptr)))
     return ROCJPEG_STATUS_INVALID_PARAMETER;
-  try {
-    auto run = [&](int a, int b) {
+  // every stream must lie inside the blob (checked before any worker reads a byte)
+  for (int i = 0; i < count; i++)
+    if (offsets[i] > blob_bytes || sizes[i] > blob_bytes - offsets[i]) return ROCJPEG_STATUS_INVALID_PARAMETER;
+  // a worker never lets an exception escape its thread (that would std::terminate the caller):
+  // the first failure is recorded and the call returns RUNTIME_ERROR
+  std::atomic<bool> failed{false};
+  auto run = [&](int a, int b) {
+    try {
       for (int i = a; i < b; i++) FillItem(blob + offsets[i], sizes[i], uint32_t(i), offsets[i], items + i);
-    };
-    const int nt = count >= 512 ? int(std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency()))) : 1;
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; t++) th.emplace_back(run, int(int64_t(count) * t / nt), int(int64_t(count) * (t + 1) / nt));
-    run(0, count / nt);
-    for (auto &x : th) x.join();
-  } catch (...) {
-    return ROCJPEG_STATUS_RUNTIME_ERROR;
+    } catch (...) {
+      failed.store(true);
+    }
+  };
+  const int nt = count >= 512 ? int(std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency()))) : 1;
+  std::vector<std::thread> th;
+  th.reserve(size_t(nt));
+  for (int t = 1; t < nt; t++) {
+    try {
+      th.emplace_back(run, int(int64_t(count) * t / nt), int(int64_t(count) * (t + 1) / nt));
+    } catch (...) {  // no thread: this range (and the ones after it) run on the calling thread
+      run(int(int64_t(count) * t / nt), count);
+      break;
+    }
   }
-  return ROCJPEG_STATUS_SUCCESS;
+  run(0, count / nt);
+  for (auto &x : th) x.join();
+  return failed.load() ? ROCJPEG_STATUS_RUNTIME_ERROR : ROCJPEG_STATUS_SUCCESS;
 }
 
 RJ_EXPORT RocJpegStatus rocJpegAmdAssignShards(RocJpegAmdWorkItem *items, int count, int num_shards,

@@ -56,7 +56,9 @@ def build_work_table(blob, offsets, sizes, base_offset=0):
     if n == 0:
         return table
     ptr, keep = _u8_pointer(blob)
-    st = lib().rocJpegAmdBuildWorkTable(ptr, offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+    if np.any(offsets.astype(np.uint64) + sizes.astype(np.uint64) > np.uint64(keep.nbytes)):
+        raise ValueError("a stream lies outside the blob")
+    st = lib().rocJpegAmdBuildWorkTable(ptr, keep.nbytes, offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
                                         sizes.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n,
                                         ctypes.c_void_p(table.ctypes.data))
     del keep

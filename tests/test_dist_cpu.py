@@ -94,6 +94,32 @@ def test_work_table_flags_bad_and_unsupported():
     assert (t["shard"] >= 0).all()
 
 
+def test_work_table_refuses_streams_outside_the_blob():
+    """An index whose offset + size runs past the blob is refused before any byte is read, by the
+    Python wrapper and by the C entry point itself (its blob_bytes bound)."""
+    import ctypes
+
+    from rocjpeg_amd import lib
+    good = open(os.path.join(ROOT, "tests", "golden", "img", "p420_q90_ri_256x128.jpg"), "rb").read()
+    blob = np.frombuffer(good, dtype=np.uint8)
+    offs = np.array([0, 16], np.uint64)
+    sizes = np.array([len(good), len(good)], np.uint32)
+    with pytest.raises(ValueError):
+        S.build_work_table(blob, offs, sizes)
+    items = np.zeros(2, dtype=S.WORK_ITEM_DTYPE)
+    st = lib().rocJpegAmdBuildWorkTable(ctypes.c_void_p(blob.ctypes.data), len(good),
+                                        offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                        sizes.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 2,
+                                        ctypes.c_void_p(items.ctypes.data))
+    assert st == -2  # ROCJPEG_STATUS_INVALID_PARAMETER
+    huge = np.array([np.uint64(2**63)], np.uint64)
+    st = lib().rocJpegAmdBuildWorkTable(ctypes.c_void_p(blob.ctypes.data), len(good),
+                                        huge.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                        sizes.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 1,
+                                        ctypes.c_void_p(items.ctypes.data))
+    assert st == -2
+
+
 def _rank(rank, world, port, q):
     import torch
     import torch.distributed as dist
