@@ -131,11 +131,21 @@ __device__ __forceinline__ int raw_value(uint32_t e) {
   return raw < half ? int(raw) - int(2 * half - 1) : int(raw);
 }
 
-template <bool kRaw, bool kSplit>
+// kPairs (the main K2 instances): each coefficient is dequantised here and stored scaled into
+// its block's pair layout (rj_math.h idct_dot2_block): entry value x quantiser (i24 multiply,
+// exact for 16-bit quantisers) x 32, the DC x 16 (raw DC differences stay as they are: restore_dc
+// finishes them).  A coefficient outside the dot2 IDCT's exact domain raises `bad` (the row goes
+// to the fix-up launch).  The entry's block in the strip supplies, through one ds_bpermute of the
+// owning lane's `lane_info` (block LDS base | q-table row << 16), where the block lives and which
+// component's quantisers apply; s_qw[c][p] = quantiser | pair-layout byte offset << 16.
+// !kPairs (the fix-up instances): raw coefficients in zigzag order, checked against the int32
+// IDCT's domain (thr, on the raw value) -- the layout idct_pass1_wide reads.
+template <bool kRaw, bool kSplit, bool kPairs>
 __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefBuf &coefs,
                                              const uint32_t *__restrict__ ent, uint32_t lane, uint32_t nb,
                                              uint32_t drop, uint32_t nblk, uint32_t cbits, EntWin &win, Nav &nv,
-                                             uint8_t *s_buf, int thr, bool &bad) {
+                                             uint8_t *s_buf, const uint32_t *s_qw, uint32_t lane_info, int thr,
+                                             bool &bad) {
   uint32_t done = 0;
   const uint32_t need = nb + drop;
   for (uint32_t moves = 0; done < need && moves < (1u << 16); moves++) {  // bounded on corrupt pieces
@@ -178,17 +188,37 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
         // after its terminator belongs to the stream
         const uint64_t term = (kRaw && kSplit) ? __ballot(p == 127 && ord < piece) : 0ull;
         const int tl = term ? __ffsll((long long)term) - 1 : 64;
+        // the entry's block in the strip, and from its lane: LDS base, quantiser row (whole wave)
+        const uint32_t info = kPairs ? uint32_t(__builtin_amdgcn_ds_bpermute(int(((blk - drop) & 63u) << 2), int(lane_info))) : 0u;
         if (!pass && ord < piece && p < 64u && blk >= drop && int(lane) < tl) {
           int v = kRaw ? raw_value(e) : int(int16_t(e & 0xFFFFu));
-          if (kRaw && (e & RJ_RE_ZERO)) v = -32768;  // zero block: marked for the DC restore
-          if (!kRaw && fix_dc && p == 0) {
-            const uint32_t bi = (blk - drop) % nblk;  // strips start at an MCU boundary
-            const uint32_t cc = (cbits >> (2 * bi)) & 3u;
-            v += cc == 0 ? nv.dcd[0] : (cc == 1 ? nv.dcd[1] : nv.dcd[2]);
+          if constexpr (kPairs) {
+            const uint32_t qe = s_qw[(info >> 16) + p];
+            if (!kRaw && fix_dc && p == 0) {
+              const uint32_t cc = info >> 22;  // q-table row = component x 64
+              v += cc == 0 ? nv.dcd[0] : (cc == 1 ? nv.dcd[1] : nv.dcd[2]);
+            }
+            const int x = __mul24(v, int(qe & 0xFFFFu));  // |v| < 2^16, q < 2^16: exact
+            int16_t sv;
+            if (kRaw && p == 0) {
+              sv = (e & RJ_RE_ZERO) ? int16_t(-32768) : int16_t(v);  // DC difference: restore_dc
+            } else {
+              const int lim = p == 0 ? RJ_DOT2_DC_MAX : RJ_DOT2_AC_MAX;
+              oob = uint32_t(x + lim) > uint32_t(2 * lim);
+              sv = int16_t(x << (p == 0 ? 4 : 5));
+            }
+            *reinterpret_cast<int16_t *>(s_buf + (info & 0xFFFFu) + (qe >> 16)) = sv;
+          } else {
+            if (kRaw && (e & RJ_RE_ZERO)) v = -32768;  // zero block: marked for the DC restore
+            if (!kRaw && fix_dc && p == 0) {
+              const uint32_t bi = (blk - drop) % nblk;  // strips start at an MCU boundary
+              const uint32_t cc = (cbits >> (2 * bi)) & 3u;
+              v += cc == 0 ? nv.dcd[0] : (cc == 1 ? nv.dcd[1] : nv.dcd[2]);
+            }
+            // outside the int32 IDCT's exact domain (raw DC: a difference, checked by restore_dc)
+            oob = (!kRaw || p != 0) && int16_t(v) != -32768 && abs(int(int16_t(v))) > thr;
+            *reinterpret_cast<int16_t *>(s_buf + __umul24(blk - drop, uint32_t(RJ_BLK_STRIDE)) + p * 2) = int16_t(v);
           }
-          // outside the int32 IDCT's exact domain (raw DC: a difference, checked by restore_dc)
-          oob = (!kRaw || p != 0) && int16_t(v) != -32768 && abs(int(int16_t(v))) > thr;
-          *reinterpret_cast<int16_t *>(s_buf + (blk - drop) * RJ_BLK_STRIDE + p * 2) = int16_t(v);
         }
         bad = bad || __ballot(oob) != 0;
         if (term) {
@@ -226,8 +256,12 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
 // the row; a restart interval starting inside the strip (every ri MCUs) resets it there.  Zero
 // blocks (marked -32768) are absolute 0 (libjpeg's insufficient data / missing marker: every
 // later block of the interval is one too).  Writes the absolute DC back into the LDS block.
+// kPairs: the DC is stored dequantised x 16 (q0: this lane's component's DC quantiser) and
+// checked against the dot2 IDCT's domain; otherwise raw, checked against thr.
+template <bool kPairs>
 __device__ __forceinline__ bool restore_dc(uint8_t *s_buf, uint32_t tid, uint32_t nb, uint32_t nblk, uint32_t c,
-                                           uint32_t mx0, uint32_t mcu_row0, uint32_t ri, int (&carry)[3], int thr) {
+                                           uint32_t mx0, uint32_t mcu_row0, uint32_t ri, int (&carry)[3], int thr,
+                                           uint32_t q0) {
   int16_t *dcp = reinterpret_cast<int16_t *>(s_buf + tid * RJ_BLK_STRIDE);
   const int d = tid < nb ? int(*dcp) : 0;
   const bool zero = d == -32768;
@@ -252,8 +286,14 @@ __device__ __forceinline__ bool restore_dc(uint8_t *s_buf, uint32_t tid, uint32_
     carry[cc] = last;
   }
   const int16_t dc = int16_t(zero ? 0 : pred);  // libjpeg keeps the predictor wide, stores (JCOEF)
-  if (tid < nb) *dcp = dc;
-  return __ballot(tid < nb && abs(int(dc)) > thr) != 0;  // outside the int32 IDCT's exact domain
+  if constexpr (kPairs) {
+    const int x = __mul24(int(dc), int(q0));
+    if (tid < nb) *dcp = int16_t(x << 4);
+    return __ballot(tid < nb && uint32_t(x + RJ_DOT2_DC_MAX) > uint32_t(2 * RJ_DOT2_DC_MAX)) != 0;
+  } else {
+    if (tid < nb) *dcp = dc;
+    return __ballot(tid < nb && abs(int(dc)) > thr) != 0;  // outside the int32 IDCT's exact domain
+  }
 }
 
 // Two sign-magnitude int16 (bit 15 = negative) -> two's complement, per half (packed ops).
@@ -410,7 +450,11 @@ __device__ __forceinline__ void rgb_strip(const uint8_t *ty, const uint8_t *tu, 
 template <bool kPlanes, bool kDense, bool kWide = false, bool kSplit = false>
 __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, int i, uint32_t my, RjCoefBuf coefs,
                                          const RjTableSet *__restrict__ tabsets, uint8_t *__restrict__ planes,
-                                         uint8_t *s_buf, uint16_t (*s_q)[64], uint32_t *wide_cnt, uint2 *wide_list) {
+                                         uint8_t *s_buf, uint32_t *s_qw, uint32_t *wide_cnt, uint2 *wide_list) {
+  // the main instances dequantise in the entry scatter into the dot2 IDCT's pair layout; the
+  // fix-up (kWide) and progressive (kDense) instances keep raw zigzag blocks and the int32 IDCT
+  constexpr bool kPairs = !kDense && !kWide;
+  uint16_t(*s_q)[64] = reinterpret_cast<uint16_t(*)[64]>(s_qw);
   RJ_STAMP(t_start);
   const uint32_t tid = threadIdx.x;
   const RjImageDev &im = imgs[i];
@@ -446,8 +490,25 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
   }
 
   const RjTableSet *ts = tabsets + im.tabset;
-  for (uint32_t k = tid; k < ncomp * 64; k += 64) s_q[k >> 6][k & 63] = ts->qz[im.comp_tq[k >> 6] & 3][k & 63];
+  if constexpr (kPairs) {
+    // s_qw[c][p] = quantiser of zigzag position p | its byte offset in the pair layout << 16
+    constexpr uint8_t kNatZ[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                   12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                   35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                   58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+    for (uint32_t k = tid; k < ncomp * 64; k += 64) {
+      const uint32_t nat = kNatZ[k & 63];
+      s_qw[k] = uint32_t(ts->qz[im.comp_tq[k >> 6] & 3][k & 63]) | rj_pair_slot(nat >> 3, nat & 7) << 16;
+    }
+  } else {
+    for (uint32_t k = tid; k < ncomp * 64; k += 64) s_q[k >> 6][k & 63] = ts->qz[im.comp_tq[k >> 6] & 3][k & 63];
+  }
 
+  // this lane's block: LDS base | its component's q-table row << 16 (parse_blocks' bpermute source),
+  // and its DC quantiser (restore_dc)
+  const uint32_t lane_info = tid * RJ_BLK_STRIDE | ((lane_blk >> 12) * 64u) << 16;
+  __syncthreads();  // s_qw / s_q written
+  const uint32_t q0 = kPairs ? s_qw[(lane_blk >> 12) * 64u] & 0xFFFFu : 0u;
   const uint32_t mcux = U(im.mcux);
   const bool dc_diff = !kDense && U(im.dc_diff) != 0;  // raw entries: restore_dc per strip
   const int thr = int(U(im.idct_thr));
@@ -521,14 +582,16 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
     if constexpr (kDense) {
       if (has_blk) load_dense_block(im, coefs.dense, lane_blk, mx0, my, inter, s_buf + tid * RJ_BLK_STRIDE);
     } else {
-      if (dc_diff) parse_blocks<true, kSplit>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, thr, wide);
-      else parse_blocks<false, false>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, thr, wide);
+      if (dc_diff)
+        parse_blocks<true, kSplit, kPairs>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, s_qw, lane_info, thr, wide);
+      else
+        parse_blocks<false, false, kPairs>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, s_qw, lane_info, thr, wide);
       drop = 0;
       if (sx + 1 < strips_x && nv.bleft) win.load(ent, nv.cur(), tid);  // next strip's window: lands behind B and C
     }
     __syncthreads();
     if (!kDense && dc_diff) {
-      wide = restore_dc(s_buf, tid, nb, nblk, lane_blk >> 12, mx0, my * mcux, ri_dc, carry, thr) || wide;
+      wide = restore_dc<kPairs>(s_buf, tid, nb, nblk, lane_blk >> 12, mx0, my * mcux, ri_dc, carry, thr, q0) || wide;
       __syncthreads();
     }
 
@@ -536,27 +599,48 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
     RJ_STAMP_ADD(0, tb - ta);
     // ---- B: lane-per-block IDCT in registers ----
     const uint32_t c_b = lane_blk >> 12;
-    int32_t v[64];
-    const int16_t *zz = reinterpret_cast<const int16_t *>(s_buf + tid * RJ_BLK_STRIDE);
-    if (has_blk)
-      dezigzag_dequant(reinterpret_cast<const uint4 *>(zz), reinterpret_cast<const uint4 *>(s_q[c_b]), v);
-    if constexpr (kDense) {  // progressive coefficients: check the dequantised values directly
-      int32_t lo = 0, hi = 0;
-#pragma unroll
-      for (int k = 0; k < 64; k++) {
-        lo = min(lo, v[k]);
-        hi = max(hi, v[k]);
-      }
-      wide = __ballot(has_blk && (lo < -16383 || hi > 16383)) != 0;
-    }
-    row_wide = row_wide || wide;
-    if constexpr (kWide)  // pass 1 now: the tiles overwrite the LDS block below
-      if (wide && has_blk) idct_pass1_wide(zz, s_q[c_b], v);
-    if constexpr (kPlanes) {
+    uint32_t o[16];
+    if constexpr (kPairs) {
+      uint32_t w[32];
       if (has_blk) {
-        uint32_t o[16];
+        const uint4 *src = reinterpret_cast<const uint4 *>(s_buf + tid * RJ_BLK_STRIDE);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const uint4 a = src[q];
+          w[4 * q] = a.x;
+          w[4 * q + 1] = a.y;
+          w[4 * q + 2] = a.z;
+          w[4 * q + 3] = a.w;
+        }
+      }
+      row_wide = row_wide || wide;
+      if constexpr (!kPlanes) __syncthreads();  // every block is in registers: the staging area becomes the sample tiles
+      if (has_blk) idct_dot2_block(w, o);
+    } else {
+      int32_t v[64];
+      const int16_t *zz = reinterpret_cast<const int16_t *>(s_buf + tid * RJ_BLK_STRIDE);
+      if (has_blk)
+        dezigzag_dequant(reinterpret_cast<const uint4 *>(zz), reinterpret_cast<const uint4 *>(s_q[c_b]), v);
+      if constexpr (kDense) {  // progressive coefficients: check the dequantised values directly
+        int32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int k = 0; k < 64; k++) {
+          lo = min(lo, v[k]);
+          hi = max(hi, v[k]);
+        }
+        wide = __ballot(has_blk && (lo < -16383 || hi > 16383)) != 0;
+      }
+      row_wide = row_wide || wide;
+      if constexpr (kWide)  // pass 1 now: the tiles overwrite the LDS block below
+        if (wide && has_blk) idct_pass1_wide(zz, s_q[c_b], v);
+      if constexpr (!kPlanes) __syncthreads();  // every block is in registers: the staging area becomes the sample tiles
+      if (has_blk) {
         if (kWide && wide) idct_pass2_wrap(v, o);
         else idct_islow_block(v, o);
+      }
+    }
+    if constexpr (kPlanes) {
+      if (has_blk) {
         const uint32_t hc = inter ? im.comp_h[c_b] : 1, vc = inter ? im.comp_v[c_b] : 1;
         const uint32_t bx = mx0 * hc + (lane_blk & 255u), by = my * vc + ((lane_blk >> 8) & 15u);
         const uint32_t pitch = im.plane_pitch[c_b];
@@ -566,11 +650,7 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
       }
       continue;
     }
-    __syncthreads();  // every block is in registers: the staging area becomes the sample tiles
     if (has_blk) {
-      uint32_t o[16];
-      if (kWide && wide) idct_pass2_wrap(v, o);
-      else idct_islow_block(v, o);
       const uint32_t twc = c_b == 0 ? tw[0] : (c_b == 1 ? tw[1] : tw[2]);
       const uint32_t toc = c_b == 0 ? toff[0] : (c_b == 1 ? toff[1] : toff[2]);
       uint8_t *dst = s_buf + toc + ((lane_blk >> 8) & 15u) * 8u * twc + (lane_blk & 255u) * 8u;
@@ -718,11 +798,11 @@ __global__ __launch_bounds__(64, RJ_K2_OCC) void k_rows(const RjImageDev *__rest
                                              const RjTableSet *__restrict__ tabsets,
                                              uint8_t *__restrict__ planes, uint32_t *wide_cnt, uint2 *wide_list) {
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];  // A/B, then tiles
-  __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
+  __shared__ __attribute__((aligned(16))) uint32_t s_qw[3 * 64];
   int i;
   uint32_t my;
   row_of_block(imgs, nimg, row_prefix, row_list, blockIdx.x, i, my);
-  row_body<kPlanes, kDense, false, kSplit>(imgs, i, my, coefs, tabsets, planes, s_buf, s_q, wide_cnt, wide_list);
+  row_body<kPlanes, kDense, false, kSplit>(imgs, i, my, coefs, tabsets, planes, s_buf, s_qw, wide_cnt, wide_list);
 }
 
 // K2 fix-up: the rows a K2 launch recorded (a strip outside the int32 IDCT's exact domain --
@@ -734,14 +814,14 @@ __global__ __launch_bounds__(64) void k_rows_fix(const RjImageDev *__restrict__ 
                                                  const RjTableSet *__restrict__ tabsets, uint8_t *__restrict__ planes,
                                                  const uint32_t *wide_cnt, const uint2 *wide_list, uint32_t cap) {
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];
-  __shared__ __attribute__((aligned(16))) uint16_t s_q[3][64];
+  __shared__ __attribute__((aligned(16))) uint32_t s_qw[3 * 64];
   const uint32_t cnt = min(U(*wide_cnt), cap);
   for (uint32_t r = blockIdx.x; r < cnt; r += gridDim.x) {
     const uint2 e = wide_list[r];
     const int i = int(U(e.x));
     if (i >= nimg) continue;
     __syncthreads();  // the previous row's tiles fully read
-    row_body<kPlanes, kDense, true, kSplit>(imgs, i, U(e.y), coefs, tabsets, planes, s_buf, s_q, nullptr, nullptr);
+    row_body<kPlanes, kDense, true, kSplit>(imgs, i, U(e.y), coefs, tabsets, planes, s_buf, s_qw, nullptr, nullptr);
   }
 }
 

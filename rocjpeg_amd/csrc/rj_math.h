@@ -197,6 +197,92 @@ __device__ __forceinline__ void idct_islow_block(int32_t (&v)[64], uint32_t (&o)
   }
 }
 
+// ---- ISLOW with packed 16-bit dot products (v_dot2c_i32_i16) ----
+// Every output of one ISLOW pass is an integer linear combination of its 8 inputs (the
+// butterfly above only multiplies by constants and adds), t[r] = sum_k A[r][k] x[k] with
+//   A[r][k] = 8192 (k = 0), and +-{11363, 10703, 9633, 8192, 6437, 4433, 2260} -- all int16,
+// and t[r] / t[7-r] share the even part (x0, x2, x4, x6) and negate the odd part.  So a pass is
+// 12 dot2 + 12 add/sub on packed input pairs instead of 12 multiplies + ~26 adds on int32, with
+// the inputs in registers at half the width.  Pair layout of a block (32 dwords, built by
+// K2's entry scatter straight into LDS, see rj_pair_slot): dword 4c + j of column c holds
+//   j = 0: (x0, x4), 1: (x2, x6), 2: (x1, x3), 3: (x5, x7)   (low half, high half)
+// Scaling: the scatter stores the dequantised coefficient x 32 (the DC x 16, its constant
+// 16384), so a pass-1 sum is 32 x (t + 1024) and DESCALE(t, 11) is its high half: the pass-2
+// pairs are packed by one v_perm per two outputs, no shifts.  Pass 2 needs only bits 18..27 of
+// its sums (range-limit mask), which wrap-around int32 arithmetic keeps exact.
+// Exact -- equal to libjpeg's wide arithmetic -- whenever every pass-1 output fits int16; the
+// fast domain K2 checks per coefficient is |DC| <= 1151 and |AC| <= 1023 (dequantised), for
+// which |pass-1 output| <= (8192 * 1151 + 53022 * 1023 + 1024) / 2048 = 31,095 (53,022: the
+// largest AC row sum of |A|); every stream from 8-bit samples at a quantiser <= 255 is inside
+// (|DC| <= 1024 + q/2, |AC| <= ~930 + q/2).  Strips outside go to the K2 fix-up launch.
+// Checked against libjpeg's arithmetic on random and worst-case blocks of that domain
+// (tools/idct_dot2_model.py).
+#define RJ_DOT2_DC_MAX 1151
+#define RJ_DOT2_AC_MAX 1023
+// The VOP3P form v_dot2_i32_i16 with the constant pair in an SGPR and the accumulator as an
+// operand (the builtin selects v_dot2c_i32_i16, whose accumulator is its destination: one extra
+// v_mov per dot product that does not continue a chain -- 128 per block).
+__device__ __forceinline__ int32_t dot2(uint32_t a, uint32_t k, int32_t c) {
+  int32_t d;
+  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(k), "v"(c));
+  return d;
+}
+__device__ __forceinline__ int32_t dot2z(uint32_t a, uint32_t k) {  // accumulator 0 (inline constant)
+  int32_t d;
+  asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "v"(a), "s"(k));
+  return d;
+}
+#define RJ_PK(lo, hi) (uint32_t(uint16_t(int16_t(lo))) | (uint32_t(uint16_t(int16_t(hi))) << 16))
+// byte offset of natural coefficient (row k, column c) in the pair layout
+__host__ __device__ constexpr uint32_t rj_pair_slot(uint32_t k, uint32_t c) {
+  return (c * 4u + ((k & 1u) ? 2u + (k >> 2) : (k >> 1) & 1u)) * 4u + ((k & 1u) ? (k >> 1) & 1u : k >> 2) * 2u;
+}
+// one pass over pairs p0 = (x0, x4), p1 = (x2, x6), p2 = (x1, x3), p3 = (x5, x7); ke0 / ke1:
+// the (x0, x4) constants of the (x0 + x4) / (x0 - x4) terms, rnd added to both
+__device__ __forceinline__ void islow_dot2_1d(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3, uint32_t ke0,
+                                              uint32_t ke1, int32_t rnd, int32_t t[8]) {
+  const int32_t e0 = dot2(p0, ke0, rnd), e1 = dot2(p0, ke1, rnd);
+  const int32_t tmp3 = dot2z(p1, RJ_PK(10703, 4433)), tmp2 = dot2z(p1, RJ_PK(4433, -10704));
+  const int32_t t10 = e0 + tmp3, t13 = e0 - tmp3, t11 = e1 + tmp2, t12 = e1 - tmp2;
+  const int32_t o0 = dot2(p3, RJ_PK(6437, 2260), dot2z(p2, RJ_PK(11363, 9633)));
+  const int32_t o1 = dot2(p3, RJ_PK(-11362, -6436), dot2z(p2, RJ_PK(9633, -2259)));
+  const int32_t o2 = dot2(p3, RJ_PK(2261, 9633), dot2z(p2, RJ_PK(6437, -11362)));
+  const int32_t o3 = dot2(p3, RJ_PK(9633, -11363), dot2z(p2, RJ_PK(2260, -6436)));
+  t[0] = t10 + o0;
+  t[7] = t10 - o0;
+  t[1] = t11 + o1;
+  t[6] = t11 - o1;
+  t[2] = t12 + o2;
+  t[5] = t12 - o2;
+  t[3] = t13 + o3;
+  t[4] = t13 - o3;
+}
+// w: the block in the pair layout (scaled as above); o as idct_islow_block
+__device__ __forceinline__ void idct_dot2_block(const uint32_t (&w)[32], uint32_t (&o)[16]) {
+  uint32_t q[4][8];  // pass-2 pairs: q[j][r] = row r's pair j
+  constexpr int kCa[4] = {0, 2, 1, 5}, kCb[4] = {4, 6, 3, 7};
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    int32_t ta[8], tb[8];
+    const int ca = kCa[j], cb = kCb[j];
+    islow_dot2_1d(w[4 * ca], w[4 * ca + 1], w[4 * ca + 2], w[4 * ca + 3], ca == 0 ? RJ_PK(16384, 8192) : RJ_PK(8192, 8192),
+                  ca == 0 ? RJ_PK(16384, -8192) : RJ_PK(8192, -8192), 32768, ta);
+    islow_dot2_1d(w[4 * cb], w[4 * cb + 1], w[4 * cb + 2], w[4 * cb + 3], RJ_PK(8192, 8192), RJ_PK(8192, -8192), 32768,
+                  tb);
+#pragma unroll
+    for (int r = 0; r < 8; r++) q[j][r] = __builtin_amdgcn_perm(uint32_t(tb[r]), uint32_t(ta[r]), 0x07060302u);
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    int32_t t[8];
+    islow_dot2_1d(q[0][r], q[1][r], q[2][r], q[3][r], RJ_PK(8192, 8192), RJ_PK(8192, -8192), RJ_PASS2_RND, t);
+    o[2 * r] = islow_pack4(islow_limit_biased(t[0]), islow_limit_biased(t[1]), islow_limit_biased(t[2]),
+                           islow_limit_biased(t[3]));
+    o[2 * r + 1] = islow_pack4(islow_limit_biased(t[4]), islow_limit_biased(t[5]), islow_limit_biased(t[6]),
+                               islow_limit_biased(t[7]));
+  }
+}
+
 // Exact ISLOW for coefficients outside the int32 domain above (only corrupt streams with large
 // quantisers get here; K2 detects them per strip and records the row, which the K2 fix-up
 // launch -- k_rows_fix, its own kernel, so none of this touches the common path's registers --
