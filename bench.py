@@ -492,7 +492,30 @@ def main():
                                  for r in range(world)])
         shard_cost = S.assign_shards(table, world, list(range(world)))
     t_build = time.perf_counter() - t_tab
-    table = S.broadcast_table(table, src=0, device=cdev)
+    # the one collective: through the library's own RCCL communicator (rocJpegAmdCommInitRank /
+    # rocJpegAmdBroadcastWorkTable, the C-ABI path a C caller takes); ranks sharing a GPU (the
+    # rehearsal) cannot form an RCCL communicator and use torch.distributed over gloo instead
+    bcast_via = "none (one rank)"
+    if world > 1:
+        total = int(sum(len(idx[r][0]) for r in range(world)))
+        comm = None
+        if not share:
+            try:
+                uid = torch.zeros(128, dtype=torch.uint8, device=cdev)
+                if rank == 0:
+                    uid.copy_(torch.frombuffer(bytearray(S.comm_unique_id()), dtype=torch.uint8))
+                dist.broadcast(uid, src=0)
+                comm = S.Comm(gpu, world, rank, bytes(uid.cpu().numpy()))
+            except RuntimeError as e:  # reported in the line, never silent
+                bcast_via = f"torch.distributed ({e})"
+        if comm is not None:
+            table = comm.broadcast_table(table, total)
+            comm.close()
+            bcast_via = "RCCL: rocJpegAmdBroadcastWorkTable (librocjpeg_amd.so)"
+        else:
+            table = S.broadcast_table(table, src=0, device=cdev)
+            if share:
+                bcast_via = "torch.distributed gloo (RJ_BENCH_SHARE_GPU rehearsal)"
     t_tab = time.perf_counter() - t_tab
     my = S.shard_of(table, rank)
     datas = [blob.get(o, s) for o, s in zip(my["stream_offset"], my["stream_bytes"])]
@@ -569,7 +592,7 @@ def main():
             "parity_timed_output": parity,
             "parity_timed_output_images": len(parity_sample(n)),
             "work_table": {"images": int(len(table)), "bytes": int(table.nbytes), "build_ms": round(t_build * 1e3, 2),
-                           "build_and_broadcast_ms": round(t_tab * 1e3, 2),
+                           "build_and_broadcast_ms": round(t_tab * 1e3, 2), "broadcast": bcast_via,
                            "lpt_imbalance": round(S.imbalance(shard_cost), 5),
                            "images_per_rank": [int((table["shard"] == r).sum()) for r in range(world)]},
             "dataset_gen_s": round(t_gen, 1),

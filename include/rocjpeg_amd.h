@@ -157,6 +157,37 @@ RocJpegStatus rocJpegAmdBuildWorkTable(const unsigned char *blob, uint64_t blob_
 RocJpegStatus rocJpegAmdAssignShards(RocJpegAmdWorkItem *items, int count, int num_shards, const int *shard_devices,
                                      uint64_t *shard_cost);
 
+/* ---- Multi-GPU batched decode through the C ABI (csrc/rj_comm.cpp) ----
+ * For a caller of the reference API with one process (or thread) per GPU, the sharded
+ * counterpart of rocJpegDecodeBatched (src/rocjpeg_decoder.cpp:196-292): the reference itself
+ * has no multi-GPU path (one device per handle, src/rocjpeg_api.cpp:107-120; the samples scale by
+ * one handle per thread, samples/jpegDecodePerf/jpegdecodeperf.cpp:228-257).  The communicator
+ * is RCCL's (loaded at run time from librccl.so.1); the work table is its only collective.
+ *   1. one rank: rocJpegAmdCommGetUniqueId; the caller sends the 128-byte id to the others
+ *   2. every rank: rocJpegAmdCommInitRank(its device, nranks, id, rank) -- collective
+ *   3. every rank: rocJpegAmdDecodeBatchedSharded with the same blob / offsets / sizes / count:
+ *      rank 0 builds the work table and assigns images by LPT (shard = rank), one RCCL broadcast
+ *      sends it, each rank parses and decodes its own images into destinations[i] (only its
+ *      entries are written; any destination memory: device, another GPU, host).
+ * rocJpegAmdShardPlan / rocJpegAmdBroadcastWorkTable expose steps of 3 for callers that parse
+ * and decode on their own (e.g. streams kept resident with rocJpegAmdStreamsToDevice). */
+typedef struct { char internal[128]; } RocJpegAmdCommId; /* = ncclUniqueId */
+typedef struct RocJpegAmdCommImpl *RocJpegAmdComm;
+RocJpegStatus rocJpegAmdCommGetUniqueId(RocJpegAmdCommId *id);
+RocJpegStatus rocJpegAmdCommInitRank(int device_id, int nranks, const RocJpegAmdCommId *id, int rank,
+                                     RocJpegAmdComm *comm);
+RocJpegStatus rocJpegAmdCommDestroy(RocJpegAmdComm comm);
+RocJpegStatus rocJpegAmdCommInfo(RocJpegAmdComm comm, int *rank, int *nranks, int *device_id);
+/* rank 0's `count` records -> every rank (each passes the same count) */
+RocJpegStatus rocJpegAmdBroadcastWorkTable(RocJpegAmdComm comm, RocJpegAmdWorkItem *items, int count);
+/* rank 0: rocJpegAmdBuildWorkTable + rocJpegAmdAssignShards over the ranks; then the broadcast */
+RocJpegStatus rocJpegAmdShardPlan(RocJpegAmdComm comm, const unsigned char *blob, uint64_t blob_bytes,
+                                  const uint64_t *offsets, const uint32_t *sizes, int count, RocJpegAmdWorkItem *items);
+RocJpegStatus rocJpegAmdDecodeBatchedSharded(RocJpegHandle handle, RocJpegAmdComm comm, const unsigned char *blob,
+                                             uint64_t blob_bytes, const uint64_t *offsets, const uint32_t *sizes,
+                                             int count, const RocJpegDecodeParams *decode_params,
+                                             RocJpegImage *destinations, RocJpegAmdWorkItem *items);
+
 #if defined(__cplusplus)
 }
 #endif

@@ -21,6 +21,8 @@ EXT_SYMBOLS = (
     "rocJpegAmdStreamGetInfo", "rocJpegAmdStreamsToDevice", "rocJpegAmdSetProfiling", "rocJpegAmdGetLastTimings",
     "rocJpegAmdSetPathPolicy", "rocJpegAmdGetStream", "rocJpegAmdStreamParseDevice", "rocJpegAmdStreamGetIntervals",
     "rocJpegAmdStreamGetDestuffBlocks", "rocJpegAmdBuildWorkTable", "rocJpegAmdAssignShards",
+    "rocJpegAmdCommGetUniqueId", "rocJpegAmdCommInitRank", "rocJpegAmdCommDestroy", "rocJpegAmdCommInfo",
+    "rocJpegAmdBroadcastWorkTable", "rocJpegAmdShardPlan", "rocJpegAmdDecodeBatchedSharded",
 )
 
 
@@ -155,6 +157,15 @@ def lib():
         L.rocJpegAmdBuildWorkTable.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                                ctypes.POINTER(ctypes.c_uint32), i32, vp]
         L.rocJpegAmdAssignShards.argtypes = [vp, i32, i32, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_uint64)]
+        L.rocJpegAmdCommGetUniqueId.argtypes = [vp]
+        L.rocJpegAmdCommInitRank.argtypes = [i32, i32, vp, i32, ctypes.POINTER(vp)]
+        L.rocJpegAmdCommDestroy.argtypes = [vp]
+        L.rocJpegAmdCommInfo.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)]
+        L.rocJpegAmdBroadcastWorkTable.argtypes = [vp, vp, i32]
+        L.rocJpegAmdShardPlan.argtypes = [vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                          ctypes.POINTER(ctypes.c_uint32), i32, vp]
+        L.rocJpegAmdDecodeBatchedSharded.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                                     ctypes.POINTER(ctypes.c_uint32), i32, vp, vp, vp]
         for name in API_SYMBOLS + EXT_SYMBOLS:
             if name != "rocJpegGetErrorName":
                 getattr(L, name).restype = i32

@@ -199,15 +199,18 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
               v += cc == 0 ? nv.dcd[0] : (cc == 1 ? nv.dcd[1] : nv.dcd[2]);
             }
             const int x = __mul24(v, int(qe & 0xFFFFu));  // |v| < 2^16, q < 2^16: exact
-            int16_t sv;
-            if (kRaw && p == 0) {
-              sv = (e & RJ_RE_ZERO) ? int16_t(-32768) : int16_t(v);  // DC difference: restore_dc
+            // straight-line selects (no divergent DC / AC branches in the scatter)
+            const bool dc = p == 0;
+            int sv;
+            if constexpr (kRaw) {  // a raw DC is a difference (restore_dc finishes it)
+              oob = !dc && uint32_t(x + RJ_DOT2_AC_MAX) > uint32_t(2 * RJ_DOT2_AC_MAX);
+              sv = dc ? ((e & RJ_RE_ZERO) ? -32768 : v) : x << 5;
             } else {
-              const int lim = p == 0 ? RJ_DOT2_DC_MAX : RJ_DOT2_AC_MAX;
+              const int lim = dc ? RJ_DOT2_DC_MAX : RJ_DOT2_AC_MAX;
               oob = uint32_t(x + lim) > uint32_t(2 * lim);
-              sv = int16_t(x << (p == 0 ? 4 : 5));
+              sv = x << (dc ? 4 : 5);
             }
-            *reinterpret_cast<int16_t *>(s_buf + (info & 0xFFFFu) + (qe >> 16)) = sv;
+            *reinterpret_cast<int16_t *>(s_buf + (info & 0xFFFFu) + (qe >> 16)) = int16_t(sv);
           } else {
             if (kRaw && (e & RJ_RE_ZERO)) v = -32768;  // zero block: marked for the DC restore
             if (!kRaw && fix_dc && p == 0) {

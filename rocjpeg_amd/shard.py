@@ -138,3 +138,64 @@ class Blob:
         k = int(np.searchsorted(self.bases, np.uint64(offset), side="right")) - 1
         o = int(offset) - int(self.bases[k])
         return bytes(self.parts[k][o:o + int(size)])
+
+
+class CommId(ctypes.Structure):
+    """RocJpegAmdCommId (= ncclUniqueId): 128 opaque bytes one rank creates and sends to the others."""
+    _fields_ = [("internal", ctypes.c_char * 128)]
+
+
+def comm_unique_id():
+    """rocJpegAmdCommGetUniqueId: the id as 128 bytes (one rank calls it; the caller distributes it)."""
+    cid = CommId()
+    st = lib().rocJpegAmdCommGetUniqueId(ctypes.byref(cid))
+    if st != 0:
+        raise RuntimeError(f"rocJpegAmdCommGetUniqueId: {Status(st)!r}")
+    return ctypes.string_at(ctypes.addressof(cid), 128)  # all 128 bytes (the c_char field would stop at a NUL)
+
+
+class Comm:
+    """The library's own RCCL communicator (include/rocjpeg_amd.h "Multi-GPU batched decode through
+    the C ABI"): the work-table broadcast and the sharded batched decode run in C++ against it, so
+    a C caller and this binding take the same path."""
+
+    def __init__(self, device_id, nranks, rank, uid):
+        cid = CommId()
+        ctypes.memmove(ctypes.addressof(cid), bytes(uid), 128)
+        self.handle = ctypes.c_void_p()
+        st = lib().rocJpegAmdCommInitRank(int(device_id), int(nranks), ctypes.byref(cid), int(rank),
+                                           ctypes.byref(self.handle))
+        if st != 0:
+            raise RuntimeError(f"rocJpegAmdCommInitRank: {Status(st)!r}")
+        self.rank, self.nranks, self.device = int(rank), int(nranks), int(device_id)
+
+    def broadcast_table(self, table, count):
+        """rank 0's `count` records -> every rank (rocJpegAmdBroadcastWorkTable); returns the table."""
+        t = np.ascontiguousarray(table) if table is not None else np.zeros(count, dtype=WORK_ITEM_DTYPE)
+        if len(t) != count:
+            raise ValueError("table length differs from count")
+        st = lib().rocJpegAmdBroadcastWorkTable(self.handle, ctypes.c_void_p(t.ctypes.data) if count else None, count)
+        if st != 0:
+            raise RuntimeError(f"rocJpegAmdBroadcastWorkTable: {Status(st)!r}")
+        return t
+
+    def decode_batched_sharded(self, dec_handle, blob, offsets, sizes, params, destinations):
+        """rocJpegAmdDecodeBatchedSharded over the whole batch (`destinations`: a ctypes array of
+        RocJpegImage, one per image; this rank writes its own).  Returns (status, table)."""
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        sizes = np.ascontiguousarray(sizes, dtype=np.uint32)
+        n = len(offsets)
+        table = np.zeros(n, dtype=WORK_ITEM_DTYPE)
+        ptr, keep = _u8_pointer(blob)
+        st = lib().rocJpegAmdDecodeBatchedSharded(dec_handle, self.handle, ptr, keep.nbytes,
+                                                  offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                                  sizes.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n,
+                                                  ctypes.byref(params), destinations,
+                                                  ctypes.c_void_p(table.ctypes.data))
+        del keep
+        return st, table
+
+    def close(self):
+        if self.handle:
+            lib().rocJpegAmdCommDestroy(self.handle)
+            self.handle = ctypes.c_void_p()

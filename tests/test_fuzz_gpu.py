@@ -169,3 +169,51 @@ def test_fuzz_coarse_quant_outside_int32_domain(dec, seed):
         ost, want = O.oracle_decode(d, int(R.OutputFormat.RGB), shp)
         assert ost == 0
         assert np.array_equal(o, want[0])
+
+
+def _patch_dqt(d, value):
+    """Every quantiser of every 8-bit DQT table set to `value` (the entropy-coded data unchanged:
+    the same coefficients, dequantised to value / original times as much)."""
+    buf = bytearray(d)
+    i = 2
+    while i + 4 <= len(buf):
+        assert buf[i] == 0xFF
+        m, ln = buf[i + 1], (buf[i + 2] << 8) | buf[i + 3]
+        if m == 0xDA:
+            break
+        if m == 0xDB:
+            j = i + 4
+            while j < i + 2 + ln:
+                assert buf[j] >> 4 == 0  # 8-bit tables only
+                buf[j + 1:j + 65] = bytes([value]) * 64
+                j += 65
+        i += 2 + ln
+    return bytes(buf)
+
+
+def test_dot2_domain_band_goes_to_the_fixup_launch(dec):
+    """Clean streams whose dequantised coefficients lie between the dot2 IDCT's exact domain
+    (|DC| <= 1151, |AC| <= 1023, rj_math.h) and the int32 IDCT's (|x| < 2^14): noise encoded with
+    quantisers 40, then every quantiser raised to 255 (coefficients up to ~+-40 dequantise to
+    ~+-10,000).  K2 flags those strips and the fix-up launch decodes their rows again -- oracle
+    bit-exact, baseline and every restart layout of _coarse_quant_jpegs."""
+    import io
+    from PIL import Image
+    rng = np.random.default_rng(11)
+    datas = []
+    for (w, h), sub, rst in [((256, 128), 2, True), ((160, 96), 0, True), ((200, 72), 2, False)]:
+        a = rng.integers(0, 255, (h, w, 3), dtype=np.uint8)
+        b = io.BytesIO()
+        kw = dict(qtables=[[40] * 64, [40] * 64], subsampling=sub)
+        if rst:
+            kw["restart_marker_blocks"] = (w + 15) // 16
+        Image.fromarray(a).save(b, "JPEG", **kw)
+        datas.append(_patch_dqt(b.getvalue(), 255))
+    dec.set_profiling(True)
+    st, outs, shapes = _decode_batch(dec, datas)
+    tm = dec.last_timings()
+    dec.set_profiling(False)
+    assert st == 0 and tm["wide_rows"] > 0
+    for d, o, shp in zip(datas, outs, shapes):
+        ost, want = O.oracle_decode(d, int(R.OutputFormat.RGB), shp)
+        assert ost == 0 and np.array_equal(o, want[0])
