@@ -136,8 +136,8 @@ __device__ __forceinline__ int raw_value(uint32_t e) {
 // exact for 16-bit quantisers) x 32, the DC x 16 (raw DC differences stay as they are: restore_dc
 // finishes them).  A coefficient outside the dot2 IDCT's exact domain raises `bad` (the row goes
 // to the fix-up launch).  The entry's block in the strip supplies, through one ds_bpermute of the
-// owning lane's `lane_info` (block LDS base | q-table row << 16), where the block lives and which
-// component's quantisers apply; s_qw[c][p] = quantiser | pair-layout byte offset << 16.
+// owning lane's `lane_info` (block LDS base | component << 16), where the block lives and which
+// component's quantisers apply; s_qw[3 p + c] = quantiser | pair-layout byte offset << 16.
 // !kPairs (the fix-up instances): raw coefficients in zigzag order, checked against the int32
 // IDCT's domain (thr, on the raw value) -- the layout idct_pass1_wide reads.
 template <bool kRaw, bool kSplit, bool kPairs>
@@ -193,9 +193,9 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
         if (!pass && ord < piece && p < 64u && blk >= drop && int(lane) < tl) {
           int v = kRaw ? raw_value(e) : int(int16_t(e & 0xFFFFu));
           if constexpr (kPairs) {
-            const uint32_t qe = s_qw[(info >> 16) + p];
+            const uint32_t qe = s_qw[3u * p + (info >> 16)];  // component-interleaved: (a/4) mod 32 banks
             if (!kRaw && fix_dc && p == 0) {
-              const uint32_t cc = info >> 22;  // q-table row = component x 64
+              const uint32_t cc = info >> 16;
               v += cc == 0 ? nv.dcd[0] : (cc == 1 ? nv.dcd[1] : nv.dcd[2]);
             }
             const int x = __mul24(v, int(qe & 0xFFFFu));  // |v| < 2^16, q < 2^16: exact
@@ -442,6 +442,34 @@ __device__ __forceinline__ void rgb_strip(const uint8_t *ty, const uint8_t *tu, 
   }
 }
 
+// Phase C for the commonest strip, 4:2:0 -> RGB over a whole strip of 10 MCUs (160 x 16 px,
+// luma tile 160 B wide, chroma tiles 80 B): lane = row pair qy = tid / 8 (8 pairs) and quad
+// columns qx = tid % 8 + 8 i, i = 0..4 (40 quads).  Every LDS and global address is the lane's
+// base plus a compile-time offset (32 B / 16 B / 96 B per i), so the loop has no address or
+// index arithmetic; same pixels, arithmetic and bytes as rgb_strip<true, true>.
+__device__ __forceinline__ void rgb_strip_420_full(const uint8_t *ty, const uint8_t *tu, const uint8_t *tv,
+                                                   uint32_t tid, uint8_t *dst, uint32_t pitch) {
+  const uint32_t qy = tid >> 3, qx0 = tid & 7u;
+  const uint8_t *yr = ty + qy * 320u + qx0 * 4u;   // luma rows 2 qy, 2 qy + 1 (tile width 160)
+  const uint32_t co = qy * 80u + qx0 * 2u;          // chroma row qy (tile width 80)
+  RJ_GLOBAL uint8_t *d = gp(dst) + (__umul24(2u * qy, pitch) + qx0 * 12u);
+  const rj_f2 m128 = {128.0f, 128.0f};
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint32_t y4 = *reinterpret_cast<const uint32_t *>(yr + 32 * i);
+    const uint32_t y4b = *reinterpret_cast<const uint32_t *>(yr + 160 + 32 * i);
+    const uint32_t u2 = *reinterpret_cast<const uint16_t *>(tu + co + 16 * i);
+    const uint32_t v2 = *reinterpret_cast<const uint16_t *>(tv + co + 16 * i);
+    const rj_f2 uu = rj_f2{u8f(u2, 0), u8f(u2, 1)} - m128, vv = rj_f2{u8f(v2, 0), u8f(v2, 1)} - m128;
+    const rj_f2 ua = {uu.x, uu.x}, ub = {uu.y, uu.y}, va = {vv.x, vv.x}, vb = {vv.y, vv.y};
+    uint32_t w0, w1, w2;
+    csc4_pk(y4, ua, ub, va, vb, w0, w1, w2);
+    *reinterpret_cast<RJ_GLOBAL uint3 *>(d + 96 * i) = make_uint3(w0, w1, w2);
+    csc4_pk(y4b, ua, ub, va, vb, w0, w1, w2);
+    *reinterpret_cast<RJ_GLOBAL uint3 *>(d + pitch + 96 * i) = make_uint3(w0, w1, w2);
+  }
+}
+
 // The work of one MCU row (one wavefront), looping over the row's strips of S MCUs.
 //   kPlanes = false: fused output (rj_decoder.cpp FusedEligible images)
 //   kPlanes = true : general path, blocks into the MCU-padded component planes (K2b reads them)
@@ -494,24 +522,26 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
 
   const RjTableSet *ts = tabsets + im.tabset;
   if constexpr (kPairs) {
-    // s_qw[c][p] = quantiser of zigzag position p | its byte offset in the pair layout << 16
+    // s_qw[3 p + c] = quantiser of zigzag position p of component c | its byte offset in the pair
+    // layout << 16 (components interleaved: the scatter's ds_read_b32 banks are (a/4) mod 32, and
+    // luma and chroma entries of one position then fall in different banks)
     constexpr uint8_t kNatZ[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
                                    12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
                                    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                                    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
     for (uint32_t k = tid; k < ncomp * 64; k += 64) {
       const uint32_t nat = kNatZ[k & 63];
-      s_qw[k] = uint32_t(ts->qz[im.comp_tq[k >> 6] & 3][k & 63]) | rj_pair_slot(nat >> 3, nat & 7) << 16;
+      s_qw[3u * (k & 63u) + (k >> 6)] = uint32_t(ts->qz[im.comp_tq[k >> 6] & 3][k & 63]) | rj_pair_slot(nat >> 3, nat & 7) << 16;
     }
   } else {
     for (uint32_t k = tid; k < ncomp * 64; k += 64) s_q[k >> 6][k & 63] = ts->qz[im.comp_tq[k >> 6] & 3][k & 63];
   }
 
-  // this lane's block: LDS base | its component's q-table row << 16 (parse_blocks' bpermute source),
+  // this lane's block: LDS base | its component << 16 (parse_blocks' bpermute source),
   // and its DC quantiser (restore_dc)
-  const uint32_t lane_info = tid * RJ_BLK_STRIDE | ((lane_blk >> 12) * 64u) << 16;
+  const uint32_t lane_info = tid * RJ_BLK_STRIDE | (lane_blk >> 12) << 16;
   __syncthreads();  // s_qw / s_q written
-  const uint32_t q0 = kPairs ? s_qw[(lane_blk >> 12) * 64u] & 0xFFFFu : 0u;
+  const uint32_t q0 = kPairs ? s_qw[lane_blk >> 12] & 0xFFFFu : 0u;
   const uint32_t mcux = U(im.mcux);
   const bool dc_diff = !kDense && U(im.dc_diff) != 0;  // raw entries: restore_dc per strip
   const int thr = int(U(im.idct_thr));
@@ -676,7 +706,8 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
     const uint8_t *ty = s_buf + toff[0], *tu = s_buf + toff[1], *tv = s_buf + toff[2];
     uint8_t *d = dst0 + (__umul24(py0, pitch0) + px0 * 3);
     if (hs1) {
-      if (vs1) rgb_strip<true, true>(ty, tu, tv, tw[0], tw[1], tid, quads_x, rows, d, pitch0);
+      if (vs1 && strip_w == 160u && tw[0] == 160u && tw[1] == 80u) rgb_strip_420_full(ty, tu, tv, tid, d, pitch0);
+      else if (vs1) rgb_strip<true, true>(ty, tu, tv, tw[0], tw[1], tid, quads_x, rows, d, pitch0);
       else rgb_strip<true, false>(ty, tu, tv, tw[0], tw[1], tid, quads_x, rows, d, pitch0);
     } else {
       if (vs1) rgb_strip<false, true>(ty, tu, tv, tw[0], tw[1], tid, quads_x, rows, d, pitch0);
