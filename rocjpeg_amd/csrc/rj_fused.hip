@@ -609,8 +609,11 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
     bool wide = false;  // some coefficient of the strip needs the exact 64-bit IDCT
     // ---- A: clear the strip's LDS blocks, expand the entry stream into them ----
     __syncthreads();  // previous strip's tiles fully read
-    for (uint32_t k = tid; k < nb * 8; k += 64)
-      *reinterpret_cast<uint4 *>(s_buf + (k >> 3) * RJ_BLK_STRIDE + (k & 7) * 16) = make_uint4(0, 0, 0, 0);
+    if (!kDense && has_blk) {  // lane b clears block b (compile-time offsets; the dense path overwrites it whole)
+      uint4 *z = reinterpret_cast<uint4 *>(s_buf + tid * RJ_BLK_STRIDE);
+#pragma unroll
+      for (int q = 0; q < 8; q++) z[q] = make_uint4(0, 0, 0, 0);
+    }
     __syncthreads();
     if constexpr (kDense) {
       if (has_blk) load_dense_block(im, coefs.dense, lane_blk, mx0, my, inter, s_buf + tid * RJ_BLK_STRIDE);
