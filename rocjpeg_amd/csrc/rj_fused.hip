@@ -126,9 +126,10 @@ struct Nav {
 // cbits: component of each block within the MCU (2 bits each), for the DC corrections.
 // libjpeg HUFF_EXTEND of a raw entry (lean K1): the s extra bits as a signed value (s = 0 -> 0)
 __device__ __forceinline__ int raw_value(uint32_t e) {
-  const uint32_t s = (e >> 16) & 15u, raw = __builtin_amdgcn_ubfe(e, 0u, s);  // K1 keeps the code bits above
-  const uint32_t half = (1u << s) >> 1;
-  return raw < half ? int(raw) - int(2 * half - 1) : int(raw);
+  const uint32_t s = (e >> 16) & 15u, m = (1u << s) - 1u;  // v_bfm_b32
+  const uint32_t raw = e & m;                               // K1 keeps the code bits above
+  const uint32_t d = m - raw;                               // top bit clear (negative) <=> raw <= d
+  return raw > d ? int(raw) : int(raw) - int(m);
 }
 
 // kPairs (the main K2 instances): each coefficient is dequantised here and stored scaled into
