@@ -106,40 +106,56 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
 // One symbol step.  SAFE: per-lane activity (blocks_left) and libjpeg's insufficient-data rule.
 // SYNC (split launch): the lane notes where its last MCU started (mpos, mleft), and a tail lane
 // records its MCU starts (recs, nr; head lanes keep nr = RJ_HL_REC and write a scratch slot).
+// Software-pipelined: a step starts with this symbol's entry `e` and its 32-bit `peek` already
+// loaded (by the previous step, or the prologue); it first advances the bit position and the
+// block / table state -- the chain the next lookup depends on -- and issues the next symbol's
+// LDS lookup, then does this symbol's remaining work (its entry into the stage, the counters)
+// while that lookup is in flight.  (Issued in the other order, the lookup's LDS latency sat
+// unhidden on every symbol: ~40 instructions and ~310 cycles per symbol.)
 #define RJ_HL_STEP(SAFE, SYNC)                                                                                  \
   do {                                                                                                    \
-    const uint32_t peek = __builtin_amdgcn_alignbit(wa, wb, q);                                           \
-    uint32_t e = s_lut[(tb >> 2) + (peek >> tsh)];                                                        \
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(e >= RJ_HL_ESC) != 0, 0)) {                          \
       RJ_HL_COUNT_ESC;                                                                                    \
       if (e >= RJ_HL_ESC) e = hl_escape(e, peek, tsh != 21u, acb, s_lut, tset, pat >> b);                 \
     }                                                                                                     \
-    /* the symbol's n bits right-aligned (code, then its s extra bits: K2 keeps the low s) */           \
-    const uint32_t raw = peek >> (e & 31u);                                                               \
-    uint32_t entry = __builtin_amdgcn_perm(e, raw, 0x07060100u); /* raw's low half, e's fields above */ \
-    entry += k << 21;                                                                                     \
-    uint32_t emit = (e >> 13) & 1u;                                                                       \
+    /* ---- the chain: bit position, block / table state, the next lookup ---- */                      \
     const uint32_t qold = q;                                                                              \
     q -= (e >> 8) & 31u;                                                                                  \
     uint32_t kn = k + ((e >> 21) & 127u) + 1u;                                                            \
-    if (SAFE) {                                                                                           \
-      entry = skip ? RJ_RE_ZERO : entry; /* libjpeg: the rest of the interval is zero blocks */          \
-      emit = skip ? 1u : emit;                                                                            \
-      kn = skip ? 64u : kn;                                                                               \
-      emit = blocks_left > 0 ? emit : 0u;                                                                 \
-    }                                                                                                     \
-    stage[ne & (kStage - 1)] = entry; /* a non-emitted write lands in the next free slot */                \
-    ne += emit;                                                                                           \
+    if (SAFE) kn = skip ? 64u : kn;                                                                       \
     {                                                                                                     \
       const bool adv = (qold ^ q) > 31u; /* the bit position entered the next word */                   \
       wa = adv ? wb : wa;                                                                                 \
       wb = adv ? wc : wb;                                                                                 \
       rr += adv ? 1u : 0u;                                                                                \
-      wc = ring[rr & (RJ_HL_WORDS - 1)];                                                                  \
     }                                                                                                     \
     const bool bend = kn >= 64u;                                                                          \
+    const uint32_t kcur = k;                                                                              \
     k = bend ? 0u : kn;                                                                                   \
     const uint32_t bn = b + 2u == nb2 ? 0u : b + 2u;                                                      \
+    b = bend ? bn : b;                                                                                    \
+    /* next symbol's table: the new block's DC table, or the current block's AC table */                 \
+    const uint32_t ids = pat >> b;                                                                        \
+    acb = bend ? ((ids >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES) : acb;                                      \
+    const uint32_t dcb = RJ_HL_DC0 + ((ids & 1u) << (RJ_HL_DC_BITS + 2));                                 \
+    const uint32_t tbn = bend ? dcb : acb;                                                                \
+    const uint32_t tshn = bend ? uint32_t(32 - RJ_HL_DC_BITS) : uint32_t(32 - RJ_HL_AC_BITS);            \
+    const uint32_t peekn = __builtin_amdgcn_alignbit(wa, wb, q);                                          \
+    const uint32_t en = s_lut[(tbn >> 2) + (peekn >> tshn)];                                              \
+    wc = ring[rr & (RJ_HL_WORDS - 1)];                                                                    \
+    /* ---- this symbol's entry, while the lookup is in flight ---- */                                  \
+    /* the symbol's n bits right-aligned (code, then its s extra bits: K2 keeps the low s) */           \
+    const uint32_t raw = peek >> (e & 31u);                                                               \
+    uint32_t entry = __builtin_amdgcn_perm(e, raw, 0x07060100u); /* raw's low half, e's fields above */ \
+    entry += kcur << 21;                                                                                  \
+    uint32_t emit = (e >> 13) & 1u;                                                                       \
+    if (SAFE) {                                                                                           \
+      entry = skip ? RJ_RE_ZERO : entry; /* libjpeg: the rest of the interval is zero blocks */          \
+      emit = skip ? 1u : emit;                                                                            \
+      emit = blocks_left > 0 ? emit : 0u;                                                                 \
+    }                                                                                                     \
+    stage[ne & (kStage - 1)] = entry; /* a non-emitted write lands in the next free slot */                \
+    ne += emit;                                                                                           \
     if (SAFE) {                                                                                           \
       const bool act = blocks_left > 0;                                                                   \
       blocks_left -= (bend && act) ? 1u : 0u;                                                             \
@@ -156,13 +172,9 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
       recs[min(nr, kRec) * kPairs] = uint16_t(0u - q);                                                     \
       nr += (ms && nr < kRec) ? 1u : 0u;                                                                  \
     }                                                                                                     \
-    b = bend ? bn : b;                                                                                    \
-    /* next symbol's table: the new block's DC table, or the current block's AC table */                 \
-    const uint32_t ids = pat >> b;                                                                        \
-    acb = bend ? ((ids >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES) : acb;                                      \
-    const uint32_t dcb = RJ_HL_DC0 + ((ids & 1u) << (RJ_HL_DC_BITS + 2));                                 \
-    tb = bend ? dcb : acb;                                                                                \
-    tsh = bend ? uint32_t(32 - RJ_HL_DC_BITS) : uint32_t(32 - RJ_HL_AC_BITS);                            \
+    e = en;                                                                                               \
+    peek = peekn;                                                                                         \
+    tsh = tshn;                                                                                           \
   } while (0)
 
 // LDS lane columns shared by a decoder lane and its mover lane: plain LDS words whose order of
@@ -341,6 +353,9 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     uint32_t acb = ((pat >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES);
     uint32_t tb = RJ_HL_DC0 + ((pat & 1u) << (RJ_HL_DC_BITS + 2));
     uint32_t tsh = 32 - RJ_HL_DC_BITS;
+    // the first symbol's peek and table entry (RJ_HL_STEP is software-pipelined)
+    uint32_t peek = __builtin_amdgcn_alignbit(wa, wb, q);
+    uint32_t e = s_lut[(tb >> 2) + (peek >> tsh)];
 #ifdef RJ_HL_STAMPS
     uint64_t st_steps = 0, st_end = 0, st_fast = 0, st_safe = 0, st_esc = 0;
 #define RJ_HL_T0 const uint64_t t0 = __builtin_amdgcn_s_memtime()
