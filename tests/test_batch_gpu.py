@@ -149,6 +149,52 @@ def test_c4_1024_default_outlier_split(dec):
     assert not bad, f"{len(bad)} images differ, first {sorted(bad)[:8]}"
 
 
+def _planar_shapes(data, fmt):
+    info = R.JpegStream(data).info()
+    return channel_shapes(fmt, info["subsampling"], info["widths"], info["heights"])
+
+
+@pytest.mark.parametrize("workload,fmt", [("c3", R.OutputFormat.YUV_PLANAR), ("c2nori", R.OutputFormat.RGB)],
+                         ids=["c3_444_422_yuv_planar", "c2nori_restartless"])
+def test_full_batch_other_configs(dec, workload, fmt):
+    """BASELINE config C3 (1024 x 1080p, 4:4:4 and 4:2:2 alternating, RI one MCU row ->
+    YUV_PLANAR: the lean K1 with two sampling geometries in one call) and the C2 no-DRI twin
+    (every interval a whole 1080p image: the self-synchronising chunk lanes), each as the bench
+    runs it -- 1024 resident images (256 distinct x 4) in one rocJpegDecodeBatched call under the
+    default handle settings -- every channel of every image compared with the oracle on the
+    device.  Reference path: src/rocjpeg_decoder.cpp:196-292."""
+    t = torch()
+    distinct, copies = 256, 4
+    datas = _c2_images(distinct, seed0=1234, workload=workload)
+    shapes = [_planar_shapes(d, fmt) for d in datas]
+    with ThreadPoolExecutor(16) as ex:
+        want = list(ex.map(lambda k: O.oracle_decode(datas[k], int(fmt), shapes[k]), range(distinct)))
+    assert all(st == 0 for st, _ in want)
+    streams = [R.JpegStream(datas[i % distinct]) for i in range(distinct * copies)]
+    dec.streams_to_device(streams)
+    outs, imgs = [], []
+    for i in range(len(streams)):
+        ts = [t.full(sh, 0xA5, dtype=t.uint8, device="cuda") for sh in shapes[i % distinct]]
+        outs.append(ts)
+        imgs.append(R.make_image([x.data_ptr() for x in ts], [sh[1] for sh in shapes[i % distinct]]))
+    dec.set_profiling(True)
+    st = dec.decode_batched(streams, R.decode_params(fmt), imgs)
+    tm = dec.last_timings()
+    dec.set_profiling(False)
+    assert st == 0, R.error_name(st)
+    assert tm["images"] == 1024
+    if workload == "c3":
+        assert tm["lean_k1"] == 1 and {i["subsampling"] for i in (R.JpegStream(d).info() for d in datas[:2])} == {0, 2}
+    else:
+        assert tm["lean_k1"] == 0 and tm["split_intervals"] == 1024  # one interval per image, chunked
+    bad = []
+    for j in range(distinct):
+        refs = [t.from_numpy(np.ascontiguousarray(w)).to("cuda") for w in want[j][1]]
+        bad += [i for i in range(j, len(streams), distinct)
+                if not all(t.equal(o, r) for o, r in zip(outs[i], refs))]
+    assert not bad, f"{len(bad)} images differ, first {sorted(bad)[:8]}"
+
+
 def _rgb_shape(data):
     """(rows, pitch) of the RGB destination, from the SOF0 header."""
     i = data.index(b"\xff\xc0")
