@@ -309,3 +309,46 @@ def test_pipelined_row_aligned_batch(pdec, fmt):
         assert ost == 0
         for c, (g, w) in enumerate(zip(G.to_host(bufs), want)):
             assert G.first_mismatch(g, w) is None, (k, c, G.first_mismatch(g, w))
+
+
+# ---- the reference's size limits (rocjpeg_vaapi_decoder.cpp:586-592: 64 .. 16384 per side) ----
+def _noise_jpeg(w, h, sub, rst_rows=1, seed=3):
+    import io
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    a = np.clip(128 + 60 * np.sin(np.arange(w, dtype=np.float32)[None, :, None] / 11.0) +
+                rng.normal(0, 20, (h, w, 3)).astype(np.float32), 0, 255)
+    b = io.BytesIO()
+    mcu_w = 16 if sub in (1, 2) else 8
+    kw = dict(quality=85, subsampling=sub)
+    if rst_rows:
+        kw["restart_marker_blocks"] = rst_rows * ((w + mcu_w - 1) // mcu_w)
+    Image.fromarray(a.astype(np.uint8)).save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+@pytest.mark.parametrize("w,h,sub,rst", [(16384, 64, 2, 1), (64, 16384, 2, 1), (16384, 80, 0, 0), (64, 64, 2, 1),
+                                         (16384, 2048, 2, 1)],
+                         ids=["16384x64_420_ri", "64x16384_420_ri", "16384x80_444_nori", "64x64_420", "16384x2048_420"])
+@pytest.mark.parametrize("fmt", [R.OutputFormat.RGB, R.OutputFormat.YUV_PLANAR], ids=["RGB", "YUV_PLANAR"])
+def test_largest_and_smallest_accepted_sizes(dec, w, h, sub, rst, fmt):
+    """The edges of the accepted size range decode like the oracle: 16384-wide rows (256-KB
+    RGB rows, 1024 MCUs per row: the longest interval a row image can have), 16384-tall
+    columns, a 16384-wide restart-less 4:4:4 strip (chunk lanes), the 64x64 minimum, and a
+    16384 x 2048 4:2:0 picture (100 MB RGB)."""
+    data = _noise_jpeg(w, h, sub, rst)
+    st, ost, got, want = run_both(dec, data, fmt)
+    assert st == 0 and ost == 0
+    for g, x in zip(got, want):
+        assert np.array_equal(g, x)
+
+
+@pytest.mark.parametrize("w,h", [(16385, 64), (64, 16385), (63, 64), (64, 63)])
+def test_sizes_outside_the_range_are_refused(dec, w, h):
+    """One pixel outside either edge: JPEG_NOT_SUPPORTED, as the reference's SubmitDecode
+    returns (rocjpeg_vaapi_decoder.cpp:586-592); the parse itself succeeds."""
+    from tests import gpu_util as G
+    data = _noise_jpeg(w, h, 2, 0)
+    s = R.JpegStream(data)
+    bufs, img = G.gpu_buffers([(h, 3 * w)])
+    assert dec.decode(s, R.decode_params(R.OutputFormat.RGB), img) == R.Status.JPEG_NOT_SUPPORTED
