@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
-"""Drop-in (non-resident) decode rate of the C2 batch by host staging thread count, plus a
-pinned-memory copy / DMA probe.  Development aid (gpurun): python tools/host_input.py"""
+"""Drop-in (non-resident) decode rate of the C2 batch by host staging thread count
+(RJ_HOST_THREADS), configurations alternating over rounds (HI_ROUNDS x HI_CALLS calls; HI_PROFILE=1
+adds a call with the handle's stage events), plus a pinned-memory copy / DMA probe (HI_PROBE=0
+skips it).  Development aid (gpurun):  python tools/host_input.py [[env]/threads ...]  e.g. 0/8 0/12
+The part before '/' was RJ_HOST_SPLIT, the host-input split measured in round 3 and not kept
+(profiles/r3_experiments/host_input_split_ab.txt)."""
 import ctypes
 import os
 import sys
@@ -31,25 +35,38 @@ def main():
     arr = (R.RocJpegImage * 1024)(*imgs)
     hs = (ctypes.c_void_p * 1024)(*[s.handle for s in streams])
     params = R.decode_params(R.OutputFormat.RGB)
-    for nt in (1, 4, 8, 16, 32):
-        os.environ["RJ_HOST_THREADS"] = str(nt)
-        dec = R.JpegDecoder(R.Backend.HARDWARE, 0)
-        L = R.lib()
-        assert L.rocJpegDecodeBatched(dec.handle, hs, 1024, ctypes.byref(params), arr) == 0
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(5):
-            assert L.rocJpegDecodeBatched(dec.handle, hs, 1024, ctypes.byref(params), arr) == 0
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / 5
-        dec.set_profiling(True)
-        L.rocJpegDecodeBatched(dec.handle, hs, 1024, ctypes.byref(params), arr)
-        t = dec.last_timings()
-        dec.set_profiling(False)
-        print(f"threads {nt:2d}: {1024 / dt:9.1f} images/s, {dt * 1e3:.2f} ms/call; profiled: host {t['host_ms']:.2f} "
-              f"h2d+stage {t['h2d_ms']:.2f} K0 {t['destuff_ms']:.2f} K1 {t['huffman_ms']:.2f} K2 {t['idct_ms']:.2f} "
-              f"total {t['total_ms']:.2f} ms", flush=True)
-        dec.close()
+    configs = sys.argv[1:] or ["0/8", "0.5,0.5/8"]
+    L = R.lib()
+    decs = {}
+    for c in configs:
+        split, _, nt = c.partition("/")
+        os.environ["RJ_HOST_SPLIT"] = split
+        os.environ["RJ_HOST_THREADS"] = nt or "8"
+        decs[c] = R.JpegDecoder(R.Backend.HARDWARE, 0)
+        assert L.rocJpegDecodeBatched(decs[c].handle, hs, 1024, ctypes.byref(params), arr) == 0
+    torch.cuda.synchronize()
+    rates = {c: [] for c in configs}
+    for rnd in range(int(os.environ.get("HI_ROUNDS", "3"))):
+        for c in configs:
+            t0 = time.perf_counter()
+            for _ in range(int(os.environ.get("HI_CALLS", "8"))):
+                assert L.rocJpegDecodeBatched(decs[c].handle, hs, 1024, ctypes.byref(params), arr) == 0
+            torch.cuda.synchronize()
+            rates[c].append(int(os.environ.get("HI_CALLS", "8")) * 1024 / (time.perf_counter() - t0))
+            if os.environ.get("HI_PROFILE"):  # one more call with the handle's stage events
+                decs[c].set_profiling(True)
+                L.rocJpegDecodeBatched(decs[c].handle, hs, 1024, ctypes.byref(params), arr)
+                t = decs[c].last_timings()
+                decs[c].set_profiling(False)
+                print(f"  profiled ({'last part' if c.split('/')[0] not in ('0', '1') else 'whole call'}): "
+                      f"host {t['host_ms']:.2f} h2d+stage {t['h2d_ms']:.2f} K0 {t['destuff_ms']:.2f} "
+                      f"K1 {t['huffman_ms']:.2f} K2 {t['idct_ms']:.2f} total {t['total_ms']:.2f} ms", flush=True)
+            print(f"round {rnd} {c:16s} {rates[c][-1]:9.1f} images/s", flush=True)
+    for c in configs:
+        print(f"{c:16s} median {sorted(rates[c])[len(rates[c]) // 2]:9.1f} images/s  ({', '.join(f'{r:.0f}' for r in rates[c])})")
+        decs[c].close()
+    if os.environ.get("HI_PROBE", "1") == "0":
+        return
     # raw probes: pinned->device DMA of 285 MB in one copy, and a 16-thread memcpy into pinned memory
     nb = int(sum(len(d) for d in datas))
     pin = torch.empty(nb, dtype=torch.uint8).pin_memory()
