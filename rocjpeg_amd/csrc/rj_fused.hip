@@ -124,6 +124,18 @@ struct Nav {
 // <= 64 entries.  Entries are consumed row by row from the window; the ordinal of an entry's
 // block is the number of block starts at or before it, so rows need no alignment to blocks.
 // cbits: component of each block within the MCU (2 bits each), for the DC corrections.
+// Lane masks straight from v_cmp into an SGPR pair.  (A __ballot of an or of compares, or of a
+// bool that is also used per lane, is re-materialised by the compiler as v_cndmask + v_cmp per
+// row of the scatter.)  v_cmp writes 0 for inactive lanes, which is the ballot's meaning.
+// ballot(p == 0 || p == 127): block starts and the terminator
+__device__ __forceinline__ uint64_t mask_start(uint32_t p) {
+  uint64_t a, b;
+  asm volatile("v_cmp_eq_u32_e64 %0, 0, %2\n\tv_cmp_eq_u32_e64 %1, %3, %2\n\ts_or_b64 %0, %0, %1"
+               : "=&s"(a), "=&s"(b)
+               : "v"(p), "s"(127u));
+  return a;
+}
+
 // libjpeg HUFF_EXTEND of a raw entry (lean K1): the s extra bits as a signed value (s = 0 -> 0)
 __device__ __forceinline__ int raw_value(uint32_t e) {
   const uint32_t s = (e >> 16) & 15u, m = (1u << s) - 1u;  // v_bfm_b32
@@ -137,7 +149,7 @@ __device__ __forceinline__ int raw_value(uint32_t e) {
 // exact for 16-bit quantisers) x 32, the DC x 16 (raw DC differences stay as they are: restore_dc
 // finishes them).  A coefficient outside the dot2 IDCT's exact domain raises `bad` (the row goes
 // to the fix-up launch).  The entry's block in the strip supplies, through one ds_bpermute of the
-// owning lane's `lane_info` (block LDS base | component << 16), where the block lives and which
+// owning lane's `lane_info` (block LDS base | 4 x component << 16), where the block lives and which
 // component's quantisers apply; s_qw[3 p + c] = quantiser | pair-layout byte offset << 16.
 // !kPairs (the fix-up instances): raw coefficients in zigzag order, checked against the int32
 // IDCT's domain (thr, on the raw value) -- the layout idct_pass1_wide reads.
@@ -176,13 +188,16 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
       for (int r = 0; r < RJ_WIN_ROWS; r++) {
         const uint32_t e = win.w[r];
         // kRaw: zigzag position at [27:21] (64..78 on corrupt data = position 63), else [22:16]
-        uint32_t p = kRaw ? (e >> 21) & 127u : (e >> 16) & 127u;
-        if (kRaw) p = p == 127u ? p : min(p, 63u);
-        const bool st = p == 0 || p == 127;
-        const uint64_t m = __ballot(st);
-        const uint32_t below = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-        const uint32_t ord = seen + below + (st ? 1u : 0u) - 1u;
-        const uint32_t blk = done + ord;  // block index counted from the first dropped one
+        const uint32_t p_raw = kRaw ? (e >> 21) & 127u : (e >> 16) & 127u;
+        const uint32_t p = (kRaw && p_raw != 127u) ? min(p_raw, 63u) : p_raw;
+        const uint64_t m = mask_start(p_raw);  // block starts (and the terminator): p_raw 0 or 127
+        // ord = block starts at or before this lane, - 1: the count of m's bits 1..lane (mbcnt of
+        // m >> 1) plus bit 0, in scalar terms -- no per-lane copy of the start flag
+        const uint64_t m1 = m >> 1;
+        const uint32_t incl = __builtin_amdgcn_mbcnt_hi(uint32_t(m1 >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m1), 0u));
+        const uint32_t ord = incl + (seen + uint32_t(m & 1u) - 1u);
+        // the entry's block in the strip (negative: a dropped block)
+        const int32_t rel = int32_t(ord + (done - drop));
         bool oob = false;
         // a split interval's tail piece may end early (its lane stopped at libjpeg's
         // insufficient-data point): the piece's remaining blocks are zero blocks, and nothing
@@ -190,13 +205,16 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
         const uint64_t term = (kRaw && kSplit) ? __ballot(p == 127 && ord < piece) : 0ull;
         const int tl = term ? __ffsll((long long)term) - 1 : 64;
         // the entry's block in the strip, and from its lane: LDS base, quantiser row (whole wave)
-        const uint32_t info = kPairs ? uint32_t(__builtin_amdgcn_ds_bpermute(int(((blk - drop) & 63u) << 2), int(lane_info))) : 0u;
-        if (!pass && ord < piece && p < 64u && blk >= drop && int(lane) < tl) {
+        // (ds_bpermute takes the source lane from address bits [7:2]: rel mod 64, no masking)
+        const uint32_t info = kPairs ? uint32_t(__builtin_amdgcn_ds_bpermute(rel << 2, int(lane_info))) : 0u;
+        if (!pass && ord < piece && p < 64u && rel >= 0 && int(lane) < tl) {
           int v = kRaw ? raw_value(e) : int(int16_t(e & 0xFFFFu));
           if constexpr (kPairs) {
-            const uint32_t qe = s_qw[3u * p + (info >> 16)];  // component-interleaved: (a/4) mod 32 banks
+            // component-interleaved s_qw[3 p + c]: (a/4) mod 32 banks; info >> 16 = 4 c (bytes)
+            const uint32_t qe = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(s_qw) +
+                                                                    __umul24(p, 12u) + (info >> 16));
             if (!kRaw && fix_dc && p == 0) {
-              const uint32_t cc = info >> 16;
+              const uint32_t cc = info >> 18;
               v += cc == 0 ? nv.dcd[0] : (cc == 1 ? nv.dcd[1] : nv.dcd[2]);
             }
             const int x = __mul24(v, int(qe & 0xFFFFu));  // |v| < 2^16, q < 2^16: exact
@@ -215,13 +233,13 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
           } else {
             if (kRaw && (e & RJ_RE_ZERO)) v = -32768;  // zero block: marked for the DC restore
             if (!kRaw && fix_dc && p == 0) {
-              const uint32_t bi = (blk - drop) % nblk;  // strips start at an MCU boundary
+              const uint32_t bi = uint32_t(rel) % nblk;  // strips start at an MCU boundary
               const uint32_t cc = (cbits >> (2 * bi)) & 3u;
               v += cc == 0 ? nv.dcd[0] : (cc == 1 ? nv.dcd[1] : nv.dcd[2]);
             }
             // outside the int32 IDCT's exact domain (raw DC: a difference, checked by restore_dc)
             oob = (!kRaw || p != 0) && int16_t(v) != -32768 && abs(int(int16_t(v))) > thr;
-            *reinterpret_cast<int16_t *>(s_buf + __umul24(blk - drop, uint32_t(RJ_BLK_STRIDE)) + p * 2) = int16_t(v);
+            *reinterpret_cast<int16_t *>(s_buf + __umul24(uint32_t(rel), uint32_t(RJ_BLK_STRIDE)) + p * 2) = int16_t(v);
           }
         }
         bad = bad || __ballot(oob) != 0;
@@ -233,7 +251,7 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
           found = true;
           break;
         }
-        const uint64_t hit = __ballot(st && ord == piece);  // start of the first block past the piece
+        const uint64_t hit = __ballot(ord == piece) & m;  // start of the first block past the piece
         seen += __popcll(m);
         if (hit) {
           nv.set_cur((uint64_t(win.base_hi) << 32 | win.base_lo) + uint32_t(r) * 64u +
@@ -538,9 +556,9 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
     for (uint32_t k = tid; k < ncomp * 64; k += 64) s_q[k >> 6][k & 63] = ts->qz[im.comp_tq[k >> 6] & 3][k & 63];
   }
 
-  // this lane's block: LDS base | its component << 16 (parse_blocks' bpermute source),
+  // this lane's block: LDS base | its component x 4 << 16 (parse_blocks' bpermute source),
   // and its DC quantiser (restore_dc)
-  const uint32_t lane_info = tid * RJ_BLK_STRIDE | (lane_blk >> 12) << 16;
+  const uint32_t lane_info = tid * RJ_BLK_STRIDE | (lane_blk >> 12) << 18;
   __syncthreads();  // s_qw / s_q written
   const uint32_t q0 = kPairs ? s_qw[lane_blk >> 12] & 0xFFFFu : 0u;
   const uint32_t mcux = U(im.mcux);

@@ -202,7 +202,7 @@ __device__ __forceinline__ void idct_islow_block(int32_t (&v)[64], uint32_t (&o)
 // butterfly above only multiplies by constants and adds), t[r] = sum_k A[r][k] x[k] with
 //   A[r][k] = 8192 (k = 0), and +-{11363, 10703, 9633, 8192, 6437, 4433, 2260} -- all int16,
 // and t[r] / t[7-r] share the even part (x0, x2, x4, x6) and negate the odd part.  So a pass is
-// 12 dot2 + 12 add/sub on packed input pairs instead of 12 multiplies + ~26 adds on int32, with
+// 14 dot2 + 8 add/sub on packed input pairs instead of 12 multiplies + ~26 adds on int32, with
 // the inputs in registers at half the width.  Pair layout of a block (32 dwords, built by
 // K2's entry scatter straight into LDS, see rj_pair_slot): dword 4c + j of column c holds
 //   j = 0: (x0, x4), 1: (x2, x6), 2: (x1, x3), 3: (x5, x7)   (low half, high half)
@@ -242,8 +242,10 @@ __host__ __device__ constexpr uint32_t rj_pair_slot(uint32_t k, uint32_t c) {
 __device__ __forceinline__ void islow_dot2_1d(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3, uint32_t ke0,
                                               uint32_t ke1, int32_t rnd, int32_t t[8]) {
   const int32_t e0 = dot2(p0, ke0, rnd), e1 = dot2(p0, ke1, rnd);
-  const int32_t tmp3 = dot2z(p1, RJ_PK(10703, 4433)), tmp2 = dot2z(p1, RJ_PK(4433, -10704));
-  const int32_t t10 = e0 + tmp3, t13 = e0 - tmp3, t11 = e1 + tmp2, t12 = e1 - tmp2;
+  // the even butterfly folded into the accumulators: t10 / t13 = e0 +- tmp3, t11 / t12 = e1 +- tmp2
+  // with tmp3 = (10703, 4433) . p1, tmp2 = (4433, -10704) . p1 (the negated pairs for the minus)
+  const int32_t t10 = dot2(p1, RJ_PK(10703, 4433), e0), t13 = dot2(p1, RJ_PK(-10703, -4433), e0);
+  const int32_t t11 = dot2(p1, RJ_PK(4433, -10704), e1), t12 = dot2(p1, RJ_PK(-4433, 10704), e1);
   const int32_t o0 = dot2(p3, RJ_PK(6437, 2260), dot2z(p2, RJ_PK(11363, 9633)));
   const int32_t o1 = dot2(p3, RJ_PK(-11362, -6436), dot2z(p2, RJ_PK(9633, -2259)));
   const int32_t o2 = dot2(p3, RJ_PK(2261, 9633), dot2z(p2, RJ_PK(6437, -11362)));
