@@ -1610,7 +1610,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
     if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
     wide(fused_rows, wcnt, wlist, false, false);
+#ifndef RJ_EXP_SKIP_K2  // timing build: K0 + K1 only (the output is not written)
     RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr, wcnt, wlist));
+#endif
     wide(general_rows, wcnt, wlist, true, false);
     RJ_HIP(LaunchRows(stream_, true, d_imgs, n, d_grows, nullptr, general_rows, cbuf, d_tabs,
                       d_planes_.as<uint8_t>(), wcnt, wlist));

@@ -70,10 +70,17 @@ __device__ __forceinline__ void hl_put(const HCol<S> &ring, uint32_t slot, const
 // the group of G staged entries [from, from + G) (from a multiple of G; the stage holds 2G) to HBM
 template <int S, int G>
 __device__ __forceinline__ void hl_flush(const HCol<S> &stage, uint32_t from, uint32_t *dst) {
+#ifdef RJ_EXP_NOENT  // timing build (with RJ_EXP_SKIP_K2): K1 writes no entries -- its time without the intermediate
+  return;
+#endif
   uint32_t w[G];
   const uint32_t s0 = from & (2 * G - 1);
 #pragma unroll
   for (int q = 0; q < G; q++) w[q] = stage[s0 + q];
+#ifdef RJ_EXP_NOSTORE  // timing build: the stage is read, nothing is stored
+  if (w[0] == 0x12345678u && w[G - 1] == 0x9ABCDEF0u) *gp(dst) = w[1];
+  return;
+#endif
   uint4 *d4 = reinterpret_cast<uint4 *>(dst);
 #pragma unroll
   for (int q = 0; q < G / 4; q++) gp(d4)[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
