@@ -639,6 +639,28 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane) {
   return uint32_t(__builtin_amdgcn_readlane(int(v), int(lane)));
 }
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return uint32_t(__builtin_amdgcn_readfirstlane(int(v))); }
+// lane `lane` of three 64-bit per-lane values set to the wave-uniform a, b, c (v_writelane: one
+// instruction per word, no per-lane compare and selects; the lane select goes through M0 -- two
+// SGPR operands would exceed the constant bus -- and the s_nop covers its SALU write)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0: reserved, but nothing else in these kernels uses it
+__device__ __forceinline__ void wl64x3(uint64_t &ra, uint64_t &rb, uint64_t &rc, uint64_t a, uint64_t b, uint64_t c,
+                                       uint32_t lane) {
+  uint32_t a0 = uint32_t(ra), a1 = uint32_t(ra >> 32), b0 = uint32_t(rb), b1 = uint32_t(rb >> 32);
+  uint32_t c0 = uint32_t(rc), c1 = uint32_t(rc >> 32);
+  asm volatile(
+      "s_mov_b32 m0, %12\n\ts_nop 3\n\tv_writelane_b32 %0, %6, m0\n\tv_writelane_b32 %1, %7, m0\n\t"
+      "v_writelane_b32 %2, %8, m0\n\tv_writelane_b32 %3, %9, m0\n\tv_writelane_b32 %4, %10, m0\n\t"
+      "v_writelane_b32 %5, %11, m0"
+      : "+v"(a0), "+v"(a1), "+v"(b0), "+v"(b1), "+v"(c0), "+v"(c1)
+      : "s"(uint32_t(a)), "s"(uint32_t(a >> 32)), "s"(uint32_t(b)), "s"(uint32_t(b >> 32)), "s"(uint32_t(c)),
+        "s"(uint32_t(c >> 32)), "s"(lane)
+      : "m0");
+  ra = (uint64_t(a1) << 32) | a0;
+  rb = (uint64_t(b1) << 32) | b0;
+  rc = (uint64_t(c1) << 32) | c0;
+}
+#pragma clang diagnostic pop
 
 __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__ imgs, int nimg,
                                                   const uint32_t *__restrict__ ivals, const uint8_t *__restrict__ destuffed,
@@ -1027,46 +1049,55 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
             newv = (info >> 11) & 3u;
             // the (r+1)-th zero-history position at or after k, lane-parallel: lane l is it when
             // bit l of the candidate mask is set with exactly r candidates below it
+            __builtin_assume(k < 64u);
             const uint64_t zm = ~nzm & band & (~0ull << k);
             const uint32_t below =
                 __builtin_amdgcn_mbcnt_hi(uint32_t(zm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(zm), 0u));
-            const uint64_t hit = __ballot(((zm >> lane) & 1u) && below == r);
+            // the lanes with exactly r candidates below them, masked by the candidates on the
+            // SALU (a ballot of the compare alone: no per-lane bit test)
+            const uint64_t hit = __ballot(below == r) & zm;
             t = hit ? ctz64(hit) : se + 1;
-            pend = uint32_t(__popcll(nzm & lomask(t) & (~0ull << k)));
+            // [k, t) lies in the band: r of its positions have zero history (every candidate when
+            // nothing hit), the others take one correction bit each
+            pend = (t - k) - min(r, uint32_t(__popcll(zm)));
             eobblk = false;
           } else {  // EOBr
-            eobrun = info >> 13;
+            eobrun = rfl(info >> 13);
             t = se + 1;
             newv = 0;
             eobblk = true;
-            pend = uint32_t(__popcll(nzm & ~lomask(k)));
+            __builtin_assume(k < 64u);
+            pend = uint32_t(__popcll(nzm & (~0ull << k)));
           }
         } else {  // a block inside an EOB run
           cbits = rl(pk_l, d);
           t = se + 1;
           newv = 0;
           eobblk = true;
-          pend = uint32_t(__popcll(nzm & ~lomask(k)));
+          __builtin_assume(k < 64u);
+          pend = uint32_t(__popcll(nzm & (~0ull << k)));
         }
         walking = true;
       } else {
         cbits = rl(pk_l, d);
       }
       const uint32_t take = min(pend, 32u - used);
-      cstr = (cstr << take) | pbits(cbits, 0, take);
+      // the top `take` bits of cbits (none for take = 0): the high word of a 64-bit shift
+      cstr = (cstr << take) | uint32_t((uint64_t(cbits) << take) >> 32);
       used += take;
       pend -= take;
       pos += used;
       if (pend) continue;  // the walk resumes at the next peek
       walking = false;
-      if (newv && min(t, 63u) <= se) {  // past Se (corrupt data): dropped, as in lane_ac_refine
-        const uint64_t bq = 1ull << min(t, 63u);
+      if (newv && t <= se) {  // past Se (corrupt data): dropped, as in lane_ac_refine
+        __builtin_assume(t < 64u);
+        const uint64_t bq = 1ull << t;
         newm |= bq;
-        if (newv == 2) sgn |= bq;
+        sgn |= newv == 2 ? bq : 0ull;
       }
       bool blk_done;
       if (eobblk) {
-        eobrun--;
+        eobrun = rfl(eobrun - 1u);
         blk_done = true;
       } else {
         k = t + 1;
@@ -1075,11 +1106,8 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
       if (!blk_done) continue;
       // ---- block end: its record into lane (u - rbase); 64 records leave together ----
       const uint32_t rb = u - rbase;
-      if (lane == rb) {
-        r_cs = cstr;
-        r_sg = sgn;
-        r_nw = newm;
-      }
+      // into lane rb by v_writelane (one instruction per word, no per-lane compare and selects)
+      wl64x3(r_cs, r_sg, r_nw, cstr, sgn, newm, rb);
       cstr = sgn = newm = 0;
       k = ss;
       u++;
