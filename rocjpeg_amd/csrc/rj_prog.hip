@@ -1039,13 +1039,13 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
       const uint32_t d = pos - pos0;
       stamp.nstep++;
       uint32_t used = 0, cbits;
-      if (!walking) {
-        if (eobrun == 0) {
+      if (__builtin_expect(!walking, 1)) {  // (hints: the common symbol falls through)
+        if (__builtin_expect(eobrun == 0, 1)) {
           const uint32_t info = rl(info_l, d);
           cbits = rl(ck_l, d);
           const uint32_t r = (info >> 6) & 15u;
           used = info & 63u;
-          if (!(info & (1u << 10))) {
+          if (__builtin_expect(!(info & (1u << 10)), 1)) {
             newv = (info >> 11) & 3u;
             // the (r+1)-th zero-history position at or after k, lane-parallel: lane l is it when
             // bit l of the candidate mask is set with exactly r candidates below it
@@ -1087,7 +1087,7 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
       used += take;
       pend -= take;
       pos += used;
-      if (pend) continue;  // the walk resumes at the next peek
+      if (__builtin_expect(pend != 0, 0)) continue;  // the walk resumes at the next peek
       walking = false;
       if (newv && t <= se) {  // past Se (corrupt data): dropped, as in lane_ac_refine
         __builtin_assume(t < 64u);
@@ -1096,14 +1096,14 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
         sgn |= newv == 2 ? bq : 0ull;
       }
       bool blk_done;
-      if (eobblk) {
+      if (__builtin_expect(eobblk, 0)) {
         eobrun = rfl(eobrun - 1u);
         blk_done = true;
       } else {
         k = t + 1;
         blk_done = k > se;
       }
-      if (!blk_done) continue;
+      if (__builtin_expect(!blk_done, 1)) continue;
       // ---- block end: its record into lane (u - rbase); 64 records leave together ----
       const uint32_t rb = u - rbase;
       // into lane rb by v_writelane (one instruction per word, no per-lane compare and selects)
