@@ -77,6 +77,17 @@ __device__ __forceinline__ void hl_flush(const HCol<S> &stage, uint32_t from, ui
   const uint32_t s0 = from & (2 * G - 1);
 #pragma unroll
   for (int q = 0; q < G; q++) w[q] = stage[s0 + q];
+#ifdef RJ_EXP_HALFSTORE  // timing build: the entries' low halves packed in pairs (half the store bytes)
+  {
+    uint32_t h[G / 2];
+#pragma unroll
+    for (int q = 0; q < G / 2; q++) h[q] = __builtin_amdgcn_perm(w[2 * q + 1], w[2 * q], 0x05040100u);
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+#pragma unroll
+    for (int q = 0; q < G / 8; q++) gp(d4)[q] = make_uint4(h[4 * q], h[4 * q + 1], h[4 * q + 2], h[4 * q + 3]);
+    return;
+  }
+#endif
 #ifdef RJ_EXP_NOSTORE  // timing build: the stage is read, nothing is stored
   if (w[0] == 0x12345678u && w[G - 1] == 0x9ABCDEF0u) *gp(dst) = w[1];
   return;
