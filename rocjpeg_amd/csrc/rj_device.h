@@ -221,13 +221,13 @@ struct RjLeanTables {  // LDS image: AC0, AC1 (first level + subtables), DC0, DC
   uint32_t ac[2][RJ_HL_AC_WORDS];
   uint32_t dc[2][RJ_HL_DC_WORDS];
 };
-// Raw entry (lean K1 -> K2): [15:0] the symbol's code and extra bits, right-aligned (its low s
-// bits are the extra bits), [19:16] s, [27:21] zigzag position
-// (0 = the block's DC, which holds the DC *difference*; 64..78 only on corrupt data: position 63;
-// 127 = end of stream), bit 28: zero block (libjpeg's insufficient-data / missing-marker blocks:
-// every coefficient 0, DC absolute).
-#define RJ_RE_TERM (127u << 21)
-#define RJ_RE_ZERO ((1u << 28))
+// Lean entry (lean K1 -> K2): [15:0] the coefficient as int16 (libjpeg HUFF_EXTEND of the
+// symbol's s extra bits, done by K1 off its bit-position chain; for position 0 the DC
+// *difference*), [22:16] zigzag position (corrupt runs past 63 clamped to 63, as libjpeg's
+// natural-order table does; 127 = end of stream), bit 23: zero block (libjpeg's
+// insufficient-data / missing-marker blocks: every coefficient 0, DC absolute).
+#define RJ_RE_TERM (127u << 16)
+#define RJ_RE_ZERO ((1u << 23))
 
 // Output jobs of the general (two-stage) path: one per written channel.
 enum RjJobKind : uint32_t {

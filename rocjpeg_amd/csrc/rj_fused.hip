@@ -136,13 +136,6 @@ __device__ __forceinline__ uint64_t mask_start(uint32_t p) {
   return a;
 }
 
-// libjpeg HUFF_EXTEND of a raw entry (lean K1): the s extra bits as a signed value (s = 0 -> 0)
-__device__ __forceinline__ int raw_value(uint32_t e) {
-  const uint32_t s = (e >> 16) & 15u, m = (1u << s) - 1u;  // v_bfm_b32
-  const uint32_t raw = e & m;                               // K1 keeps the code bits above
-  const uint32_t d = m - raw;                               // top bit clear (negative) <=> raw <= d
-  return raw > d ? int(raw) : int(raw) - int(m);
-}
 
 // kPairs (the main K2 instances): each coefficient is dequantised here and stored scaled into
 // its block's pair layout (rj_math.h idct_dot2_block): entry value x quantiser (i24 multiply,
@@ -187,9 +180,9 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
 #pragma unroll
       for (int r = 0; r < RJ_WIN_ROWS; r++) {
         const uint32_t e = win.w[r];
-        // kRaw: zigzag position at [27:21] (64..78 on corrupt data = position 63), else [22:16]
-        const uint32_t p_raw = kRaw ? (e >> 21) & 127u : (e >> 16) & 127u;
-        const uint32_t p = (kRaw && p_raw != 127u) ? min(p_raw, 63u) : p_raw;
+        // zigzag position at [22:16] (127: end of stream; lean K1 clamps corrupt runs to 63)
+        const uint32_t p_raw = (e >> 16) & 127u;
+        const uint32_t p = p_raw;
         const uint64_t m = mask_start(p_raw);  // block starts (and the terminator): p_raw 0 or 127
         // ord = block starts at or before this lane, - 1: the count of m's bits 1..lane (mbcnt of
         // m >> 1) plus bit 0, in scalar terms -- no per-lane copy of the start flag
@@ -208,7 +201,7 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
         // (ds_bpermute takes the source lane from address bits [7:2]: rel mod 64, no masking)
         const uint32_t info = kPairs ? uint32_t(__builtin_amdgcn_ds_bpermute(rel << 2, int(lane_info))) : 0u;
         if (!pass && ord < piece && p < 64u && rel >= 0 && int(lane) < tl) {
-          int v = kRaw ? raw_value(e) : int(int16_t(e & 0xFFFFu));
+          int v = int(int16_t(e & 0xFFFFu));  // lean entries: K1 applied HUFF_EXTEND
           if constexpr (kPairs) {
             // component-interleaved s_qw[3 p + c]: (a/4) mod 32 banks; info >> 16 = 4 c (bytes)
             const uint32_t qe = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(s_qw) +

@@ -162,10 +162,14 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
     const uint32_t en = s_lut[(tbn >> 2) + (peekn >> tshn)];                                              \
     wc = ring[rr & (RJ_HL_WORDS - 1)];                                                                    \
     /* ---- this symbol's entry, while the lookup is in flight ---- */                                  \
-    /* the symbol's n bits right-aligned (code, then its s extra bits: K2 keeps the low s) */           \
+    /* the coefficient: HUFF_EXTEND of the s extra bits (the low s of the symbol's n bits,          \
+       right-aligned), and its position kcur + R clamped to 63 (libjpeg's natural-order table) */   \
     const uint32_t raw = peek >> (e & 31u);                                                               \
-    uint32_t entry = __builtin_amdgcn_perm(e, raw, 0x07060100u); /* raw's low half, e's fields above */ \
-    entry += kcur << 21;                                                                                  \
+    const uint32_t xm = (1u << ((e >> 16) & 15u)) - 1u; /* v_bfm */                                      \
+    const uint32_t xb = raw & xm;                                                                         \
+    const uint32_t xv = xb > xm - xb ? xb : xb - xm; /* top extra bit clear: negative */               \
+    const uint32_t xp = min(kcur + ((e >> 21) & 127u), 63u);                                              \
+    uint32_t entry = __builtin_amdgcn_perm(xp, xv, 0x05040100u); /* value's low half | position << 16 */ \
     uint32_t emit = (e >> 13) & 1u;                                                                       \
     if (SAFE) {                                                                                           \
       entry = skip ? RJ_RE_ZERO : entry; /* libjpeg: the rest of the interval is zero blocks */          \
