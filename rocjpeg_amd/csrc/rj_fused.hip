@@ -490,6 +490,35 @@ __device__ __forceinline__ void rgb_strip_420_full(const uint8_t *ty, const uint
 //   kWide = true   : the fix-up pass (k_rows_fix): strips with coefficients outside the int32
 //                    IDCT's exact domain take the 64-bit IDCT.  Otherwise such a row is appended
 //                    to wide_list (as (image, row); wide_cnt counts) for the fix-up launch.
+// The descriptor's byte fields (ncomp .. comp_blk0, bytes [16, 80) of RjImageDev) as 16 dwords.
+// Read by wave-uniform dword loads (s_load), so a field is an SALU bit-field extract and a per-lane
+// index a select of three words: byte fields read one by one go through the vector memory path,
+// each waiting on the one before (the block's component picks its sampling factors), which put
+// ~10 dependent memory round trips in front of every row.
+struct ImBytes {
+  static constexpr uint32_t kBase = 16, kWords = 16;
+  uint32_t w[kWords];
+  __device__ __forceinline__ explicit ImBytes(const RjImageDev &im) {
+    static_assert(offsetof(RjImageDev, ncomp) == kBase && offsetof(RjImageDev, tabset) == kBase + 4 * kWords,
+                  "RjImageDev byte fields moved");
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(&im) + kBase);
+#pragma unroll
+    for (uint32_t k = 0; k < kWords; k++) w[k] = p[k];
+  }
+  // field at a compile-time byte offset
+  __device__ __forceinline__ uint32_t at(uint32_t off) const {
+    off -= kBase;
+    return (w[off >> 2] >> ((off & 3u) * 8u)) & 255u;
+  }
+  // element `idx` (per lane, < 10) of the byte array at offset `arr`
+  __device__ __forceinline__ uint32_t lane_at(uint32_t arr, uint32_t idx) const {
+    const uint32_t o = arr - kBase + idx, w0 = (arr - kBase) >> 2, q = (o >> 2) - w0;
+    const uint32_t wd = q == 0 ? w[w0] : (q == 1 ? w[w0 + 1] : w[w0 + 2]);
+    return (wd >> ((o & 3u) * 8u)) & 255u;
+  }
+};
+#define RJ_OFF(f) uint32_t(offsetof(RjImageDev, f))
+
 template <bool kPlanes, bool kDense, bool kWide = false, bool kSplit = false>
 __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, int i, uint32_t my, RjCoefBuf coefs,
                                          const RjTableSet *__restrict__ tabsets, uint8_t *__restrict__ planes,
@@ -501,12 +530,13 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
   RJ_STAMP(t_start);
   const uint32_t tid = threadIdx.x;
   const RjImageDev &im = imgs[i];
-  const uint32_t hmax = U(im.hmax), vmax = U(im.vmax);
+  const ImBytes ib(im);
+  const uint32_t hmax = ib.at(RJ_OFF(hmax)), vmax = ib.at(RJ_OFF(vmax));
   const uint32_t mcu_w = 8 * hmax, mcu_h = 8 * vmax;
-  const uint32_t nblk = U(im.nblk_mcu);
+  const uint32_t nblk = ib.at(RJ_OFF(nblk_mcu));
   const uint32_t S = U(rj_fused_strip_mcus(hmax, nblk));  // MCUs per strip
-  const bool inter = U(im.interleaved) != 0;
-  const uint32_t ncomp = inter ? U(im.ncomp) : 1;
+  const bool inter = ib.at(RJ_OFF(interleaved)) != 0;
+  const uint32_t ncomp = inter ? ib.at(RJ_OFF(ncomp)) : 1;
 
   // tile geometry (component c: width S*hc*8, height vc*8), all offsets multiples of 8
   uint32_t tw[3], toff[3];
@@ -515,7 +545,8 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
 #pragma unroll
     for (int c = 0; c < 3; c++) {
       const bool has = c < int(ncomp);
-      const uint32_t hc = (inter && has) ? im.comp_h[c] : 1, vc = (inter && has) ? im.comp_v[c] : 1;
+      const uint32_t hc = (inter && has) ? ib.at(RJ_OFF(comp_h) + c) : 1;
+      const uint32_t vc = (inter && has) ? ib.at(RJ_OFF(comp_v) + c) : 1;
       tw[c] = U(S * hc * 8);
       toff[c] = U(off);
       off += has ? tw[c] * vc * 8 : 0;
@@ -526,9 +557,10 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
   uint32_t lane_blk;  // bx | by << 8 | c << 12
   {
     const uint32_t mcu_l = tid / nblk, b_l = tid - mcu_l * nblk;
-    const uint32_t c = inter ? im.blk_comp[b_l] : 0;
-    const uint32_t bx = mcu_l * (inter ? im.comp_h[c] : 1) + (inter ? im.blk_dx[b_l] : 0);
-    const uint32_t by = inter ? im.blk_dy[b_l] : 0;
+    const uint32_t c = inter ? ib.lane_at(RJ_OFF(blk_comp), b_l) : 0;
+    const uint32_t hc = (ib.w[(RJ_OFF(comp_h) - ImBytes::kBase) >> 2] >> (8u * c)) & 255u;
+    const uint32_t bx = mcu_l * (inter ? hc : 1) + (inter ? ib.lane_at(RJ_OFF(blk_dx), b_l) : 0);
+    const uint32_t by = inter ? ib.lane_at(RJ_OFF(blk_dy), b_l) : 0;
     lane_blk = (bx & 255u) | (by << 8) | (c << 12);
   }
 
@@ -541,12 +573,21 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
                                    12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
                                    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                                    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
-    for (uint32_t k = tid; k < ncomp * 64; k += 64) {
-      const uint32_t nat = kNatZ[k & 63];
-      s_qw[3u * (k & 63u) + (k >> 6)] = uint32_t(ts->qz[im.comp_tq[k >> 6] & 3][k & 63]) | rj_pair_slot(nat >> 3, nat & 7) << 16;
-    }
+    const uint32_t nat = kNatZ[tid];
+    const uint32_t slot = rj_pair_slot(nat >> 3, nat & 7) << 16;
+    uint32_t q[3];  // loaded unconditionally (the table index is masked): one memory round trip
+#pragma unroll
+    for (uint32_t c = 0; c < 3; c++) q[c] = ts->qz[ib.at(RJ_OFF(comp_tq) + c) & 3][tid];
+#pragma unroll
+    for (uint32_t c = 0; c < 3; c++)
+      if (c < ncomp) s_qw[3u * tid + c] = q[c] | slot;
   } else {
-    for (uint32_t k = tid; k < ncomp * 64; k += 64) s_q[k >> 6][k & 63] = ts->qz[im.comp_tq[k >> 6] & 3][k & 63];
+    uint32_t q[3];
+#pragma unroll
+    for (uint32_t c = 0; c < 3; c++) q[c] = ts->qz[ib.at(RJ_OFF(comp_tq) + c) & 3][tid];
+#pragma unroll
+    for (uint32_t c = 0; c < 3; c++)
+      if (c < ncomp) s_q[c][tid] = uint16_t(q[c]);
   }
 
   // this lane's block: LDS base | its component x 4 << 16 (parse_blocks' bpermute source),
@@ -563,8 +604,9 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
   const uint32_t strips_x = (mcux + S - 1) / S;
   const uint32_t *ent = coefs.ent;
   uint32_t cbits = 0;  // component of each block within the MCU
-  for (uint32_t b = 0; b < nblk; b++) cbits |= (inter ? uint32_t(im.blk_comp[b] & 3) : 0u) << (2 * b);
-  cbits = U(cbits);
+#pragma unroll
+  for (uint32_t b = 0; b < RJ_MAX_BLK_MCU; b++)
+    if (b < nblk && inter) cbits |= (ib.at(RJ_OFF(blk_comp) + b) & 3u) << (2 * b);
   // the row's first block: its interval, the piece holding it, blocks to skip inside the piece
   Nav nv;
   uint32_t drop = 0;
@@ -598,9 +640,9 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
   uint8_t *const dst0 = im.dst[0], *const dst1 = im.dst[1], *const dst2 = im.dst[2];
   const uint32_t pitch0 = U(im.dst_pitch[0]), pitch1 = U(im.dst_pitch[1]);
   const uint32_t W = U(im.width), H = U(im.height);
-  const uint32_t fmt = U(im.fmt);
-  const uint32_t hs1 = U((ncomp == 3) ? (hmax / im.comp_h[1] == 2 ? 1u : 0u) : 0u);
-  const uint32_t vs1 = U((ncomp == 3) ? (vmax / im.comp_v[1] == 2 ? 1u : 0u) : 0u);
+  const uint32_t fmt = ib.at(RJ_OFF(fmt));
+  const uint32_t hs1 = (ncomp == 3) ? (hmax / ib.at(RJ_OFF(comp_h) + 1) == 2 ? 1u : 0u) : 0u;
+  const uint32_t vs1 = (ncomp == 3) ? (vmax / ib.at(RJ_OFF(comp_v) + 1) == 2 ? 1u : 0u) : 0u;
   const bool al_y = ((reinterpret_cast<uintptr_t>(dst0) | pitch0) & 3) == 0;
   const bool al_rgbp = ((reinterpret_cast<uintptr_t>(dst0) | reinterpret_cast<uintptr_t>(dst1) |
                          reinterpret_cast<uintptr_t>(dst2) | pitch0) & 3) == 0;
