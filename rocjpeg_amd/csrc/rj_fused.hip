@@ -92,6 +92,15 @@ struct EntWin {
 #pragma unroll
     for (int r = 0; r < RJ_WIN_ROWS; r++) w[r] = gp(p)[r * 64u + lane];
   }
+  // wait here for the window's loads.  vmcnt is in order on gfx9: a wait for a window row issued
+  // after the previous strip's pixel stores waits for those stores too.  parse_blocks' walk over a
+  // window has no waits when every path into it settled the window first: after each load inside
+  // parse_blocks and the row's first, and in row_body after the IDCT for the next strip's window
+  // (loaded at the end of phase A, waited before phase C's stores).
+  __device__ __forceinline__ void settle() {
+#pragma unroll
+    for (int r = 0; r < RJ_WIN_ROWS; r++) asm volatile("" : "+v"(w[r]));
+  }
 };
 
 // Position in the image's entry streams: the next block's DC entry inside the current piece
@@ -157,26 +166,30 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
   for (uint32_t moves = 0; done < need && moves < (1u << 16); moves++) {  // bounded on corrupt pieces
     if (nv.bleft == 0) {  // next piece, or the first piece of the next interval (synchronous reload)
       if (nv.seg >= im.nseg) break;
-      const RjPiece *pb = coefs.piece + rj_seg_lane0_k<kSplit>(coefs, im.seg_prefix + nv.seg);
-      if (nv.pj + 1 < gp(pb)->npieces) {
+      // U(): the slot load completes here, on every path (a load left in flight into the merge
+      // below made the waitcnt pass put a vmcnt(0) in the scatter's window loop, which then also
+      // waited for the previous strip's pixel stores)
+      const RjPiece *pb = coefs.piece + U(rj_seg_lane0_k<kSplit>(coefs, im.seg_prefix + nv.seg));
+      if (nv.pj + 1 < U(gp(pb)->npieces)) {
         nv.pj++;
       } else {
         nv.seg++;
         nv.pj = 0;
         if (nv.seg >= im.nseg) break;
-        pb = coefs.piece + rj_seg_lane0_k<kSplit>(coefs, im.seg_prefix + nv.seg);
+        pb = coefs.piece + U(rj_seg_lane0_k<kSplit>(coefs, im.seg_prefix + nv.seg));
       }
       nv.take(pb + nv.pj);
       if (kRaw && kSplit && nv.pj > 0) nv.skip = U(gp(pb + nv.pj)->npieces);  // a split interval's tail
       win.load(ent, nv.cur(), lane);
+      win.settle();
     }
     // a split tail's piece starts after `skip` blocks of its stream: pass over them first
     const bool pass = kSplit && nv.skip != 0;
     const uint32_t piece = pass ? nv.skip : min(need - done, nv.bleft);  // blocks taken from this piece
     const bool fix_dc = !kRaw && (nv.dcd[0] | nv.dcd[1] | nv.dcd[2]) != 0;
     uint32_t seen = 0;                                  // block starts before the current row
-    bool found = false;
-    for (uint32_t guard = 0; !found && guard < (1u << 20); guard++) {  // bounded even on a corrupt stream
+    // one pass over the window in registers; true when the piece ends inside it
+    auto walk = [&]() __attribute__((always_inline)) -> bool {
 #pragma unroll
       for (int r = 0; r < RJ_WIN_ROWS; r++) {
         const uint32_t e = win.w[r];
@@ -241,23 +254,30 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
           for (uint32_t z = t_ord + lane; z < piece; z += 64)
             if (done + z >= drop) *reinterpret_cast<int16_t *>(s_buf + (done + z - drop) * RJ_BLK_STRIDE) = int16_t(-32768);
           nv.set_cur((uint64_t(win.base_hi) << 32 | win.base_lo) + uint32_t(r) * 64u + uint32_t(tl));
-          found = true;
-          break;
+          return true;
         }
         const uint64_t hit = __ballot(ord == piece) & m;  // start of the first block past the piece
         seen += __popcll(m);
         if (hit) {
           nv.set_cur((uint64_t(win.base_hi) << 32 | win.base_lo) + uint32_t(r) * 64u +
                      uint32_t(__ffsll((long long)hit) - 1));
-          found = true;
-          break;
+          return true;
         }
       }
-      if (!found) win.load(ent, (uint64_t(win.base_hi) << 32 | win.base_lo) + RJ_WIN_ROWS * 64u, lane);
+      return false;
+    };
+    bool found = false;
+    for (uint32_t guard = 0; !found && guard < (1u << 20); guard++) {  // bounded even on a corrupt stream
+      if (guard) {  // the next window, settled: walk() then has no waits on any path (see EntWin::settle)
+        win.load(ent, (uint64_t(win.base_hi) << 32 | win.base_lo) + RJ_WIN_ROWS * 64u, lane);
+        win.settle();
+      }
+      found = walk();
     }
     if (pass) {
       nv.skip = 0;
       win.load(ent, nv.cur(), lane);  // the piece proper starts mid-window
+      win.settle();
     } else {
       done += piece;
       nv.bleft -= piece;
@@ -633,6 +653,7 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
       drop = U(rel - gp(pb + pj)->first_blk);
     }
     win.load(ent, nv.cur(), tid);
+    win.settle();
   }
 
   // output descriptor, read once before the strip loop (the output stores could otherwise
@@ -706,6 +727,7 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
       row_wide = row_wide || wide;
       if constexpr (!kPlanes) __syncthreads();  // every block is in registers: the staging area becomes the sample tiles
       if (has_blk) idct_dot2_block(w, o);
+      if constexpr (!kDense) win.settle();  // the next strip's window, before this strip's pixel stores
     } else {
       int32_t v[64];
       const int16_t *zz = reinterpret_cast<const int16_t *>(s_buf + tid * RJ_BLK_STRIDE);
