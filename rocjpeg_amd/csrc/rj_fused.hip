@@ -212,7 +212,7 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
         const int tl = term ? __ffsll((long long)term) - 1 : 64;
         // the entry's block in the strip, and from its lane: LDS base, quantiser row (whole wave)
         // (ds_bpermute takes the source lane from address bits [7:2]: rel mod 64, no masking)
-        const uint32_t info = kPairs ? uint32_t(__builtin_amdgcn_ds_bpermute(rel << 2, int(lane_info))) : 0u;
+        const uint32_t info = kPairs ? uint32_t(__builtin_amdgcn_ds_bpermute(int(uint32_t(rel) << 2), int(lane_info))) : 0u;
         if (!pass && ord < piece && p < 64u && rel >= 0 && int(lane) < tl) {
           int v = int(int16_t(e & 0xFFFFu));  // lean entries: K1 applied HUFF_EXTEND
           if constexpr (kPairs) {
