@@ -225,9 +225,10 @@ struct RjLeanTables {  // LDS image: AC0, AC1 (first level + subtables), DC0, DC
 // symbol's s extra bits, done by K1 off its bit-position chain; for position 0 the DC
 // *difference*), [22:16] zigzag position (corrupt runs past 63 clamped to 63, as libjpeg's
 // natural-order table does; 127 = end of stream), bit 23: zero block (libjpeg's
-// insufficient-data / missing-marker blocks: every coefficient 0, DC absolute).
+// insufficient-data / missing-marker blocks: every coefficient 0, DC absolute), whose value
+// field holds -32768 -- the marker restore_dc reads (no real DC difference is: |diff| <= 32767).
 #define RJ_RE_TERM (127u << 16)
-#define RJ_RE_ZERO ((1u << 23))
+#define RJ_RE_ZERO ((1u << 23) | 0x8000u)
 
 // Output jobs of the general (two-stage) path: one per written channel.
 enum RjJobKind : uint32_t {

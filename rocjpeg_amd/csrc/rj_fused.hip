@@ -163,6 +163,7 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
                                              bool &bad) {
   uint32_t done = 0;
   const uint32_t need = nb + drop;
+  uint32_t bad_l = 0;  // this lane stored a coefficient outside the IDCT's exact domain (one ballot at the end)
   for (uint32_t moves = 0; done < need && moves < (1u << 16); moves++) {  // bounded on corrupt pieces
     if (nv.bleft == 0) {  // next piece, or the first piece of the next interval (synchronous reload)
       if (nv.seg >= im.nseg) break;
@@ -188,6 +189,11 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
     const uint32_t piece = pass ? nv.skip : min(need - done, nv.bleft);  // blocks taken from this piece
     const bool fix_dc = !kRaw && (nv.dcd[0] | nv.dcd[1] | nv.dcd[2]) != 0;
     uint32_t seen = 0;                                  // block starts before the current row
+    // entries stored: 0 <= rel < piece + done - drop (ord < piece, and not a dropped block), as
+    // one unsigned compare of 4 rel
+    const int32_t lim_s = int32_t(piece + done) - int32_t(drop);
+    const uint32_t st_lim4 = (pass || lim_s < 0) ? 0u : uint32_t(lim_s) * 4u;
+    const uint32_t end4 = uint32_t(lim_s) * 4u;  // rel4 of the block past the piece
     // one pass over the window in registers; true when the piece ends inside it
     auto walk = [&]() __attribute__((always_inline)) -> bool {
 #pragma unroll
@@ -201,10 +207,13 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
         // m >> 1) plus bit 0, in scalar terms -- no per-lane copy of the start flag
         const uint64_t m1 = m >> 1;
         const uint32_t incl = __builtin_amdgcn_mbcnt_hi(uint32_t(m1 >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m1), 0u));
-        const uint32_t ord = incl + (seen + uint32_t(m & 1u) - 1u);
-        // the entry's block in the strip (negative: a dropped block)
+        const uint32_t ord0 = seen + uint32_t(m & 1u) - 1u;  // ord = incl + ord0
+        const uint32_t ord = incl + ord0;
+        // the entry's block in the strip (negative: a dropped block), and 4x it in one
+        // v_lshl_add from the mbcnt: the bpermute address, the store bound and the piece end all
+        // compare on rel4 (4 rel mod 2^32 -- |rel| < 2^30)
         const int32_t rel = int32_t(ord + (done - drop));
-        bool oob = false;
+        const uint32_t rel4 = (incl << 2) + (ord0 + (done - drop)) * 4u;
         // a split interval's tail piece may end early (its lane stopped at libjpeg's
         // insufficient-data point): the piece's remaining blocks are zero blocks, and nothing
         // after its terminator belongs to the stream
@@ -212,8 +221,8 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
         const int tl = term ? __ffsll((long long)term) - 1 : 64;
         // the entry's block in the strip, and from its lane: LDS base, quantiser row (whole wave)
         // (ds_bpermute takes the source lane from address bits [7:2]: rel mod 64, no masking)
-        const uint32_t info = kPairs ? uint32_t(__builtin_amdgcn_ds_bpermute(int(uint32_t(rel) << 2), int(lane_info))) : 0u;
-        if (!pass && ord < piece && p < 64u && rel >= 0 && int(lane) < tl) {
+        const uint32_t info = kPairs ? uint32_t(__builtin_amdgcn_ds_bpermute(int(rel4), int(lane_info))) : 0u;
+        if (rel4 < st_lim4 && p < 64u && (!(kRaw && kSplit) || int(lane) < tl)) {
           int v = int(int16_t(e & 0xFFFFu));  // lean entries: K1 applied HUFF_EXTEND
           if constexpr (kPairs) {
             // component-interleaved s_qw[3 p + c]: (a/4) mod 32 banks; info >> 16 = 4 c (bytes)
@@ -223,32 +232,41 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
               const uint32_t cc = info >> 18;
               v += cc == 0 ? nv.dcd[0] : (cc == 1 ? nv.dcd[1] : nv.dcd[2]);
             }
-            const int x = __mul24(v, int(qe & 0xFFFFu));  // |v| < 2^16, q < 2^16: exact
+            // |v| < 2^15, q < 2^16: exact in the i24 multiply.  Raw entries: one SDWA multiply of
+            // the entry's low half (sign-extended) by the quantiser (low half of qe)
+            int x;
+            if constexpr (kRaw)
+              asm("v_mul_i32_i24_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0"
+                  : "=v"(x) : "v"(e), "v"(qe));
+            else
+              x = __mul24(v, int(qe & 0xFFFFu));
             // straight-line selects (no divergent DC / AC branches in the scatter)
             const bool dc = p == 0;
             int sv;
             if constexpr (kRaw) {  // a raw DC is a difference (restore_dc finishes it)
-              oob = !dc && uint32_t(x + RJ_DOT2_AC_MAX) > uint32_t(2 * RJ_DOT2_AC_MAX);
-              sv = dc ? ((e & RJ_RE_ZERO) ? -32768 : v) : x << 5;
+              const bool oob = !dc && uint32_t(x + RJ_DOT2_AC_MAX) > uint32_t(2 * RJ_DOT2_AC_MAX);
+              bad_l = oob ? 1u : bad_l;
+              // the DC difference is the entry's low half (ds_write_b16); a zero block's is -32768
+              sv = dc ? int(e) : x << 5;
             } else {
               const int lim = dc ? RJ_DOT2_DC_MAX : RJ_DOT2_AC_MAX;
-              oob = uint32_t(x + lim) > uint32_t(2 * lim);
+              const bool oob = uint32_t(x + lim) > uint32_t(2 * lim);
+              bad_l = oob ? 1u : bad_l;
               sv = x << (dc ? 4 : 5);
             }
             *reinterpret_cast<int16_t *>(s_buf + (info & 0xFFFFu) + (qe >> 16)) = int16_t(sv);
           } else {
-            if (kRaw && (e & RJ_RE_ZERO)) v = -32768;  // zero block: marked for the DC restore
             if (!kRaw && fix_dc && p == 0) {
               const uint32_t bi = uint32_t(rel) % nblk;  // strips start at an MCU boundary
               const uint32_t cc = (cbits >> (2 * bi)) & 3u;
               v += cc == 0 ? nv.dcd[0] : (cc == 1 ? nv.dcd[1] : nv.dcd[2]);
             }
             // outside the int32 IDCT's exact domain (raw DC: a difference, checked by restore_dc)
-            oob = (!kRaw || p != 0) && int16_t(v) != -32768 && abs(int(int16_t(v))) > thr;
+            const bool oob = (!kRaw || p != 0) && int16_t(v) != -32768 && abs(int(int16_t(v))) > thr;
+            bad_l = oob ? 1u : bad_l;
             *reinterpret_cast<int16_t *>(s_buf + __umul24(uint32_t(rel), uint32_t(RJ_BLK_STRIDE)) + p * 2) = int16_t(v);
           }
         }
-        bad = bad || __ballot(oob) != 0;
         if (term) {
           const uint32_t t_ord = pass ? piece : __builtin_amdgcn_readlane(ord, tl);
           for (uint32_t z = t_ord + lane; z < piece; z += 64)
@@ -256,7 +274,7 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
           nv.set_cur((uint64_t(win.base_hi) << 32 | win.base_lo) + uint32_t(r) * 64u + uint32_t(tl));
           return true;
         }
-        const uint64_t hit = __ballot(ord == piece) & m;  // start of the first block past the piece
+        const uint64_t hit = __ballot(rel4 == end4) & m;  // start of the first block past the piece (ord == piece)
         seen += __popcll(m);
         if (hit) {
           nv.set_cur((uint64_t(win.base_hi) << 32 | win.base_lo) + uint32_t(r) * 64u +
@@ -283,6 +301,7 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
       nv.bleft -= piece;
     }
   }
+  if (__ballot(bad_l != 0) != 0) bad = true;
 }
 
 // DC prediction of a strip of raw-entry blocks (lean K1 wrote differences; T.81 F.2.1.3.1):
