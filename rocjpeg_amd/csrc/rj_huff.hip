@@ -29,7 +29,7 @@ namespace rj {
 #define RJ_HL_CHUNKS 8                      // 16-B chunks in a lane's bit ring
 #define RJ_HL_WORDS (RJ_HL_CHUNKS * 4)      // 32 words
 #ifndef RJ_HL_PHASE
-#define RJ_HL_PHASE 8                       // symbols per phase of the whole-interval launch
+#define RJ_HL_PHASE 16                      // symbols per phase of the whole-interval launch (8: +3.5 % K1)
 #endif
 // LDS byte offsets of the four tables (RjLeanTables order)
 #define RJ_HL_AC_BYTES (RJ_HL_AC_WORDS * 4)
