@@ -1032,7 +1032,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t off_fold = AlignUp(off_plane + prog_lanes.size() * sizeof(uint32_t), 256);
   const uint64_t off_lean = AlignUp(off_fold + fold_jobs.size() * sizeof(RjFoldJob), 256);
   const uint64_t off_wide = AlignUp(off_lean + (lean ? tabs.size() * sizeof(RjLeanTables) : 0), 256);
-  const uint64_t off_stage = AlignUp(off_wide + kWideSites * sizeof(uint32_t), 256);
+  // K0's block -> image map: the image holding block 64 k, for k <= ds_total / 64 (+ a sentinel)
+  const uint32_t n_dsmap = ds_total / 64u + 2u;
+  const uint64_t off_dsmap = AlignUp(off_wide + kWideSites * sizeof(uint32_t), 256);
+  const uint64_t off_stage = AlignUp(off_dsmap + n_dsmap * sizeof(uint32_t), 256);
   const uint64_t blob_a = AlignUp(off_stage + stage_bytes, 256);
   // (a lean launch may split intervals: head + tail lanes, up to 2 per interval + one wave of padding)
   const uint64_t n_lane_seg = any_split ? lane_seg.size() : (sorted ? (lean ? 2ull * seg_total + 64 : seg_total) : 0);
@@ -1217,6 +1220,14 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint2 *d_row_list = reinterpret_cast<const uint2 *>(dbase + off_row_list);
   const uint32_t *d_lane_seg = reinterpret_cast<const uint32_t *>(dbase + off_lane_seg);
   std::memset(h + off_wide, 0, kWideSites * sizeof(uint32_t));
+  {
+    uint32_t *map = reinterpret_cast<uint32_t *>(h + off_dsmap);
+    for (uint32_t k = 0; k < n_dsmap; k++) map[k] = uint32_t(n - 1);
+    for (int i = 0; i < n; i++) {  // images in block order: image i holds [ds_prefix, next ds_prefix)
+      const uint32_t b0 = imgs[i].ds_prefix, b1 = i + 1 < n ? imgs[i + 1].ds_prefix : ds_total;
+      for (uint32_t k = (b0 + 63u) / 64u; k * 64u < b1; k++) map[k] = uint32_t(i);
+    }
+  }
   uint32_t *const d_wide_cnt = reinterpret_cast<uint32_t *>(dbase + off_wide);
   uint64_t wide_used = 0;
   wide_sites_.clear();
@@ -1234,7 +1245,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   RJ_HIP(hipMemcpyAsync(dbase, h, blob_a, hipMemcpyHostToDevice, stream_));
   if (cbuf.count) RJ_HIP(hipMemsetAsync(cbuf.count, 0, sizeof(unsigned long long), stream_));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
-  RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>()));
+  RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>(),
+                      reinterpret_cast<const uint32_t *>(dbase + off_dsmap)));
   const uint8_t *k1_src = d_destuff_.as<uint8_t>();
   if (prog_images) {  // progressive images: K1p level by level, then their K2 rows (dense)
     const uint32_t *d_plane = reinterpret_cast<const uint32_t *>(dbase + off_plane);

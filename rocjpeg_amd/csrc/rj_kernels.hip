@@ -37,12 +37,25 @@ __device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v, uint32_t &to
 // (b[i] == 00 && b[i-1] == FF) or (b[i] == FF && b[i+1] == FF).
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ imgs, int nimg,
-                                                uint8_t *__restrict__ destuffed) {
+                                                uint8_t *__restrict__ destuffed, const uint32_t *__restrict__ ds_map) {
   static_assert(RJ_DS_BLOCK == 2048u, "8 chunks of 256 B per block");
   constexpr int kIt = RJ_DS_BLOCK / 256;
   const uint32_t g = blockIdx.x;
   const uint32_t lane = threadIdx.x;
-  const int i = __builtin_amdgcn_readfirstlane(upper_index(nimg, g, [&](int k) { return imgs[k].ds_prefix; }));
+  // the block's image: between the owners of blocks 64 (g / 64) and 64 (g / 64 + 1) (the host's
+  // map), usually one or two images apart -- a search over all images was ten dependent loads
+  // in front of every block's data loads, which made K0 latency-bound
+  int lo = 0, hi = nimg - 1;
+  if (ds_map != nullptr) {
+    lo = int(ds_map[g >> 6]);
+    hi = int(ds_map[(g >> 6) + 1]);
+  }
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (imgs[mid].ds_prefix <= g) lo = mid;
+    else hi = mid - 1;
+  }
+  const int i = __builtin_amdgcn_readfirstlane(lo);
   const RjImageDev &im = imgs[i];
   const RjDsBlock blk = gp(im.ds)[g - im.ds_prefix];
   const RJ_GLOBAL uint8_t *src = gp(im.ecs + blk.src_off);
@@ -130,9 +143,10 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
   }
 }
 
-hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nblocks, uint8_t *destuffed) {
+hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nblocks, uint8_t *destuffed,
+                         const uint32_t *ds_map) {
   if (nblocks == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_destuff, dim3(nblocks), dim3(64), 0, st, imgs, nimg, destuffed);
+  hipLaunchKernelGGL(k_destuff, dim3(nblocks), dim3(64), 0, st, imgs, nimg, destuffed, ds_map);
   return hipGetLastError();
 }
 
