@@ -188,6 +188,36 @@ RocJpegStatus rocJpegAmdDecodeBatchedSharded(RocJpegHandle handle, RocJpegAmdCom
                                              int count, const RocJpegDecodeParams *decode_params,
                                              RocJpegImage *destinations, RocJpegAmdWorkItem *items);
 
+/* The resident form of the sharded call, for a caller that decodes the same batch repeatedly
+ * (rocJpegAmdDecodeBatchedSharded = Create + Decode + Destroy):
+ *   rocJpegAmdShardCreate   every rank, collective: the plan on rank 0, the broadcast, then this
+ *                           rank parses its images with the GPU marker scan
+ *                           (rocJpegAmdStreamParseDevice) and keeps their bitstreams and interval
+ *                           tables resident in the HBM of `handle`'s device;
+ *   rocJpegAmdShardDecode   no collective: rocJpegDecodeBatched over this rank's resident images,
+ *                           image i of the batch into destinations[i] (`count` entries in batch
+ *                           order, as at create; only this rank's are written);
+ *   rocJpegAmdShardGetImages  this rank's batch indices;
+ *   rocJpegAmdShardDestroy.
+ * Collective error rules (create, plan, broadcast): every rank takes part in the broadcast on
+ * every path once its communicator exists; when rank 0's plan fails every rank returns that
+ * status; a rank whose own arguments are invalid returns INVALID_PARAMETER after the broadcast
+ * (the other ranks still decode their shares).  A shard is used by one thread at a time. */
+typedef struct RocJpegAmdShardImpl *RocJpegAmdShard;
+RocJpegStatus rocJpegAmdShardCreate(RocJpegHandle handle, RocJpegAmdComm comm, const unsigned char *blob,
+                                    uint64_t blob_bytes, const uint64_t *offsets, const uint32_t *sizes, int count,
+                                    RocJpegAmdWorkItem *items, RocJpegAmdShard *shard);
+RocJpegStatus rocJpegAmdShardDecode(RocJpegAmdShard shard, const RocJpegDecodeParams *decode_params,
+                                    RocJpegImage *destinations);
+RocJpegStatus rocJpegAmdShardGetImages(RocJpegAmdShard shard, int *num_images, int *indices, int capacity);
+RocJpegStatus rocJpegAmdShardDestroy(RocJpegAmdShard shard);
+
+/* ABI revision of this header's extensions (rocJpegAmdGetAbiVersion returns the library's).
+ * 2: rocJpegAmdBuildWorkTable takes blob_bytes; RocJpegAmdTimings as above.
+ * 3: the resident sharded entry points; the work-table broadcast carries a status header. */
+#define ROCJPEG_AMD_ABI_VERSION 3
+RocJpegStatus rocJpegAmdGetAbiVersion(int *version);
+
 #if defined(__cplusplus)
 }
 #endif

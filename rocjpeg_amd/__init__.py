@@ -23,7 +23,10 @@ EXT_SYMBOLS = (
     "rocJpegAmdStreamGetDestuffBlocks", "rocJpegAmdBuildWorkTable", "rocJpegAmdAssignShards",
     "rocJpegAmdCommGetUniqueId", "rocJpegAmdCommInitRank", "rocJpegAmdCommDestroy", "rocJpegAmdCommInfo",
     "rocJpegAmdBroadcastWorkTable", "rocJpegAmdShardPlan", "rocJpegAmdDecodeBatchedSharded",
+    "rocJpegAmdShardCreate", "rocJpegAmdShardDecode", "rocJpegAmdShardGetImages", "rocJpegAmdShardDestroy",
+    "rocJpegAmdGetAbiVersion",
 )
+ABI_VERSION = 3  # include/rocjpeg_amd.h ROCJPEG_AMD_ABI_VERSION
 
 
 class Status(enum.IntEnum):  # api/rocjpeg.h:53-67
@@ -166,9 +169,18 @@ def lib():
                                           ctypes.POINTER(ctypes.c_uint32), i32, vp]
         L.rocJpegAmdDecodeBatchedSharded.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                                      ctypes.POINTER(ctypes.c_uint32), i32, vp, vp, vp]
+        L.rocJpegAmdShardCreate.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                            ctypes.POINTER(ctypes.c_uint32), i32, vp, ctypes.POINTER(vp)]
+        L.rocJpegAmdShardDecode.argtypes = [vp, vp, vp]
+        L.rocJpegAmdShardGetImages.argtypes = [vp, ctypes.POINTER(i32), vp, i32]
+        L.rocJpegAmdShardDestroy.argtypes = [vp]
+        L.rocJpegAmdGetAbiVersion.argtypes = [ctypes.POINTER(i32)]
         for name in API_SYMBOLS + EXT_SYMBOLS:
             if name != "rocJpegGetErrorName":
                 getattr(L, name).restype = i32
+        v = ctypes.c_int()
+        if L.rocJpegAmdGetAbiVersion(ctypes.byref(v)) != 0 or v.value != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH}: extension ABI {v.value}, this binding needs {ABI_VERSION} (rebuild)")
         _lib = L
     return _lib
 

@@ -514,11 +514,96 @@ __device__ __forceinline__ void rgb_strip_420_full(const uint8_t *ty, const uint
     const rj_f2 uu = rj_f2{u8f(u2, 0), u8f(u2, 1)} - m128, vv = rj_f2{u8f(v2, 0), u8f(v2, 1)} - m128;
     const rj_f2 ua = {uu.x, uu.x}, ub = {uu.y, uu.y}, va = {vv.x, vv.x}, vb = {vv.y, vv.y};
     uint32_t w0, w1, w2;
+#if defined(RJ_EXP_K2C) && RJ_EXP_K2C == 3  // timing probe: stores issued, no tile reads or CSC
+    w0 = tid; w1 = tid + 1; w2 = tid + 2;
+    *reinterpret_cast<RJ_GLOBAL uint3 *>(d + 96 * i) = make_uint3(w0, w1, w2);
+    *reinterpret_cast<RJ_GLOBAL uint3 *>(d + pitch + 96 * i) = make_uint3(w0, w1, w2);
+    continue;
+#endif
     csc4_pk(y4, ua, ub, va, vb, w0, w1, w2);
+#if defined(RJ_EXP_K2C) && RJ_EXP_K2C == 2  // timing probe: CSC live, no global store (runtime-false guard)
+    if (pitch == 0x7FFFFFF1u)
+#endif
     *reinterpret_cast<RJ_GLOBAL uint3 *>(d + 96 * i) = make_uint3(w0, w1, w2);
     csc4_pk(y4b, ua, ub, va, vb, w0, w1, w2);
+#if defined(RJ_EXP_K2C) && RJ_EXP_K2C == 2
+    if (pitch == 0x7FFFFFF1u)
+#endif
     *reinterpret_cast<RJ_GLOBAL uint3 *>(d + pitch + 96 * i) = make_uint3(w0, w1, w2);
   }
+}
+
+// Phase C store shape for the full 4:2:0 strip (round 4).  rgb_strip_420_full stores 12 B per
+// lane: one wave instruction covers 8 rows x 96 B, i.e. 8-16 partial cache lines, ten such
+// instructions per lane and strip.  Here the same lanes compute the same pixels (arithmetic and
+// bytes as rgb_strip_420_full) but write them into an LDS image of the strip's RGB rows; the
+// wave then reads the image back as 16-B pieces in row-major order and stores piece p of the
+// image from lane p mod 64: each global store is a dwordx4 whose 64 lanes cover 1 KB of
+// consecutive row segments.  The strip goes in two column halves (pixels 0..95 = bytes 0..287,
+// 96..159 = bytes 288..479), so that the image fits beside the sample tiles in the block area:
+// tiles 3,840 B + image 16 x 288 B = 8,448 B of the 9,216.  d: the strip's first output byte
+// (16-B aligned, as is the pitch: the host-side condition is checked by the caller).
+#ifndef RJ_K2_STORE
+#define RJ_K2_STORE 1  // 0: rgb_strip_420_full (12-B stores), 1: staged dwordx4
+#endif
+template <int kI0, int kNI>
+__device__ __forceinline__ void rgb_420_half_staged(const uint8_t *ty, const uint8_t *tu, const uint8_t *tv,
+                                                    uint32_t tid, uint8_t *stage, RJ_GLOBAL uint8_t *d,
+                                                    uint32_t pitch) {
+  constexpr uint32_t kSW = 96u * kNI;  // image row bytes
+  constexpr uint32_t kPR = kSW / 16u;  // 16-B pieces per row
+  constexpr uint32_t kNP = 16u * kPR;  // pieces of the image
+  uint32_t t0 = tid;  // opaque: the lane's LDS addresses are not hoisted out of the strip loop
+  asm volatile("" : "+v"(t0));
+  const uint32_t qy = t0 >> 3, qx0 = t0 & 7u;
+  const uint8_t *yr = ty + qy * 320u + qx0 * 4u;
+  const uint32_t co = qy * 80u + qx0 * 2u;
+  uint32_t *im0 = reinterpret_cast<uint32_t *>(stage + qy * (2u * kSW) + qx0 * 12u);
+  uint32_t *im1 = im0 + kSW / 4u;
+  const rj_f2 m128 = {128.0f, 128.0f};
+#pragma unroll
+  for (int i = 0; i < kNI; i++) {
+    const int ii = kI0 + i;
+    const uint32_t y4 = *reinterpret_cast<const uint32_t *>(yr + 32 * ii);
+    const uint32_t y4b = *reinterpret_cast<const uint32_t *>(yr + 160 + 32 * ii);
+    const uint32_t u2 = *reinterpret_cast<const uint16_t *>(tu + co + 16 * ii);
+    const uint32_t v2 = *reinterpret_cast<const uint16_t *>(tv + co + 16 * ii);
+    const rj_f2 uu = rj_f2{u8f(u2, 0), u8f(u2, 1)} - m128, vv = rj_f2{u8f(v2, 0), u8f(v2, 1)} - m128;
+    const rj_f2 ua = {uu.x, uu.x}, ub = {uu.y, uu.y}, va = {vv.x, vv.x}, vb = {vv.y, vv.y};
+    uint32_t w0, w1, w2;
+    csc4_pk(y4, ua, ub, va, vb, w0, w1, w2);
+    im0[24 * i] = w0;
+    im0[24 * i + 1] = w1;
+    im0[24 * i + 2] = w2;
+    csc4_pk(y4b, ua, ub, va, vb, w0, w1, w2);
+    im1[24 * i] = w0;
+    im1[24 * i + 1] = w1;
+    im1[24 * i + 2] = w2;
+  }
+  __syncthreads();  // the image is written (one wave: the wait for its LDS stores)
+  // the lane's piece addresses are recomputed per strip: hoisted out of the strip loop they
+  // would hold ~8 VGPRs across the IDCT (the kernel sits at 128)
+  uint32_t t = tid;
+  asm volatile("" : "+v"(t));
+#pragma unroll
+  for (uint32_t m = 0; m < (kNP + 63u) / 64u; m++) {
+    const uint32_t p = m * 64u + t;
+    if ((m + 1u) * 64u <= kNP || p < kNP) {
+      const uint32_t row = p / kPR, col = p - row * kPR;
+      const uint4 v = *reinterpret_cast<const uint4 *>(stage + p * 16u);
+#if defined(RJ_EXP_K2C) && RJ_EXP_K2C == 1  // timing probe: no global store (runtime-false guard)
+      if (pitch == 0x7FFFFFF1u)
+#endif
+#ifdef RJ_K2_NT
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w},
+                                  reinterpret_cast<RJ_GLOBAL u32x4 *>(d + (__umul24(row, pitch) + col * 16u)));
+#else
+      *reinterpret_cast<RJ_GLOBAL uint4 *>(d + (__umul24(row, pitch) + col * 16u)) = v;
+#endif
+    }
+  }
+  __syncthreads();  // the image is read before the next half overwrites it
 }
 
 // The work of one MCU row (one wavefront), looping over the row's strips of S MCUs.
@@ -684,6 +769,7 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
   const uint32_t hs1 = (ncomp == 3) ? (hmax / ib.at(RJ_OFF(comp_h) + 1) == 2 ? 1u : 0u) : 0u;
   const uint32_t vs1 = (ncomp == 3) ? (vmax / ib.at(RJ_OFF(comp_v) + 1) == 2 ? 1u : 0u) : 0u;
   const bool al_y = ((reinterpret_cast<uintptr_t>(dst0) | pitch0) & 3) == 0;
+  const bool al16 = ((reinterpret_cast<uintptr_t>(dst0) | pitch0) & 15) == 0;  // staged 16-B stores (RJ_K2_STORE)
   const bool al_rgbp = ((reinterpret_cast<uintptr_t>(dst0) | reinterpret_cast<uintptr_t>(dst1) |
                          reinterpret_cast<uintptr_t>(dst2) | pitch0) & 3) == 0;
   const bool al_uv = ((reinterpret_cast<uintptr_t>(dst1) | reinterpret_cast<uintptr_t>(dst2) | pitch1) & 3) == 0;
@@ -745,7 +831,12 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
       }
       row_wide = row_wide || wide;
       if constexpr (!kPlanes) __syncthreads();  // every block is in registers: the staging area becomes the sample tiles
+#if defined(RJ_EXP_K2C) && RJ_EXP_K2C == 4  // timing probe: no IDCT (the block's first dwords as samples)
+      if (has_blk)
+        for (int q = 0; q < 16; q++) o[q] = w[q] ^ w[q + 16];
+#else
       if (has_blk) idct_dot2_block(w, o);
+#endif
       if constexpr (!kDense) win.settle();  // the next strip's window, before this strip's pixel stores
     } else {
       int32_t v[64];
@@ -804,7 +895,15 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
     const uint8_t *ty = s_buf + toff[0], *tu = s_buf + toff[1], *tv = s_buf + toff[2];
     uint8_t *d = dst0 + (__umul24(py0, pitch0) + px0 * 3);
     if (hs1) {
-      if (vs1 && strip_w == 160u && tw[0] == 160u && tw[1] == 80u) rgb_strip_420_full(ty, tu, tv, tid, d, pitch0);
+      if (vs1 && strip_w == 160u && tw[0] == 160u && tw[1] == 80u) {
+        if (RJ_K2_STORE == 1 && al16) {
+          uint8_t *stage = s_buf + 3840u;  // past the tiles (toff[2] + 640)
+          rgb_420_half_staged<0, 3>(ty, tu, tv, tid, stage, gp(d), pitch0);
+          rgb_420_half_staged<3, 2>(ty, tu, tv, tid, stage, gp(d) + 288u, pitch0);
+        } else {
+          rgb_strip_420_full(ty, tu, tv, tid, d, pitch0);
+        }
+      }
       else if (vs1) rgb_strip<true, true>(ty, tu, tv, tw[0], tw[1], tid, quads_x, rows, d, pitch0);
       else rgb_strip<true, false>(ty, tu, tv, tw[0], tw[1], tid, quads_x, rows, d, pitch0);
     } else {

@@ -1089,9 +1089,13 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
       pos += used;
       if (__builtin_expect(pend != 0, 0)) continue;  // the walk resumes at the next peek
       walking = false;
-      if (newv && t <= se) {  // past Se (corrupt data): dropped, as in lane_ac_refine
-        __builtin_assume(t < 64u);
-        const uint64_t bq = 1ull << t;
+      // a new coefficient whose zero run overshoots the band (corrupt data): at Se = 63 libjpeg
+      // stores it at natural position 63 (jpeg_natural_order[64] == 63, oracle kZigzag[64]), as
+      // lane_ac_refine does; past a smaller Se it is dropped (see lane_ac_first)
+      const uint32_t tc = min(t, 63u);
+      if (newv && tc <= se) {
+        __builtin_assume(tc < 64u);
+        const uint64_t bq = 1ull << tc;
         newm |= bq;
         sgn |= newv == 2 ? bq : 0ull;
       }

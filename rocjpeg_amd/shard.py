@@ -199,3 +199,44 @@ class Comm:
         if self.handle:
             lib().rocJpegAmdCommDestroy(self.handle)
             self.handle = ctypes.c_void_p()
+
+
+class Shard:
+    """This rank's share of a sharded batch, resident on the handle's GPU (rocJpegAmdShardCreate:
+    plan on rank 0 + broadcast + GPU marker-scan parse of this rank's images).  decode() is
+    rocJpegAmdShardDecode: rocJpegDecodeBatched over the resident images, image i of the batch
+    into destinations[i].  Collective at create: every rank of the communicator calls it."""
+
+    def __init__(self, comm, dec_handle, blob, offsets, sizes):
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        sizes = np.ascontiguousarray(sizes, dtype=np.uint32)
+        n = len(offsets)
+        self.table = np.zeros(n, dtype=WORK_ITEM_DTYPE)
+        self.count = n
+        ptr, keep = _u8_pointer(blob)
+        self.handle = ctypes.c_void_p()
+        self.status = lib().rocJpegAmdShardCreate(dec_handle, comm.handle, ptr, keep.nbytes,
+                                                  offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                                  sizes.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n,
+                                                  ctypes.c_void_p(self.table.ctypes.data) if n else None,
+                                                  ctypes.byref(self.handle))
+        del keep
+
+    def images(self):
+        """This rank's batch indices."""
+        cnt = ctypes.c_int()
+        st = lib().rocJpegAmdShardGetImages(self.handle, ctypes.byref(cnt), None, 0)
+        if st != 0:
+            raise RuntimeError(f"rocJpegAmdShardGetImages: {Status(st)!r}")
+        idx = (ctypes.c_int * max(1, cnt.value))()
+        lib().rocJpegAmdShardGetImages(self.handle, ctypes.byref(cnt), idx, cnt.value)
+        return [idx[k] for k in range(cnt.value)]
+
+    def decode(self, params, destinations):
+        """destinations: a ctypes array of RocJpegImage, one per image of the batch."""
+        return lib().rocJpegAmdShardDecode(self.handle, ctypes.byref(params), destinations)
+
+    def close(self):
+        if self.handle:
+            lib().rocJpegAmdShardDestroy(self.handle)
+            self.handle = ctypes.c_void_p()

@@ -4,7 +4,10 @@ library's own RCCL communicator, the work-table broadcast and rocJpegAmdDecodeBa
 has one MI355X, and RCCL refuses two ranks on one device, so these run the communicator at one
 rank: the whole sharded call (table build, LPT, broadcast, parse, decode) from Python and from a
 plain C program (tests/c/jpegdecode_sharded_c.c, one forked process per rank), every image
-compared with the oracle.  The table logic at 2 / 4 / 8 ranks is tests/test_dist_cpu.py."""
+compared with the oracle.  The multi-rank protocol (chunked table exchange with rank 0's status,
+error paths, the resident shard entry points) runs with 3 ranks sharing the GPU through the
+library's shared-memory test transport (RJ_COMM_TEST_SHM).  The table logic over gloo at 2 and 4
+ranks is tests/test_dist_cpu.py."""
 import ctypes
 import os
 import struct
@@ -118,3 +121,48 @@ def test_plain_c_caller_sharded(tmp_path):
         shapes = G.channel_shapes(fmt, info["subsampling"], info["widths"], info["heights"])
         ost, want = O.oracle_decode(data, int(fmt), shapes)
         assert ost == 0 and got[k] == b"".join(np.ascontiguousarray(w).tobytes() for w in want)
+
+
+def test_multi_rank_protocol_shared_gpu(tmp_path):
+    """3 processes, one GPU, the library's communicator over its shared-memory test transport
+    (csrc/rj_comm.cpp ShmBus; RCCL refuses two ranks on one device): the same chunks, header and
+    checks as the RCCL broadcast.  tests/comm_rank_worker.py runs, on every rank in step:
+    the resident shard (rocJpegAmdShardCreate / Decode twice, own images oracle-exact, the rest
+    untouched), a 9,000-record table (three chunks), a rank with no destinations, a failed plan
+    on rank 0, a rank with a different count, and one more exchange to show the ranks stayed in
+    step (no error path may leave a rank waiting in the collective)."""
+    import json
+    import sys
+    world = 3
+    shm = f"/dev/shm/rj_comm_test_{os.getpid()}"
+    if os.path.exists(shm):
+        os.unlink(shm)
+    env = dict(os.environ, RJ_COMM_TEST_SHM=shm)
+    outs = [str(tmp_path / f"r{r}.json") for r in range(world)]
+    procs = [subprocess.Popen([sys.executable, "-m", "tests.comm_rank_worker", str(r), str(world), outs[r]],
+                              cwd=O.ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(world)]
+    try:
+        logs = [p.communicate(timeout=240)[0] for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        if os.path.exists(shm):
+            os.unlink(shm)
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-3000:]
+    res = [json.load(open(o)) for o in outs]
+    n = len(res[0]["table_shard"])
+    assert all(r["create"] == 0 and r["decode"] == [0, 0] for r in res)
+    assert all(r["table_shard"] == res[0]["table_shard"] for r in res)
+    assert sorted(i for r in res for i in r["images"]) == list(range(n))
+    assert all(len(r["images"]) > 0 for r in res)
+    assert all(r["oracle_exact"] and r["others_untouched"] for r in res)
+    assert all(r["big_table"][0] == 0 and r["big_table"][1] == res[0]["big_table"][1] for r in res)
+    inv = int(R.Status.INVALID_PARAMETER)
+    assert res[1]["bad_rank1"][0] == inv
+    assert all(res[r]["bad_rank1"] == [0, True] for r in (0, 2))
+    assert all(r["plan_fail"] == inv for r in res)
+    assert [r["count_mismatch"] for r in res] == [0, 0, inv]
+    assert all(r["after"] == [0, [5, 6, 7]] for r in res)

@@ -1,4 +1,4 @@
-"""Multi-GPU batched decode on CPU (gloo, world_size 2): the work table rank 0 builds from the
+"""Multi-GPU batched decode on CPU (gloo, world_size 2 and 4): the work table rank 0 builds from the
 JPEG headers (rocJpegAmdBuildWorkTable), the LPT shards (rocJpegAmdAssignShards) and the one
 broadcast (rocjpeg_amd/shard.py) -- SURVEY.md 8e.  No GPU: decode calls are not made here."""
 import io
@@ -142,7 +142,7 @@ def _rank(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_table_broadcast_and_shards_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -158,11 +158,11 @@ def test_table_broadcast_and_shards_gloo(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     # the table round-trips bit for bit
-    assert got[0][0] == got[1][0]
+    assert all(got[r][0] == got[0][0] for r in range(world))
     table = np.frombuffer(got[0][0], dtype=S.WORK_ITEM_DTYPE)
     assert len(table) == 2000 and np.array_equal(table["index"], np.arange(2000))
     # every image on exactly one rank
-    allidx = got[0][1] + got[1][1]
+    allidx = [i for r in range(world) for i in got[r][1]]
     assert sorted(allidx) == list(range(2000))
     assert all(got[r][2] for r in range(world))
     cost = [int(table["cost"][table["shard"] == r].sum()) for r in range(world)]

@@ -84,3 +84,26 @@ def test_csc_gray_is_identity_within_rounding():
     for y in (0, 17, 128, 255):
         O.oracle().oj_csc_pixel(y, 128, 128, rgb)
         assert list(rgb) == [y, y, y]
+
+
+def test_crafted_refine_overshoot_matches_libjpeg_turbo():
+    """The Se = 63 refinement overshoot of tests/jpeg_craft.py: the oracle's coefficients put the
+    new coefficient at natural index 63 (libjpeg jdphuff.c natural_order[64] == 63), and its
+    grayscale ISLOW plane equals Pillow's libjpeg-turbo decode of the same bytes (grayscale: no
+    upsampling or colour conversion in between)."""
+    import io
+
+    PIL = pytest.importorskip("PIL.Image")
+    from tests import jpeg_craft as C
+
+    data = C.prog_gray_refine_overshoot(64, 64)
+    st, coefs, dims = O.decode_coefs(data)
+    assert st == 0 and dims == [(8, 8)]
+    blocks = coefs.reshape(-1, 64)
+    for b, blk in enumerate(blocks):
+        assert set(np.nonzero(blk)[0]) == {1, 19, 63}
+        assert blk[63] == (1 if (b >> 2) & 1 else -1)
+        assert blk[19] == (1 if b & 1 else -1)
+    st, planes, _ = O.decode_planes(data)
+    assert st == 0
+    assert np.array_equal(np.asarray(PIL.open(io.BytesIO(data))), planes[0])

@@ -118,6 +118,22 @@ def test_progressive_truncated(dec, ent):
             assert G.first_mismatch(got[0], want[0]) is None, (name, G.first_mismatch(got[0], want[0]))
 
 
+@pytest.mark.parametrize("fmt", [R.OutputFormat.RGB, R.OutputFormat.Y])
+def test_ac_refine_zero_run_overshoot_at_se63(dec, fmt):
+    """A Se = 63 AC refinement whose new coefficient's zero run passes position 63 (corrupt
+    data no encoder writes): libjpeg stores it at natural index 63 (jdphuff.c, natural_order[64]
+    == 63).  The crafted stream (tests/jpeg_craft.py) hits it in every block; the oracle's
+    result on it equals libjpeg-turbo's (tests/test_oracle_golden.py).  k_prog_wave must store
+    it there too (the clamp to 63 had been lost)."""
+    from tests import gpu_util as G
+    from tests import jpeg_craft as C
+    data = C.prog_gray_refine_overshoot(64, 64)
+    st, ost, got, want = run_both(dec, data, fmt)
+    assert st == ost == 0
+    for c, (g, w) in enumerate(zip(got, want)):
+        assert G.first_mismatch(g, w) is None, (c, G.first_mismatch(g, w))
+
+
 @pytest.mark.parametrize("resident", [False, True], ids=["staged", "resident"])
 @pytest.mark.parametrize("fmt", [R.OutputFormat.RGB, R.OutputFormat.YUV_PLANAR, R.OutputFormat.NATIVE])
 def test_batch_mixed_progressive_and_baseline(dec, fmt, resident):
