@@ -339,6 +339,212 @@ class BatchRun:
         torch.cuda.empty_cache()
 
 
+def _sub(arr, ctype, start, k):
+    """k entries of a ctypes array from `start` (no copy)."""
+    return (ctype * k).from_address(ctypes.addressof(arr) + start * ctypes.sizeof(ctype))
+
+
+def _shape_loop(call, n, k, budget_s=0.6, min_calls=8):
+    """Synchronous calls of k images each, cycling over n images, for ~budget_s: (images/s,
+    per-call latency mean / p50 / p90 in ms).  The timing brackets each call only, as
+    jpegdecodeperf.cpp:153-157 does."""
+    lat, start = [], 0
+    call(0, k)  # warm (first use of this shape)
+    t_end = time.perf_counter() + budget_s
+    while len(lat) < min_calls or time.perf_counter() < t_end:
+        if start + k > n:
+            start = 0
+        t0 = time.perf_counter()
+        call(start, k)
+        lat.append(time.perf_counter() - t0)
+        start += k
+    a = np.array(lat) * 1e3
+    return {"images_per_s": round(k * len(a) / (a.sum() * 1e-3), 1), "calls": len(a),
+            "latency_ms": {"mean": round(float(a.mean()), 4), "p50": round(float(np.median(a)), 4),
+                           "p90": round(float(np.percentile(a, 90)), 4)}}
+
+
+def call_shapes(dec, datas, fmt, dev, threads=8):
+    """The reference's default call shapes, on the same C2 images:
+      - rocJpegDecode, one image per call (samples/jpegDecode/jpegdecode.cpp:163);
+      - rocJpegDecodeBatched at 16 and 128 images per call;
+      - jpegdecodeperf's default: batch 1 per rocJpegDecodeBatched, `threads` host threads with
+        one handle each (jpegdecodeperf.cpp:201-202, 228-257), per-thread rates summed
+        (:268-271, 281-300); once with streams from rocJpegStreamParse (host memory, as the
+        sample does) and once resident.
+    Resident streams unless stated.  Returns a dict for the JSON line."""
+    import threading
+    import torch
+    import rocjpeg_amd as R
+    L = R.lib()
+    res = {}
+    b = BatchRun(dec, datas[:256], fmt, dev)
+    n = b.n
+    p = ctypes.byref(b.params)
+
+    def one(start, k):
+        st = L.rocJpegDecode(dec.handle, b.hs[start], p, ctypes.byref(b.arr[start]))
+        if st != 0:
+            raise RuntimeError(R.error_name(st))
+
+    def batched(start, k):
+        st = L.rocJpegDecodeBatched(dec.handle, _sub(b.hs, ctypes.c_void_p, start, k), k, p,
+                                    _sub(b.arr, R.RocJpegImage, start, k))
+        if st != 0:
+            raise RuntimeError(R.error_name(st))
+
+    res["decode_batch1"] = _shape_loop(one, n, 1)
+    res["batched_16"] = _shape_loop(batched, n, 16)
+    res["batched_128"] = _shape_loop(batched, n, 128)
+    shapes = b.shapes
+    b.close()
+
+    def perf_threads(resident, budget_s=1.0):
+        """jpegdecodeperf: each thread its own handle, its own images, batch 1."""
+        per = max(1, min(len(datas), 256) // threads)
+        rates, errs = [0.0] * threads, []
+        barrier = threading.Barrier(threads)
+
+        def worker(t):
+            try:
+                d = R.JpegDecoder(R.Backend.HARDWARE, dev.index or 0)
+                mine = datas[t * per:(t + 1) * per]
+                if resident:
+                    st_, streams = d.parse_device(mine)
+                    if st_ != 0:
+                        raise RuntimeError(R.error_name(st_))
+                else:
+                    streams = [R.JpegStream(x) for x in mine]
+                hs = (ctypes.c_void_p * len(streams))(*[s.handle for s in streams])
+                shp = shapes[0]
+                outs = [torch.empty(r * q, dtype=torch.uint8, device=dev) for r, q in shp]
+                img = R.make_image([o.data_ptr() for o in outs], [q for _, q in shp])
+                par = R.decode_params(fmt)
+                for j in range(2):  # warm
+                    L.rocJpegDecodeBatched(d.handle, _sub(hs, ctypes.c_void_p, j % len(streams), 1), 1,
+                                           ctypes.byref(par), ctypes.byref(img))
+                barrier.wait()
+                tot, cnt, t_end = 0.0, 0, time.perf_counter() + budget_s
+                while time.perf_counter() < t_end:
+                    j = cnt % len(streams)
+                    t0 = time.perf_counter()
+                    st_ = L.rocJpegDecodeBatched(d.handle, _sub(hs, ctypes.c_void_p, j, 1), 1, ctypes.byref(par),
+                                                 ctypes.byref(img))
+                    tot += time.perf_counter() - t0
+                    if st_ != 0:
+                        raise RuntimeError(R.error_name(st_))
+                    cnt += 1
+                rates[t] = cnt / tot if tot > 0 else 0.0
+                for s_ in streams:
+                    s_.close()
+                d.close()
+            except Exception as e:  # reported, never silent
+                errs.append(repr(e))
+                try:
+                    barrier.abort()
+                except Exception:
+                    pass
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        if errs:
+            return {"error": errs[0]}
+        return {"images_per_s_summed": round(sum(rates), 1), "threads": threads,
+                "per_thread_images_per_s": [round(r, 1) for r in rates]}
+
+    res[f"perf_threads{threads}_batch1_host_streams"] = perf_threads(False)
+    res[f"perf_threads{threads}_batch1_resident"] = perf_threads(True)
+    res["note"] = ("1080p 4:2:0 C2 images -> RGB; latency = host wall time of one synchronous call; "
+                   "jpegdecodeperf-style rates are per-thread images/s summed (jpegdecodeperf.cpp:268-271)")
+    return res
+
+
+def combined_blob(name, world, count, rank):
+    """The whole batch as one file on the node: the ranks' dataset parts concatenated (rank 0
+    writes it once; every rank memory-maps it).  Returns (path, offsets, sizes) of all
+    world x count images, offsets into that file."""
+    import torch.distributed as dist
+    base = os.path.join(data_dir(), f"{name}_v{GEN_VERSION}_all_w{world}_n{count}")
+    if rank == 0 and not (os.path.exists(base + ".bin") and os.path.exists(base + ".idx.npy")):
+        offs, sizes, pos = [], [], 0
+        tmp = f"{base}.{os.getpid()}"
+        with open(tmp + ".bin", "wb") as f:
+            for r in range(world):
+                pb = part_base(name, r, count)
+                idx = np.load(pb + ".idx.npy")
+                offs.append(idx[0].astype(np.uint64) + np.uint64(pos))
+                sizes.append(idx[1])
+                with open(pb + ".bin", "rb") as g:
+                    while True:
+                        chunk = g.read(64 << 20)
+                        if not chunk:
+                            break
+                        f.write(chunk)
+                        pos += len(chunk)
+        np.save(tmp + ".idx.npy", np.stack([np.concatenate(offs), np.concatenate(sizes)]))
+        os.replace(tmp + ".bin", base + ".bin")
+        os.replace(tmp + ".idx.npy", base + ".idx.npy")
+    dist.barrier()
+    idx = np.load(base + ".idx.npy")
+    return base + ".bin", idx[0], idx[1]
+
+
+class ShardRun(BatchRun):
+    """A rank's share of a sharded batch through the C ABI: rocJpegAmdShardCreate (collective:
+    plan + broadcast + GPU parse of this rank's images, resident), then each step is
+    rocJpegAmdShardDecode with destinations for the whole batch (only this rank's are real)."""
+
+    def __init__(self, dec, comm, blob, offs, sizes, fmt, dev):
+        import torch
+        import rocjpeg_amd as R
+        from rocjpeg_amd import shard as S
+        from tests.gpu_util import channel_shapes
+        self.R, self.dec, self.fmt, self.comm = R, dec, fmt, comm
+        t0 = time.perf_counter()
+        self.shard = S.Shard(comm, dec.handle, blob, offs, sizes)
+        if self.shard.status != 0:
+            raise RuntimeError(f"rocJpegAmdShardCreate: {R.error_name(self.shard.status)}")
+        self.parse_s = time.perf_counter() - t0
+        self.mine = self.shard.images()
+        self.datas = [bytes(blob[int(offs[i]):int(offs[i]) + int(sizes[i])]) for i in self.mine]
+        self.streams = [R.JpegStream(d) for d in self.datas]  # host-parsed twins: shapes, host-input rate
+        self.shapes = []
+        for st in self.streams:
+            nc, css, w, h = dec.image_info(st)
+            self.shapes.append(channel_shapes(fmt, css, w, h))
+        total = sum(r * p for shp in self.shapes for r, p in shp)
+        self.out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+        imgs, self.views, off = [], [], 0
+        for shp in self.shapes:
+            ptrs, pitches, vv = [], [], []
+            for r, p in shp:
+                ptrs.append(self.out[off:].data_ptr())
+                pitches.append(p)
+                vv.append(self.out[off:off + r * p].view(r, p))
+                off += r * p
+            imgs.append(R.make_image(ptrs, pitches))
+            self.views.append(vv)
+        self.params = R.decode_params(fmt)
+        self.n = len(self.mine)
+        self.arr = (R.RocJpegImage * max(1, self.n))(*imgs)
+        self.arr_all = (R.RocJpegImage * len(offs))()
+        for k, i in enumerate(self.mine):
+            self.arr_all[i] = imgs[k]
+
+    def step(self):
+        st = self.shard.decode(self.params, self.arr_all)
+        if st != 0:
+            raise RuntimeError(self.R.error_name(st))
+
+    def close(self):
+        self.shard.close()
+        self.comm.close()
+        super().close()
+
+
 def kernel_table(t, n):
     """(summed launch ms per call, launches per call, units (images) per launch) per kernel of
     a profiled pass; the pipelined K1/K2 launches each take an equal share of the intervals."""
@@ -476,54 +682,46 @@ def main():
 
     import rocjpeg_amd as R
     from rocjpeg_amd import shard as S
-    # ---- the work table: rank 0 reads every part's headers, LPT over the ranks, one broadcast ----
-    parts = [np.memmap(mine[0], dtype=np.uint8, mode="r") if r == rank else None for r in range(world)]
-    idx = [None] * world
-    for r in range(world):
-        base = part_base(args.workload, r, args.batch)
-        if parts[r] is None:
-            parts[r] = np.memmap(base + ".bin", dtype=np.uint8, mode="r")
-        idx[r] = np.load(base + ".idx.npy")
-    blob = S.Blob(parts)
-    t_tab = time.perf_counter()
-    table, shard_cost = None, None
-    if rank == 0:
-        table = S.concat_tables([S.build_work_table(np.asarray(parts[r]), idx[r][0], idx[r][1], blob.part_base(r))
-                                 for r in range(world)])
-        shard_cost = S.assign_shards(table, world, list(range(world)))
-    t_build = time.perf_counter() - t_tab
-    # the one collective: through the library's own RCCL communicator (rocJpegAmdCommInitRank /
-    # rocJpegAmdBroadcastWorkTable, the C-ABI path a C caller takes); ranks sharing a GPU (the
-    # rehearsal) cannot form an RCCL communicator and use torch.distributed over gloo instead
-    bcast_via = "none (one rank)"
-    if world > 1:
-        total = int(sum(len(idx[r][0]) for r in range(world)))
-        comm = None
-        if not share:
-            try:
-                uid = torch.zeros(128, dtype=torch.uint8, device=cdev)
-                if rank == 0:
-                    uid.copy_(torch.frombuffer(bytearray(S.comm_unique_id()), dtype=torch.uint8))
-                dist.broadcast(uid, src=0)
-                comm = S.Comm(gpu, world, rank, bytes(uid.cpu().numpy()))
-            except RuntimeError as e:  # reported in the line, never silent
-                bcast_via = f"torch.distributed ({e})"
-        if comm is not None:
-            table = comm.broadcast_table(table, total)
-            comm.close()
-            bcast_via = "RCCL: rocJpegAmdBroadcastWorkTable (librocjpeg_amd.so)"
-        else:
-            table = S.broadcast_table(table, src=0, device=cdev)
-            if share:
-                bcast_via = "torch.distributed gloo (RJ_BENCH_SHARE_GPU rehearsal)"
-    t_tab = time.perf_counter() - t_tab
-    my = S.shard_of(table, rank)
-    datas = [blob.get(o, s) for o, s in zip(my["stream_offset"], my["stream_bytes"])]
-
     dec = R.JpegDecoder(R.Backend.HARDWARE, gpu)
     dec.set_path_policy(args.path)
     fmt = getattr(R.OutputFormat, wl["fmt"])
-    run = BatchRun(dec, datas, fmt, dev)
+    t_tab = time.perf_counter()
+    shard_cost, bcast_via = None, "none (one rank)"
+    if world == 1:
+        # N = 1: the drop-in call itself, rocJpegDecodeBatched over resident streams
+        raw = np.memmap(mine[0], dtype=np.uint8, mode="r")
+        datas = [bytes(raw[int(o):int(o) + int(z)]) for o, z in zip(mine[1], mine[2])]
+        table = S.build_work_table(raw, mine[1], mine[2])
+        del raw
+        shard_cost = S.assign_shards(table, 1)
+        t_build = t_tab = time.perf_counter() - t_tab
+        run = BatchRun(dec, datas, fmt, dev)
+    else:
+        # N > 1: the C-ABI sharded entry a C caller uses (include/rocjpeg_amd.h): the batch is one
+        # blob on the node (the ranks' parts concatenated), rocJpegAmdShardCreate plans on rank 0,
+        # broadcasts the 64-B work table over the library's own communicator (RCCL; ranks that
+        # share a GPU in the RJ_BENCH_SHARE_GPU rehearsal use its shared-memory test transport)
+        # and keeps this rank's images resident; each step is rocJpegAmdShardDecode.
+        path, offs, sizes = combined_blob(args.workload, world, args.batch, rank)
+        blob = np.memmap(path, dtype=np.uint8, mode="r")
+        if share:
+            os.environ["RJ_COMM_TEST_SHM"] = f"/dev/shm/rj_bench_comm_{os.environ.get('MASTER_PORT', '0')}"
+            if rank == 0 and os.path.exists(os.environ["RJ_COMM_TEST_SHM"]):
+                os.unlink(os.environ["RJ_COMM_TEST_SHM"])
+            dist.barrier()
+        uid = torch.zeros(128, dtype=torch.uint8, device=cdev)
+        if rank == 0 and not share:
+            uid.copy_(torch.frombuffer(bytearray(S.comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, src=0)
+        comm = S.Comm(gpu, world, rank, bytes(uid.cpu().numpy()))
+        t_tab = time.perf_counter()
+        run = ShardRun(dec, comm, blob, offs, sizes, fmt, dev)
+        t_tab = t_build = time.perf_counter() - t_tab
+        table = run.shard.table
+        shard_cost = [int(table["cost"][table["shard"] == r].sum()) for r in range(world)]
+        bcast_via = ("rocJpegAmdShardCreate / rocJpegAmdShardDecode (librocjpeg_amd.so): work table over "
+                     + ("the shared-memory test transport (RJ_BENCH_SHARE_GPU rehearsal)" if share else "RCCL"))
+    datas = run.datas
     n = run.n
 
     elapsed = run.timed(args.steps, args.warmup, world, cdev)
@@ -555,6 +753,13 @@ def main():
         s.parse(s._data)
     parse_host_rate = n / (time.perf_counter() - t_p)
     del host_streams
+
+    shapes_res = None
+    if rank == 0 and world == 1 and not args.no_extras:
+        try:
+            shapes_res = call_shapes(dec, datas, fmt, dev)
+        except Exception as e:  # reported in the line, never silent
+            shapes_res = {"error": repr(e)}
 
     res = None
     if rank == 0:
@@ -591,12 +796,15 @@ def main():
                                    "gpu_marker_scan": round(n / run.parse_s, 1)},
             "parity_timed_output": parity,
             "parity_timed_output_images": len(parity_sample(n)),
-            "work_table": {"images": int(len(table)), "bytes": int(table.nbytes), "build_ms": round(t_build * 1e3, 2),
-                           "build_and_broadcast_ms": round(t_tab * 1e3, 2), "broadcast": bcast_via,
+            "work_table": {"images": int(len(table)), "bytes": int(table.nbytes),
+                           "build_ms" if world == 1 else "create_ms": round(t_build * 1e3, 2),
+                           "broadcast": bcast_via,
                            "lpt_imbalance": round(S.imbalance(shard_cost), 5),
                            "images_per_rank": [int((table["shard"] == r).sum()) for r in range(world)]},
             "dataset_gen_s": round(t_gen, 1),
         }
+        if shapes_res is not None:
+            res["call_shapes"] = shapes_res
         if t["prog_images"]:
             res["progressive_detail"] = {"images": t["prog_images"], "intervals": t["prog_intervals"],
                                          "levels": t["prog_levels"], "k1p_ms": round(t["prog_entropy_ms"], 4),

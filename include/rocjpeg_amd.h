@@ -134,7 +134,9 @@ typedef struct {
   int32_t dest_device;         /* device the decoded image is written on */
   uint32_t index;              /* position in the batch */
   uint64_t cost;               /* LPT weight: ROCJPEG_AMD_COST_BYTE x ecs_bytes + pixels
-                                  (progressive: ROCJPEG_AMD_COST_BYTE_PROG per byte) */
+                                  + ROCJPEG_AMD_COST_INTERVAL x mean restart-interval bytes
+                                  (capped at ROCJPEG_AMD_COST_INTERVAL_CAP); progressive:
+                                  ROCJPEG_AMD_COST_BYTE_PROG per byte + pixels */
   uint64_t reserved;
 } RocJpegAmdWorkItem;
 #define ROCJPEG_AMD_WORK_PROGRESSIVE 1u
@@ -142,6 +144,8 @@ typedef struct {
 #define ROCJPEG_AMD_WORK_UNSUPPORTED 4u /* parsed, but the decode call would refuse it */
 #define ROCJPEG_AMD_COST_BYTE 8u        /* measured: K1 spends ~8x per ECS byte what K2 spends per pixel */
 #define ROCJPEG_AMD_COST_BYTE_PROG 120u /* progressive scans: serial refinement chains */
+#define ROCJPEG_AMD_COST_INTERVAL 64u   /* per byte of the mean restart interval: K1's chain length */
+#define ROCJPEG_AMD_COST_INTERVAL_CAP 12288u /* longer intervals are cut into chunk lanes (rj_entropy.hip) */
 
 /* Fill items[0..count) from the JPEGs at blob + offsets[i] (sizes[i] bytes each, inside the
  * blob_bytes of the blob: INVALID_PARAMETER otherwise, before anything is read).  Returns

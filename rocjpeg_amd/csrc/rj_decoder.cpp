@@ -528,7 +528,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   jobs.clear();
   uint64_t destuff_total = 0, coef_blocks = 0, ent_total = 0, plane_bytes = 0, stage_bytes = 0;
   uint32_t seg_total = 0, rows_total = 0, chunk_total = 0, ds_total = 0;
-  uint64_t ecs_bytes = 0, out_bytes = 0, ecs_stage_bytes = 0;
+  uint64_t ecs_bytes = 0, out_bytes = 0, ecs_stage_bytes = 0, ecs_copy_bytes = 0;
   std::vector<uint64_t> &stage_off = sc_.stage_off, &ecs_off = sc_.ecs_off;
   stage_off.assign(n, UINT64_MAX);
   ecs_off.assign(n, UINT64_MAX);
@@ -622,8 +622,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       // staging, which is uploaded in chunks as the host threads fill it
       stage_off[i] = stage_bytes;
       stage_bytes += AlignUp(p.segs.size() * sizeof(RjSegDev), 256) + AlignUp(p.ds.size() * sizeof(RjDsBlock), 256);
-      ecs_off[i] = ecs_stage_bytes;
-      ecs_stage_bytes += AlignUp(in.ecs_size + 16, 256);  // K0 reads <= 8 B past the end
+      if (s->pinned_ecs() == nullptr) {  // copied by the host threads (offsets in the copy space)
+        ecs_off[i] = ecs_copy_bytes;
+        ecs_copy_bytes += AlignUp(in.ecs_size + 16, 256);  // K0 reads <= 8 B past the end
+      }
       if (p.progressive)
         stage_bytes += AlignUp(p.pscans.size() * sizeof(RjProgScanDev), 256) +
                        AlignUp(p.pivals.size() * sizeof(RjProgIvalDev), 256) +
@@ -1012,6 +1014,44 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     for (int i = 0; i < n; i++) imgs[i].dc_diff = streams[i]->plan().progressive ? 0u : 1u;
   timings_.lean_k1 = lean ? 1u : 0u;
 
+  // ---- non-resident bitstreams: runs of streams whose ECS sit next to each other in the
+  // parse-time pinned arena (rj_pinned.h) go up with one DMA per run, straight from the arena;
+  // the device staging mirrors each run (gaps included).  Streams without a pinned copy follow
+  // in the copy space, filled by the host threads below. ----
+  std::vector<PinRun> &pin_runs = sc_.pin_runs;
+  pin_runs.clear();
+  uint64_t pin_bytes = 0;
+  {
+    constexpr uint64_t kMaxGap = 64u << 10;  // bytes between two slots a run may carry along
+    for (int i = 0; i < n; i++) {
+      if (stage_off[i] == UINT64_MAX) continue;
+      const uint8_t *hp = streams[i]->pinned_ecs();
+      if (hp == nullptr) continue;
+      const uint64_t len = uint64_t(streams[i]->info().ecs_size) + 16;
+      const PinnedChunk *ch = streams[i]->pinned_chunk();
+      if (!pin_runs.empty() && pin_runs.back().chunk == ch && hp >= pin_runs.back().host &&
+          uint64_t(hp - pin_runs.back().host) <= pin_runs.back().len + kMaxGap) {
+        PinRun &r = pin_runs.back();
+        r.len = std::max<uint64_t>(r.len, uint64_t(hp - r.host) + len);
+      } else {
+        pin_runs.push_back(PinRun{hp, len, 0, ch});
+      }
+      ecs_off[i] = uint64_t(hp - pin_runs.back().host) | (uint64_t(pin_runs.size() - 1) << 40);  // run-relative for now
+    }
+    for (PinRun &r : pin_runs) {
+      r.dev = pin_bytes;
+      pin_bytes += AlignUp(r.len, 256);
+    }
+    for (int i = 0; i < n; i++) {
+      if (stage_off[i] == UINT64_MAX) continue;
+      if (streams[i]->pinned_ecs() != nullptr)
+        ecs_off[i] = pin_runs[ecs_off[i] >> 40].dev + (ecs_off[i] & ((1ull << 40) - 1));
+      else
+        ecs_off[i] += pin_bytes;
+    }
+    ecs_stage_bytes = pin_bytes + ecs_copy_bytes;
+  }
+
   // ---- one pinned staging blob, uploaded in two parts: A (descriptors, tables, non-resident
   // bitstreams) before K0; B (K1 lane order, K2 row lists) after K0 is launched -- the lane
   // sort and row classes below are host work that then runs while K0 executes. ----
@@ -1096,7 +1136,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   uint8_t *h = h_stage_.data();
   uint8_t *dbase = d_desc_.as<uint8_t>();
   if (ecs_stage_bytes) {
-    RJ_CHECK(h_ecs_.Ensure(ecs_stage_bytes));
+    if (ecs_copy_bytes) RJ_CHECK(h_ecs_.Ensure(ecs_copy_bytes));
     RJ_CHECK(d_ecs_.Ensure(ecs_stage_bytes));
   }
   uint8_t *hecs = h_ecs_.data();
@@ -1136,7 +1176,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
   }
   if (profiling_) RJ_HIP(hipEventRecord(ev_[0], stream_));
-  if (stage_bytes || ecs_stage_bytes) {
+  for (const PinRun &r : pin_runs)  // parse-time pinned bitstreams: straight to the device
+    RJ_HIP(hipMemcpyAsync(decs + r.dev, r.host, r.len, hipMemcpyHostToDevice, stream_));
+  if (stage_bytes || ecs_copy_bytes) {
     // host threads copy the non-resident streams' tables and bitstreams into pinned memory, in
     // chunks of consecutive images (~2 MB of bitstream each); this thread uploads the finished
     // prefix of the staging area in DMA transfers of >= 32 MB (a 285-MB batch in 4-MB transfers
@@ -1152,7 +1194,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         chunk_img.push_back(uint32_t(i));
         acc = 0;
       }
-      acc += streams[i]->info().ecs_size;
+      acc += streams[i]->pinned_ecs() ? 4096u : streams[i]->info().ecs_size;  // pinned: tables only
     }
     chunk_img.push_back(uint32_t(n));
     const int nchunk = int(chunk_img.size()) - 1;
@@ -1175,7 +1217,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
               std::memcpy(h + vo, p.pivals.data(), p.pivals.size() * sizeof(RjProgIvalDev));
               if (!p.ptabs.empty()) std::memcpy(h + to, p.ptabs.data(), p.ptabs.size() * sizeof(RjHuffDev));
             }
-            std::memcpy(hecs + ecs_off[i], s->info().ecs, s->info().ecs_size);
+            if (s->pinned_ecs() == nullptr)
+              std::memcpy(hecs + (ecs_off[i] - pin_bytes), s->info().ecs, s->info().ecs_size);
           }
         },
         [&](int k) {
@@ -1183,16 +1226,17 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
           while (i0 < i1 && stage_off[i0] == UINT64_MAX) i0++;
           uint64_t lo = UINT64_MAX, hi = 0;
           for (uint32_t i = i0; i < i1; i++)
-            if (stage_off[i] != UINT64_MAX) {
-              lo = std::min(lo, ecs_off[i]);
-              hi = std::max(hi, ecs_off[i] + streams[i]->info().ecs_size);
+            if (stage_off[i] != UINT64_MAX && streams[i]->pinned_ecs() == nullptr) {  // copy space
+              lo = std::min(lo, ecs_off[i] - pin_bytes);
+              hi = std::max(hi, ecs_off[i] - pin_bytes + streams[i]->info().ecs_size);
             }
           if (hi > lo) {
             dma_lo = std::min(dma_lo, lo);
             dma_hi = std::max(dma_hi, hi);
           }
           if (dma_hi > dma_lo && (dma_hi - dma_lo >= kDmaBytes || k == nchunk - 1) && up_err == hipSuccess) {
-            up_err = hipMemcpyAsync(decs + dma_lo, hecs + dma_lo, dma_hi - dma_lo, hipMemcpyHostToDevice, stream_);
+            up_err = hipMemcpyAsync(decs + pin_bytes + dma_lo, hecs + dma_lo, dma_hi - dma_lo, hipMemcpyHostToDevice,
+                                    stream_);
             dma_lo = UINT64_MAX;
             dma_hi = 0;
           }

@@ -136,8 +136,15 @@ class Decoder {
   hipEvent_t k1s_[kMaxPipe] = {}, k2s_[kMaxPipe] = {}, k2e_[kMaxPipe] = {};  // profiling: launch spans
   DeviceBuffer d_count_;  // profiling: entries written by K1
 
+  // a run of non-resident streams whose parse-time pinned copies are adjacent (one DMA)
+  struct PinRun {
+    const uint8_t *host;
+    uint64_t len, dev;  // bytes; offset in the device ECS staging
+    const PinnedChunk *chunk;
+  };
   // host planning scratch, reused across calls (no per-call allocation / page faults)
   struct Scratch {
+    std::vector<PinRun> pin_runs;
     std::vector<RjImageDev> imgs;
     std::vector<RjJobDev> jobs;
     std::vector<uint64_t> stage_off, ecs_off;

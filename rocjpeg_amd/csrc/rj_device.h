@@ -204,11 +204,17 @@ struct RjTableSet {
 
 // ---- lean K1 (rj_huff.hip): "row" images, whose every restart interval lies inside one MCU
 // row, are decoded into raw entries and K2 restores the DC predictions ----
-// One 32-bit table entry per code prefix; every field the symbol step needs is in it:
-//   [4:0]  (32 - n) & 31, n = code bits + extra bits (the bit-field offset of the extra bits)
-//   [12:8] n                       [13] the symbol writes an entry (DC; AC coefficient)
-//   [19:16] s (extra bits)         [27:21] R: zigzag run (DC 0; AC r; ZRL 15; EOB 63 -> k >= 64)
-//   bit 31: code longer than the first level: [7:0] = AC second-level subtable, 0xFF = search
+// One 32-bit table entry per code prefix; every field the symbol step needs is in it, for the
+// symbol the prefix starts with (high half) and, where the prefix also holds the whole code of
+// the symbol after it, for that second symbol (low half: a two-symbol step, rj_huff.hip):
+//   [20:16] n1 = code bits + extra bits   [24:21] s1 (extra bits)
+//   [30:25] R1: zigzag run (DC 0; AC r; ZRL 15; EOB 63 -> k >= 64)
+//   [31]    code longer than the first level: [7:0] = AC second-level subtable, 0xFF = search
+//   [4:0]   n2    [8:5] s2    [14:9] R2    [15] the second symbol is present
+// A second symbol is recorded only after an AC coefficient or ZRL whose bits and the second
+// code all lie inside the first-level key; the step takes it when the first symbol leaves the
+// block open (k + R1 + 1 < 64).  Whether a symbol writes an entry follows from the fields: a DC
+// symbol (k == 0) always, an AC symbol when s != 0.
 // First levels: DC 9 bits, AC 11 bits; AC codes of 12..16 bits: up to RJ_HL_SUBS subtables of
 // 32 entries (the next 5 bits) per table.
 #define RJ_HL_DC_BITS 9
@@ -217,6 +223,7 @@ struct RjTableSet {
 #define RJ_HL_AC_WORDS ((1 << RJ_HL_AC_BITS) + RJ_HL_SUBS * 32)
 #define RJ_HL_DC_WORDS (1 << RJ_HL_DC_BITS)
 #define RJ_HL_ESC 0x80000000u
+#define RJ_HL_PAIR 0x8000u
 struct RjLeanTables {  // LDS image: AC0, AC1 (first level + subtables), DC0, DC1
   uint32_t ac[2][RJ_HL_AC_WORDS];
   uint32_t dc[2][RJ_HL_DC_WORDS];

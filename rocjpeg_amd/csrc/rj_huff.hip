@@ -29,8 +29,9 @@ namespace rj {
 #define RJ_HL_CHUNKS 8                      // 16-B chunks in a lane's bit ring
 #define RJ_HL_WORDS (RJ_HL_CHUNKS * 4)      // 32 words
 #ifndef RJ_HL_PHASE
-#define RJ_HL_PHASE 16                      // symbols per phase of the whole-interval launch (8: +3.5 % K1)
+#define RJ_HL_PHASE 8                       // steps (1-2 symbols each) per phase of the whole-interval launch
 #endif
+#define RJ_HL_GROUP 16                      // entries per flush group (RJ_ENT_GROUP)
 // LDS byte offsets of the four tables (RjLeanTables order)
 #define RJ_HL_AC_BYTES (RJ_HL_AC_WORDS * 4)
 #define RJ_HL_DC0 (2 * RJ_HL_AC_BYTES)
@@ -98,7 +99,7 @@ __device__ __forceinline__ void hl_flush(const HCol<S> &stage, uint32_t from, ui
 }
 
 // Codes the first level does not resolve (rare): AC second level, or libjpeg's canonical
-// search (jpeg_huff_decode) on the table in HBM, repacked into the entry format.
+// search (jpeg_huff_decode) on the table in HBM, repacked into the entry format (one symbol).
 __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool isdc, uint32_t acbase,
                                            const uint32_t *s_lut, const RjTableSet *ts, uint32_t ids) {
   const uint32_t sub = e & 0xFFu;
@@ -116,20 +117,22 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
     }
   const uint32_t s = sym & 15u, r = sym >> 4;
   const uint32_t R = isdc ? 0u : (s ? r : (r == 15 ? 15u : 63u));
-  const uint32_t emit = (isdc || s) ? 1u : 0u;
-  const uint32_t n = len + s;
-  return ((32u - n) & 31u) | (n << 8) | (emit << 13) | (s << 16) | (R << 21);
+  return ((len + s) << 16) | (s << 21) | (R << 25);
 }
 
-// One symbol step.  SAFE: per-lane activity (blocks_left) and libjpeg's insufficient-data rule.
-// SYNC (split launch): the lane notes where its last MCU started (mpos, mleft), and a tail lane
-// records its MCU starts (recs, nr; head lanes keep nr = RJ_HL_REC and write a scratch slot).
+// One symbol step -- one or two symbols (rj_device.h RjLeanTables: a table entry may carry the
+// code that follows the first one, when both lie inside the first-level key).  SAFE: per-lane
+// activity (blocks_left) and libjpeg's insufficient-data rule.  SYNC (split launch): the lane
+// notes where its last MCU started (mpos, mleft), and a tail lane records its MCU starts (recs,
+// nr; head lanes keep nr = RJ_HL_REC and write a scratch slot).  A block ends at most once per
+// step (the second symbol is taken only when the first leaves the block open), so MCU starts,
+// the insufficient-data rule and the records see the same block boundaries as one symbol per
+// step would.
 // Software-pipelined: a step starts with this symbol's entry `e` and its 32-bit `peek` already
 // loaded (by the previous step, or the prologue); it first advances the bit position and the
 // block / table state -- the chain the next lookup depends on -- and issues the next symbol's
-// LDS lookup, then does this symbol's remaining work (its entry into the stage, the counters)
-// while that lookup is in flight.  (Issued in the other order, the lookup's LDS latency sat
-// unhidden on every symbol: ~40 instructions and ~310 cycles per symbol.)
+// LDS lookup, then does this step's remaining work (its entries into the stage, the counters)
+// while that lookup is in flight.
 #define RJ_HL_STEP(SAFE, SYNC)                                                                                  \
   do {                                                                                                    \
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(e >= RJ_HL_ESC) != 0, 0)) {                          \
@@ -138,8 +141,14 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
     }                                                                                                     \
     /* ---- the chain: bit position, block / table state, the next lookup ---- */                      \
     const uint32_t qold = q;                                                                              \
-    q -= (e >> 8) & 31u;                                                                                  \
-    uint32_t kn = k + ((e >> 21) & 127u) + 1u;                                                            \
+    const uint32_t R1 = (e >> 25) & 63u, n1 = (e >> 16) & 31u;                                            \
+    const uint32_t k1 = k + R1 + 1u;                                                                      \
+    /* the second symbol: present, and the first leaves the block open (k >= 1: an AC symbol) */       \
+    bool use2 = (e & RJ_HL_PAIR) != 0u && k + R1 - 1u < 62u;                                              \
+    if (SAFE) use2 = use2 && !skip;                                                                       \
+    const uint32_t n2 = e & 31u, R2 = (e >> 9) & 63u;                                                     \
+    q -= n1 + (use2 ? n2 : 0u);                                                                           \
+    uint32_t kn = use2 ? k1 + R2 + 1u : k1;                                                               \
     if (SAFE) kn = skip ? 64u : kn;                                                                       \
     {                                                                                                     \
       const bool adv = (qold ^ q) > 31u; /* the bit position entered the next word */                   \
@@ -161,16 +170,17 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
     const uint32_t peekn = __builtin_amdgcn_alignbit(wa, wb, q);                                          \
     const uint32_t en = s_lut[(tbn >> 2) + (peekn >> tshn)];                                              \
     wc = ring[rr & (RJ_HL_WORDS - 1)];                                                                    \
-    /* ---- this symbol's entry, while the lookup is in flight ---- */                                  \
-    /* the coefficient: HUFF_EXTEND of the s extra bits (the low s of the symbol's n bits,          \
-       right-aligned), and its position kcur + R clamped to 63 (libjpeg's natural-order table) */   \
-    const uint32_t raw = peek >> (e & 31u);                                                               \
-    const uint32_t xm = (1u << ((e >> 16) & 15u)) - 1u; /* v_bfm */                                      \
+    /* ---- this step's entries, while the lookup is in flight ---- */                                  \
+    /* a coefficient: HUFF_EXTEND of the s extra bits (the low s of the symbol's n bits,            \
+       right-aligned), and its position clamped to 63 (libjpeg's natural-order table) */            \
+    const uint32_t s1 = (e >> 21) & 15u;                                                                  \
+    const uint32_t raw = peek >> (32u - n1);                                                              \
+    const uint32_t xm = (1u << s1) - 1u; /* v_bfm */                                                     \
     const uint32_t xb = raw & xm;                                                                         \
     const uint32_t xv = xb > xm - xb ? xb : xb - xm; /* top extra bit clear: negative */               \
-    const uint32_t xp = min(kcur + ((e >> 21) & 127u), 63u);                                              \
+    const uint32_t xp = min(kcur + R1, 63u);                                                              \
     uint32_t entry = __builtin_amdgcn_perm(xp, xv, 0x05040100u); /* value's low half | position << 16 */ \
-    uint32_t emit = (e >> 13) & 1u;                                                                       \
+    uint32_t emit = (kcur == 0u || s1 != 0u) ? 1u : 0u; /* DC always; AC coefficients */              \
     if (SAFE) {                                                                                           \
       entry = skip ? RJ_RE_ZERO : entry; /* libjpeg: the rest of the interval is zero blocks */          \
       emit = skip ? 1u : emit;                                                                            \
@@ -178,6 +188,18 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
     }                                                                                                     \
     stage[ne & (kStage - 1)] = entry; /* a non-emitted write lands in the next free slot */                \
     ne += emit;                                                                                           \
+    {                                                                                                     \
+      const uint32_t s2 = (e >> 5) & 15u;                                                                 \
+      const uint32_t raw2 = peek >> ((32u - n1 - n2) & 31u);                                              \
+      const uint32_t xm2 = (1u << s2) - 1u;                                                               \
+      const uint32_t xb2 = raw2 & xm2;                                                                    \
+      const uint32_t xv2 = xb2 > xm2 - xb2 ? xb2 : xb2 - xm2;                                             \
+      const uint32_t xp2 = min(k1 + R2, 63u);                                                             \
+      uint32_t emit2 = (use2 && s2 != 0u) ? 1u : 0u;                                                      \
+      if (SAFE) emit2 = blocks_left > 0 ? emit2 : 0u;                                                     \
+      stage[ne & (kStage - 1)] = __builtin_amdgcn_perm(xp2, xv2, 0x05040100u);                            \
+      ne += emit2;                                                                                        \
+    }                                                                                                     \
     if (SAFE) {                                                                                           \
       const bool act = blocks_left > 0;                                                                   \
       blocks_left -= (bend && act) ? 1u : 0u;                                                             \
@@ -232,6 +254,8 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0, uint32_t nlanes, const uint8_t *__restrict__ destuffed,
     const RjTableSet *__restrict__ tabsets, const RjLeanTables *__restrict__ lean, RjCoefBuf coefs, RjHuffSplit split) {
   constexpr uint32_t kStage = 2 * GROUP;
+  // a phase adds <= 2 PHASE entries to < GROUP pending ones: the stage must hold them
+  static_assert(2 * PHASE <= GROUP + 1, "stage too small for a phase of two-symbol steps");
   constexpr uint32_t kPairs = kSplit ? DEC / 2 : 1;
   __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_HL_WORDS][DEC];
   __shared__ __attribute__((aligned(16))) uint32_t s_stage[kStage][DEC];
@@ -504,11 +528,11 @@ hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uin
                            RjCoefBuf coefs, uint32_t extra_lds, const RjHuffSplit *split) {
   if (nlanes == 0) return hipSuccess;
   if (split != nullptr) {  // outliers split: one decoder wave per SIMD, two workgroups per CU
-    hipLaunchKernelGGL((k_huff<RJ_HL_SPLIT_DEC, 8, true, 8>), dim3((nlanes + RJ_HL_SPLIT_DEC - 1) / RJ_HL_SPLIT_DEC),
+    hipLaunchKernelGGL((k_huff<RJ_HL_SPLIT_DEC, 8, true, 4>), dim3((nlanes + RJ_HL_SPLIT_DEC - 1) / RJ_HL_SPLIT_DEC),
                        dim3(2 * RJ_HL_SPLIT_DEC), 0, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs,
                        *split);
   } else {
-    hipLaunchKernelGGL((k_huff<256, RJ_HL_PHASE, false, RJ_HL_PHASE>), dim3((nlanes + 255) / 256), dim3(512), extra_lds,
+    hipLaunchKernelGGL((k_huff<256, RJ_HL_GROUP, false, RJ_HL_PHASE>), dim3((nlanes + 255) / 256), dim3(512), extra_lds,
                        st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs, RjHuffSplit{0, 0});
   }
   return hipGetLastError();

@@ -1,0 +1,105 @@
+// rj_pinned.cpp -- the pinned host arena of parsed bitstreams (rj_pinned.h).
+#include "rj_pinned.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+namespace rj {
+
+struct PinnedChunk {
+  uint8_t *base = nullptr;
+  size_t size = 0;
+};
+
+namespace {
+
+constexpr size_t kChunkBytes = 64ull << 20;
+constexpr size_t kMaxFreeChunks = 8;  // released chunks kept for reuse (512 MB)
+
+struct Arena {
+  std::mutex mu;
+  std::shared_ptr<PinnedChunk> cur;  // the chunk slots are carved from
+  size_t used = 0;
+  std::vector<uint8_t *> free_chunks;  // buffers of released kChunkBytes chunks
+  int state = 0;                        // 0 unprobed, 1 usable, -1 disabled
+};
+
+Arena &TheArena() {
+  static Arena *a = new Arena;  // never destroyed: slots may outlive static destructors
+  return *a;
+}
+
+void ReturnBuffer(uint8_t *p, size_t size) {
+  Arena &a = TheArena();
+  {
+    std::lock_guard<std::mutex> l(a.mu);
+    if (size == kChunkBytes && a.free_chunks.size() < kMaxFreeChunks) {
+      a.free_chunks.push_back(p);
+      return;
+    }
+  }
+  (void)hipHostFree(p);
+}
+
+// caller holds a.mu
+std::shared_ptr<PinnedChunk> NewChunk(Arena &a, size_t size) {
+  uint8_t *p = nullptr;
+  if (size == kChunkBytes && !a.free_chunks.empty()) {
+    p = a.free_chunks.back();
+    a.free_chunks.pop_back();
+  } else if (hipHostMalloc(reinterpret_cast<void **>(&p), size, hipHostMallocNonCoherent) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return std::shared_ptr<PinnedChunk>(new PinnedChunk{p, size}, [](PinnedChunk *c) {
+    ReturnBuffer(c->base, c->size);
+    delete c;
+  });
+}
+
+}  // namespace
+
+PinnedSlot PinnedAlloc(size_t bytes) {
+  PinnedSlot s;
+  Arena &a = TheArena();
+  const size_t need = (bytes + 255) & ~size_t(255);
+  std::shared_ptr<PinnedChunk> retired;  // released after the lock (its deleter takes the lock)
+  std::lock_guard<std::mutex> l(a.mu);
+  if (a.state == 0) {
+    const char *v = std::getenv("ROCJPEG_AMD_PARSE_PIN");
+    int ndev = 0;
+    const bool off = v != nullptr && v[0] == '0';
+    a.state = (!off && hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0) ? 1 : -1;
+    (void)hipGetLastError();
+  }
+  if (a.state < 0 || bytes == 0) return s;
+  std::shared_ptr<PinnedChunk> c;
+  uint8_t *p = nullptr;
+  if (need > kChunkBytes / 4) {  // a large stream gets a chunk of its own
+    c = NewChunk(a, need);
+    if (c) p = c->base;
+  } else {
+    if (!a.cur || a.used + need > a.cur->size) {
+      retired = std::move(a.cur);
+      a.cur = NewChunk(a, kChunkBytes);
+      a.used = 0;
+    }
+    if (a.cur) {
+      c = a.cur;
+      p = c->base + a.used;
+      a.used += need;
+    }
+  }
+  if (p != nullptr) {
+    s.ptr = p;
+    s.bytes = bytes;
+    s.chunk = std::move(c);
+  }
+  return s;
+}
+
+}  // namespace rj

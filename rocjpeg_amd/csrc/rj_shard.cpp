@@ -55,7 +55,15 @@ void FillItem(const unsigned char *data, uint32_t size, uint32_t index, uint64_t
     const uint32_t total = p.mcux * p.mcuy, ri = in.restart_interval;
     it->restart_intervals = (ri && total) ? (total + ri - 1) / ri : 1u;
   }
-  it->cost = (it->flags & ROCJPEG_AMD_WORK_UNSUPPORTED) ? 0 : per_byte * it->ecs_bytes + uint64_t(in.width) * in.height;
+  // K1's time on a shard is set by its longest serial chain as well as by its total bytes: the
+  // mean restart-interval length (capped where the chunk lanes take over, RJ_SPLIT_BYTES) weighs
+  // in, so LPT deals images with long intervals (e.g. the 3840-wide rows of C4) across the shards
+  // before the rest
+  const uint64_t ival = p.progressive ? 0u : std::min<uint64_t>(it->ecs_bytes / std::max(1u, it->restart_intervals),
+                                                                ROCJPEG_AMD_COST_INTERVAL_CAP);
+  it->cost = (it->flags & ROCJPEG_AMD_WORK_UNSUPPORTED)
+                 ? 0
+                 : per_byte * it->ecs_bytes + uint64_t(in.width) * in.height + ROCJPEG_AMD_COST_INTERVAL * ival;
 }
 
 }  // namespace

@@ -40,15 +40,14 @@ uint64_t Fnv1a(uint64_t h, const void *p, size_t n) {
 
 }  // namespace
 
-// Lean K1 entry of a resolved code (rj_device.h RjLeanTables).  libjpeg semantics: DC symbol =
-// difference category s; AC symbol (r, s): s != 0 a coefficient after r zeros, (15, 0) ZRL, any
-// other (r, 0) ends the block (decode_mcu: `if (r != 15) break`).
+// Lean K1 entry of a resolved code (rj_device.h RjLeanTables), the first-symbol half.  libjpeg
+// semantics: DC symbol = difference category s; AC symbol (r, s): s != 0 a coefficient after r
+// zeros, (15, 0) ZRL, any other (r, 0) ends the block (decode_mcu: `if (r != 15) break`).
 static uint32_t LeanEntry(uint32_t len, uint32_t sym, bool is_dc) {
   const uint32_t s = sym & 15u, r = sym >> 4;
   const uint32_t R = is_dc ? 0u : (s ? r : (r == 15 ? 15u : 63u));
-  const uint32_t emit = (is_dc || s) ? 1u : 0u;
   const uint32_t n = len + s;
-  return ((32u - n) & 31u) | (n << 8) | (emit << 13) | (s << 16) | (R << 21);
+  return (n << 16) | (s << 21) | (R << 25);
 }
 
 static void FillLeanBad(bool is_dc, uint32_t *first, uint32_t *subs) {
@@ -57,6 +56,27 @@ static void FillLeanBad(bool is_dc, uint32_t *first, uint32_t *subs) {
   for (int e = 0; e < (1 << B); e++) first[e] = bad;
   if (subs)
     for (int e = 0; e < RJ_HL_SUBS * 32; e++) subs[e] = bad;
+}
+
+// The second-symbol halves of an AC first level (rj_device.h): for each key whose first symbol
+// is an AC coefficient or ZRL with n1 < RJ_HL_AC_BITS, the code that starts at bit n1, if it is
+// complete inside the key (its extra bits may run past it: the step reads them from its 32-bit
+// peek, n1 + n2 <= 11 + 10 bits).
+static void AddLeanPairs(uint32_t *first) {
+  const uint32_t B = RJ_HL_AC_BITS;
+  std::vector<uint32_t> one(first, first + (1u << B));  // first-symbol entries only
+  for (uint32_t key = 0; key < (1u << B); key++) {
+    const uint32_t e = one[key];
+    if (e & RJ_HL_ESC) continue;
+    const uint32_t n1 = (e >> 16) & 31u, s1 = (e >> 21) & 15u, R1 = (e >> 25) & 63u;
+    if (R1 == 63u || n1 >= B || (s1 == 0 && R1 != 15u) || n1 == 17u) continue;  // EOB / bad: no second
+    const uint32_t rest = (key << n1) & ((1u << B) - 1u);  // the bits after symbol 1, left-aligned
+    const uint32_t e2 = one[rest];
+    if (e2 & RJ_HL_ESC) continue;
+    const uint32_t n2 = (e2 >> 16) & 31u, s2 = (e2 >> 21) & 15u, R2 = (e2 >> 25) & 63u;
+    if (n2 == 17u || n2 - s2 > B - n1) continue;  // bad, or the code is not inside the key
+    first[key] = e | n2 | (s2 << 5) | (R2 << 9) | RJ_HL_PAIR;
+  }
 }
 
 bool BuildLeanTable(const uint8_t bits[16], const uint8_t *vals, bool is_dc, uint32_t *first, uint32_t *subs) {
@@ -147,6 +167,7 @@ bool BuildHuffman(const uint8_t bits[16], const uint8_t *vals, bool is_dc, RjHuf
 bool Stream::Parse(const uint8_t *d, uint32_t n, bool defer_scan) {
   std::lock_guard<std::mutex> lock(mu_);  // rocjpeg_parser.cpp:44
   ReleaseResident();
+  pin_ = PinnedSlot();
   generation_++;
   lean_.reset();
   info_ = StreamInfo();
@@ -157,7 +178,10 @@ bool Stream::Parse(const uint8_t *d, uint32_t n, bool defer_scan) {
   if (d == nullptr || n < 4) return false;
   if (d[0] != 0xFF || d[1] != 0xD8) return false;  // :64-67
   if (IsProgressiveStream(d, n)) {  // SOF2: rj_prog_stream.cpp
-    if (ParseProgressive(d, n)) return true;
+    if (ParseProgressive(d, n)) {
+      PinEcs();
+      return true;
+    }
     plan_ = DecodePlan();
     plan_.status = -3;
     return false;
@@ -280,7 +304,19 @@ bool Stream::Parse(const uint8_t *d, uint32_t n, bool defer_scan) {
   s.ecs = d + (sos ? pos : n);
   s.ecs_size = sos ? uint32_t(end - pos) : 0;
   BuildPlan();
+  PinEcs();
   return true;
+}
+
+// While the parse is reading the bytes anyway: a copy in pinned memory, from which a later
+// decode call uploads runs of consecutively parsed streams with one DMA each and no host copy
+// (rj_decoder.cpp).  Streams the decoder would refuse are not copied.
+void Stream::PinEcs() {
+  if (plan_.status != 0 || info_.ecs_size == 0) return;
+  pin_ = PinnedAlloc(size_t(info_.ecs_size) + 16);
+  if (pin_.ptr == nullptr) return;
+  std::memcpy(pin_.ptr, info_.ecs, info_.ecs_size);
+  std::memset(pin_.ptr + info_.ecs_size, 0, 16);  // K0 reads <= 8 B past the end
 }
 
 void Stream::BuildPlan() {
@@ -524,6 +560,8 @@ const RjLeanTables *Stream::LeanTables() {
       if (!plan_.ht_valid[id] ||
           !BuildLeanTable(info_.ht[id].ac_bits, info_.ht[id].ac_vals, false, t->ac[id], ac_subs))
         FillLeanBad(false, t->ac[id], ac_subs);
+      else
+        AddLeanPairs(t->ac[id]);
     }
     lean_ = std::move(t);
   }

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "rj_device.h"
+#include "rj_pinned.h"
 
 namespace rj {
 
@@ -114,6 +115,10 @@ class Stream {
   } resident;
   void ReleaseResident();
   ~Stream() { ReleaseResident(); }
+  // the entropy-coded bytes (+ 16 zero bytes) copied at parse time into the pinned arena
+  // (rj_pinned.h); nullptr when the stream borrows the caller's bytes only
+  const uint8_t *pinned_ecs() const { return pin_.ptr; }
+  const PinnedChunk *pinned_chunk() const { return pin_.id(); }
   // lean K1 tables (rj_huff.hip) of this stream's DHTs, built on first use (callers hold mutex())
   const RjLeanTables *LeanTables();
 
@@ -124,8 +129,10 @@ class Stream {
   bool scan_pending_ = false;
   bool ParseProgressive(const uint8_t *data, uint32_t size);  // SOF2 (beyond the reference)
   void BuildProgressivePlan(const uint8_t *data);
+  void PinEcs();             // copy the ECS into the pinned arena (decodable streams)
   StreamInfo info_;
   DecodePlan plan_;
+  PinnedSlot pin_;
   std::unique_ptr<RjLeanTables> lean_;
   uint64_t generation_ = 0;
   std::mutex mu_;

@@ -197,7 +197,7 @@ def test_oversubscribed_tables_are_refused_without_writes(tmp_path):
     subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address", "-D__HIP_PLATFORM_AMD__",
                     "-I/opt/rocm/include", f"-I{csrc}", f"-I{INCLUDE}",
                     os.path.join(O.ROOT, "tests", "c", "huff_tables_asan.cpp"),
-                    os.path.join(csrc, "rj_stream.cpp"), os.path.join(csrc, "rj_prog_stream.cpp"),
+                    os.path.join(csrc, "rj_stream.cpp"), os.path.join(csrc, "rj_prog_stream.cpp"), os.path.join(csrc, "rj_pinned.cpp"),
                     "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib", "-o", str(exe)],
                    check=True, capture_output=True)
     bad = tmp_path / "bad.jpg"

@@ -154,10 +154,11 @@ def _planar_shapes(data, fmt):
     return channel_shapes(fmt, info["subsampling"], info["widths"], info["heights"])
 
 
-@pytest.mark.parametrize("workload,fmt", [("c3", R.OutputFormat.YUV_PLANAR), ("c2nori", R.OutputFormat.RGB)],
-                         ids=["c3_444_422_yuv_planar", "c2nori_restartless"])
+@pytest.mark.parametrize("workload,fmt", [("c3", R.OutputFormat.YUV_PLANAR), ("c2nori", R.OutputFormat.RGB),
+                                          ("c5", R.OutputFormat.RGB)],
+                         ids=["c3_444_422_yuv_planar", "c2nori_restartless", "c5_progressive_distinct"])
 def test_full_batch_other_configs(dec, workload, fmt):
-    """BASELINE config C3 (1024 x 1080p, 4:4:4 and 4:2:2 alternating, RI one MCU row ->
+    """BASELINE config C5 (progressive 1080p 4:2:0, 256 distinct images x 4), C3 (1024 x 1080p, 4:4:4 and 4:2:2 alternating, RI one MCU row ->
     YUV_PLANAR: the lean K1 with two sampling geometries in one call) and the C2 no-DRI twin
     (every interval a whole 1080p image: the self-synchronising chunk lanes), each as the bench
     runs it -- 1024 resident images (256 distinct x 4) in one rocJpegDecodeBatched call under the
@@ -185,6 +186,11 @@ def test_full_batch_other_configs(dec, workload, fmt):
     assert tm["images"] == 1024
     if workload == "c3":
         assert tm["lean_k1"] == 1 and {i["subsampling"] for i in (R.JpegStream(d).info() for d in datas[:2])} == {0, 2}
+    elif workload == "c5":
+        # 256 DISTINCT progressive images (x 4) in one call, the bench's one-grid pipelined
+        # layout: every image's ten scans run side by side with producer / consumer waits whose
+        # timing now differs from image to image (the 96-copy test had one chain)
+        assert tm["prog_images"] == 1024 and len(set(datas)) == distinct
     else:
         assert tm["lean_k1"] == 0 and tm["split_intervals"] == 1024  # one interval per image, chunked
     bad = []
