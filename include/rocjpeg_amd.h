@@ -49,6 +49,11 @@ RocJpegStatus rocJpegAmdStreamGetIntervals(RocJpegStreamHandle stream, RocJpegAm
 RocJpegStatus rocJpegAmdStreamGetDestuffBlocks(RocJpegStreamHandle stream, uint32_t *out4, uint32_t capacity,
                                                uint32_t *count, uint32_t *ecs_size);
 
+/* The lean K1 lookup tables of a parsed baseline stream (rj_device.h RjLeanTables: AC0, AC1
+ * first levels + subtables, DC0, DC1, 32-bit entries), for tests and tooling; `bytes` is the
+ * size of `out`, *needed receives the table image size. */
+RocJpegStatus rocJpegAmdStreamGetLeanTables(RocJpegStreamHandle stream, void *out, size_t bytes, size_t *needed);
+
 /* Per-stage device time of the most recent decode call, measured with HIP events on the
  * handle's internal stream (enable with rocJpegAmdSetProfiling first). */
 typedef struct {

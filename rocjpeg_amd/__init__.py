@@ -24,7 +24,7 @@ EXT_SYMBOLS = (
     "rocJpegAmdCommGetUniqueId", "rocJpegAmdCommInitRank", "rocJpegAmdCommDestroy", "rocJpegAmdCommInfo",
     "rocJpegAmdBroadcastWorkTable", "rocJpegAmdShardPlan", "rocJpegAmdDecodeBatchedSharded",
     "rocJpegAmdShardCreate", "rocJpegAmdShardDecode", "rocJpegAmdShardGetImages", "rocJpegAmdShardDestroy",
-    "rocJpegAmdGetAbiVersion",
+    "rocJpegAmdGetAbiVersion", "rocJpegAmdStreamGetLeanTables",
 )
 ABI_VERSION = 3  # include/rocjpeg_amd.h ROCJPEG_AMD_ABI_VERSION
 
@@ -175,6 +175,7 @@ def lib():
         L.rocJpegAmdShardGetImages.argtypes = [vp, ctypes.POINTER(i32), vp, i32]
         L.rocJpegAmdShardDestroy.argtypes = [vp]
         L.rocJpegAmdGetAbiVersion.argtypes = [ctypes.POINTER(i32)]
+        L.rocJpegAmdStreamGetLeanTables.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
         for name in API_SYMBOLS + EXT_SYMBOLS:
             if name != "rocJpegGetErrorName":
                 getattr(L, name).restype = i32

@@ -4,7 +4,9 @@
 // ROCJPEG_STATUS_INVALID_PARAMETER, parse failure -> ROCJPEG_STATUS_BAD_JPEG, allocation
 // failure at create -> ROCJPEG_STATUS_NOT_INITIALIZED, any C++ exception ->
 // ROCJPEG_STATUS_RUNTIME_ERROR.  No exception crosses the ABI.
+#include <cstring>
 #include <exception>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -235,4 +237,16 @@ RJ_EXPORT RocJpegStatus rocJpegAmdGetStream(RocJpegHandle handle, void **hip_str
   if (handle == nullptr || hip_stream == nullptr) return ROCJPEG_STATUS_INVALID_PARAMETER;
   *hip_stream = AsDecoder(handle)->stream();
   return ROCJPEG_STATUS_SUCCESS;
+}
+
+RJ_EXPORT RocJpegStatus rocJpegAmdStreamGetLeanTables(RocJpegStreamHandle s, void *out, size_t bytes, size_t *needed) {
+  if (s == nullptr || needed == nullptr) return ROCJPEG_STATUS_INVALID_PARAMETER;
+  return Guard([&] {
+    rj::Stream *st = AsStream(s);
+    std::lock_guard<std::mutex> lock(st->mutex());
+    *needed = sizeof(RjLeanTables);
+    if (st->plan().progressive || st->plan().status != 0) return int(ROCJPEG_STATUS_JPEG_NOT_SUPPORTED);
+    if (out != nullptr && bytes >= sizeof(RjLeanTables)) std::memcpy(out, st->LeanTables(), sizeof(RjLeanTables));
+    return int(ROCJPEG_STATUS_SUCCESS);
+  });
 }

@@ -211,9 +211,10 @@ struct RjTableSet {
 //   [30:25] R1: zigzag run (DC 0; AC r; ZRL 15; EOB 63 -> k >= 64)
 //   [31]    code longer than the first level: [7:0] = AC second-level subtable, 0xFF = search
 //   [4:0]   n2    [8:5] s2    [14:9] R2    [15] the second symbol is present
-// A second symbol is recorded only after an AC coefficient or ZRL whose bits and the second
-// code all lie inside the first-level key; the step takes it when the first symbol leaves the
-// block open (k + R1 + 1 < 64).  Whether a symbol writes an entry follows from the fields: a DC
+// A second symbol (always an AC symbol) is recorded only after a DC difference, an AC
+// coefficient or ZRL whose bits and the second code all lie inside the first-level key (for a
+// DC table: read with the AC table of the components that use it, when that is one table); the
+// step takes it when the first symbol leaves the block open (k + R1 + 1 < 64).  Whether a symbol writes an entry follows from the fields: a DC
 // symbol (k == 0) always, an AC symbol when s != 0.
 // First levels: DC 9 bits, AC 11 bits; AC codes of 12..16 bits: up to RJ_HL_SUBS subtables of
 // 32 entries (the next 5 bits) per table.

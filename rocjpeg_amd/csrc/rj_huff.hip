@@ -143,8 +143,8 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
     const uint32_t qold = q;                                                                              \
     const uint32_t R1 = (e >> 25) & 63u, n1 = (e >> 16) & 31u;                                            \
     const uint32_t k1 = k + R1 + 1u;                                                                      \
-    /* the second symbol: present, and the first leaves the block open (k >= 1: an AC symbol) */       \
-    bool use2 = (e & RJ_HL_PAIR) != 0u && k + R1 - 1u < 62u;                                              \
+    /* the second symbol: present, and the first leaves the block open */                            \
+    bool use2 = (e & RJ_HL_PAIR) != 0u && k1 < 64u;                                                       \
     if (SAFE) use2 = use2 && !skip;                                                                       \
     const uint32_t n2 = e & 31u, R2 = (e >> 9) & 63u;                                                     \
     q -= n1 + (use2 ? n2 : 0u);                                                                           \

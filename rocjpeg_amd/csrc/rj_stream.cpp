@@ -58,23 +58,25 @@ static void FillLeanBad(bool is_dc, uint32_t *first, uint32_t *subs) {
     for (int e = 0; e < RJ_HL_SUBS * 32; e++) subs[e] = bad;
 }
 
-// The second-symbol halves of an AC first level (rj_device.h): for each key whose first symbol
-// is an AC coefficient or ZRL with n1 < RJ_HL_AC_BITS, the code that starts at bit n1, if it is
-// complete inside the key (its extra bits may run past it: the step reads them from its 32-bit
-// peek, n1 + n2 <= 11 + 10 bits).
-static void AddLeanPairs(uint32_t *first) {
-  const uint32_t B = RJ_HL_AC_BITS;
-  std::vector<uint32_t> one(first, first + (1u << B));  // first-symbol entries only
+// The second-symbol halves of a first level (rj_device.h): for each key of `first` (B bits)
+// whose symbol leaves its block open -- a DC difference, an AC coefficient or ZRL -- with
+// n1 < B, the AC code that starts at bit n1, if it is complete inside the key (its extra bits
+// may run past it: the step reads them from its 32-bit peek, n1 + n2 <= 11 + 10 bits).
+// `ac` (RJ_HL_AC_BITS keys, single-symbol entries): the AC table the second symbol is read with.
+static void AddLeanPairs(uint32_t *first, uint32_t B, bool is_dc, const uint32_t *ac) {
+  const uint32_t BA = RJ_HL_AC_BITS;
   for (uint32_t key = 0; key < (1u << B); key++) {
-    const uint32_t e = one[key];
+    const uint32_t e = first[key];
     if (e & RJ_HL_ESC) continue;
     const uint32_t n1 = (e >> 16) & 31u, s1 = (e >> 21) & 15u, R1 = (e >> 25) & 63u;
-    if (R1 == 63u || n1 >= B || (s1 == 0 && R1 != 15u) || n1 == 17u) continue;  // EOB / bad: no second
-    const uint32_t rest = (key << n1) & ((1u << B) - 1u);  // the bits after symbol 1, left-aligned
-    const uint32_t e2 = one[rest];
+    if (n1 >= B || n1 == 17u) continue;                                   // no room / bad code
+    if (!is_dc && (R1 == 63u || (s1 == 0 && R1 != 15u))) continue;       // EOB: the block ends
+    const uint32_t avail = B - n1;                                        // key bits after symbol 1
+    const uint32_t rest = ((key << n1) & ((1u << B) - 1u)) << (BA - B);  // left-aligned AC key
+    const uint32_t e2 = ac[rest];
     if (e2 & RJ_HL_ESC) continue;
     const uint32_t n2 = (e2 >> 16) & 31u, s2 = (e2 >> 21) & 15u, R2 = (e2 >> 25) & 63u;
-    if (n2 == 17u || n2 - s2 > B - n1) continue;  // bad, or the code is not inside the key
+    if (n2 == 17u || n2 - s2 > avail) continue;  // bad, or the code is not inside the key
     first[key] = e | n2 | (s2 << 5) | (R2 << 9) | RJ_HL_PAIR;
   }
 }
@@ -551,6 +553,7 @@ void Stream::CompleteFromDevice(uint32_t ecs_size, const RjSegDev *segs, uint32_
 const RjLeanTables *Stream::LeanTables() {
   if (!lean_) {
     auto t = std::make_unique<RjLeanTables>();
+    bool ac_ok[2] = {false, false};
     for (int id = 0; id < 2; id++) {
       // only slots BuildPlanHeader accepted; an unused, invalid slot stays all 'bad' entries
       uint32_t *ac_subs = t->ac[id] + (1 << RJ_HL_AC_BITS);
@@ -561,7 +564,23 @@ const RjLeanTables *Stream::LeanTables() {
           !BuildLeanTable(info_.ht[id].ac_bits, info_.ht[id].ac_vals, false, t->ac[id], ac_subs))
         FillLeanBad(false, t->ac[id], ac_subs);
       else
-        AddLeanPairs(t->ac[id]);
+        ac_ok[id] = true;
+    }
+    // a DC table's second symbols are read with the AC table of the components that use it:
+    // only when every scan component with that DC table has the same AC table
+    int ac_of_dc[2] = {-1, -1};
+    bool mixed[2] = {false, false};
+    for (int c = 0; c < info_.scan_ncomp && c < 4; c++) {
+      const int td = info_.scomp[c].td & 1, ta = info_.scomp[c].ta & 1;
+      if (ac_of_dc[td] < 0) ac_of_dc[td] = ta;
+      else if (ac_of_dc[td] != ta) mixed[td] = true;
+    }
+    uint32_t single[2][1 << RJ_HL_AC_BITS];  // AC first levels before their pairs
+    for (int id = 0; id < 2; id++) std::memcpy(single[id], t->ac[id], sizeof(single[id]));
+    for (int id = 0; id < 2; id++) {
+      if (ac_ok[id]) AddLeanPairs(t->ac[id], RJ_HL_AC_BITS, false, single[id]);
+      const int ta = ac_of_dc[id];
+      if (ta >= 0 && !mixed[id] && ac_ok[ta] && plan_.ht_valid[id]) AddLeanPairs(t->dc[id], RJ_HL_DC_BITS, true, single[ta]);
     }
     lean_ = std::move(t);
   }
