@@ -175,9 +175,10 @@ def lib():
         L.rocJpegAmdShardGetImages.argtypes = [vp, ctypes.POINTER(i32), vp, i32]
         L.rocJpegAmdShardDestroy.argtypes = [vp]
         L.rocJpegAmdGetAbiVersion.argtypes = [ctypes.POINTER(i32)]
-        L.rocJpegAmdStreamGetLeanTables.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+        if hasattr(L, "rocJpegAmdStreamGetLeanTables"):  # (absent from same-ABI A/B builds of older commits)
+            L.rocJpegAmdStreamGetLeanTables.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
         for name in API_SYMBOLS + EXT_SYMBOLS:
-            if name != "rocJpegGetErrorName":
+            if name != "rocJpegGetErrorName" and (name in API_SYMBOLS or hasattr(L, name)):
                 getattr(L, name).restype = i32
         v = ctypes.c_int()
         if L.rocJpegAmdGetAbiVersion(ctypes.byref(v)) != 0 or v.value != ABI_VERSION:
