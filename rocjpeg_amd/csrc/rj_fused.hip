@@ -533,6 +533,67 @@ __device__ __forceinline__ void rgb_strip_420_full(const uint8_t *ty, const uint
   }
 }
 
+// Phase C for the full 4:2:0 strip, with line-contiguous 16-B stores and no staging (round 4;
+// the default, RJ_K2_STORE 2).  Measured (profiles/r4_experiments/k2_store_probes_ab.txt): the
+// IDCT and the CSC are hidden behind the rest of K2, while rgb_strip_420_full's 12-B stores --
+// each wave instruction 8 rows x 96 B -- cost ~0.9 ms of its 2.4 and the LDS-staged dwordx4 form
+// below halves that but pays as much again for the LDS round trip.  Here a lane produces one
+// 16-B piece of an output row directly: piece j (bytes 16 j .. 16 j + 15 of the strip's 480-B
+// row) starts at byte o = j mod 3 of pixel p0 = 5 j + j / 3; the lane converts the 8 pixels
+// from the even pixel pe = p0 & ~1 (24 bytes, as two rgb_strip_420_full quads, same arithmetic
+// and bytes) and selects its 16 bytes from byte 3 (p0 - pe) + o.  Task t = (row pair t / 30,
+// piece t mod 30) takes the two rows of that pair (they share the chroma row); 240 tasks over 4
+// passes of the wave, and a wave store instruction covers ~2 whole 480-B row segments.  The
+// 8-pixel window of the last piece reads 2 pixels past the row inside LDS; they are not output.
+// d: the strip's first output byte, d and pitch 16-B aligned (checked by the caller).
+__device__ __forceinline__ void rgb_strip_420_direct(const uint8_t *ty, const uint8_t *tu, const uint8_t *tv,
+                                                     uint32_t tid, RJ_GLOBAL uint8_t *d, uint32_t pitch) {
+  uint32_t t0 = tid;  // opaque: the lane's addresses are recomputed per strip, not hoisted
+  asm volatile("" : "+v"(t0));
+  const rj_f2 m128 = {128.0f, 128.0f};
+#pragma unroll
+  for (uint32_t m = 0; m < 4; m++) {
+    const uint32_t t = t0 + 64u * m;
+    if (m == 3 && t >= 240u) break;
+    const uint32_t qy = t / 30u, j = t - 30u * qy;
+    const uint32_t j3 = j / 3u;
+    const uint32_t p0 = 5u * j + j3, o = j - 3u * j3;
+    const uint32_t pe = p0 & ~1u;
+    const uint32_t off = 3u * (p0 - pe) + o;  // 0..5: the piece's first byte in the 24-B window
+    // luma of pixels pe .. pe + 7, rows 2 qy and 2 qy + 1 (pe even: 2-B aligned)
+    const uint32_t ya = qy * 320u + pe;
+    const uint32_t *yw = reinterpret_cast<const uint32_t *>(ty + (ya & ~3u));
+    const uint32_t ysh = ya & 3u;
+    const uint32_t a0 = yw[0], a1 = yw[1], a2 = yw[2];
+    const uint32_t b0 = yw[40], b1 = yw[41], b2 = yw[42];  // the next row: +160 B
+    // chroma of those pixels: bytes pe / 2 .. pe / 2 + 3 of chroma row qy
+    const uint32_t ca = qy * 80u + (pe >> 1);
+    const uint32_t csh = ca & 3u;
+    const uint32_t *uw = reinterpret_cast<const uint32_t *>(tu + (ca & ~3u));
+    const uint32_t *vw = reinterpret_cast<const uint32_t *>(tv + (ca & ~3u));
+    const uint32_t u4 = __builtin_amdgcn_alignbyte(uw[1], uw[0], csh);
+    const uint32_t v4 = __builtin_amdgcn_alignbyte(vw[1], vw[0], csh);
+    const rj_f2 uu0 = rj_f2{u8f(u4, 0), u8f(u4, 1)} - m128, vv0 = rj_f2{u8f(v4, 0), u8f(v4, 1)} - m128;
+    const rj_f2 uu1 = rj_f2{u8f(u4, 2), u8f(u4, 3)} - m128, vv1 = rj_f2{u8f(v4, 2), u8f(v4, 3)} - m128;
+    const uint32_t q = off >> 2, sh = off & 3u;
+    const uint32_t row0 = __umul24(2u * qy, pitch) + 16u * j;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const uint32_t w0 = r ? b0 : a0, w1 = r ? b1 : a1, w2 = r ? b2 : a2;
+      const uint32_t y4a = __builtin_amdgcn_alignbyte(w1, w0, ysh), y4b = __builtin_amdgcn_alignbyte(w2, w1, ysh);
+      uint32_t e[6];
+      csc4_pk(y4a, rj_f2{uu0.x, uu0.x}, rj_f2{uu0.y, uu0.y}, rj_f2{vv0.x, vv0.x}, rj_f2{vv0.y, vv0.y}, e[0], e[1], e[2]);
+      csc4_pk(y4b, rj_f2{uu1.x, uu1.x}, rj_f2{uu1.y, uu1.y}, rj_f2{vv1.x, vv1.x}, rj_f2{vv1.y, vv1.y}, e[3], e[4], e[5]);
+      uint32_t w[5];
+#pragma unroll
+      for (int k = 0; k < 5; k++) w[k] = q ? e[k + 1] : e[k];
+      const uint4 piece = make_uint4(__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
+                                     __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh));
+      *reinterpret_cast<RJ_GLOBAL uint4 *>(d + (row0 + (r ? pitch : 0u))) = piece;
+    }
+  }
+}
+
 // Phase C store shape for the full 4:2:0 strip (round 4).  rgb_strip_420_full stores 12 B per
 // lane: one wave instruction covers 8 rows x 96 B, i.e. 8-16 partial cache lines, ten such
 // instructions per lane and strip.  Here the same lanes compute the same pixels (arithmetic and
@@ -544,7 +605,7 @@ __device__ __forceinline__ void rgb_strip_420_full(const uint8_t *ty, const uint
 // tiles 3,840 B + image 16 x 288 B = 8,448 B of the 9,216.  d: the strip's first output byte
 // (16-B aligned, as is the pitch: the host-side condition is checked by the caller).
 #ifndef RJ_K2_STORE
-#define RJ_K2_STORE 1  // 0: rgb_strip_420_full (12-B stores), 1: staged dwordx4
+#define RJ_K2_STORE 2  // 0: rgb_strip_420_full (12-B stores), 1: staged dwordx4, 2: rgb_strip_420_direct
 #endif
 template <int kI0, int kNI>
 __device__ __forceinline__ void rgb_420_half_staged(const uint8_t *ty, const uint8_t *tu, const uint8_t *tv,
@@ -896,7 +957,9 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
     uint8_t *d = dst0 + (__umul24(py0, pitch0) + px0 * 3);
     if (hs1) {
       if (vs1 && strip_w == 160u && tw[0] == 160u && tw[1] == 80u) {
-        if (RJ_K2_STORE == 1 && al16) {
+        if (RJ_K2_STORE == 2 && al16) {
+          rgb_strip_420_direct(ty, tu, tv, tid, gp(d), pitch0);
+        } else if (RJ_K2_STORE == 1 && al16) {
           uint8_t *stage = s_buf + 3840u;  // past the tiles (toff[2] + 640)
           rgb_420_half_staged<0, 3>(ty, tu, tv, tid, stage, gp(d), pitch0);
           rgb_420_half_staged<3, 2>(ty, tu, tv, tid, stage, gp(d) + 288u, pitch0);

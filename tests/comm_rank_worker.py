@@ -53,6 +53,7 @@ def main():
             ts = [torch.full(s, 0xA5, dtype=torch.uint8, device="cuda:0") for s in shapes]
             outs.append((ts, shapes))
             imgs.append(R.make_image([t.data_ptr() for t in ts], [s[1] for s in shapes]))
+        torch.cuda.synchronize()  # the fills (torch's stream) before the decodes (the handle's)
         return outs, (R.RocJpegImage * len(imgs))(*imgs)
 
     def check(outs, idx):

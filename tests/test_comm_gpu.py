@@ -55,6 +55,7 @@ def test_comm_one_rank_sharded_decode_matches_oracle():
                 outs.append((ts, shapes))
                 imgs.append(R.make_image([t.data_ptr() for t in ts], [s[1] for s in shapes]))
             arr = (R.RocJpegImage * len(imgs))(*imgs)
+            torch.cuda.synchronize()  # the fills before the decode (another stream)
             st, table = comm.decode_batched_sharded(dec.handle, blob, offs, sizes, R.decode_params(fmt), arr)
             assert st == 0, R.error_name(st)
             torch.cuda.synchronize()

@@ -74,6 +74,8 @@ def test_threads_own_handles_concurrent(fmt):
                     b = [torch.full(s, 0xA5, dtype=torch.uint8, device="cuda:0") for s in shapes]
                     bufs.append(b)
                     imgs.append(R.make_image([x.data_ptr() for x in b], [s[1] for s in shapes]))
+                # the fills run on torch's stream, the decode on the handle's: wait for them
+                torch.cuda.synchronize()
                 if rnd == 1:  # one batched call over the thread's images
                     st = dec.decode_batched(streams, R.decode_params(fmt), imgs)
                     assert st == 0, R.error_name(st)
@@ -108,6 +110,7 @@ def test_threads_share_one_handle():
                     s = R.JpegStream(datas[k])
                     shapes = wants[k][0]
                     b = [torch.full(x, 0xA5, dtype=torch.uint8, device="cuda:0") for x in shapes]
+                    torch.cuda.synchronize()  # the fill (torch's stream) before the decode (the handle's)
                     st = dec.decode(s, R.decode_params(fmt), R.make_image([x.data_ptr() for x in b], [x[1] for x in shapes]))
                     assert st == 0, R.error_name(st)
                     torch.cuda.synchronize()
