@@ -605,7 +605,7 @@ __device__ __forceinline__ void rgb_strip_420_direct(const uint8_t *ty, const ui
 // tiles 3,840 B + image 16 x 288 B = 8,448 B of the 9,216.  d: the strip's first output byte
 // (16-B aligned, as is the pitch: the host-side condition is checked by the caller).
 #ifndef RJ_K2_STORE
-#define RJ_K2_STORE 2  // 0: rgb_strip_420_full (12-B stores), 1: staged dwordx4, 2: rgb_strip_420_direct
+#define RJ_K2_STORE 0  // 0: rgb_strip_420_full (12-B stores), 1: staged dwordx4, 2: rgb_strip_420_direct
 #endif
 template <int kI0, int kNI>
 __device__ __forceinline__ void rgb_420_half_staged(const uint8_t *ty, const uint8_t *tu, const uint8_t *tv,
