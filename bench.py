@@ -549,8 +549,8 @@ def kernel_table(t, n):
     """(summed launch ms per call, launches per call, units (images) per launch) per kernel of
     a profiled pass; the pipelined K1/K2 launches each take an equal share of the intervals."""
     kern = {}
-    if t["k1_launches"]:  # lean K1 (row images) is k_huff, the chunk-lane K1 k_entropy
-        k1 = "k_huff" if t["lean_k1"] else "k_entropy"
+    if t["k1_launches"]:  # lean K1 (row images) is k_huff, the chunk-lane K1 k_huff_chunk (k_entropy: RJ_K1_CHUNK=0)
+        k1 = "k_huff" if t["lean_k1"] else ("k_huff_chunk" if t["chunk_k1"] else "k_entropy")
         kern[k1] = (t["k1_launch_ms_sum"], t["k1_launches"], n / t["k1_launches"])
     if t["k2_launches"]:
         kern["k_rows"] = (t["k2_launch_ms_sum"], t["k2_launches"], n / t["k2_launches"])
@@ -582,7 +582,7 @@ def roofline(t, n, workload, per_image_bytes):
         r["traffic"], r["traffic_source"] = tr
     # intermediate-inclusive figures (what the kernels actually move through HBM by design)
     entb = t["entry_bytes"]
-    if dom in ("k_entropy", "k_huff") and t["k1_launches"]:
+    if dom in ("k_entropy", "k_huff", "k_huff_chunk") and t["k1_launches"]:
         b = (t["ecs_bytes"] + entb) / t["k1_launches"]
         r["achieved_incl_intermediates"] = round(b / (avg_ms * 1e-3) / 1e9, 2)
     if "k_rows" in kern:
@@ -789,7 +789,7 @@ def main():
             "huffman_detail": {"intervals": t["intervals"], "chunks": t["chunks"],
                                "split_intervals": t["split_intervals"], "serial_fallbacks": t["serial_fallbacks"],
                                "entry_bytes_per_image": round(t["entry_bytes"] / n), "lean_k1": t["lean_k1"],
-                               "lean_split": t["lean_split"]},
+                               "lean_split": t["lean_split"], "chunk_k1": t["chunk_k1"]},
             "end_to_end_algorithmic_GBps": round(imgs_total * per_img / elapsed / 1e9, 2),
             "host_input_images_per_s_per_gpu": round(host_rate, 1) if host_rate else None,
             "parse_images_per_s": {"host_1_thread": round(parse_host_rate, 1),

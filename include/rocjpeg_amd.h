@@ -107,6 +107,8 @@ typedef struct {
   uint32_t wide_rows;
   /* lean K1 outlier split: intervals decoded by a head and a tail lane (rj_huff.hip) */
   uint32_t lean_split;
+  /* 1: K1 ran the chunk-lane kernel on the lean machinery (rj_huff.hip k_huff_chunk) */
+  uint32_t chunk_k1;
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);
@@ -224,7 +226,7 @@ RocJpegStatus rocJpegAmdShardDestroy(RocJpegAmdShard shard);
 /* ABI revision of this header's extensions (rocJpegAmdGetAbiVersion returns the library's).
  * 2: rocJpegAmdBuildWorkTable takes blob_bytes; RocJpegAmdTimings as above.
  * 3: the resident sharded entry points; the work-table broadcast carries a status header. */
-#define ROCJPEG_AMD_ABI_VERSION 3
+#define ROCJPEG_AMD_ABI_VERSION 4
 RocJpegStatus rocJpegAmdGetAbiVersion(int *version);
 
 #if defined(__cplusplus)

@@ -159,6 +159,7 @@ int Decoder::Initialize() {
   if (const char *l = getenv("RJ_LPT")) lpt_ = atoi(l) != 0;
   if (const char *l = getenv("RJ_K1_SOLO")) k1_solo_lds_ = uint32_t(std::max(0, atoi(l)));
   if (const char *so = getenv("RJ_SPLIT_OUTLIERS")) outlier_split_ = atoi(so) != 0;
+  if (const char *kc = getenv("RJ_K1_CHUNK")) k1_chunk_ = atoi(kc) != 0;
   if (const char *sf = getenv("RJ_SPLIT_OUTLIER_FRAC")) outlier_frac_ = atof(sf);
   if (const char *st = getenv("RJ_SPLIT_OUTLIER_T")) outlier_t_ = std::max(0.5, std::min(1.0, atof(st)));
   cu_count_ = std::max(1, prop.multiProcessorCount);
@@ -1013,6 +1014,11 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (lean)
     for (int i = 0; i < n; i++) imgs[i].dc_diff = streams[i]->plan().progressive ? 0u : 1u;
   timings_.lean_k1 = lean ? 1u : 0u;
+  // ---- otherwise K1 is the chunk-lane kernel on the lean machinery (rj_huff.hip k_huff_chunk:
+  // absolute DC entries, rj_entropy.hip's records / resolution / serial fallback) ----
+  bool hc = !lean && k1_chunk_ && seg_total > 0;
+  for (int i = 0; i < n && hc; i++) hc = streams[i]->plan().progressive || streams[i]->plan().nblk_mcu <= RJ_MAX_BLK_MCU;
+  timings_.chunk_k1 = hc ? 1u : 0u;
 
   // ---- non-resident bitstreams: runs of streams whose ECS sit next to each other in the
   // parse-time pinned arena (rj_pinned.h) go up with one DMA per run, straight from the arena;
@@ -1071,7 +1077,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t off_plane = AlignUp(off_pgrows + n * sizeof(uint32_t), 256);
   const uint64_t off_fold = AlignUp(off_plane + prog_lanes.size() * sizeof(uint32_t), 256);
   const uint64_t off_lean = AlignUp(off_fold + fold_jobs.size() * sizeof(RjFoldJob), 256);
-  const uint64_t off_wide = AlignUp(off_lean + (lean ? tabs.size() * sizeof(RjLeanTables) : 0), 256);
+  const uint64_t off_wide = AlignUp(off_lean + ((lean || hc) ? tabs.size() * sizeof(RjLeanTables) : 0), 256);
   // K0's block -> image map: the image holding block 64 k, for k <= ds_total / 64 (+ a sentinel)
   const uint32_t n_dsmap = ds_total / 64u + 2u;
   const uint64_t off_dsmap = AlignUp(off_wide + kWideSites * sizeof(uint32_t), 256);
@@ -1245,7 +1251,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   }
   std::memcpy(h + off_imgs, imgs.data(), n * sizeof(RjImageDev));
   for (size_t t = 0; t < tabs.size(); t++) std::memcpy(h + off_tabs + t * sizeof(RjTableSet), tabs[t], sizeof(RjTableSet));
-  if (lean)
+  if (lean || hc)
     for (size_t t = 0; t < tabs.size(); t++)
       std::memcpy(h + off_lean + t * sizeof(RjLeanTables), owner_stream[t]->LeanTables(), sizeof(RjLeanTables));
   const RjLeanTables *d_lean = reinterpret_cast<const RjLeanTables *>(dbase + off_lean);
@@ -1628,6 +1634,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       if (lean)
         RJ_HIP(LaunchHuffLanes(st, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g], k1_src,
                                d_tabs, d_lean, cbuf));
+      else if (hc)
+        RJ_HIP(LaunchHuffChunks(st, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g], 0u,
+                                d_destuff_.as<uint8_t>(), d_tabs, d_lean, cbuf, epoch_));
       else
         RJ_HIP(LaunchEntropyLanes(st, d_imgs, n, lane_off[g], lane_off[g + 1] - lane_off[g], d_destuff_.as<uint8_t>(),
                                   d_tabs, cbuf, epoch_));
@@ -1659,8 +1668,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
     } else {
       for (int stage = 0; stage < 3; stage++) {
-        RJ_HIP(LaunchEntropy(stream_, stage, d_imgs, n, lanes_wg, lanes_dev, seg_total, d_destuff_.as<uint8_t>(),
-                             d_tabs, cbuf, epoch_));
+        if (stage == 0 && hc)
+          RJ_HIP(LaunchHuffChunks(stream_, d_imgs, n, 0u, lanes_wg, lanes_dev, d_destuff_.as<uint8_t>(), d_tabs,
+                                  d_lean, cbuf, epoch_));
+        else
+          RJ_HIP(LaunchEntropy(stream_, stage, d_imgs, n, lanes_wg, lanes_dev, seg_total, d_destuff_.as<uint8_t>(),
+                               d_tabs, cbuf, epoch_));
         if (profiling_ && stage < 2) RJ_HIP(hipEventRecord(ev_[6 + stage], stream_));
       }
     }

@@ -114,6 +114,7 @@ class Decoder {
   // workgroups past the first round (LPT order: the shortest) then wait for the CUs that finish
   // first instead of doubling up on a CU beside a long-interval workgroup
   uint32_t k1_solo_lds_ = 16384;
+  bool k1_chunk_ = true;           // env RJ_K1_CHUNK=0: chunk-layout calls take k_entropy's K1 (A/B)
   bool outlier_split_ = true;      // env RJ_SPLIT_OUTLIERS=0: never split the outlier intervals (one decoder wave per SIMD)
   double outlier_t_ = 9.0 / 16;    // env RJ_SPLIT_OUTLIER_T: outliers are longer than this share of the longest interval
   double outlier_frac_ = 0.7;      // env RJ_SPLIT_OUTLIER_FRAC: at most this share of the intervals split in that mode

@@ -438,7 +438,8 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
       RJ_HL_T1(!safe);
       // ---- phase end: words below rr - 2 (the one in wa) are free for the mover; a full stage
       // group leaves (< GROUP stay pending); wait until the next phase's words are in the ring ----
-      lds_st(&s_dec[L], rr - 2u);
+      // (rr = 1 until the first word is used up: rr - 2 would read as RJ_HL_FIN)
+      lds_st(&s_dec[L], max(rr, 2u) - 2u);
       if (ne - fl >= GROUP) {
         hl_flush<DEC, GROUP>(stage, fl, ent + fl);
         fl += GROUP;
@@ -508,6 +509,406 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     if (coefs.count) atomicAdd(&s_ne, ne + 1);
   }
   if (tid == 0 && coefs.count != nullptr && s_ne != 0) atomicAdd(coefs.count, (unsigned long long)s_ne);
+}
+
+// ---------------------------------------------------------------------------------------
+// Chunk lanes (k_huff_chunk): K1 of calls whose intervals are not all MCU rows -- long or
+// restart-less intervals (every reference fixture, BASELINE's C2 no-DRI
+// twin).  The lean machinery above (mover waves, one table entry per code with its follower,
+// the software-pipelined step) over the chunk layout of rj_entropy.hip: an interval of
+// rj_chunks(len) > 1 chunks gets one lane per chunk (reverse order), chunk c > 0 starts
+// speculatively at its first byte as if a Y block began there and records its state every
+// RJ_RECORD_EVERY block starts; a lane that runs past its own end compares its block starts with
+// the records of the chunk it entered and stops at the first equal state.  Records, the per-lane
+// result (RjChunkRes), k_resolve and the serial fallback (k_entropy<true>) are rj_entropy.hip's,
+// unchanged.  Entries carry ABSOLUTE DC values (the lane keeps libjpeg's three predictors; a
+// speculative chunk's are corrected per piece by k_resolve), so the images of such a call take
+// K2's DC-correcting path (dc_diff = 0).  Intervals of one chunk are decoded whole, exactly
+// (libjpeg's insufficient-data and missing-marker rules, as the lean launch), into one piece.
+template <int kScope>
+__device__ __forceinline__ void hc_put_record(RjRecord *r, uint32_t pos, uint32_t b, uint32_t epoch, uint32_t ne,
+                                              uint32_t rb, int p0, int p1, int p2) {
+  *gp(reinterpret_cast<int4 *>(&r->pred[0])) = make_int4(p0, p1, p2, 0);
+  if (kScope == __HIP_MEMORY_SCOPE_WORKGROUP) {
+    *gp(reinterpret_cast<uint4 *>(r)) = make_uint4(pos, (b & 15u) | (epoch << 4), ne, rb);
+  } else {
+    *gp(reinterpret_cast<uint2 *>(&r->ne)) = make_uint2(ne, rb);
+    __hip_atomic_store(reinterpret_cast<uint64_t *>(r), uint64_t(pos) | (uint64_t((b & 15u) | (epoch << 4)) << 32),
+                       __ATOMIC_RELAXED, kScope);
+  }
+}
+
+// The chunk-lane step: RJ_HL_STEP plus the DC predictors (absolute DC entries) and, at a block
+// end of a chunk lane, its records / sync search / stop conditions (SAFE phases only: a lane
+// inside its own chunk cannot stop).
+#define RJ_HC_STEP(SAFE)                                                                                        \
+  do {                                                                                                    \
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(e >= RJ_HL_ESC) != 0, 0)) {                          \
+      if (e >= RJ_HL_ESC) e = hl_escape(e, peek, tsh != 21u, acb, s_lut, tset, pat >> b);                 \
+    }                                                                                                     \
+    const uint32_t qold = q;                                                                              \
+    const uint32_t R1 = (e >> 25) & 63u, n1 = (e >> 16) & 31u;                                            \
+    const uint32_t k1 = k + R1 + 1u;                                                                      \
+    bool use2 = (e & RJ_HL_PAIR) != 0u && k1 < 64u;                                                       \
+    if (SAFE) use2 = use2 && !skip;                                                                       \
+    const uint32_t n2 = e & 31u, R2 = (e >> 9) & 63u;                                                     \
+    q -= n1 + (use2 ? n2 : 0u);                                                                           \
+    uint32_t kn = use2 ? k1 + R2 + 1u : k1;                                                               \
+    if (SAFE) kn = skip ? 64u : kn;                                                                       \
+    {                                                                                                     \
+      const bool adv = (qold ^ q) > 31u;                                                                  \
+      wa = adv ? wb : wa;                                                                                 \
+      wb = adv ? wc : wb;                                                                                 \
+      rr += adv ? 1u : 0u;                                                                                \
+    }                                                                                                     \
+    const bool bend = kn >= 64u;                                                                          \
+    const uint32_t kcur = k, bcur = b;                                                                    \
+    k = bend ? 0u : kn;                                                                                   \
+    const uint32_t bn = b + 2u == nb2 ? 0u : b + 2u;                                                      \
+    b = bend ? bn : b;                                                                                    \
+    const uint32_t ids = pat >> b;                                                                        \
+    acb = bend ? ((ids >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES) : acb;                                      \
+    const uint32_t dcb = RJ_HL_DC0 + ((ids & 1u) << (RJ_HL_DC_BITS + 2));                                 \
+    const uint32_t tbn = bend ? dcb : acb;                                                                \
+    const uint32_t tshn = bend ? uint32_t(32 - RJ_HL_DC_BITS) : uint32_t(32 - RJ_HL_AC_BITS);            \
+    const uint32_t peekn = __builtin_amdgcn_alignbit(wa, wb, q);                                          \
+    const uint32_t en = s_lut[(tbn >> 2) + (peekn >> tshn)];                                              \
+    wc = ring[rr & (RJ_HL_WORDS - 1)];                                                                    \
+    /* ---- entries; a DC symbol's value is the predictor of its block's component + the difference */ \
+    const uint32_t s1 = (e >> 21) & 15u;                                                                  \
+    const uint32_t raw = peek >> (32u - n1);                                                              \
+    const uint32_t xm = (1u << s1) - 1u;                                                                  \
+    const uint32_t xb = raw & xm;                                                                         \
+    const uint32_t xv = xb > xm - xb ? xb : xb - xm;                                                      \
+    const bool isdc = kcur == 0u;                                                                         \
+    const uint32_t cc = (cpat >> bcur) & 3u;                                                              \
+    const int pdc = (cc == 0u ? pred0 : (cc == 1u ? pred1 : pred2)) + int(xv);                            \
+    const uint32_t xp = min(kcur + R1, 63u);                                                              \
+    uint32_t entry = __builtin_amdgcn_perm(xp, isdc ? uint32_t(pdc) : xv, 0x05040100u);                   \
+    uint32_t emit = (isdc || s1 != 0u) ? 1u : 0u;                                                         \
+    const bool act = blocks_left > 0;                                                                     \
+    if (SAFE) {                                                                                           \
+      entry = skip ? 0u : entry; /* libjpeg: the rest of the interval is zero blocks (DC 0, absolute) */  \
+      emit = skip ? 1u : emit;                                                                            \
+      emit = act ? emit : 0u;                                                                             \
+    }                                                                                                     \
+    {   /* a stopped lane's predictors stay those of its stop point (RjChunkRes.pred) */                  \
+      const bool upd = isdc && (!(SAFE) || (act && !skip));                                               \
+      pred0 = (upd && cc == 0u) ? pdc : pred0;                                                            \
+      pred1 = (upd && cc == 1u) ? pdc : pred1;                                                            \
+      pred2 = (upd && cc == 2u) ? pdc : pred2;                                                            \
+    }                                                                                                     \
+    stage[ne & (kStage - 1)] = entry;                                                                     \
+    ne += emit;                                                                                           \
+    {                                                                                                     \
+      const uint32_t s2 = (e >> 5) & 15u;                                                                 \
+      const uint32_t raw2 = peek >> ((32u - n1 - n2) & 31u);                                              \
+      const uint32_t xm2 = (1u << s2) - 1u;                                                               \
+      const uint32_t xb2 = raw2 & xm2;                                                                    \
+      const uint32_t xv2 = xb2 > xm2 - xb2 ? xb2 : xb2 - xm2;                                             \
+      const uint32_t xp2 = min(k1 + R2, 63u);                                                             \
+      uint32_t emit2 = (use2 && s2 != 0u) ? 1u : 0u;                                                      \
+      if (SAFE) emit2 = act ? emit2 : 0u;                                                                 \
+      stage[ne & (kStage - 1)] = __builtin_amdgcn_perm(xp2, xv2, 0x05040100u);                             \
+      ne += emit2;                                                                                        \
+    }                                                                                                     \
+    if (SAFE) {                                                                                           \
+      blocks_left -= (bend && act) ? 1u : 0u;                                                             \
+      skip = skip || (bend && bn == 0u && (0u - q) > nbits_skip);                                         \
+    } else {                                                                                              \
+      blocks_left -= bend ? 1u : 0u;                                                                      \
+    }                                                                                                     \
+    if (chunk && bend && act) { /* a block start of a chunk lane (divergent: ~1 step in 6) */           \
+      rb++;                                                                                               \
+      const uint32_t pos = start_bit + (0u - q);                                                          \
+      if (spec && nrec < RJ_MAX_RECORDS && rb % RJ_RECORD_EVERY == 0 && pos < end_bit && !rp) {            \
+        rp = true;                                                                                        \
+        rp_pos = pos;                                                                                     \
+        rp_b = b >> 1;                                                                                    \
+        rp_ne = ne;                                                                                       \
+        rp_rb = rb;                                                                                       \
+        rp_p0 = pred0;                                                                                    \
+        rp_p1 = pred1;                                                                                    \
+        rp_p2 = pred2;                                                                                    \
+      }                                                                                                   \
+      if (SAFE) {                                                                                         \
+        if (pos >= next_tgt_bit && tgt < next_chunks) { /* entered the next later chunk */              \
+          tgt++;                                                                                          \
+          j = 0;                                                                                          \
+          next_tgt_bit += clen_bits;                                                                      \
+        }                                                                                                 \
+        if (tgt && cache_tj == (tgt << 16 | j) && uint32_t(cache >> 36) == (epoch & 0x0FFFFFFFu)) {      \
+          const uint32_t cpos = uint32_t(cache);                                                          \
+          if (cpos == pos && uint32_t(cache >> 32 & 15u) == (b >> 1)) {                                   \
+            status = RJ_CHUNK_SYNC; /* identical state from here on: the later chunk owns the rest */     \
+            s_tgt = tgt;                                                                                  \
+            s_rec = j;                                                                                    \
+          } else if (cpos < pos) {                                                                        \
+            j++;                                                                                          \
+          }                                                                                               \
+        }                                                                                                 \
+        if (status == 0 && pos >= nbits_abs) {                                                            \
+          if (pos > nbits_abs) rb_over = rb - 1;                                                          \
+          status = RJ_CHUNK_DONE;                                                                         \
+        }                                                                                                 \
+        if (status == 0 && (pos > ov_bit || ne + 2 * RJ_ENT_PER_BLOCK > cap)) status = RJ_CHUNK_FAIL;     \
+        if (status != 0) blocks_left = 0;                                                                 \
+      }                                                                                                   \
+    }                                                                                                     \
+    e = en;                                                                                               \
+    peek = peekn;                                                                                         \
+    tsh = tshn;                                                                                           \
+  } while (0)
+
+template <int kScope>
+__global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0,
+                                                      uint32_t nlanes, const uint8_t *__restrict__ destuffed,
+                                                      const RjTableSet *__restrict__ tabsets,
+                                                      const RjLeanTables *__restrict__ lean, RjCoefBuf coefs,
+                                                      uint32_t epoch) {
+  constexpr int DEC = RJ_K1_WG;  // the chunk layout's granule (an interval of <= DEC chunks in one workgroup)
+  constexpr int GROUP = RJ_HL_GROUP, PHASE = RJ_HL_PHASE;
+  constexpr uint32_t kStage = 2 * GROUP;
+  static_assert(2 * PHASE <= GROUP + 1, "stage too small for a phase of two-symbol steps");
+  __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_HL_WORDS][DEC];
+  __shared__ __attribute__((aligned(16))) uint32_t s_stage[kStage][DEC];
+  __shared__ __attribute__((aligned(16))) uint32_t s_lut[RJ_HL_LUT_WORDS];
+  __shared__ uint32_t s_dec[DEC];
+  __shared__ uint32_t s_mov[DEC];
+  __shared__ uint32_t s_T, s_ne;
+  const uint32_t tid = threadIdx.x;
+  const bool mover = tid >= uint32_t(DEC);
+  const uint32_t L = mover ? tid - DEC : tid;
+  if (tid == 0) s_ne = 0;
+  const uint32_t g = lane0 + blockIdx.x * DEC + L;
+  bool pending = g < lane0 + nlanes;
+  uint32_t gseg = 0, c = 0, nch = 1;
+  int i = 0;
+  if (pending) {
+    gseg = rj_lane_seg(coefs, g);
+    pending = gseg != 0xFFFFFFFFu;
+  }
+  if (pending) {
+    i = upper_index(nimg, gseg, [&](int qq) { return imgs[qq].seg_prefix; });
+    nch = rj_chunks(gp(imgs[i].segs)[gseg - imgs[i].seg_prefix].src_len);
+    c = nch - 1 - (g - rj_seg_lane0(coefs, gseg));  // reverse order: later chunks on earlier lanes
+  }
+  const RjImageDev &im = imgs[i];
+  const uint32_t my_ts = im.tabset;
+  while (__syncthreads_or(pending)) {
+    if (tid == 0) s_T = 0xFFFFFFFFu;
+    __syncthreads();
+    if (pending) atomicMin(&s_T, my_ts);
+    if (!mover) {
+      s_dec[L] = 0;
+      s_mov[L] = 0;
+    }
+    __syncthreads();
+    const uint32_t T = s_T;
+    {
+      const uint4 *src = reinterpret_cast<const uint4 *>(lean + T);
+      uint4 *d4 = reinterpret_cast<uint4 *>(s_lut);
+      for (uint32_t w = tid; w < RJ_HL_LUT_WORDS / 4; w += 2 * DEC) d4[w] = gp(src)[w];
+    }
+    __syncthreads();
+    if (!(pending && my_ts == T)) continue;
+    pending = false;
+    const uint32_t seg = gseg - im.seg_prefix;
+    const RjSegDev sg = gp(im.segs)[seg];
+    const bool chunk = nch > 1;
+    const uint32_t nbytes = sg.dst_len;
+    const uint32_t clen = chunk ? rj_chunk_len(nbytes, nch) : nbytes;
+    const uint32_t b0 = chunk ? min(c * clen, nbytes) : 0u, b1 = chunk ? min(b0 + clen, nbytes) : nbytes;
+    const bool empty = chunk && c > 0 && b0 >= nbytes;  // no data left for this chunk (16-B rounding)
+    const uint32_t lane_bytes = empty ? 0u : nbytes - b0;  // the lane may read on to the data's end
+    const uint4 *src = reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off + b0);
+    const uint32_t nchunks = (lane_bytes + 15) / 16;
+    const HCol<DEC> ring{&s_ring[0][L]};
+
+    if (mover) {  // the lean mover (k_huff)
+      uint32_t cm = 0, na = 0;
+      uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, p2 = p0, p3 = p0;
+      for (;;) {
+        const uint32_t rd = lds_ld(&s_dec[L]);
+        if (na > 0) {
+          hl_put(ring, cm & (RJ_HL_CHUNKS - 1), p0);
+          if (na > 1) hl_put(ring, (cm + 1) & (RJ_HL_CHUNKS - 1), p1);
+          if (na > 2) hl_put(ring, (cm + 2) & (RJ_HL_CHUNKS - 1), p2);
+          if (na > 3) hl_put(ring, (cm + 3) & (RJ_HL_CHUNKS - 1), p3);
+          cm += na;
+          lds_st(&s_mov[L], cm);
+          na = 0;
+        }
+        const bool fin = rd == RJ_HL_FIN;
+        const uint32_t live = fin ? RJ_HL_CHUNKS : cm - (rd >> 2);
+        const uint32_t n = min(RJ_HL_CHUNKS - live, 4u);
+        if (n > 0) {
+          p0 = *gp(cm < nchunks ? src + cm : rj_hl_zero);
+          if (n > 1) p1 = *gp(cm + 1 < nchunks ? src + cm + 1 : rj_hl_zero);
+          if (n > 2) p2 = *gp(cm + 2 < nchunks ? src + cm + 2 : rj_hl_zero);
+          if (n > 3) p3 = *gp(cm + 3 < nchunks ? src + cm + 3 : rj_hl_zero);
+          na = n;
+        }
+        if (__builtin_amdgcn_ballot_w64(!fin) == 0) break;
+        if (__builtin_amdgcn_ballot_w64(n > 0) == 0) __builtin_amdgcn_s_sleep(4);
+      }
+      continue;
+    }
+
+    // ---- decoder ----
+    const uint32_t nblk = im.nblk_mcu;
+    uint32_t pat = 0, cpat = 0;  // per block b (2 bits each): DC / AC table; component
+    for (uint32_t bb = 0; bb < nblk; bb++) {
+      const uint32_t cc = im.blk_comp[bb] & 3;
+      pat |= ((im.comp_td[cc] & 1u) | ((im.comp_ta[cc] & 1u) << 1)) << (2 * bb);
+      cpat |= cc << (2 * bb);
+    }
+    const uint32_t nb2 = 2 * nblk;
+    const uint32_t nbits = lane_bytes * 8u;  // data bits from the lane's first bit
+    const uint32_t nbits_skip = chunk ? 0xFFFFFFFFu : nbits;  // chunk lanes never zero-fill (DONE instead)
+    const uint32_t blocks = sg.mcu_count * nblk;
+    const uint64_t ent_abs = im.ent_off + sg.ent_off;
+    const uint32_t rcap = chunk ? uint32_t(rj_chunk_cap(rj_chunk_len(sg.src_len, nch))) : 0u;
+    const uint64_t ent_lane = ent_abs + (chunk ? uint64_t(c) * rcap : 0u);
+    uint32_t *ent = coefs.ent + ent_lane;
+    const RjTableSet *tset = tabsets + T;
+    const HCol<DEC> stage{&s_stage[0][L]};
+    // chunk-lane state (rj_entropy.hip decode_lane)
+    const uint32_t start_bit = b0 * 8u, end_bit = b1 * 8u, nbits_abs = nbytes * 8u;
+    const uint32_t clen_bits = clen * 8u, ov_bit = end_bit + RJ_OVERLAP_CHUNKS * clen * 8u;
+    const uint32_t cap = rcap, next_chunks = chunk ? nch - 1 - c : 0u;
+    const bool spec = chunk && c > 0;
+    RjRecord *const rec_mine = coefs.rec + uint64_t(g) * RJ_MAX_RECORDS;
+    const RjRecord *const rec_next = rec_mine - RJ_MAX_RECORDS;  // chunk c + 1 sits on lane g - 1
+    uint32_t rb = 0, nrec = 0, tgt = 0, j = 0, status = 0, rb_over = 0xFFFFFFFFu, s_tgt = 0, s_rec = 0;
+    uint32_t next_tgt_bit = end_bit;
+    uint64_t cache = 0;
+    uint32_t cache_tj = 0xFFFFFFFFu;
+    bool rp = false;
+    uint32_t rp_pos = 0, rp_b = 0, rp_ne = 0, rp_rb = 0;
+    int rp_p0 = 0, rp_p1 = 0, rp_p2 = 0;
+    int pred0 = 0, pred1 = 0, pred2 = 0;
+    if (empty) {
+      RjChunkRes o = {};
+      o.status = RJ_CHUNK_DONE;
+      o.rb_over = 0xFFFFFFFFu;
+      *gp(coefs.res + g) = o;
+      hc_put_record<kScope>(rec_mine, 0xFFFFFFFFu, 0u, epoch, 0u, 0u, 0, 0, 0);
+      lds_st(&s_dec[L], RJ_HL_FIN);
+      continue;
+    }
+    if (spec) {  // the chunk's first bit is a block start by assumption: record 0
+      hc_put_record<kScope>(rec_mine, start_bit, 0u, epoch, 0u, 0u, 0, 0, 0);
+      nrec = 1;
+    }
+#define RJ_HC_WAIT_RING(upto)                                                                     \
+  {                                                                                               \
+    uint32_t cmv = lds_ld(&s_mov[L]);                                                             \
+    while (__builtin_amdgcn_ballot_w64(4u * cmv < (upto)) != 0) {                                 \
+      __builtin_amdgcn_s_sleep(2);                                                                \
+      cmv = lds_ld(&s_mov[L]);                                                                    \
+    }                                                                                             \
+    avail = 4u * cmv;                                                                             \
+    asm volatile("" ::: "memory");                                                                \
+  }
+    uint32_t avail = 0;
+    RJ_HC_WAIT_RING(uint32_t(PHASE) + 2u);
+    uint32_t q = 0;
+    uint32_t wa = 0, wb = ring[0], wc = ring[1];
+    uint32_t rr = 1;
+    uint32_t ne = 0, fl = 0;
+    bool skip = !chunk && (sg.flags & RJ_SEG_MISSING) != 0;
+    uint32_t blocks_left = chunk ? 0x7FFFFFFFu : blocks;
+    uint32_t b = 0, k = 0;
+    uint32_t acb = ((pat >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES);
+    uint32_t tb = RJ_HL_DC0 + ((pat & 1u) << (RJ_HL_DC_BITS + 2));
+    uint32_t tsh = 32 - RJ_HL_DC_BITS;
+    uint32_t peek = __builtin_amdgcn_alignbit(wa, wb, q);
+    uint32_t e = s_lut[(tb >> 2) + (peek >> tsh)];
+    while (__builtin_amdgcn_ballot_w64(blocks_left > 0) != 0) {
+      if (blocks_left == 0) continue;
+      // ---- phase start: the captured record leaves; the record being sought is loaded ----
+      if (rp) {
+        hc_put_record<kScope>(rec_mine + nrec, rp_pos, rp_b, epoch, rp_ne, rp_rb, rp_p0, rp_p1, rp_p2);
+        nrec++;
+        rp = false;
+      }
+      const uint32_t pos0 = start_bit + (0u - q);
+      // lanes inside their own chunk (and exact lanes away from their end) cannot stop this phase
+      const bool safe = __builtin_amdgcn_ballot_w64(
+                            chunk ? pos0 + PHASE * 31u >= end_bit
+                                  : !(blocks_left >= PHASE && !skip && (0u - q) + PHASE * 31u < nbits)) != 0;
+      uint64_t rec_ld = 0;
+      uint32_t rec_ld_tj = 0xFFFFFFFFu;
+      const bool seek = chunk && pos0 + PHASE * 31u >= end_bit;
+      if (__builtin_amdgcn_ballot_w64(seek) != 0) {
+        const uint32_t t = tgt ? tgt : 1u;
+        const bool have = seek && t <= next_chunks && j < RJ_MAX_RECORDS;
+        const RjRecord *r = have ? rec_next - int64_t(t - 1) * RJ_MAX_RECORDS + j : rec_mine;
+        rec_ld = __hip_atomic_load(reinterpret_cast<const uint64_t *>(r), __ATOMIC_RELAXED, kScope);
+        rec_ld_tj = have ? (t << 16 | j) : 0xFFFFFFFFu;
+      }
+      if (!safe) {
+#pragma unroll
+        for (uint32_t s_ = 0; s_ < PHASE; s_++) RJ_HC_STEP(false);
+      } else {
+#pragma unroll
+        for (uint32_t s_ = 0; s_ < PHASE; s_++) RJ_HC_STEP(true);
+      }
+      lds_st(&s_dec[L], max(rr, 2u) - 2u);
+      if (ne - fl >= GROUP) {
+        hl_flush<DEC, GROUP>(stage, fl, ent + fl);
+        fl += GROUP;
+      }
+      cache = rec_ld;
+      cache_tj = rec_ld_tj;
+      if (__builtin_amdgcn_ballot_w64(avail < rr + PHASE + 1u) != 0) {
+        RJ_HC_WAIT_RING(rr + PHASE + 1u);
+        wc = ring[rr & (RJ_HL_WORDS - 1)];
+      }
+    }
+#undef RJ_HC_WAIT_RING
+    lds_st(&s_dec[L], RJ_HL_FIN);
+    if (rp) hc_put_record<kScope>(rec_mine + nrec, rp_pos, rp_b, epoch, rp_ne, rp_rb, rp_p0, rp_p1, rp_p2);
+    stage[ne & (kStage - 1)] = RJ_ENT_TERM;
+    while (fl < ne + 1) {
+      hl_flush<DEC, GROUP>(stage, fl, ent + fl);
+      fl += GROUP;
+    }
+    if (chunk) {
+      RjChunkRes o;
+      o.status = status;
+      o.tgt = s_tgt;
+      o.rec = s_rec;
+      o.rb = rb;
+      o.ne = ne;
+      o.pred[0] = pred0;
+      o.pred[1] = pred1;
+      o.pred[2] = pred2;
+      o.rb_over = rb_over;
+      o.pad[0] = start_bit + (0u - q);
+      o.pad[1] = end_bit;
+      o.pad[2] = 0;
+      *gp(coefs.res + g) = o;
+    } else {
+      *gp(coefs.piece + rj_seg_lane0(coefs, gseg)) = RjPiece{ent_abs, 0u, blocks, 1u, {0, 0, 0}};
+    }
+    if (coefs.count) atomicAdd(&s_ne, ne + 1);
+  }
+  if (tid == 0 && coefs.count != nullptr && s_ne != 0) atomicAdd(coefs.count, (unsigned long long)s_ne);
+}
+
+hipError_t LaunchHuffChunks(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t lanes_wg,
+                            uint32_t lanes_dev, const uint8_t *destuffed, const RjTableSet *tabsets,
+                            const RjLeanTables *lean, RjCoefBuf coefs, uint32_t epoch) {
+  if (lanes_wg)
+    hipLaunchKernelGGL((k_huff_chunk<__HIP_MEMORY_SCOPE_WORKGROUP>), dim3((lanes_wg + RJ_K1_WG - 1) / RJ_K1_WG),
+                       dim3(2 * RJ_K1_WG), 0, st, imgs, nimg, lane0, lanes_wg, destuffed, tabsets, lean, coefs, epoch);
+  if (lanes_dev)
+    hipLaunchKernelGGL((k_huff_chunk<__HIP_MEMORY_SCOPE_AGENT>), dim3((lanes_dev + RJ_K1_WG - 1) / RJ_K1_WG),
+                       dim3(2 * RJ_K1_WG), 0, st, imgs, nimg, lane0 + lanes_wg, lanes_dev, destuffed, tabsets, lean,
+                       coefs, epoch);
+  return hipGetLastError();
 }
 
 #ifdef RJ_HL_STAMPS

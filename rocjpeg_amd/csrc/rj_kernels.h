@@ -33,6 +33,12 @@ hipError_t LaunchEntropyLanes(hipStream_t st, const RjImageDev *imgs, int nimg, 
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
                            RjCoefBuf coefs, uint32_t extra_lds = 0, const RjHuffSplit *split = nullptr);
+// K1 chunk lanes on the lean machinery (rj_huff.hip k_huff_chunk): stage 0 of LaunchEntropy's
+// layout (from lane0: lanes_wg lanes with workgroup-scope records, then lanes_dev), absolute DC entries.
+hipError_t LaunchHuffChunks(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t lanes_wg,
+                            uint32_t lanes_dev,
+                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
+                            RjCoefBuf coefs, uint32_t epoch);
 // K2b (general path): every output format / ROI of rocjpeg_decoder.cpp:143-180 from the planes.
 hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobDev *jobs, int njobs, uint32_t total_rows,
                             const uint8_t *planes);

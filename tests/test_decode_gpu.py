@@ -343,6 +343,27 @@ def test_largest_and_smallest_accepted_sizes(dec, w, h, sub, rst, fmt):
         assert np.array_equal(g, x)
 
 
+@pytest.mark.parametrize("color", [(128, 128, 128), (200, 30, 90)], ids=["gray128", "color"])
+@pytest.mark.parametrize("rst", [1, 0], ids=["ri_row", "nori"])
+def test_flat_images_with_two_bit_blocks(dec, color, rst):
+    """A flat 1080p picture with optimised tables: every block is a 1-bit DC code and a 1-bit EOB
+    (one two-symbol K1 step), so a lane's first phases use less than one 32-bit word of its bit
+    ring and the decoder's consumed-word count starts below zero -- it must not read as the
+    lane's end to the mover that feeds the ring (rj_huff.hip RJ_HL_FIN).  Lean K1 (row
+    intervals) and the chunk lanes (no restart markers)."""
+    import io
+    from PIL import Image
+    b = io.BytesIO()
+    kw = dict(quality=90, subsampling=2, optimize=True)
+    if rst:
+        kw["restart_marker_blocks"] = 1920 // 16
+    Image.new("RGB", (1920, 1080), color).save(b, "JPEG", **kw)
+    st, ost, got, want = run_both(dec, b.getvalue(), R.OutputFormat.RGB)
+    assert st == 0 and ost == 0
+    for g, x in zip(got, want):
+        assert np.array_equal(g, x)
+
+
 @pytest.mark.parametrize("w,h", [(16385, 64), (64, 16385), (63, 64), (64, 63)])
 def test_sizes_outside_the_range_are_refused(dec, w, h):
     """One pixel outside either edge: JPEG_NOT_SUPPORTED, as the reference's SubmitDecode
