@@ -100,10 +100,14 @@ struct RjHuffSplit {
 // Chunking of an interval of `bytes` raw entropy-coded bytes: intervals shorter than
 // RJ_SPLIT_BYTES are decoded by one lane with the exact serial semantics (so a call whose
 // restart intervals are MCU rows keeps the lean K1); longer ones get about RJ_CHUNK_BYTES per
-// lane (3 KB measured best for restart-less 1080p: 81k -> 118k images/s over 8 KB chunks; the
-// resynchronisation costs ~1,000 bits per chunk boundary).
+// lane.  5 KB measured best for the chunk lanes of k_huff_chunk on restart-less 1080p (c2nori,
+// same box: 3 KB 150k, 4 KB 140k, 5 KB 178k, 5.5 KB 171k, 6 KB 168k, 7 KB 155k, 8 KB 149k
+// images/s, profiles/r4_experiments/k1_chunk_bytes_ab.txt): a 1024-image batch then fills the
+// chip's 65,536 decoder lanes (one workgroup per CU) in one round; the resynchronisation costs
+// ~1,000 bits per chunk boundary.  k_entropy's chunk lanes (two workgroups per CU)
+// measured best at 3 KB.
 #ifndef RJ_CHUNK_BYTES
-#define RJ_CHUNK_BYTES 3072u
+#define RJ_CHUNK_BYTES 5120u
 #endif
 #define RJ_SPLIT_BYTES 12288u
 #define RJ_OVERLAP_CHUNKS 3u      // a lane may decode this many chunk lengths past its own end
