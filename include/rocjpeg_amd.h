@@ -109,6 +109,8 @@ typedef struct {
   uint32_t lean_split;
   /* 1: K1 ran the chunk-lane kernel on the lean machinery (rj_huff.hip k_huff_chunk) */
   uint32_t chunk_k1;
+  /* the call's chunk length in bytes: intervals of at least twice this are cut into chunks */
+  uint32_t chunk_bytes;
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);
@@ -225,8 +227,9 @@ RocJpegStatus rocJpegAmdShardDestroy(RocJpegAmdShard shard);
 
 /* ABI revision of this header's extensions (rocJpegAmdGetAbiVersion returns the library's).
  * 2: rocJpegAmdBuildWorkTable takes blob_bytes; RocJpegAmdTimings as above.
- * 3: the resident sharded entry points; the work-table broadcast carries a status header. */
-#define ROCJPEG_AMD_ABI_VERSION 4
+ * 3: the resident sharded entry points; the work-table broadcast carries a status header.
+ * 4: RocJpegAmdTimings.chunk_k1.  5: RocJpegAmdTimings.chunk_bytes (the call's chunk length). */
+#define ROCJPEG_AMD_ABI_VERSION 5
 RocJpegStatus rocJpegAmdGetAbiVersion(int *version);
 
 #if defined(__cplusplus)

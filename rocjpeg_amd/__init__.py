@@ -26,7 +26,7 @@ EXT_SYMBOLS = (
     "rocJpegAmdShardCreate", "rocJpegAmdShardDecode", "rocJpegAmdShardGetImages", "rocJpegAmdShardDestroy",
     "rocJpegAmdGetAbiVersion", "rocJpegAmdStreamGetLeanTables",
 )
-ABI_VERSION = 4  # include/rocjpeg_amd.h ROCJPEG_AMD_ABI_VERSION
+ABI_VERSION = 5  # include/rocjpeg_amd.h ROCJPEG_AMD_ABI_VERSION
 
 
 class Status(enum.IntEnum):  # api/rocjpeg.h:53-67
@@ -107,7 +107,7 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("prog_kernel_bytes", ctypes.c_uint64 * 3),
                 ("routed_images", ctypes.c_uint32), ("lean_k1", ctypes.c_uint32),
                 ("wide_rows", ctypes.c_uint32), ("lean_split", ctypes.c_uint32),
-                ("chunk_k1", ctypes.c_uint32)]
+                ("chunk_k1", ctypes.c_uint32), ("chunk_bytes", ctypes.c_uint32)]
 
 
 class RocJpegAmdInterval(ctypes.Structure):  # include/rocjpeg_amd.h

@@ -160,6 +160,7 @@ int Decoder::Initialize() {
   if (const char *l = getenv("RJ_K1_SOLO")) k1_solo_lds_ = uint32_t(std::max(0, atoi(l)));
   if (const char *so = getenv("RJ_SPLIT_OUTLIERS")) outlier_split_ = atoi(so) != 0;
   if (const char *kc = getenv("RJ_K1_CHUNK")) k1_chunk_ = atoi(kc) != 0;
+  if (const char *cm = getenv("RJ_CHUNK_MIN")) chunk_min_ = uint32_t(std::max(16, atoi(cm)));
   if (const char *sf = getenv("RJ_SPLIT_OUTLIER_FRAC")) outlier_frac_ = atof(sf);
   if (const char *st = getenv("RJ_SPLIT_OUTLIER_T")) outlier_t_ = std::max(0.5, std::min(1.0, atof(st)));
   cu_count_ = std::max(1, prop.multiProcessorCount);
@@ -951,11 +952,48 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   }
 
   const auto t_lanes = std::chrono::steady_clock::now();
+  // ---- the call's chunk length (rj_device.h rj_chunks_cb): the baseline bytes over one round of
+  // the chip's K1 decoder lanes, at least chunk_min_ -- a large batch of short intervals keeps
+  // one lane per interval (the lean K1), a restart-less or small call is cut to fill the chip ----
+  uint64_t src_total = 0;
+  uint32_t src_max = 0;
+  for (int i = 0; i < n; i++) {
+    const DecodePlan &p = streams[i]->plan();
+    src_total += p.src_total;
+    src_max = std::max(src_max, p.src_max);
+  }
+  // (a call whose intervals alone fill half a round keeps them whole below RJ_SPLIT_BYTES: lean
+  // K1 with its outlier split)
+  const uint64_t round_lanes = uint64_t(cu_count_) * RJ_K1_WG;
+  uint64_t cb_fill = std::max<uint64_t>(chunk_min_, (src_total + round_lanes - 1) / round_lanes);
+  if (2ull * seg_total >= round_lanes) {
+    cb_fill = std::max<uint64_t>(cb_fill, RJ_SPLIT_BYTES / 2);
+  } else {
+    // the lanes pack into workgroups with padding (an interval's chunks never straddle one):
+    // lengthen the chunks until the layout is one workgroup per CU (a second round doubles K1)
+    for (int it = 0; it < 8 && cb_fill < (1u << 30); it++) {
+      uint64_t lanes = 0, dev = 0;
+      for (int i = 0; i < n; i++)
+        for (const RjSegDev &sg : streams[i]->plan().segs) {
+          const uint32_t nch = rj_chunks_cb(sg.src_len, uint32_t(cb_fill));
+          if (nch > RJ_K1_WG) {
+            dev += nch;
+          } else {
+            if (lanes % RJ_K1_WG + nch > RJ_K1_WG) lanes = AlignUp(lanes, RJ_K1_WG);
+            lanes += nch;
+          }
+        }
+      const uint64_t wgs = (lanes + RJ_K1_WG - 1) / RJ_K1_WG + (dev + RJ_K1_WG - 1) / RJ_K1_WG;
+      if (wgs <= uint64_t(cu_count_)) break;
+      cb_fill = cb_fill * wgs / uint64_t(cu_count_) + 16;
+    }
+  }
+  const uint32_t chunk_bytes = uint32_t(std::min<uint64_t>(1u << 30, cb_fill));
+  timings_.chunk_bytes = chunk_bytes;
   // ---- K1 lane layout (rj_device.h RjCoefBuf): one lane per chunk; an interval of at most
   // RJ_K1_WG chunks never straddles a workgroup (padding lanes), longer ones go after them.
   // Common case -- no interval split -- is the identity (lane = interval), nothing uploaded. ----
-  bool any_split = false;
-  for (int i = 0; i < n && !any_split; i++) any_split = streams[i]->plan().nchunks != streams[i]->plan().segs.size();
+  const bool any_split = rj_chunks_cb(src_max, chunk_bytes) > 1;
   std::vector<uint32_t> &seg_lane0 = sc_.seg_lane0, &lane_seg = sc_.lane_seg;
   seg_lane0.clear();
   lane_seg.clear();
@@ -966,7 +1004,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     uint32_t gs = 0;
     for (int i = 0; i < n; i++)
       for (const RjSegDev &sg : streams[i]->plan().segs) {
-        const uint32_t nch = rj_chunks(sg.src_len);
+        const uint32_t nch = rj_chunks_cb(sg.src_len, chunk_bytes);
         split_intervals += nch > 1 ? 1u : 0u;
         if (nch <= RJ_K1_WG) {
           if (lanes_wg % RJ_K1_WG + nch > RJ_K1_WG) lanes_wg = uint32_t(AlignUp(lanes_wg, RJ_K1_WG));
@@ -986,7 +1024,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       for (const RjSegDev &sg : streams[i]->plan().segs) {
         if (seg_lane0[gs] == UINT32_MAX) {
           seg_lane0[gs] = lanes_all;
-          lanes_all += rj_chunks(sg.src_len);
+          lanes_all += rj_chunks_cb(sg.src_len, chunk_bytes);
         }
         gs++;
       }
@@ -994,12 +1032,30 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     gs = 0;
     for (int i = 0; i < n; i++)
       for (const RjSegDev &sg : streams[i]->plan().segs) {
-        const uint32_t nch = rj_chunks(sg.src_len);
+        const uint32_t nch = rj_chunks_cb(sg.src_len, chunk_bytes);
         for (uint32_t q = 0; q < nch; q++) lane_seg[seg_lane0[gs] + q] = gs;
         gs++;
       }
   }
   const uint32_t lanes_dev = lanes_all - lanes_wg;
+  // the split intervals' chunk regions, after the images' serial regions (rj_chunk_regions)
+  std::vector<unsigned long long> &seg_ent = sc_.seg_ent;
+  seg_ent.clear();
+  if (any_split) {
+    seg_ent.assign(seg_total, 0ull);
+    uint64_t at = AlignUp(ent_total, RJ_ENT_GROUP);
+    uint32_t gs = 0;
+    for (int i = 0; i < n; i++)
+      for (const RjSegDev &sg : streams[i]->plan().segs) {
+        const uint32_t nch = rj_chunks_cb(sg.src_len, chunk_bytes);
+        if (nch > 1) {
+          seg_ent[gs] = at;
+          at += rj_chunk_regions(sg.src_len, nch);
+        }
+        gs++;
+      }
+    ent_total = at;
+  }
 
   // ---- lean K1 (rj_huff.hip): when every baseline image of the call is a "row" image (each
   // restart interval inside one MCU row) and no interval is split, K1 writes raw entries and K2
@@ -1087,7 +1143,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t n_lane_seg = any_split ? lane_seg.size() : (sorted ? (lean ? 2ull * seg_total + 64 : seg_total) : 0);
   const uint64_t off_lane_seg = blob_a;
   const uint64_t off_seg_lane0 = AlignUp(off_lane_seg + n_lane_seg * 4, 256);
-  const uint64_t off_row_list = AlignUp(off_seg_lane0 + uint64_t(seg_lane0.size()) * 4, 256);
+  const uint64_t off_seg_ent = AlignUp(off_seg_lane0 + uint64_t(seg_lane0.size()) * 4, 256);
+  const uint64_t off_row_list = AlignUp(off_seg_ent + uint64_t(seg_ent.size()) * 8, 256);
   const uint64_t n_row_list = ngroups > 1 ? uint64_t(fused_rows) + general_rows : 0;  // upper bound
   const uint64_t blob = AlignUp(off_row_list + n_row_list * sizeof(uint2), 256);
   RJ_CHECK(h_stage_.Ensure(blob));
@@ -1114,6 +1171,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   cbuf.dense = d_coef_.as<uint32_t>();
   cbuf.wide_flag = d_wide_flag_;
   cbuf.piece_shift = 0;
+  cbuf.chunk_bytes = chunk_bytes;
+  cbuf.seg_ent = nullptr;  // set with the split layout below
   if (profiling_) {
     RJ_CHECK(d_count_.Ensure(256));
     cbuf.count = d_count_.as<unsigned long long>();
@@ -1598,8 +1657,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (any_split) {
     std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(lane_seg.size()) * 4);
     std::memcpy(h + off_seg_lane0, seg_lane0.data(), uint64_t(seg_lane0.size()) * 4);
+    std::memcpy(h + off_seg_ent, seg_ent.data(), uint64_t(seg_ent.size()) * 8);
     cbuf.lane_seg = d_lane_seg;
     cbuf.seg_lane0 = reinterpret_cast<const uint32_t *>(dbase + off_seg_lane0);
+    cbuf.seg_ent = reinterpret_cast<const unsigned long long *>(dbase + off_seg_ent);
   } else if (sorted) {  // lanes in length order; pieces stay at the interval's own slot
     if (nsplit) std::memcpy(h + off_lane_seg, sc_.lane_split.data(), uint64_t(nl_split) * 4);
     else std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(seg_total) * 4);
@@ -1837,9 +1898,11 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       timings_.k1_launches = (lanes_wg ? 1u : 0u) + (lanes_dev ? 1u : 0u);
       timings_.k2_launch_ms_sum = ms[3];
       timings_.k2_launches = (fused_rows ? 1u : 0u) + (general_rows ? 1u : 0u);
-      std::vector<uint32_t> fb(seg_total);
-      RJ_HIP(hipMemcpy(fb.data(), d_fallback_.as<uint32_t>(), fb.size() * 4, hipMemcpyDeviceToHost));
-      for (uint32_t f : fb) timings_.serial_fallbacks += f ? 1u : 0u;
+      if (!lean) {  // (the lean launch has no resolution: the flags are another call's)
+        std::vector<uint32_t> fb(seg_total);
+        RJ_HIP(hipMemcpy(fb.data(), d_fallback_.as<uint32_t>(), fb.size() * 4, hipMemcpyDeviceToHost));
+        for (uint32_t f : fb) timings_.serial_fallbacks += f ? 1u : 0u;
+      }
     }
     if (prog_images) {
       RJ_HIP(hipEventElapsedTime(&timings_.prog_entropy_ms, prog_ev_[0], prog_ev_[1]));
@@ -1894,7 +1957,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       for (int h = 0; h < 8; h++) fprintf(stderr, " %u", hist[h]);
       fprintf(stderr, " | iters mean %.0f max %u\n", (nsync + ndone) ? sum_it / (nsync + ndone) : 0.0, max_it);
       if (n == 1 && Dbg(kDebugK1Pieces)) {  // one image: its first interval's pieces and chunks
-        const uint32_t l0 = seg_lane0[0], nch = rj_chunks(streams[0]->plan().segs[0].src_len);
+        const uint32_t l0 = seg_lane0[0], nch = rj_chunks_cb(streams[0]->plan().segs[0].src_len, timings_.chunk_bytes);
         std::vector<RjPiece> pc(nch);
         RJ_HIP(hipMemcpy(pc.data(), d_piece_.as<RjPiece>() + l0, nch * sizeof(RjPiece), hipMemcpyDeviceToHost));
         fprintf(stderr, "[K1] seg0 lanes %u.. nch %u npieces %u\n", l0, nch, pc[0].npieces);

@@ -114,6 +114,7 @@ class Decoder {
   // workgroups past the first round (LPT order: the shortest) then wait for the CUs that finish
   // first instead of doubling up on a CU beside a long-interval workgroup
   uint32_t k1_solo_lds_ = 16384;
+  uint32_t chunk_min_ = RJ_CHUNK_MIN_BYTES;  // env RJ_CHUNK_MIN: floor of the call's chunk length (bytes)
   bool k1_chunk_ = true;           // env RJ_K1_CHUNK=0: chunk-layout calls take k_entropy's K1 (A/B)
   bool outlier_split_ = true;      // env RJ_SPLIT_OUTLIERS=0: never split the outlier intervals (one decoder wave per SIMD)
   double outlier_t_ = 9.0 / 16;    // env RJ_SPLIT_OUTLIER_T: outliers are longer than this share of the longest interval
@@ -146,6 +147,7 @@ class Decoder {
   // host planning scratch, reused across calls (no per-call allocation / page faults)
   struct Scratch {
     std::vector<PinRun> pin_runs;
+    std::vector<unsigned long long> seg_ent;  // per interval: its chunk regions (split intervals)
     std::vector<RjImageDev> imgs;
     std::vector<RjJobDev> jobs;
     std::vector<uint64_t> stage_off, ecs_off;

@@ -76,6 +76,8 @@ struct RjCoefBuf {
   const uint32_t *dense;      // progressive images: dense coefficients (RjImageDev.coef_off)
   uint32_t *wide_flag;        // host-mapped: set by K2 when it recorded a row for the fix-up
   uint32_t piece_shift;       // identity layout: interval s's pieces start at s << piece_shift
+  uint32_t chunk_bytes;       // the call's chunk length (rj_chunks_cb; 0: no interval split)
+  const unsigned long long *seg_ent;  // per interval: first entry of its chunk regions (split ones)
 };
 // Lean K1 split launch (rj_huff.hip): an interval decoded by a head lane from its start and a
 // tail lane from rj_split_byte(dst_len); lane_seg entries carry the role in their top bits.
@@ -97,25 +99,39 @@ struct RjHuffSplit {
 #define RJ_RECORD_EVERY 8         // one record every 8th block start of a chunk's head
 #endif
 
-// Chunking of an interval of `bytes` raw entropy-coded bytes: intervals shorter than
-// RJ_SPLIT_BYTES are decoded by one lane with the exact serial semantics (so a call whose
-// restart intervals are MCU rows keeps the lean K1); longer ones get about RJ_CHUNK_BYTES per
-// lane.  5 KB measured best for the chunk lanes of k_huff_chunk on restart-less 1080p (c2nori,
-// same box: 3 KB 150k, 4 KB 140k, 5 KB 178k, 5.5 KB 171k, 6 KB 168k, 7 KB 155k, 8 KB 149k
-// images/s, profiles/r4_experiments/k1_chunk_bytes_ab.txt): a 1024-image batch then fills the
-// chip's 65,536 decoder lanes (one workgroup per CU) in one round; the resynchronisation costs
-// ~1,000 bits per chunk boundary.  k_entropy's chunk lanes (two workgroups per CU)
-// measured best at 3 KB.
+// Chunking of an interval of `bytes` raw entropy-coded bytes is decided per call
+// (rj_decoder.cpp): the chunk length `cb` is the call's baseline bytes over one round of the
+// chip's K1 decoder lanes (one k_huff_chunk workgroup of RJ_K1_WG lanes per CU), never below
+// the handle's minimum; an interval of at least two chunk lengths is cut into floor(bytes / cb)
+// chunks, one lane each, shorter ones are decoded whole by one lane with the exact serial
+// semantics (so a large batch of MCU-row intervals keeps the lean K1).  A fixed 5 KB measured
+// best on a 1024-image restart-less 1080p batch (c2nori, same box: 3 KB 150k, 4 KB 140k, 5 KB
+// 178k, 5.5 KB 171k, 6 KB 168k, 7 KB 155k, 8 KB 149k images/s,
+// profiles/r4_experiments/k1_chunk_bytes_ab.txt) -- exactly the length that fills one round --
+// and small calls want short chunks (their lanes would leave the chip idle).  The
+// resynchronisation costs ~1,000 bits per chunk boundary.
+// RJ_CHUNK_BYTES: the parse-time default geometry (RjSegDev.chunk0, introspection only).
 #ifndef RJ_CHUNK_BYTES
 #define RJ_CHUNK_BYTES 5120u
 #endif
+#define RJ_CHUNK_MIN_BYTES 512u  // default floor of the call's chunk length (env RJ_CHUNK_MIN)
 #define RJ_SPLIT_BYTES 12288u
-#define RJ_OVERLAP_CHUNKS 3u      // a lane may decode this many chunk lengths past its own end
+#define RJ_OVERLAP_CHUNKS 3u      // a lane may decode this many chunk lengths past its own end,
+#define RJ_OVERLAP_MIN_BYTES 4096u  // and at least this many bytes (resynchronisation is long-tailed)
 #define RJ_CHUNK_ENT_PER_BYTE 4u  // region budget of a chunk lane (typical ~1.7); overflow -> serial path
 __host__ __device__ inline uint32_t rj_chunks(uint32_t bytes) {
   if (bytes < RJ_SPLIT_BYTES) return 1u;
   const uint32_t n = (bytes + RJ_CHUNK_BYTES / 2) / RJ_CHUNK_BYTES;
   return n < 2 ? 1u : (n > 4096 ? 4096u : n);
+}
+// chunks of an interval under a call's chunk length cb (0: never split)
+__host__ __device__ inline uint32_t rj_chunks_cb(uint32_t bytes, uint32_t cb) {
+  if (cb == 0 || uint64_t(bytes) < 2ull * cb) return 1u;
+  const uint32_t n = bytes / cb;
+  return n > 4096 ? 4096u : n;
+}
+__host__ __device__ inline uint32_t rj_nch(const RjCoefBuf &c, uint32_t src_len) {
+  return rj_chunks_cb(src_len, c.chunk_bytes);
 }
 // chunk length in bytes (16-B multiple); chunk c covers [c*len, min((c+1)*len, bytes))
 __host__ __device__ inline uint32_t rj_chunk_len(uint32_t bytes, uint32_t nch) {
@@ -123,19 +139,24 @@ __host__ __device__ inline uint32_t rj_chunk_len(uint32_t bytes, uint32_t nch) {
 }
 __host__ __device__ inline uint64_t rj_group(uint64_t n) { return (n + RJ_ENT_GROUP - 1) / RJ_ENT_GROUP * RJ_ENT_GROUP; }
 // entry region of one chunk of a split interval: a lane decodes at most its chunk +
-// RJ_OVERLAP_CHUNKS more; it stops (and the interval goes to the serial path) before it would
-// overflow.  The regions of an interval together hold its serial decode (>= 8 entries/byte).
-__host__ __device__ inline uint64_t rj_chunk_cap(uint32_t clen) {
-  return rj_group(uint64_t(RJ_CHUNK_ENT_PER_BYTE) * clen * (1 + RJ_OVERLAP_CHUNKS) + 2 * RJ_ENT_PER_BLOCK);
+// rj_chunk_reach more bytes; it stops (and the interval goes to the serial path, into its own
+// region) before it would overflow.
+__host__ __device__ inline uint32_t rj_chunk_reach(uint32_t clen) {
+  return RJ_OVERLAP_CHUNKS * clen > RJ_OVERLAP_MIN_BYTES ? RJ_OVERLAP_CHUNKS * clen : RJ_OVERLAP_MIN_BYTES;
 }
-// entries reserved for an interval: one serial stream (zero-bit decode of the last MCU after
-// the data ends, then one zero DC entry per skipped block), or the chunk regions of a split one
-// (their sum also holds the serial re-decode of a failed split interval)
+__host__ __device__ inline uint64_t rj_chunk_cap(uint32_t clen) {
+  return rj_group(uint64_t(RJ_CHUNK_ENT_PER_BYTE) * (uint64_t(clen) + rj_chunk_reach(clen)) + 2 * RJ_ENT_PER_BLOCK);
+}
+// entries reserved for an interval at parse time: one serial stream (zero-bit decode of the
+// last MCU after the data ends, then one zero DC entry per skipped block) -- an exact lane's
+// output, or the serial re-decode of a split interval the resolution failed
 __host__ __device__ inline uint64_t rj_interval_entries(uint32_t bytes, uint64_t blocks, uint32_t nblk_mcu) {
-  const uint32_t nch = rj_chunks(bytes);
-  if (nch == 1) return rj_group(8ull * bytes + blocks + uint64_t(nblk_mcu) * RJ_ENT_PER_BLOCK + 1);
-  return uint64_t(nch) * rj_chunk_cap(rj_chunk_len(bytes, nch)) +
-         rj_group(blocks + uint64_t(nblk_mcu) * RJ_ENT_PER_BLOCK + 1);
+  return rj_group(8ull * bytes + blocks + uint64_t(nblk_mcu) * RJ_ENT_PER_BLOCK + 1);
+}
+// the chunk regions of an interval a call cuts into nch chunks (RjCoefBuf.seg_ent: placed by
+// the call after the images' serial regions)
+__host__ __device__ inline uint64_t rj_chunk_regions(uint32_t bytes, uint32_t nch) {
+  return uint64_t(nch) * rj_chunk_cap(rj_chunk_len(bytes, nch));
 }
 
 // One restart interval of one image (host parser rj_stream.cpp builds these).

@@ -14,7 +14,7 @@
 //     at the first equal state -- from there on both decodes are identical.  k_resolve chains
 //     the sync points into pieces (which part of which chunk stream holds which blocks, and
 //     the DC-predictor correction of each piece); an interval whose chunks did not sync within
-//     RJ_OVERLAP_CHUNKS, or whose data ends before its blocks (truncated stream), is decoded
+//     rj_chunk_reach, or whose data ends before its blocks (truncated stream), is decoded
 //     again serially by k_entropy<true>.  Chunks are laid out in reverse order over the lanes,
 //     so the chunk a lane has to read records from was dispatched no later than itself.
 //
@@ -622,7 +622,7 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
   if (pending) {
     i = upper_index(nimg, gseg, [&](int q) { return imgs[q].seg_prefix; });
     if (!kFallback) {
-      nch = rj_chunks(gp(imgs[i].segs)[gseg - imgs[i].seg_prefix].src_len);
+      nch = rj_nch(coefs, gp(imgs[i].segs)[gseg - imgs[i].seg_prefix].src_len);
       c = nch - 1 - (g - rj_seg_lane0(coefs, gseg));  // reverse order: later chunks on earlier lanes
     }
   }
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
         J.start_bit = 0;
         J.ent = ent_base;
         J.pieces = coefs.piece + lane_first;
-        J.slots = rj_chunks(sg.src_len);
+        J.slots = rj_nch(coefs, sg.src_len);  // the interval's lanes: piece slots
         J.ent_abs = ent_abs;
         J.mcux = im.mcux;
         J.mcu_first = sg.mcu_first;
@@ -702,9 +702,9 @@ __global__ __launch_bounds__(RJ_WG, 2) void k_entropy(const RjImageDev *__restri
         J.start_bit = b0 * 8u;
         J.end_bit = b1 * 8u;
         J.clen_bits = clen * 8u;
-        J.ov_bit = J.end_bit + RJ_OVERLAP_CHUNKS * clen * 8u;
+        J.ov_bit = J.end_bit + rj_chunk_reach(clen) * 8u;
         const uint32_t rcap = uint32_t(rj_chunk_cap(rj_chunk_len(sg.src_len, nch)));
-        J.ent = ent_base + uint64_t(c) * rcap;
+        J.ent = coefs.ent + gp(coefs.seg_ent)[gseg] + uint64_t(c) * rcap;
         J.cap = rcap;
         J.spec = c > 0;
         J.rec = coefs.rec + uint64_t(g) * RJ_MAX_RECORDS;
@@ -728,13 +728,13 @@ __global__ __launch_bounds__(256) void k_resolve(const RjImageDev *__restrict__ 
   const int i = upper_index(nimg, g, [&](int q) { return imgs[q].seg_prefix; });
   const RjImageDev &im = imgs[i];
   const RjSegDev sg = gp(im.segs)[g - im.seg_prefix];
-  const uint32_t nch = rj_chunks(sg.src_len);
+  const uint32_t nch = rj_nch(coefs, sg.src_len);
   bool ok = true;
   if (nch > 1) {
     const uint32_t total = sg.mcu_count * im.nblk_mcu;
     const uint32_t lane_first = rj_seg_lane0(coefs, g);  // lane of chunk c: lane_first + nch-1-c
     const uint64_t rcap = rj_chunk_cap(rj_chunk_len(sg.src_len, nch));
-    const uint64_t ent0 = im.ent_off + sg.ent_off;
+    const uint64_t ent0 = gp(coefs.seg_ent)[g];  // the call's chunk regions of this interval
     RjPiece *pieces = coefs.piece + lane_first;
     uint32_t c = 0, vs_rb = 0, vs_ne = 0, T = 0, np = 0;
     int32_t D[3] = {0, 0, 0};

@@ -88,9 +88,20 @@ struct EntWin {
   __device__ __forceinline__ void load(const uint32_t *__restrict__ ent, uint64_t at, uint32_t lane) {
     base_lo = U(uint32_t(at));
     base_hi = U(uint32_t(at >> 32));
+#ifdef RJ_EXP_E16  // timing probe: 16-bit entries (rj_huff.hip hl_flush), expanded to the 32-bit form
+    const uint16_t *p16 = reinterpret_cast<const uint16_t *>(ent) + at;
+#pragma unroll
+    for (int r = 0; r < RJ_WIN_ROWS; r++) {
+      const uint32_t h = gp(p16)[r * 64u + lane];
+      const uint32_t pos = h >> 10;
+      const int32_t v = __builtin_amdgcn_sbfe(int32_t(h), 0, 10);
+      w[r] = v == -512 ? (pos == 63u ? RJ_RE_TERM : RJ_RE_ZERO) : ((uint32_t(v) & 0xFFFFu) | (pos << 16));
+    }
+#else
     const uint32_t *p = ent + at;
 #pragma unroll
     for (int r = 0; r < RJ_WIN_ROWS; r++) w[r] = gp(p)[r * 64u + lane];
+#endif
   }
   // wait here for the window's loads.  vmcnt is in order on gfx9: a wait for a window row issued
   // after the previous strip's pixel stores waits for those stores too.  parse_blocks' walk over a

@@ -93,6 +93,25 @@ __device__ __forceinline__ void hl_flush(const HCol<S> &stage, uint32_t from, ui
   if (w[0] == 0x12345678u && w[G - 1] == 0x9ABCDEF0u) *gp(dst) = w[1];
   return;
 #endif
+#ifdef RJ_EXP_E16  // timing probe (lean calls only): 16-bit entries, position 6 b | value 10 b
+  {                 // (clamped: wrong pixels where |value| > 511); -512 marks TERM (pos 63) / ZERO
+    uint32_t h[G / 2];
+#pragma unroll
+    for (int q = 0; q < G; q++) {
+      const uint32_t e = w[q], pos = (e >> 16) & 127u;
+      const int32_t v = min(max(int32_t(int16_t(e & 0xFFFFu)), -511), 511);
+      uint32_t x = (pos << 10) | (uint32_t(v) & 0x3FFu);
+      x = (e & (1u << 23)) ? 0x200u : x;
+      x = pos == 127u ? ((63u << 10) | 0x200u) : x;
+      if (q & 1) h[q / 2] |= x << 16;
+      else h[q / 2] = x;
+    }
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+#pragma unroll
+    for (int q = 0; q < G / 8; q++) gp(d4)[q] = make_uint4(h[4 * q], h[4 * q + 1], h[4 * q + 2], h[4 * q + 3]);
+    return;
+  }
+#endif
   uint4 *d4 = reinterpret_cast<uint4 *>(dst);
 #pragma unroll
   for (int q = 0; q < G / 4; q++) gp(d4)[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
@@ -362,6 +381,11 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     const uint64_t tail_abs = kSplit ? split.ent + uint64_t((g >> 6) * 32u + (g & 31u)) * split.cap : 0u;
     const uint64_t ent_abs = tail ? tail_abs : im.ent_off + sg.ent_off;
     uint32_t *ent = coefs.ent + ent_abs;
+#ifdef RJ_EXP_E16
+#define RJ_HL_DST(f) reinterpret_cast<uint32_t *>(reinterpret_cast<uint16_t *>(coefs.ent) + ent_abs + (f))
+#else
+#define RJ_HL_DST(f) (ent + (f))
+#endif
     RjPiece *piece = coefs.piece + rj_seg_lane0_k<kSplit>(coefs, gseg);
     const RjTableSet *tset = tabsets + T;  // canonical search (escape path)
     const HCol<DEC> stage{&s_stage[0][L]};
@@ -441,7 +465,7 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
       // (rr = 1 until the first word is used up: rr - 2 would read as RJ_HL_FIN)
       lds_st(&s_dec[L], max(rr, 2u) - 2u);
       if (ne - fl >= GROUP) {
-        hl_flush<DEC, GROUP>(stage, fl, ent + fl);
+        hl_flush<DEC, GROUP>(stage, fl, RJ_HL_DST(fl));
         fl += GROUP;
       }
       if (kSplit) {
@@ -495,7 +519,7 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
 #endif
     stage[ne & (kStage - 1)] = RJ_RE_TERM;
     while (fl < ne + 1) {  // [fl, ne]: at most 2 GROUP entries, the terminator included
-      hl_flush<DEC, GROUP>(stage, fl, ent + fl);
+      hl_flush<DEC, GROUP>(stage, fl, RJ_HL_DST(fl));
       fl += GROUP;
     }
     if (!tail) {
@@ -514,9 +538,10 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
 // ---------------------------------------------------------------------------------------
 // Chunk lanes (k_huff_chunk): K1 of calls whose intervals are not all MCU rows -- long or
 // restart-less intervals (every reference fixture, BASELINE's C2 no-DRI
-// twin).  The lean machinery above (mover waves, one table entry per code with its follower,
-// the software-pipelined step) over the chunk layout of rj_entropy.hip: an interval of
-// rj_chunks(len) > 1 chunks gets one lane per chunk (reverse order), chunk c > 0 starts
+// twin; small calls, whose intervals the call cuts to fill the chip).  The lean machinery above
+// (mover waves, one table entry per code with its follower, the software-pipelined step) over
+// the chunk layout of rj_entropy.hip: an interval of rj_nch > 1 chunks gets one lane per chunk
+// (reverse order, regions at RjCoefBuf.seg_ent), chunk c > 0 starts
 // speculatively at its first byte as if a Y block began there and records its state every
 // RJ_RECORD_EVERY block starts; a lane that runs past its own end compares its block starts with
 // the records of the chunk it entered and stops at the first equal state.  Records, the per-lane
@@ -690,7 +715,7 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
   }
   if (pending) {
     i = upper_index(nimg, gseg, [&](int qq) { return imgs[qq].seg_prefix; });
-    nch = rj_chunks(gp(imgs[i].segs)[gseg - imgs[i].seg_prefix].src_len);
+    nch = rj_nch(coefs, gp(imgs[i].segs)[gseg - imgs[i].seg_prefix].src_len);
     c = nch - 1 - (g - rj_seg_lane0(coefs, gseg));  // reverse order: later chunks on earlier lanes
   }
   const RjImageDev &im = imgs[i];
@@ -769,13 +794,13 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     const uint32_t blocks = sg.mcu_count * nblk;
     const uint64_t ent_abs = im.ent_off + sg.ent_off;
     const uint32_t rcap = chunk ? uint32_t(rj_chunk_cap(rj_chunk_len(sg.src_len, nch))) : 0u;
-    const uint64_t ent_lane = ent_abs + (chunk ? uint64_t(c) * rcap : 0u);
+    const uint64_t ent_lane = chunk ? gp(coefs.seg_ent)[gseg] + uint64_t(c) * rcap : ent_abs;
     uint32_t *ent = coefs.ent + ent_lane;
     const RjTableSet *tset = tabsets + T;
     const HCol<DEC> stage{&s_stage[0][L]};
     // chunk-lane state (rj_entropy.hip decode_lane)
     const uint32_t start_bit = b0 * 8u, end_bit = b1 * 8u, nbits_abs = nbytes * 8u;
-    const uint32_t clen_bits = clen * 8u, ov_bit = end_bit + RJ_OVERLAP_CHUNKS * clen * 8u;
+    const uint32_t clen_bits = clen * 8u, ov_bit = end_bit + rj_chunk_reach(clen) * 8u;
     const uint32_t cap = rcap, next_chunks = chunk ? nch - 1 - c : 0u;
     const bool spec = chunk && c > 0;
     RjRecord *const rec_mine = coefs.rec + uint64_t(g) * RJ_MAX_RECORDS;

@@ -519,8 +519,12 @@ void FinishSegs(DecodePlan &p) {
   p.seg_lenblk.resize(p.segs.size());
   bool aligned = p.segs.size() == p.mcuy;
   uint32_t m = 0;
+  p.src_total = 0;
+  p.src_max = 0;
   for (size_t q = 0; q < p.segs.size(); q++) {
     const RjSegDev &sg = p.segs[q];
+    p.src_total += sg.src_len;
+    p.src_max = std::max(p.src_max, sg.src_len);
     p.seg_bucket[q] = uint16_t(std::min<uint32_t>(sg.src_len >> 5, 4095u));
     p.seg_lenblk[q] = ((sg.flags & RJ_SEG_MISSING) ? 0u : uint64_t(sg.dst_len)) |
                       (uint64_t(sg.mcu_count) * p.nblk_mcu << 32);

@@ -55,6 +55,8 @@ struct DecodePlan {
   std::vector<uint16_t> seg_bucket;
   std::vector<uint64_t> seg_lenblk;  // per interval: destuffed bytes (0: missing) | blocks << 32 (split planning)
   bool rows_aligned = false;
+  uint64_t src_total = 0;          // entropy-coded bytes of the intervals (call-time chunk length)
+  uint32_t src_max = 0;            // the longest interval's
   std::vector<RjDsBlock> ds;       // K0 blocks over all intervals
   uint64_t destuff_bytes = 0;      // destuffed buffer size incl. per-interval alignment
   uint64_t entries = 0;            // sparse-coefficient entries reserved (worst case)

@@ -225,7 +225,8 @@ def pdec(request):
     from tests import gpu_util as G
     G.torch()
     policy, groups, extra = request.param
-    env = {"RJ_PIPE_MIN": "1", "RJ_PIPE_GROUPS": str(groups), **extra}
+    # (RJ_CHUNK_MIN: no call-time interval split, so that these small calls keep the layouts)
+    env = {"RJ_PIPE_MIN": "1", "RJ_PIPE_GROUPS": str(groups), "RJ_CHUNK_MIN": str(1 << 30), **extra}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
