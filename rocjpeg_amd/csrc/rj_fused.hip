@@ -85,18 +85,17 @@ __device__ __forceinline__ void store_bytes(uint8_t *d, uint32_t n, const uint32
 struct EntWin {
   uint32_t w[RJ_WIN_ROWS];
   uint32_t base_lo, base_hi;
+#ifdef RJ_EXP_E16
+  bool raw = false;
+#endif
   __device__ __forceinline__ void load(const uint32_t *__restrict__ ent, uint64_t at, uint32_t lane) {
     base_lo = U(uint32_t(at));
     base_hi = U(uint32_t(at >> 32));
-#ifdef RJ_EXP_E16  // timing probe: 16-bit entries (rj_huff.hip hl_flush), expanded to the 32-bit form
+#ifdef RJ_EXP_E16  // timing probe: 16-bit entries (rj_huff.hip hl_flush), expanded by settle()
     const uint16_t *p16 = reinterpret_cast<const uint16_t *>(ent) + at;
 #pragma unroll
-    for (int r = 0; r < RJ_WIN_ROWS; r++) {
-      const uint32_t h = gp(p16)[r * 64u + lane];
-      const uint32_t pos = h >> 10;
-      const int32_t v = __builtin_amdgcn_sbfe(int32_t(h), 0, 10);
-      w[r] = v == -512 ? (pos == 63u ? RJ_RE_TERM : RJ_RE_ZERO) : ((uint32_t(v) & 0xFFFFu) | (pos << 16));
-    }
+    for (int r = 0; r < RJ_WIN_ROWS; r++) w[r] = gp(p16)[r * 64u + lane];
+    raw = true;
 #else
     const uint32_t *p = ent + at;
 #pragma unroll
@@ -109,6 +108,17 @@ struct EntWin {
   // parse_blocks and the row's first, and in row_body after the IDCT for the next strip's window
   // (loaded at the end of phase A, waited before phase C's stores).
   __device__ __forceinline__ void settle() {
+#ifdef RJ_EXP_E16
+    if (raw) {
+#pragma unroll
+      for (int r = 0; r < RJ_WIN_ROWS; r++) {
+        const uint32_t h = w[r], pos = h >> 10;
+        const int32_t v = __builtin_amdgcn_sbfe(int32_t(h), 0, 10);
+        w[r] = v == -512 ? (pos == 63u ? RJ_RE_TERM : RJ_RE_ZERO) : ((uint32_t(v) & 0xFFFFu) | (pos << 16));
+      }
+      raw = false;
+    }
+#endif
 #pragma unroll
     for (int r = 0; r < RJ_WIN_ROWS; r++) asm volatile("" : "+v"(w[r]));
   }
