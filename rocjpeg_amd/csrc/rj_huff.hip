@@ -1,21 +1,27 @@
-// rj_huff.hip -- lean K1: baseline Huffman decode of "row" images (every restart interval
-// inside one MCU row), one lane per interval (T.81 F.2.2, libjpeg jdhuff.c semantics).
+// rj_huff.hip -- K1: baseline Huffman decode (T.81 F.2.2, libjpeg jdhuff.c semantics).
+//   k_huff        the lean launch for "row" images (every restart interval inside one MCU row),
+//                 one lane per interval (and, for outlier intervals, a head + tail lane pair);
+//   k_huff_chunk  every other call: rj_entropy.hip's chunk layout (one lane per chunk of a split
+//                 interval, one per whole interval otherwise), records and resolution.
 //
 // The reference hands this step to VCN (src/rocjpeg_vaapi_decoder.cpp:677-689).  At ~1 wave per
 // SIMD (a C2 batch has 68 intervals per image) the serial symbol chain is issue-bound, so the
 // step keeps only what the bit position depends on:
 //   * one 32-bit table entry per code prefix carries every field the step uses (rj_device.h
-//     RjLeanTables): bit count, extra-bit width, run, whether it writes an entry;
-//   * the step writes the *raw* symbol (extra bits + size + zigzag position): sign extension
-//     and the DC prediction move to K2 (rj_fused.hip), which sees 64 blocks at once and needs
-//     a handful of instructions per strip for them;
+//     RjLeanTables): bit count, extra-bit width, run -- and, where it fits the key, the code
+//     that follows with its own fields (two symbols per step);
+//   * the entry written per coefficient is its HUFF_EXTENDed value and zigzag position; the DC
+//     is a difference in the lean launch (K2, rj_fused.hip, restores the predictions for 64
+//     blocks at once) and absolute in the chunk launch (the lane keeps libjpeg's predictors);
 //   * bits: the two stream words holding the bit position in registers, the next one read one
-//     step ahead from the lane's LDS ring; a 32-bit peek is one v_alignbit_b32 (q = -pos);
+//     step ahead from the lane's LDS ring, which a mover wave beside each decoder wave keeps
+//     filled; a 32-bit peek is one v_alignbit_b32 (q = -pos);
 //   * block / MCU bookkeeping: the block index inside the MCU selects the tables through a
-//     2-bit-per-block pattern.
-// Everything else (ring refills from HBM, stage flushes, libjpeg's insufficient-data and
-// missing-marker rules) happens at wave-uniform phase boundaries every RJ_HL_PHASE symbols, and
-// the per-lane activity / end-of-data selects only in the phases where some lane may finish.
+//     2-bit-per-block pattern; the step is software-pipelined (the next lookup is issued before
+//     this symbol's entry is written).
+// Everything else (stage flushes, libjpeg's insufficient-data and missing-marker rules, the
+// chunk lanes' records and sync tests) happens at wave-uniform phase boundaries every
+// RJ_HL_PHASE steps, or only in the phases where some lane may finish or stop.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
