@@ -180,7 +180,6 @@ int Decoder::Initialize() {
     if (getenv(dbg_names[k])) dbg_ |= 1u << k;
   if (const char *pp = getenv("RJ_PROG_PIPE")) prog_pipe_enabled_ = atoi(pp) != 0;
   if (const char *pw = getenv("RJ_PROG_WAVE_ALL")) prog_wave_all_ = atoi(pw) != 0;
-  if (const char *pl = getenv("RJ_PROG_LANE_REFINE")) prog_lane_refine_ = atoi(pl) != 0;
   for (auto *arr : {k1s_, k2s_, k2e_})
     for (int q = 0; q < kMaxPipe; q++) RJ_HIP(hipEventCreate(&arr[q]));
   (void)backend_;  // HARDWARE and HYBRID both run the HIP decoder
@@ -790,7 +789,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     // refinement grid -- with ten waves per image one grid outgrows the chip's wave slots several
     // times over (C5 1080p: 1024 images 111 ms one grid vs 117 ms two; 2048 images 243 vs 200)
     prog_wave_all = prog_pipe && (prog_wave_all_ >= 0 ? prog_wave_all_ != 0 : prog_images <= kProgWaveAllImages);
-    auto in_lanes = [&](uint32_t kind) { return !prog_pipe && (kind != RJ_PK_AC_REFINE || prog_lane_refine_); };
+    auto in_lanes = [&](uint32_t kind) { return !prog_pipe && kind != RJ_PK_AC_REFINE; };
     // algorithmic bytes of an interval: destuffed bytes read + what its decode writes (DC first:
     // one halfword per block; DC refinement: one bit per block; AC first: the band's halfwords +
     // the nonzero mask; AC refinement: mask read + one 32-B record per block)
@@ -805,7 +804,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     std::vector<uint32_t> &bk = sc_.prog_bucket;
     for (uint32_t L = 0; L < nlev; L++) {
       prog_level_off[L] = uint32_t(prog_lanes.size());
-      for (uint32_t K = 0; K < 4; K++) {  // AC refinement: waves, below (lanes with prog_lane_refine_)
+      for (uint32_t K = 0; K < 3; K++) {  // AC refinement: waves, below
         if (!in_lanes(K)) continue;
         bk.assign(kPB + 1, 0);
         uint32_t cnt = 0;
@@ -908,7 +907,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
           for (uint32_t q = 0; q < p.pivals.size(); q++) {
             const RjProgIvalDev &iv = p.pivals[q];
             const RjProgScanDev &sc = p.pscans[iv.scan];
-            if (sc.level == L && sc.kind == RJ_PK_AC_REFINE && !in_lanes(sc.kind) && !(iv.flags & RJ_SEG_MISSING)) {
+            if (sc.level == L && sc.kind == RJ_PK_AC_REFINE && !(iv.flags & RJ_SEG_MISSING)) {
               prog_lanes.push_back(imgs[i].pival_prefix + q);
               timings_.prog_kernel_bytes[1] += ival_bytes(sc, iv);
             }

@@ -19,10 +19,11 @@
 // atomics: two lanes of one level may share a dword across band edges).
 //
 // Per lane everything on the symbol chain is on-chip: the first-level LUT of the lane's table
-// (9 bits; DC first: two 8-bit tables) in a lane-interleaved LDS column, the bitstream in a
-// 32-word LDS ring, and (AC refinement) the nonzero masks of the coming blocks in a 32-entry LDS
-// ring.  Both rings are topped up at wave-uniform phase boundaries with loads issued one phase
-// before they are committed; the symbol loop itself reads no HBM.
+// (9 bits; DC first: two 8-bit tables) in a lane-interleaved LDS column and the bitstream in a
+// 32-word LDS ring, topped up at wave-uniform phase boundaries with loads issued one phase before
+// they are committed; the symbol loop itself reads no HBM.  AC refinements are decoded by
+// k_prog_wave below (a lane-per-interval refinement decoder, round 1's lane_ac_refine, measured
+// 2x slower than the wave decoder in round 4 and was removed).
 #include <hip/hip_runtime.h>
 
 #include "rj_device.h"
@@ -34,7 +35,6 @@ namespace rj {
 #define RJ_PW 64       // one wave per workgroup
 #define RJ_PPHASE 8    // iterations per phase; an iteration consumes <= 32 bits and <= 1 block
 #define RJ_PRING 32    // bit ring words per lane
-#define RJ_PNZ 32      // nonzero-mask ring entries per lane
 #define RJ_PVALS 48    // symbol words per lane (AC tables: <= 162 symbols)
 
 struct PRow {  // lane-interleaved LDS column: word w of this lane at base[w * 64]
@@ -386,156 +386,6 @@ __device__ __forceinline__ void lane_ac_first(const PLaneIn &L, PGeo &g, PBits &
 __device__ __forceinline__ uint64_t lomask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
 __device__ __forceinline__ uint32_t ctz64(uint64_t x) { return uint32_t(__builtin_ctzll(x)); }
 
-__device__ __forceinline__ void lane_ac_refine(const PLaneIn &L, PGeo &g, PBits &br, const HRow &lut, const VRow &vals,
-                               unsigned long long *rec, const unsigned long long *nz, uint32_t nzbase, PRow nzr) {
-  const RjProgScanDev &sc = L.sc;
-  const RjHuffDev *gt = L.active ? L.im->ptabs + sc.tab[0] : nullptr;
-  if (L.active) {
-    const uint4 *src = reinterpret_cast<const uint4 *>(gt->lut);
-    for (uint32_t q = 0; q < 64; q++) {
-      const uint4 v = gp(src)[q];
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        lut[q * 8u + 2 * j] = uint16_t(w[j] & 0xFFFFu);
-        lut[q * 8u + 2 * j + 1] = uint16_t(w[j] >> 16);
-      }
-    }
-  }
-  PLong lg;  // AC codes longer than 9 bits
-  if (L.active) {
-    lg.load(gt, 0);
-    load_vals(gt, vals, 0, RJ_PVALS);
-  }
-  const uint32_t ss = sc.ss, se = sc.se;
-  const uint64_t band = lomask(se + 1) & ~lomask(ss);
-  const uint32_t nbits = L.iv.dst_len * 8u;
-  // nonzero-mask ring: masks of units [0, ntop) relative to the interval are committed
-  const unsigned long long *nzsrc = nz + nzbase;
-  const uint32_t nlast = g.nunits ? g.nunits - 1 : 0u;
-  uint32_t ntop = 0;
-  auto nz_put = [&](const uint2 &m) {
-    nzr[2 * (ntop & (RJ_PNZ - 1))] = m.x;
-    nzr[2 * (ntop & (RJ_PNZ - 1)) + 1] = m.y;
-    ntop++;
-  };
-  {
-    uint2 m[24];
-#pragma unroll
-    for (uint32_t q = 0; q < 24; q++) m[q] = *gp(reinterpret_cast<const uint2 *>(nzsrc + min(q, nlast)));
-#pragma unroll
-    for (int q = 0; q < 24; q++) nz_put(m[q]);
-  }
-  uint32_t urel = 0;  // unit relative to the interval (ring index)
-  auto nz_get = [&](uint32_t ur) {
-    const uint32_t sl = ur & (RJ_PNZ - 1);
-    return (uint64_t(nzr[2 * sl + 1]) << 32) | nzr[2 * sl];
-  };
-  uint64_t nzm = nz_get(0) & band;
-  uint32_t k = ss, eobrun = 0, t = 0, newv = 0;  // newv: 0 none, 1 positive, 2 negative
-  bool walking = false, eobblk = false;
-  // this block's record: its correction bits in walk order (one per previously nonzero position
-  // of the band, ascending -- k_prog_fold deposits them onto those positions), new coefficients
-  uint64_t cstr = 0, sgn = 0, blk_new = 0;
-  uint32_t pend = 0;  // correction bits left before the walk reaches t
-  bool active = L.active;
-  while (__any(active)) {
-    uint4 pa, pb;
-    const bool rb = br.room();
-    br.issue(pa, pb);
-    uint2 pm[8];
-    const bool rn = ntop + 8 - urel <= RJ_PNZ;
-#pragma unroll
-    for (uint32_t q = 0; q < 8; q++) pm[q] = *gp(reinterpret_cast<const uint2 *>(nzsrc + min(ntop + q, nlast)));
-#pragma unroll 1
-    for (int it = 0; it < RJ_PPHASE; it++) {
-      if (!active) continue;
-      const uint32_t peek = br.peek();
-      uint32_t used = 0;
-      if (!walking) {
-        if (eobrun) {
-          // handled below (shared with the EOB symbol)
-        } else {
-          uint32_t e = lut[peek >> 23];
-          const uint32_t el = plong_decode(lg, peek, vals);
-          e = (e & 0x8000u) ? el : e;
-          const uint32_t len = e >> 8, r = (e >> 4) & 15u, s = e & 15u;
-          used = len;
-          if (s || r == 15) {
-            if (s) {
-              newv = pbits(peek, used, 1) ? 1u : 2u;
-              used++;
-            } else {
-              newv = 0;
-            }
-            // the (r+1)-th not-yet-nonzero position at or after k (libjpeg's zero-run walk)
-            uint64_t z = ~nzm & band & ~lomask(k);
-            for (uint32_t j = 0; j < r; j++) z &= z - 1;
-            t = z ? ctz64(z) : se + 1;
-            pend = uint32_t(__popcll(nzm & lomask(t) & ~lomask(k)));
-          } else {  // EOBr: this block's rest and 2^r + bits - 1 more blocks
-            eobrun = (1u << r) + pbits(peek, used, r);
-            used += r;
-            t = se + 1;
-            newv = 0;
-            eobblk = true;
-            pend = uint32_t(__popcll(nzm & ~lomask(k)));
-          }
-        }
-        if (eobrun && !eobblk) {  // a block inside an EOB run: every nonzero position of the band
-          t = se + 1;
-          newv = 0;
-          eobblk = true;
-          pend = uint32_t(__popcll(nzm & ~lomask(k)));
-        }
-        walking = true;
-      }
-      // correction bits of the nonzero positions in [k, t): appended in walk order, at most
-      // 32 - used per iteration (the walk resumes next iteration)
-      const uint32_t take = min(pend, 32u - used);
-      cstr = (cstr << take) | pbits(peek, used, take);
-      used += take;
-      pend -= take;
-      br.pos += used;
-      bool blk_done = false;
-      if (pend == 0) {
-        walking = false;
-        if (newv && min(t, 63u) <= se) {  // past Se (corrupt data): dropped, see lane_ac_first
-          const uint64_t bq = 1ull << min(t, 63u);
-          blk_new |= bq;
-          if (newv == 2) sgn |= bq;
-        }
-        if (eobblk) {
-          eobblk = false;
-          eobrun--;
-          blk_done = true;
-        } else {
-          k = t + 1;
-          blk_done = k > se;
-        }
-      }
-      if (blk_done) {
-        if (cstr | blk_new) {  // the record stays zero (memset) for a block with nothing to apply
-          uint4 *r4 = reinterpret_cast<uint4 *>(rec + uint64_t(g.u) * 4u);
-          *gp(r4) = make_uint4(uint32_t(cstr), uint32_t(cstr >> 32), uint32_t(sgn), uint32_t(sgn >> 32));
-          *gp(r4 + 1) = make_uint4(uint32_t(blk_new), uint32_t(blk_new >> 32), 0u, 0u);
-        }
-        cstr = sgn = blk_new = 0;
-        k = ss;
-        unit_step(g, 1);
-        urel++;
-        if (g.u >= g.nunits || br.pos > nbits) active = false;
-        else nzm = nz_get(urel) & band;
-      }
-    }
-    br.commit(pa, pb, rb);
-    if (rn) {
-#pragma unroll
-      for (int q = 0; q < 8; q++) nz_put(pm[q]);
-    }
-  }
-}
-
 __global__ __launch_bounds__(RJ_PW) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_prog(const RjImageDev *__restrict__ imgs, int nimg,
                                                 const uint32_t *__restrict__ lanes, uint32_t nlanes,
                                                 const uint8_t *__restrict__ destuffed, uint32_t *__restrict__ coef,
@@ -544,7 +394,6 @@ __global__ __launch_bounds__(RJ_PW) __attribute__((amdgpu_waves_per_eu(1, 1))) v
   __shared__ uint16_t s_lut[RJ_LUT_L1 * RJ_PW];
   __shared__ uint32_t s_vals[RJ_PVALS * RJ_PW];
   __shared__ uint32_t s_ring[RJ_PRING * RJ_PW];
-  __shared__ uint32_t s_nz[2 * RJ_PNZ * RJ_PW];
   const uint32_t lane = threadIdx.x;
   const uint32_t gl = blockIdx.x * RJ_PW + lane;
   const uint32_t gi = gl < nlanes ? *gp(lanes + gl) : 0xFFFFFFFFu;
@@ -605,8 +454,7 @@ __global__ __launch_bounds__(RJ_PW) __attribute__((amdgpu_waves_per_eu(1, 1))) v
     case RJ_PK_AC_FIRST:
       lane_ac_first(L, g, br, lut, vals, coef16, nzi, nzbase);
       break;
-    default:
-      lane_ac_refine(L, g, br, lut, vals, rec, nzi, nzbase, PRow{s_nz + lane});
+    default:  // AC refinements are never given to the lanes (k_prog_wave decodes them)
       break;
   }
 }
@@ -630,8 +478,8 @@ hipError_t LaunchProgressive(hipStream_t st, const RjImageDev *imgs, int nimg, c
 // positions through readlane -- the refinement state machine (zero-run targets, EOB runs,
 // correction-bit counts on the 64-bit nonzero mask) is SALU work.  The bitstream window (64 + 64
 // words), the coming blocks' nonzero masks and the pending records live one per lane in VGPRs;
-// records leave 64 blocks at a time (coalesced).  Refinement output is identical to
-// lane_ac_refine (same records, k_prog_fold applies them); a first scan's block is assembled
+// records leave 64 blocks at a time (coalesced), one 32-B record per block that k_prog_fold
+// applies (its correction bits in walk order, new positions, signs); a first scan's block is assembled
 // across the lanes (lane q = coefficient q) and leaves as one masked 16-bit store, exactly the
 // halfwords lane_ac_first writes.
 // ---------------------------------------------------------------------------------------
@@ -1090,8 +938,8 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
       if (__builtin_expect(pend != 0, 0)) continue;  // the walk resumes at the next peek
       walking = false;
       // a new coefficient whose zero run overshoots the band (corrupt data): at Se = 63 libjpeg
-      // stores it at natural position 63 (jpeg_natural_order[64] == 63, oracle kZigzag[64]), as
-      // lane_ac_refine does; past a smaller Se it is dropped (see lane_ac_first)
+      // stores it at natural position 63 (jpeg_natural_order[64] == 63, oracle kZigzag[64]);
+      // past a smaller Se it is dropped (see lane_ac_first)
       const uint32_t tc = min(t, 63u);
       if (newv && tc <= se) {
         __builtin_assume(tc < 64u);
