@@ -884,6 +884,42 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
     stamp.nwin++;
     // ---- scalar chain over the window ----
     while (!done && pos - pos0 < 64) {
+#ifndef RJ_PW_NO_FAST
+      // ---- fast path: the common symbol (no EOB, no pending walk, its correction bits inside
+      // this peek, the block not ending with it), as a tight loop with none of the rare state
+      // live; anything else leaves it with the symbol unconsumed for the general step below,
+      // which decodes it exactly as it would have ----
+      if (__builtin_expect(!walking && eobrun == 0, 1)) {
+        for (;;) {
+          const uint32_t df = pos - pos0;
+          if (df >= 64) break;
+          const uint32_t info = rl(info_l, df);
+          if (info & (1u << 10)) break;  // EOBr
+          const uint32_t r = (info >> 6) & 15u, usedf = info & 63u;
+          __builtin_assume(k < 64u);
+          const uint64_t zm = ~nzm & band & (~0ull << k);
+          const uint32_t below =
+              __builtin_amdgcn_mbcnt_hi(uint32_t(zm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(zm), 0u));
+          const uint64_t hit = __ballot(below == r) & zm;
+          const uint32_t tf = hit ? ctz64(hit) : se + 1;
+          const uint32_t pf = (tf - k) - min(r, uint32_t(__popcll(zm)));
+          if (usedf + pf > 32u || tf + 1u > se) break;  // walk across peeks, or the block ends
+          const uint32_t cb = rl(ck_l, df);
+          cstr = (cstr << pf) | uint32_t((uint64_t(cb) << pf) >> 32);
+          pos += usedf + pf;
+          const uint32_t nvf = (info >> 11) & 3u;
+          if (nvf) {  // tf < se <= 63 here
+            __builtin_assume(tf < 64u);
+            const uint64_t bq = 1ull << tf;
+            newm |= bq;
+            sgn |= nvf == 2 ? bq : 0ull;
+          }
+          k = tf + 1;
+          stamp.nstep++;
+        }
+        if (pos - pos0 >= 64) continue;  // the window is used up: the next one
+      }
+#endif
       const uint32_t d = pos - pos0;
       stamp.nstep++;
       uint32_t used = 0, cbits;
