@@ -901,21 +901,22 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
           const uint32_t below =
               __builtin_amdgcn_mbcnt_hi(uint32_t(zm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(zm), 0u));
           const uint64_t hit = __ballot(below == r) & zm;
-          const uint32_t tf = hit ? ctz64(hit) : se + 1;
+          // s_ff1: the lowest set bit, -1 for none (then tf >= se and the symbol leaves the loop)
+          uint32_t tf;
+          asm("s_ff1_i32_b64 %0, %1" : "=s"(tf) : "s"(hit));
           const uint32_t pf = (tf - k) - min(r, uint32_t(__popcll(zm)));
-          if (usedf + pf > 32u || tf + 1u > se) break;  // walk across peeks, or the block ends
+          // walk across peeks, or the block ends (one compare: tf >= se also covers no hit)
+          if ((usedf + pf > 32u) | (tf >= se)) break;
           const uint32_t cb = rl(ck_l, df);
           cstr = (cstr << pf) | uint32_t((uint64_t(cb) << pf) >> 32);
           pos += usedf + pf;
           const uint32_t nvf = (info >> 11) & 3u;
-          if (nvf) {  // tf < se <= 63 here
-            __builtin_assume(tf < 64u);
-            const uint64_t bq = 1ull << tf;
-            newm |= bq;
-            sgn |= nvf == 2 ? bq : 0ull;
-          }
+          // tf < se <= 63 here; a new coefficient's bit, branch-free (nvf 0: none, 2: negative)
+          __builtin_assume(tf < 64u);
+          const uint64_t bq = nvf ? 1ull << tf : 0ull;
+          newm |= bq;
+          sgn |= nvf == 2 ? bq : 0ull;
           k = tf + 1;
-          stamp.nstep++;
         }
         if (pos - pos0 >= 64) continue;  // the window is used up: the next one
       }
