@@ -1074,10 +1074,22 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
     const uint32_t cq = cw >> 2;
     const uint32_t cwmax = min(cw, cW > cx0 ? cW - cx0 : 0u);
     const uint32_t crows = min(ch, cH > cy0 ? cH - cy0 : 0u);
-    for (uint32_t k = tid; k < 2 * cq * crows; k += 64) {
-      const uint32_t second = k >= cq * crows ? 1u : 0u;
-      const uint32_t kk = k - second * cq * crows;
-      const uint32_t y = kk / cq, x = (kk - y * cq) * 4;
+    // lane walks quads tid, tid + 64, ... of the U plane's strip, then of the V plane's, with an
+    // incremental (row, quad) (a division only at the start and where it enters the V plane)
+    const uint32_t cqd = max(cq, 1u);  // (no iteration when cq = 0)
+    const uint32_t tot = cq * crows, csy = 64 / cqd, csx = 64 - csy * cqd;
+    uint32_t second = 0, y = tid / cqd, xq = tid - y * cqd;
+    for (uint32_t k = tid; k < 2 * tot; k += 64, xq += csx, y += csy) {
+      if (xq >= cq) {
+        xq -= cq;
+        y++;
+      }
+      if (second == 0 && k >= tot) {
+        second = 1;
+        y = (k - tot) / cqd;
+        xq = (k - tot) - y * cqd;
+      }
+      const uint32_t x = xq * 4;
       if (x >= cwmax) continue;
       const uint32_t n = min(4u, cwmax - x);
       const uint32_t s4 = *reinterpret_cast<const uint32_t *>(s_buf + (second ? toff[2] : toff[1]) +
