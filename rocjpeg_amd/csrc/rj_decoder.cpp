@@ -1172,6 +1172,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   cbuf.wide_flag = d_wide_flag_;
   cbuf.piece_shift = 0;
   cbuf.chunk_bytes = chunk_bytes;
+  // chunk warm-up (k_huff_chunk): up to half a chunk while the call's lanes leave the chip half
+  // idle, an eighth once they fill it (profiles/r4_experiments/k1_chunk_warmup_ab.txt)
+  cbuf.warm_shift = 2ull * lanes_all <= uint64_t(cu_count_) * RJ_K1_WG ? 1u : 3u;
   cbuf.seg_ent = nullptr;  // set with the split layout below
   if (profiling_) {
     RJ_CHECK(d_count_.Ensure(256));

@@ -77,6 +77,7 @@ struct RjCoefBuf {
   uint32_t *wide_flag;        // host-mapped: set by K2 when it recorded a row for the fix-up
   uint32_t piece_shift;       // identity layout: interval s's pieces start at s << piece_shift
   uint32_t chunk_bytes;       // the call's chunk length (rj_chunks_cb; 0: no interval split)
+  uint32_t warm_shift;        // k_huff_chunk warm-up: min(RJ_CHUNK_WARM_BYTES, chunk length >> warm_shift)
   const unsigned long long *seg_ent;  // per interval: first entry of its chunk regions (split ones)
 };
 // Lean K1 split launch (rj_huff.hip): an interval decoded by a head lane from its start and a
@@ -118,6 +119,9 @@ struct RjHuffSplit {
 #define RJ_SPLIT_BYTES 12288u
 #define RJ_OVERLAP_CHUNKS 3u      // a lane may decode this many chunk lengths past its own end,
 #define RJ_OVERLAP_MIN_BYTES 4096u  // and at least this many bytes (resynchronisation is long-tailed)
+#ifndef RJ_CHUNK_WARM_BYTES
+#define RJ_CHUNK_WARM_BYTES 512u  // k_huff_chunk: the most a speculative lane starts before its chunk (16-B multiple)
+#endif
 #define RJ_CHUNK_ENT_PER_BYTE 4u  // region budget of a chunk lane (typical ~1.7); overflow -> serial path
 __host__ __device__ inline uint32_t rj_chunks(uint32_t bytes) {
   if (bytes < RJ_SPLIT_BYTES) return 1u;
@@ -145,7 +149,8 @@ __host__ __device__ inline uint32_t rj_chunk_reach(uint32_t clen) {
   return RJ_OVERLAP_CHUNKS * clen > RJ_OVERLAP_MIN_BYTES ? RJ_OVERLAP_CHUNKS * clen : RJ_OVERLAP_MIN_BYTES;
 }
 __host__ __device__ inline uint64_t rj_chunk_cap(uint32_t clen) {
-  return rj_group(uint64_t(RJ_CHUNK_ENT_PER_BYTE) * (uint64_t(clen) + rj_chunk_reach(clen)) + 2 * RJ_ENT_PER_BLOCK);
+  return rj_group(uint64_t(RJ_CHUNK_ENT_PER_BYTE) * (uint64_t(clen) + RJ_CHUNK_WARM_BYTES + rj_chunk_reach(clen)) +
+                  2 * RJ_ENT_PER_BLOCK);
 }
 // entries reserved for an interval at parse time: one serial stream (zero-bit decode of the
 // last MCU after the data ends, then one zero DC entry per skipped block) -- an exact lane's

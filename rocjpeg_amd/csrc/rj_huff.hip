@@ -652,8 +652,9 @@ __device__ __forceinline__ void hc_put_record(RjRecord *r, uint32_t pos, uint32_
     if (chunk && bend && act) { /* a block start of a chunk lane (divergent: ~1 step in 6) */           \
       rb++;                                                                                               \
       const uint32_t pos = start_bit + (0u - q);                                                          \
-      if (spec && nrec < RJ_MAX_RECORDS && rb % RJ_RECORD_EVERY == 0 && pos < end_bit && !rp) {            \
+      if (spec && nrec < RJ_MAX_RECORDS && rb >= rec_rb && pos >= own_bit && pos < end_bit && !rp) {        \
         rp = true;                                                                                        \
+        rec_rb = rb + RJ_RECORD_EVERY;                                                                    \
         rp_pos = pos;                                                                                     \
         rp_b = b >> 1;                                                                                    \
         rp_ne = ne;                                                                                       \
@@ -751,8 +752,19 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     const uint32_t clen = chunk ? rj_chunk_len(nbytes, nch) : nbytes;
     const uint32_t b0 = chunk ? min(c * clen, nbytes) : 0u, b1 = chunk ? min(b0 + clen, nbytes) : nbytes;
     const bool empty = chunk && c > 0 && b0 >= nbytes;  // no data left for this chunk (16-B rounding)
-    const uint32_t lane_bytes = empty ? 0u : nbytes - b0;  // the lane may read on to the data's end
-    const uint4 *src = reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off + b0);
+    // a speculative lane starts `warm` bytes before its chunk, so that its decode has usually
+    // resynchronised with the true one by the chunk start, where its records begin: the lane
+    // before then meets a record right after it crosses, instead of running on through the
+    // (long-tailed) resynchronisation distance itself.  At most half a chunk (the lane has to be
+    // past its chunk start, with its first record out, before the lane before it gets there),
+    // and an eighth when the call's lanes fill the chip (the warm-up is then extra work, not
+    // idle time): RjCoefBuf.warm_shift.
+    const uint32_t warm = (chunk && c > 0 && !empty)
+                              ? min(b0, min(uint32_t(RJ_CHUNK_WARM_BYTES), (clen >> coefs.warm_shift) & ~15u))
+                              : 0u;
+    const uint32_t bs = b0 - warm;  // 16-B aligned: b0 and the warm-up both are
+    const uint32_t lane_bytes = empty ? 0u : nbytes - bs;  // the lane may read on to the data's end
+    const uint4 *src = reinterpret_cast<const uint4 *>(destuffed + im.destuff_off + sg.dst_off + bs);
     const uint32_t nchunks = (lane_bytes + 15) / 16;
     const HCol<DEC> ring{&s_ring[0][L]};
 
@@ -805,7 +817,7 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     const RjTableSet *tset = tabsets + T;
     const HCol<DEC> stage{&s_stage[0][L]};
     // chunk-lane state (rj_entropy.hip decode_lane)
-    const uint32_t start_bit = b0 * 8u, end_bit = b1 * 8u, nbits_abs = nbytes * 8u;
+    const uint32_t start_bit = bs * 8u, own_bit = b0 * 8u, end_bit = b1 * 8u, nbits_abs = nbytes * 8u;
     const uint32_t clen_bits = clen * 8u, ov_bit = end_bit + rj_chunk_reach(clen) * 8u;
     const uint32_t cap = rcap, next_chunks = chunk ? nch - 1 - c : 0u;
     const bool spec = chunk && c > 0;
@@ -813,6 +825,7 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     const RjRecord *const rec_next = rec_mine - RJ_MAX_RECORDS;  // chunk c + 1 sits on lane g - 1
     uint32_t rb = 0, nrec = 0, tgt = 0, j = 0, status = 0, rb_over = 0xFFFFFFFFu, s_tgt = 0, s_rec = 0;
     uint32_t next_tgt_bit = end_bit;
+    uint32_t rec_rb = 0;  // blocks before the next record may be taken (its first: at the chunk start)
     uint64_t cache = 0;
     uint32_t cache_tj = 0xFFFFFFFFu;
     bool rp = false;
@@ -828,9 +841,10 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
       lds_st(&s_dec[L], RJ_HL_FIN);
       continue;
     }
-    if (spec) {  // the chunk's first bit is a block start by assumption: record 0
+    if (spec && warm == 0) {  // no warm-up: the chunk's first bit is a block start by assumption
       hc_put_record<kScope>(rec_mine, start_bit, 0u, epoch, 0u, 0u, 0, 0, 0);
       nrec = 1;
+      rec_rb = RJ_RECORD_EVERY;
     }
 #define RJ_HC_WAIT_RING(upto)                                                                     \
   {                                                                                               \
