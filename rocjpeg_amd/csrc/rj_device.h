@@ -115,7 +115,8 @@ struct RjHuffSplit {
 #ifndef RJ_CHUNK_BYTES
 #define RJ_CHUNK_BYTES 5120u
 #endif
-#define RJ_CHUNK_MIN_BYTES 512u  // default floor of the call's chunk length (env RJ_CHUNK_MIN)
+#define RJ_CHUNK_MIN_BYTES 384u  // default floor of the call's chunk length (env RJ_CHUNK_MIN; sweep:
+                                 // profiles/r4_experiments/call_shape_chunking.txt)
 #define RJ_SPLIT_BYTES 12288u
 #define RJ_OVERLAP_CHUNKS 3u      // a lane may decode this many chunk lengths past its own end,
 #define RJ_OVERLAP_MIN_BYTES 4096u  // and at least this many bytes (resynchronisation is long-tailed)

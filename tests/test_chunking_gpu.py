@@ -1,6 +1,6 @@
 """Per-call chunk geometry (rj_decoder.cpp, rj_device.h rj_chunks_cb): a call
 whose intervals cannot fill the chip cuts them into chunks of the call's length (the call's
-bytes over one round of decoder lanes, at least the handle's floor, 512 B by default), decoded
+bytes over one round of decoder lanes, at least the handle's floor, 384 B by default), decoded
 by the self-synchronising chunk lanes (rj_huff.hip k_huff_chunk) with rj_entropy.hip's
 resolution and serial fallback.  Small calls of row-interval images -- the reference's
 rocJpegDecode shape -- therefore run the chunk path on intervals of a few KB, with damaged
@@ -77,11 +77,12 @@ def _check(datas, bufs_all, shapes_all, fmt=R.OutputFormat.RGB):
 @pytest.mark.parametrize("fmt", [R.OutputFormat.RGB, R.OutputFormat.YUV_PLANAR], ids=["RGB", "YUV_PLANAR"])
 def test_one_row_image_is_split_at_the_floor(dec, fmt):
     """One 1080p image with one MCU row per interval (68 intervals of ~4 KB): the call cuts
-    every interval into 512-B chunks and decodes it like the oracle."""
+    every interval into chunks of the floor (384 B, rj_device.h RJ_CHUNK_MIN_BYTES) and decodes it
+    like the oracle."""
     data = O.fixture_bytes(RI_1080)
     st, tm, bufs, shapes = _decode_batch(dec, [data], fmt)
     assert st == 0
-    assert tm["chunk_bytes"] == 512 and tm["lean_k1"] == 0 and tm["chunk_k1"] == 1
+    assert tm["chunk_bytes"] == 384 and tm["lean_k1"] == 0 and tm["chunk_k1"] == 1
     assert tm["split_intervals"] > 0 and tm["chunks"] > tm["intervals"]
     _check([data], bufs, shapes, fmt)
 
