@@ -180,6 +180,7 @@ int Decoder::Initialize() {
     if (getenv(dbg_names[k])) dbg_ |= 1u << k;
   if (const char *pp = getenv("RJ_PROG_PIPE")) prog_pipe_enabled_ = atoi(pp) != 0;
   if (const char *pw = getenv("RJ_PROG_WAVE_ALL")) prog_wave_all_ = atoi(pw) != 0;
+  if (const char *pd = getenv("RJ_PROG_DC_LANES")) prog_dc_lanes_ = atoi(pd) != 0;
   for (auto *arr : {k1s_, k2s_, k2e_})
     for (int q = 0; q < kMaxPipe; q++) RJ_HIP(hipEventCreate(&arr[q]));
   (void)backend_;  // HARDWARE and HYBRID both run the HIP decoder
@@ -789,7 +790,13 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     // refinement grid -- with ten waves per image one grid outgrows the chip's wave slots several
     // times over (C5 1080p: 1024 images 111 ms one grid vs 117 ms two; 2048 images 243 vs 200)
     prog_wave_all = prog_pipe && (prog_wave_all_ >= 0 ? prog_wave_all_ != 0 : prog_images <= kProgWaveAllImages);
-    auto in_lanes = [&](uint32_t kind) { return !prog_pipe && kind != RJ_PK_AC_REFINE; };
+    // DC scans in lanes (one lane per interval, 64 images per wave) on the side stream in the
+    // pipelined layouts too: nothing in the wave grid waits for them, and the wave decoder's
+    // scalar chains are what a batch runs out of
+    auto in_lanes = [&](uint32_t kind) {
+      return prog_pipe ? (prog_dc_lanes_ && (kind == RJ_PK_DC_FIRST || kind == RJ_PK_DC_REFINE))
+                       : kind != RJ_PK_AC_REFINE;
+    };
     // algorithmic bytes of an interval: destuffed bytes read + what its decode writes (DC first:
     // one halfword per block; DC refinement: one bit per block; AC first: the band's halfwords +
     // the nonzero mask; AC refinement: mask read + one 32-B record per block)
@@ -878,7 +885,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         const DecodePlan &p = streams[i]->plan();
         if (!p.progressive) continue;
         keys_of(p, streams[i]->info().ncomp);
-        for (const RjProgIvalDev &iv : p.pivals) bucket[scan_key[iv.scan] + 1]++;
+        for (const RjProgIvalDev &iv : p.pivals)
+          if (!in_lanes(p.pscans[iv.scan].kind)) bucket[scan_key[iv.scan] + 1]++;
       }
       for (uint32_t b = 0; b < nkeys; b++) bucket[b + 1] += bucket[b];
       const uint32_t base = uint32_t(prog_lanes.size());
@@ -890,6 +898,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         keys_of(p, streams[i]->info().ncomp);
         for (uint32_t q = 0; q < p.pivals.size(); q++) {
           const RjProgIvalDev &iv = p.pivals[q];
+          if (in_lanes(p.pscans[iv.scan].kind)) continue;
           // missing intervals too: they report DONE
           prog_lanes[base + bucket[scan_key[iv.scan]]++] = imgs[i].pival_prefix + q;
           if (!(iv.flags & RJ_SEG_MISSING)) timings_.prog_kernel_bytes[1] += ival_bytes(p.pscans[iv.scan], iv);

@@ -165,6 +165,7 @@ class Decoder {
   std::vector<hipEvent_t> prog_lev_ev_;  // development (RJ_DEBUG_PROG): per-level K1p spans
   hipEvent_t prog_join_[2] = {};         // pipelined refinement: side stream fork / join
   bool prog_pipe_enabled_ = true;        // env RJ_PROG_PIPE=0: level-by-level refinement
+  bool prog_dc_lanes_ = true;            // env RJ_PROG_DC_LANES=0: pipelined layouts decode DC scans in waves
   int prog_wave_all_ = -1;               // env RJ_PROG_WAVE_ALL=0/1: force the pipelined layout (-1: by batch)
   // profiling: one event pair per progressive launch, on the stream it runs on; kind 0 k_prog,
   // 1 k_prog_wave, 2 k_prog_fold
