@@ -859,6 +859,10 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
   uint32_t pos = 0, k = ss, eobrun = 0, u = 0;
   uint64_t nzm = uint64_t(rl(uint32_t(nzw), 0)) | (uint64_t(rl(uint32_t(nzw >> 32), 0)) << 32);
   nzm &= band;
+  // the block's zero-history positions and, in lane l, how many of them lie below l: the fast
+  // path's zero-run target is then the candidate whose rank is (rank of k) + r, one compare
+  uint64_t zmb = ~nzm & band;
+  uint32_t rank_l = __builtin_amdgcn_mbcnt_hi(uint32_t(zmb >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(zmb), 0u));
   uint64_t cstr = 0, sgn = 0, newm = 0;
   uint32_t pend = 0, t = 0, newv = 0;
   bool walking = false, eobblk = false, done = nunits == 0;
@@ -867,7 +871,7 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
     candidates(pos, pk_l, e_l);
     // per candidate offset, everything that depends only on the bits there (lane-parallel, off
     // the chain): bits used by the symbol and its extra bits, run length r, EOB flag, new
-    // value (1 positive, 2 negative), EOB-run length; and the 32 bits after them (corrections)
+    // value (bit 0: one, bit 1: negative), EOB-run length; and the 32 bits after them (corrections)
     uint32_t info_l, ck_l;
     {
       const uint32_t len = e_l >> 8, r = (e_l >> 4) & 15u, s = e_l & 15u;
@@ -875,7 +879,7 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
       const uint32_t extra = eob ? r : (s ? 1u : 0u);
       const uint32_t eb = pbits(pk_l, len, extra);
       const uint32_t used = len + extra;
-      const uint32_t nv = s ? (eb ? 1u : 2u) : 0u;
+      const uint32_t nv = s ? (eb ? 1u : 3u) : 0u;
       const uint32_t run = eob ? (1u << r) + eb : 0u;
       info_l = used | (r << 6) | (eob ? 1u << 10 : 0u) | (nv << 11) | (run << 13);
       ck_l = used < 32 ? pk_l << used : 0u;
@@ -890,33 +894,37 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
       // live; anything else leaves it with the symbol unconsumed for the general step below,
       // which decodes it exactly as it would have ----
       if (__builtin_expect(!walking && eobrun == 0, 1)) {
+        __builtin_assume(k < 64u);
+        // zero-history positions below k; inside the loop it follows the target: k = tf + 1
+        uint32_t rk = uint32_t(__popcll(zmb & ~(~0ull << k)));
+        const uint64_t zmf = zmb & ~(1ull << se);
         for (;;) {
           const uint32_t df = pos - pos0;
           if (df >= 64) break;
           const uint32_t info = rl(info_l, df);
           if (info & (1u << 10)) break;  // EOBr
           const uint32_t r = (info >> 6) & 15u, usedf = info & 63u;
-          __builtin_assume(k < 64u);
-          const uint64_t zm = ~nzm & band & (~0ull << k);
-          const uint32_t below =
-              __builtin_amdgcn_mbcnt_hi(uint32_t(zm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(zm), 0u));
-          const uint64_t hit = __ballot(below == r) & zm;
-          // s_ff1: the lowest set bit, -1 for none (then tf >= se and the symbol leaves the loop)
+          // the (r+1)-th zero-history position at or after k: rank rk + r (a lane of lower rank
+          // in zmb lies below k; none of another rank can match); the lanes' rank relative to k
+          // is formed off the symbol's readlane
+          const uint32_t rel = rank_l - rk;
+          // (zmf: without Se -- a target at Se, or none, ends the block: the general step)
+          const uint64_t hit = __ballot(rel == r) & zmf;
+          if (!hit) break;
           uint32_t tf;
           asm("s_ff1_i32_b64 %0, %1" : "=s"(tf) : "s"(hit));
-          const uint32_t pf = (tf - k) - min(r, uint32_t(__popcll(zm)));
-          // walk across peeks, or the block ends (one compare: tf >= se also covers no hit)
-          if ((usedf + pf > 32u) | (tf >= se)) break;
+          // [k, tf) holds r zero-history positions; the others take a correction bit each
+          const uint32_t pf = (tf - k) - r;
+          if (usedf + pf > 32u) break;  // the walk crosses into the next peek
           const uint32_t cb = rl(ck_l, df);
           cstr = (cstr << pf) | uint32_t((uint64_t(cb) << pf) >> 32);
           pos += usedf + pf;
-          const uint32_t nvf = (info >> 11) & 3u;
-          // tf < se <= 63 here; a new coefficient's bit, branch-free (nvf 0: none, 2: negative)
+          // tf < se <= 63 here; a new coefficient's bit and its sign bit, shifted into place
           __builtin_assume(tf < 64u);
-          const uint64_t bq = nvf ? 1ull << tf : 0ull;
-          newm |= bq;
-          sgn |= nvf == 2 ? bq : 0ull;
+          newm |= uint64_t((info >> 11) & 1u) << tf;
+          sgn |= uint64_t((info >> 12) & 1u) << tf;
           k = tf + 1;
+          rk += r + 1u;
         }
         if (pos - pos0 >= 64) continue;  // the window is used up: the next one
       }
@@ -982,7 +990,7 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
         __builtin_assume(tc < 64u);
         const uint64_t bq = 1ull << tc;
         newm |= bq;
-        sgn |= newv == 2 ? bq : 0ull;
+        sgn |= newv == 3 ? bq : 0ull;
       }
       bool blk_done;
       if (__builtin_expect(eobblk, 0)) {
@@ -1023,6 +1031,8 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
       }
       const uint32_t nl = u - nbase;
       nzm = (uint64_t(rl(uint32_t(nzw), nl)) | (uint64_t(rl(uint32_t(nzw >> 32), nl)) << 32)) & band;
+      zmb = ~nzm & band;
+      rank_l = __builtin_amdgcn_mbcnt_hi(uint32_t(zmb >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(zmb), 0u));
     }
   }
   finish(nbase);  // every exit (an empty interval never flushed)

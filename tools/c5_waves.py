@@ -1,5 +1,6 @@
 """Development: per-scan wave timing of C5 images (RJ_DEBUG_WAVES=1 output on stderr) for one
-image and for a batch, to separate the refinement chain from the batch's contention."""
+image and for batches (sizes as arguments, default 1 64; 64 distinct images repeated), to
+separate the refinement chain from the batch's contention."""
 import os
 import sys
 
@@ -15,8 +16,8 @@ def main():
     gen = bench.WORKLOADS["c5"]["gen"]
     datas = [bench._make_jpeg((s, gen)) for s in range(1234, 1234 + 64)]
     dec = R.JpegDecoder(R.Backend.HARDWARE, 0)
-    for bs in (1, 64):
-        streams = [R.JpegStream(d) for d in datas[:bs]]
+    for bs in [int(a) for a in sys.argv[1:]] or [1, 64]:
+        streams = [R.JpegStream(datas[k % len(datas)]) for k in range(bs)]
         dec.streams_to_device(streams)
         outs = [t.empty((1080, 5760), dtype=t.uint8, device="cuda") for _ in range(bs)]
         imgs = [R.make_image([o.data_ptr()], [o.shape[1]]) for o in outs]
