@@ -680,6 +680,8 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         dist.barrier()  # every part is on disk
 
+    if share and world > 1:  # the test build of the library carries the shared-memory test transport
+        os.environ["RJ_LIB_PATH"] = os.path.join(ROOT, "rocjpeg_amd", "librocjpeg_amd_testcomm.so")
     import rocjpeg_amd as R
     from rocjpeg_amd import shard as S
     dec = R.JpegDecoder(R.Backend.HARDWARE, gpu)

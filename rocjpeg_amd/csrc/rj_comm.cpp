@@ -125,7 +125,9 @@ struct RocJpegAmdCommImpl {
 // share ONE GPU (RCCL refuses two ranks on one device) and the multi-rank protocol above -- the
 // chunking, the status header, the checks, the error paths -- runs with real device buffers and
 // copies on a one-GPU box (tests/test_comm_gpu.py).  Same chunks, same order, same buffers as
-// the RCCL broadcast; only the wire differs.  Never set in production.
+// the RCCL broadcast; only the wire differs.  Compiled only into the test build of the library
+// (-DRJ_COMM_TEST_TRANSPORT: rocjpeg_amd/librocjpeg_amd_testcomm.so); the product library has
+// no such switch.
 struct ShmBus {
   std::atomic<uint32_t> gen;   // chunks rank 0 has published
   std::atomic<uint32_t> acks;  // chunks taken by receivers, summed
@@ -218,8 +220,10 @@ RJ_EXPORT RocJpegStatus rocJpegAmdCommInitRank(int device_id, int nranks, const 
   } else if (hipMalloc(&c->dbuf, kChunkBytes) != hipSuccess) {
     c->dbuf = nullptr;
     st = ROCJPEG_STATUS_OUTOF_MEMORY;
+#ifdef RJ_COMM_TEST_TRANSPORT
   } else if (const char *shm = std::getenv("RJ_COMM_TEST_SHM")) {
     if ((c->shm = MapShm(shm)) == nullptr) st = ROCJPEG_STATUS_NOT_INITIALIZED;
+#endif
   } else {
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
@@ -309,7 +313,10 @@ RocJpegStatus BroadcastWithStatus(RocJpegAmdCommImpl *c, RocJpegAmdWorkItem *ite
         h.check = Fnv(items, size_t(total) * sizeof(RocJpegAmdWorkItem), Fnv(&h, offsetof(TableHeader, check)));
         std::memcpy(buf.data(), &h, sizeof(h));
       }
-      if (hipMemcpyAsync(c->dbuf, buf.data(), kChunkBytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+      // synchronised before the next chunk rewrites the pageable host buffer (an
+      // asynchronous copy from pageable memory may still be reading it)
+      if (hipMemcpyAsync(c->dbuf, buf.data(), kChunkBytes, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+          hipStreamSynchronize(c->stream) != hipSuccess) {
         st = ROCJPEG_STATUS_EXECUTION_FAILED;
         if (k == 0) chunks = 1;  // the receivers find a stale header in chunk 0 and stop after it
       }

@@ -85,22 +85,12 @@ __device__ __forceinline__ void store_bytes(uint8_t *d, uint32_t n, const uint32
 struct EntWin {
   uint32_t w[RJ_WIN_ROWS];
   uint32_t base_lo, base_hi;
-#ifdef RJ_EXP_E16
-  bool raw = false;
-#endif
   __device__ __forceinline__ void load(const uint32_t *__restrict__ ent, uint64_t at, uint32_t lane) {
     base_lo = U(uint32_t(at));
     base_hi = U(uint32_t(at >> 32));
-#ifdef RJ_EXP_E16  // timing probe: 16-bit entries (rj_huff.hip hl_flush), expanded by settle()
-    const uint16_t *p16 = reinterpret_cast<const uint16_t *>(ent) + at;
-#pragma unroll
-    for (int r = 0; r < RJ_WIN_ROWS; r++) w[r] = gp(p16)[r * 64u + lane];
-    raw = true;
-#else
     const uint32_t *p = ent + at;
 #pragma unroll
     for (int r = 0; r < RJ_WIN_ROWS; r++) w[r] = gp(p)[r * 64u + lane];
-#endif
   }
   // wait here for the window's loads.  vmcnt is in order on gfx9: a wait for a window row issued
   // after the previous strip's pixel stores waits for those stores too.  parse_blocks' walk over a
@@ -108,17 +98,6 @@ struct EntWin {
   // parse_blocks and the row's first, and in row_body after the IDCT for the next strip's window
   // (loaded at the end of phase A, waited before phase C's stores).
   __device__ __forceinline__ void settle() {
-#ifdef RJ_EXP_E16
-    if (raw) {
-#pragma unroll
-      for (int r = 0; r < RJ_WIN_ROWS; r++) {
-        const uint32_t h = w[r], pos = h >> 10;
-        const int32_t v = __builtin_amdgcn_sbfe(int32_t(h), 0, 10);
-        w[r] = v == -512 ? (pos == 63u ? RJ_RE_TERM : RJ_RE_ZERO) : ((uint32_t(v) & 0xFFFFu) | (pos << 16));
-      }
-      raw = false;
-    }
-#endif
 #pragma unroll
     for (int r = 0; r < RJ_WIN_ROWS; r++) asm volatile("" : "+v"(w[r]));
   }
@@ -535,157 +514,11 @@ __device__ __forceinline__ void rgb_strip_420_full(const uint8_t *ty, const uint
     const rj_f2 uu = rj_f2{u8f(u2, 0), u8f(u2, 1)} - m128, vv = rj_f2{u8f(v2, 0), u8f(v2, 1)} - m128;
     const rj_f2 ua = {uu.x, uu.x}, ub = {uu.y, uu.y}, va = {vv.x, vv.x}, vb = {vv.y, vv.y};
     uint32_t w0, w1, w2;
-#if defined(RJ_EXP_K2C) && RJ_EXP_K2C == 3  // timing probe: stores issued, no tile reads or CSC
-    w0 = tid; w1 = tid + 1; w2 = tid + 2;
-    *reinterpret_cast<RJ_GLOBAL uint3 *>(d + 96 * i) = make_uint3(w0, w1, w2);
-    *reinterpret_cast<RJ_GLOBAL uint3 *>(d + pitch + 96 * i) = make_uint3(w0, w1, w2);
-    continue;
-#endif
     csc4_pk(y4, ua, ub, va, vb, w0, w1, w2);
-#if defined(RJ_EXP_K2C) && RJ_EXP_K2C == 2  // timing probe: CSC live, no global store (runtime-false guard)
-    if (pitch == 0x7FFFFFF1u)
-#endif
     *reinterpret_cast<RJ_GLOBAL uint3 *>(d + 96 * i) = make_uint3(w0, w1, w2);
     csc4_pk(y4b, ua, ub, va, vb, w0, w1, w2);
-#if defined(RJ_EXP_K2C) && RJ_EXP_K2C == 2
-    if (pitch == 0x7FFFFFF1u)
-#endif
     *reinterpret_cast<RJ_GLOBAL uint3 *>(d + pitch + 96 * i) = make_uint3(w0, w1, w2);
   }
-}
-
-// Phase C for the full 4:2:0 strip, with line-contiguous 16-B stores and no staging (round 4;
-// the default, RJ_K2_STORE 2).  Measured (profiles/r4_experiments/k2_store_probes_ab.txt): the
-// IDCT and the CSC are hidden behind the rest of K2, while rgb_strip_420_full's 12-B stores --
-// each wave instruction 8 rows x 96 B -- cost ~0.9 ms of its 2.4 and the LDS-staged dwordx4 form
-// below halves that but pays as much again for the LDS round trip.  Here a lane produces one
-// 16-B piece of an output row directly: piece j (bytes 16 j .. 16 j + 15 of the strip's 480-B
-// row) starts at byte o = j mod 3 of pixel p0 = 5 j + j / 3; the lane converts the 8 pixels
-// from the even pixel pe = p0 & ~1 (24 bytes, as two rgb_strip_420_full quads, same arithmetic
-// and bytes) and selects its 16 bytes from byte 3 (p0 - pe) + o.  Task t = (row pair t / 30,
-// piece t mod 30) takes the two rows of that pair (they share the chroma row); 240 tasks over 4
-// passes of the wave, and a wave store instruction covers ~2 whole 480-B row segments.  The
-// 8-pixel window of the last piece reads 2 pixels past the row inside LDS; they are not output.
-// d: the strip's first output byte, d and pitch 16-B aligned (checked by the caller).
-__device__ __forceinline__ void rgb_strip_420_direct(const uint8_t *ty, const uint8_t *tu, const uint8_t *tv,
-                                                     uint32_t tid, RJ_GLOBAL uint8_t *d, uint32_t pitch) {
-  uint32_t t0 = tid;  // opaque: the lane's addresses are recomputed per strip, not hoisted
-  asm volatile("" : "+v"(t0));
-  const rj_f2 m128 = {128.0f, 128.0f};
-#pragma unroll
-  for (uint32_t m = 0; m < 4; m++) {
-    const uint32_t t = t0 + 64u * m;
-    if (m == 3 && t >= 240u) break;
-    const uint32_t qy = t / 30u, j = t - 30u * qy;
-    const uint32_t j3 = j / 3u;
-    const uint32_t p0 = 5u * j + j3, o = j - 3u * j3;
-    const uint32_t pe = p0 & ~1u;
-    const uint32_t off = 3u * (p0 - pe) + o;  // 0..5: the piece's first byte in the 24-B window
-    // luma of pixels pe .. pe + 7, rows 2 qy and 2 qy + 1 (pe even: 2-B aligned)
-    const uint32_t ya = qy * 320u + pe;
-    const uint32_t *yw = reinterpret_cast<const uint32_t *>(ty + (ya & ~3u));
-    const uint32_t ysh = ya & 3u;
-    const uint32_t a0 = yw[0], a1 = yw[1], a2 = yw[2];
-    const uint32_t b0 = yw[40], b1 = yw[41], b2 = yw[42];  // the next row: +160 B
-    // chroma of those pixels: bytes pe / 2 .. pe / 2 + 3 of chroma row qy
-    const uint32_t ca = qy * 80u + (pe >> 1);
-    const uint32_t csh = ca & 3u;
-    const uint32_t *uw = reinterpret_cast<const uint32_t *>(tu + (ca & ~3u));
-    const uint32_t *vw = reinterpret_cast<const uint32_t *>(tv + (ca & ~3u));
-    const uint32_t u4 = __builtin_amdgcn_alignbyte(uw[1], uw[0], csh);
-    const uint32_t v4 = __builtin_amdgcn_alignbyte(vw[1], vw[0], csh);
-    const rj_f2 uu0 = rj_f2{u8f(u4, 0), u8f(u4, 1)} - m128, vv0 = rj_f2{u8f(v4, 0), u8f(v4, 1)} - m128;
-    const rj_f2 uu1 = rj_f2{u8f(u4, 2), u8f(u4, 3)} - m128, vv1 = rj_f2{u8f(v4, 2), u8f(v4, 3)} - m128;
-    const uint32_t q = off >> 2, sh = off & 3u;
-    const uint32_t row0 = __umul24(2u * qy, pitch) + 16u * j;
-#pragma unroll
-    for (int r = 0; r < 2; r++) {
-      const uint32_t w0 = r ? b0 : a0, w1 = r ? b1 : a1, w2 = r ? b2 : a2;
-      const uint32_t y4a = __builtin_amdgcn_alignbyte(w1, w0, ysh), y4b = __builtin_amdgcn_alignbyte(w2, w1, ysh);
-      uint32_t e[6];
-      csc4_pk(y4a, rj_f2{uu0.x, uu0.x}, rj_f2{uu0.y, uu0.y}, rj_f2{vv0.x, vv0.x}, rj_f2{vv0.y, vv0.y}, e[0], e[1], e[2]);
-      csc4_pk(y4b, rj_f2{uu1.x, uu1.x}, rj_f2{uu1.y, uu1.y}, rj_f2{vv1.x, vv1.x}, rj_f2{vv1.y, vv1.y}, e[3], e[4], e[5]);
-      uint32_t w[5];
-#pragma unroll
-      for (int k = 0; k < 5; k++) w[k] = q ? e[k + 1] : e[k];
-      const uint4 piece = make_uint4(__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
-                                     __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh));
-      *reinterpret_cast<RJ_GLOBAL uint4 *>(d + (row0 + (r ? pitch : 0u))) = piece;
-    }
-  }
-}
-
-// Phase C store shape for the full 4:2:0 strip (round 4).  rgb_strip_420_full stores 12 B per
-// lane: one wave instruction covers 8 rows x 96 B, i.e. 8-16 partial cache lines, ten such
-// instructions per lane and strip.  Here the same lanes compute the same pixels (arithmetic and
-// bytes as rgb_strip_420_full) but write them into an LDS image of the strip's RGB rows; the
-// wave then reads the image back as 16-B pieces in row-major order and stores piece p of the
-// image from lane p mod 64: each global store is a dwordx4 whose 64 lanes cover 1 KB of
-// consecutive row segments.  The strip goes in two column halves (pixels 0..95 = bytes 0..287,
-// 96..159 = bytes 288..479), so that the image fits beside the sample tiles in the block area:
-// tiles 3,840 B + image 16 x 288 B = 8,448 B of the 9,216.  d: the strip's first output byte
-// (16-B aligned, as is the pitch: the host-side condition is checked by the caller).
-#ifndef RJ_K2_STORE
-#define RJ_K2_STORE 0  // 0: rgb_strip_420_full (12-B stores), 1: staged dwordx4, 2: rgb_strip_420_direct
-#endif
-template <int kI0, int kNI>
-__device__ __forceinline__ void rgb_420_half_staged(const uint8_t *ty, const uint8_t *tu, const uint8_t *tv,
-                                                    uint32_t tid, uint8_t *stage, RJ_GLOBAL uint8_t *d,
-                                                    uint32_t pitch) {
-  constexpr uint32_t kSW = 96u * kNI;  // image row bytes
-  constexpr uint32_t kPR = kSW / 16u;  // 16-B pieces per row
-  constexpr uint32_t kNP = 16u * kPR;  // pieces of the image
-  uint32_t t0 = tid;  // opaque: the lane's LDS addresses are not hoisted out of the strip loop
-  asm volatile("" : "+v"(t0));
-  const uint32_t qy = t0 >> 3, qx0 = t0 & 7u;
-  const uint8_t *yr = ty + qy * 320u + qx0 * 4u;
-  const uint32_t co = qy * 80u + qx0 * 2u;
-  uint32_t *im0 = reinterpret_cast<uint32_t *>(stage + qy * (2u * kSW) + qx0 * 12u);
-  uint32_t *im1 = im0 + kSW / 4u;
-  const rj_f2 m128 = {128.0f, 128.0f};
-#pragma unroll
-  for (int i = 0; i < kNI; i++) {
-    const int ii = kI0 + i;
-    const uint32_t y4 = *reinterpret_cast<const uint32_t *>(yr + 32 * ii);
-    const uint32_t y4b = *reinterpret_cast<const uint32_t *>(yr + 160 + 32 * ii);
-    const uint32_t u2 = *reinterpret_cast<const uint16_t *>(tu + co + 16 * ii);
-    const uint32_t v2 = *reinterpret_cast<const uint16_t *>(tv + co + 16 * ii);
-    const rj_f2 uu = rj_f2{u8f(u2, 0), u8f(u2, 1)} - m128, vv = rj_f2{u8f(v2, 0), u8f(v2, 1)} - m128;
-    const rj_f2 ua = {uu.x, uu.x}, ub = {uu.y, uu.y}, va = {vv.x, vv.x}, vb = {vv.y, vv.y};
-    uint32_t w0, w1, w2;
-    csc4_pk(y4, ua, ub, va, vb, w0, w1, w2);
-    im0[24 * i] = w0;
-    im0[24 * i + 1] = w1;
-    im0[24 * i + 2] = w2;
-    csc4_pk(y4b, ua, ub, va, vb, w0, w1, w2);
-    im1[24 * i] = w0;
-    im1[24 * i + 1] = w1;
-    im1[24 * i + 2] = w2;
-  }
-  __syncthreads();  // the image is written (one wave: the wait for its LDS stores)
-  // the lane's piece addresses are recomputed per strip: hoisted out of the strip loop they
-  // would hold ~8 VGPRs across the IDCT (the kernel sits at 128)
-  uint32_t t = tid;
-  asm volatile("" : "+v"(t));
-#pragma unroll
-  for (uint32_t m = 0; m < (kNP + 63u) / 64u; m++) {
-    const uint32_t p = m * 64u + t;
-    if ((m + 1u) * 64u <= kNP || p < kNP) {
-      const uint32_t row = p / kPR, col = p - row * kPR;
-      const uint4 v = *reinterpret_cast<const uint4 *>(stage + p * 16u);
-#if defined(RJ_EXP_K2C) && RJ_EXP_K2C == 1  // timing probe: no global store (runtime-false guard)
-      if (pitch == 0x7FFFFFF1u)
-#endif
-#ifdef RJ_K2_NT
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w},
-                                  reinterpret_cast<RJ_GLOBAL u32x4 *>(d + (__umul24(row, pitch) + col * 16u)));
-#else
-      *reinterpret_cast<RJ_GLOBAL uint4 *>(d + (__umul24(row, pitch) + col * 16u)) = v;
-#endif
-    }
-  }
-  __syncthreads();  // the image is read before the next half overwrites it
 }
 
 // The work of one MCU row (one wavefront), looping over the row's strips of S MCUs.
@@ -851,7 +684,6 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
   const uint32_t hs1 = (ncomp == 3) ? (hmax / ib.at(RJ_OFF(comp_h) + 1) == 2 ? 1u : 0u) : 0u;
   const uint32_t vs1 = (ncomp == 3) ? (vmax / ib.at(RJ_OFF(comp_v) + 1) == 2 ? 1u : 0u) : 0u;
   const bool al_y = ((reinterpret_cast<uintptr_t>(dst0) | pitch0) & 3) == 0;
-  const bool al16 = ((reinterpret_cast<uintptr_t>(dst0) | pitch0) & 15) == 0;  // staged 16-B stores (RJ_K2_STORE)
   const bool al_rgbp = ((reinterpret_cast<uintptr_t>(dst0) | reinterpret_cast<uintptr_t>(dst1) |
                          reinterpret_cast<uintptr_t>(dst2) | pitch0) & 3) == 0;
   const bool al_uv = ((reinterpret_cast<uintptr_t>(dst1) | reinterpret_cast<uintptr_t>(dst2) | pitch1) & 3) == 0;
@@ -913,12 +745,7 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
       }
       row_wide = row_wide || wide;
       if constexpr (!kPlanes) __syncthreads();  // every block is in registers: the staging area becomes the sample tiles
-#if defined(RJ_EXP_K2C) && RJ_EXP_K2C == 4  // timing probe: no IDCT (the block's first dwords as samples)
-      if (has_blk)
-        for (int q = 0; q < 16; q++) o[q] = w[q] ^ w[q + 16];
-#else
       if (has_blk) idct_dot2_block(w, o);
-#endif
       if constexpr (!kDense) win.settle();  // the next strip's window, before this strip's pixel stores
     } else {
       int32_t v[64];
@@ -978,15 +805,7 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
     uint8_t *d = dst0 + (__umul24(py0, pitch0) + px0 * 3);
     if (hs1) {
       if (vs1 && strip_w == 160u && tw[0] == 160u && tw[1] == 80u) {
-        if (RJ_K2_STORE == 2 && al16) {
-          rgb_strip_420_direct(ty, tu, tv, tid, gp(d), pitch0);
-        } else if (RJ_K2_STORE == 1 && al16) {
-          uint8_t *stage = s_buf + 3840u;  // past the tiles (toff[2] + 640)
-          rgb_420_half_staged<0, 3>(ty, tu, tv, tid, stage, gp(d), pitch0);
-          rgb_420_half_staged<3, 2>(ty, tu, tv, tid, stage, gp(d) + 288u, pitch0);
-        } else {
-          rgb_strip_420_full(ty, tu, tv, tid, d, pitch0);
-        }
+        rgb_strip_420_full(ty, tu, tv, tid, d, pitch0);
       }
       else if (vs1) rgb_strip<true, true>(ty, tu, tv, tw[0], tw[1], tid, quads_x, rows, d, pitch0);
       else rgb_strip<true, false>(ty, tu, tv, tw[0], tw[1], tid, quads_x, rows, d, pitch0);

@@ -63,6 +63,20 @@ static void FillLeanBad(bool is_dc, uint32_t *first, uint32_t *subs) {
 // n1 < B, the AC code that starts at bit n1, if it is complete inside the key (its extra bits
 // may run past it: the step reads them from its 32-bit peek, n1 + n2 <= 11 + 10 bits).
 // `ac` (RJ_HL_AC_BITS keys, single-symbol entries): the AC table the second symbol is read with.
+// The AC table each DC table's two-symbol entries are read with: the AC table of every scan
+// component that uses that DC table, or -1 when none uses it or two components disagree.
+static void DcPairMap(const StreamInfo &s, int (&ac_of_dc)[2]) {
+  ac_of_dc[0] = ac_of_dc[1] = -1;
+  bool mixed[2] = {false, false};
+  for (int c = 0; c < s.scan_ncomp && c < 4; c++) {
+    const int td = s.scomp[c].td & 1, ta = s.scomp[c].ta & 1;
+    if (ac_of_dc[td] < 0) ac_of_dc[td] = ta;
+    else if (ac_of_dc[td] != ta) mixed[td] = true;
+  }
+  for (int t = 0; t < 2; t++)
+    if (mixed[t]) ac_of_dc[t] = -1;
+}
+
 static void AddLeanPairs(uint32_t *first, uint32_t B, bool is_dc, const uint32_t *ac) {
   const uint32_t BA = RJ_HL_AC_BITS;
   for (uint32_t key = 0; key < (1u << B); key++) {
@@ -411,6 +425,11 @@ bool Stream::BuildPlanHeader() {
     std::memcpy(kp, s.ht, sizeof(s.ht));
     kp += sizeof(s.ht);
     std::memcpy(kp, s.qt_zz, sizeof(s.qt_zz));
+    kp += sizeof(s.qt_zz);
+    int ac_of_dc[2];
+    DcPairMap(s, ac_of_dc);
+    *kp++ = uint8_t(ac_of_dc[0] < 0 ? 0xFF : ac_of_dc[0]);
+    *kp++ = uint8_t(ac_of_dc[1] < 0 ? 0xFF : ac_of_dc[1]);
   }
   h = Fnv1a(h, p.table_key, sizeof(p.table_key));
   p.table_hash = h;
@@ -571,20 +590,16 @@ const RjLeanTables *Stream::LeanTables() {
         ac_ok[id] = true;
     }
     // a DC table's second symbols are read with the AC table of the components that use it:
-    // only when every scan component with that DC table has the same AC table
-    int ac_of_dc[2] = {-1, -1};
-    bool mixed[2] = {false, false};
-    for (int c = 0; c < info_.scan_ncomp && c < 4; c++) {
-      const int td = info_.scomp[c].td & 1, ta = info_.scomp[c].ta & 1;
-      if (ac_of_dc[td] < 0) ac_of_dc[td] = ta;
-      else if (ac_of_dc[td] != ta) mixed[td] = true;
-    }
+    // only when every scan component with that DC table has the same AC table (the map is part
+    // of table_key, so every stream sharing these tables has the same map)
+    int ac_of_dc[2];
+    DcPairMap(info_, ac_of_dc);
     uint32_t single[2][1 << RJ_HL_AC_BITS];  // AC first levels before their pairs
     for (int id = 0; id < 2; id++) std::memcpy(single[id], t->ac[id], sizeof(single[id]));
     for (int id = 0; id < 2; id++) {
       if (ac_ok[id]) AddLeanPairs(t->ac[id], RJ_HL_AC_BITS, false, single[id]);
       const int ta = ac_of_dc[id];
-      if (ta >= 0 && !mixed[id] && ac_ok[ta] && plan_.ht_valid[id]) AddLeanPairs(t->dc[id], RJ_HL_DC_BITS, true, single[ta]);
+      if (ta >= 0 && ac_ok[ta] && plan_.ht_valid[id]) AddLeanPairs(t->dc[id], RJ_HL_DC_BITS, true, single[ta]);
     }
     lean_ = std::move(t);
   }

@@ -65,8 +65,11 @@ struct DecodePlan {
   uint8_t ht_valid[2] = {};        // DHT slot loaded and both its tables valid (BuildHuffman)
   uint16_t qmax[4] = {1, 1, 1, 1}; // largest entry of each quant table slot (the IDCT's exact domain)
   // De-duplication key: the raw DHT/DQT content the derived tables are a function of (the
-  // batch planner compares these ~670 B instead of the 14.5 KB RjTableSet) and its hash.
-  static constexpr size_t kTableKeyBytes = 2 + 2 * (16 + 12 + 16 + 162) + 4 * 64;
+  // batch planner compares these ~670 B instead of the 14.5 KB RjTableSet) and its hash.  The
+  // last two bytes are the AC table each DC table's two-symbol entries pair with (Stream::
+  // LeanTables; 0xFF: none), so streams with equal tables but another component-to-table map
+  // get table sets of their own.
+  static constexpr size_t kTableKeyBytes = 2 + 2 * (16 + 12 + 16 + 162) + 4 * 64 + 2;
   uint8_t table_key[kTableKeyBytes] = {};
   uint64_t table_hash = 0;
 

@@ -120,3 +120,98 @@ def prog_gray_refine_overshoot(w=64, h=64):
     out += sos_gray(0, 0, 1, 63, 1, 0) + scan_acr
     out += b"\xff\xd9"
     return bytes(out)
+
+
+ZIGZAG_NAT = [0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34, 27, 20,
+              13, 6, 7, 14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52,
+              45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63]  # natural index of zigzag position k
+
+
+def _magnitude(v):
+    """(size category, extra bits) of a coefficient value (T.81 F.1.2.1)."""
+    v = int(v)
+    s = abs(v).bit_length()
+    return s, (v if v >= 0 else v + (1 << s) - 1) & ((1 << s) - 1)
+
+
+def baseline_symbols(blocks):
+    """DC size categories and AC run/size symbols a block list (natural order, int) uses."""
+    dcs, acs, pred = set(), set(), 0
+    for blk in blocks:
+        dcs.add(_magnitude(blk[0] - pred)[0])
+        pred = blk[0]
+        run = 0
+        for k in range(1, 64):
+            v = blk[ZIGZAG_NAT[k]]
+            if v == 0:
+                run += 1
+                continue
+            while run > 15:
+                acs.add(0xF0)
+                run -= 16
+            acs.add((run << 4) | _magnitude(v)[0])
+            run = 0
+        if run:
+            acs.add(0x00)
+    return dcs, acs
+
+
+def baseline_420(w, h, coefs, dims, qz, dc_len, ac_len, comp_tables):
+    """Baseline interleaved 3-component JPEG (Y 2x2, Cb / Cr 1x1, no DRI) from quantised
+    coefficients in natural order (tests/oracle_lib.decode_coefs layout: per component a raster
+    of blocks).  qz: two quant tables in zigzag order (Y, chroma); dc_len / ac_len: two tables
+    each ({symbol: code length}); comp_tables: per component (td, ta)."""
+    codes_dc = [canonical_codes(t)[0] for t in dc_len]
+    codes_ac = [canonical_codes(t)[0] for t in ac_len]
+    comps, off = [], 0
+    for (bw_, bh_) in dims:
+        comps.append(coefs[off:off + bw_ * bh_ * 64].reshape(bh_, bw_, 64))
+        off += bw_ * bh_ * 64
+    mcux, mcuy = (w + 15) // 16, (h + 15) // 16
+    bw = BitWriter()
+    pred = [0, 0, 0]
+
+    def block(c, blk):
+        td, ta = comp_tables[c]
+        d = int(blk[0]) - pred[c]
+        pred[c] = int(blk[0])
+        s, e = _magnitude(d)
+        bw.put(*codes_dc[td][s])
+        if s:
+            bw.put(e, s)
+        run = 0
+        for k in range(1, 64):
+            v = int(blk[ZIGZAG_NAT[k]])
+            if v == 0:
+                run += 1
+                continue
+            while run > 15:
+                bw.put(*codes_ac[ta][0xF0])
+                run -= 16
+            s, e = _magnitude(v)
+            bw.put(*codes_ac[ta][(run << 4) | s])
+            bw.put(e, s)
+            run = 0
+        if run:
+            bw.put(*codes_ac[ta][0x00])
+
+    for my in range(mcuy):
+        for mx in range(mcux):
+            for by in range(2):
+                for bx in range(2):
+                    block(0, comps[0][2 * my + by, 2 * mx + bx])
+            block(1, comps[1][my, mx])
+            block(2, comps[2][my, mx])
+    ecs = bw.flush()
+    out = bytearray(b"\xff\xd8")
+    out += dqt(0, qz[0]) + dqt(1, qz[1])
+    out += _seg(0xC0, struct.pack(">BHHB", 8, h, w, 3) + bytes([1, 0x22, 0, 2, 0x11, 1, 3, 0x11, 1]))
+    for t in range(2):
+        out += dht(0, t, dc_len[t]) + dht(1, t, ac_len[t])
+    sos = bytes([3])
+    for c in range(3):
+        td, ta = comp_tables[c]
+        sos += bytes([c + 1, (td << 4) | ta])
+    out += _seg(0xDA, sos + bytes([0, 63, 0])) + ecs
+    out += b"\xff\xd9"
+    return bytes(out)

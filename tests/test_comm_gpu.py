@@ -138,7 +138,9 @@ def test_multi_rank_protocol_shared_gpu(tmp_path):
     shm = f"/dev/shm/rj_comm_test_{os.getpid()}"
     if os.path.exists(shm):
         os.unlink(shm)
-    env = dict(os.environ, RJ_COMM_TEST_SHM=shm)
+    # the test build of the library: the product library has no test transport
+    env = dict(os.environ, RJ_COMM_TEST_SHM=shm,
+               RJ_LIB_PATH=os.path.join(O.ROOT, "rocjpeg_amd", "librocjpeg_amd_testcomm.so"))
     outs = [str(tmp_path / f"r{r}.json") for r in range(world)]
     procs = [subprocess.Popen([sys.executable, "-m", "tests.comm_rank_worker", str(r), str(world), outs[r]],
                               cwd=O.ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)

@@ -374,3 +374,55 @@ def test_sizes_outside_the_range_are_refused(dec, w, h):
     s = R.JpegStream(data)
     bufs, img = G.gpu_buffers([(h, 3 * w)])
     assert dec.decode(s, R.decode_params(R.OutputFormat.RGB), img) == R.Status.JPEG_NOT_SUPPORTED
+
+
+# ---- table de-duplication across streams (the DC table's two-symbol entries) ----
+def remapped_pair(w=128, h=64):
+    """Two baseline 4:2:0 streams with identical DHT and DQT bytes that code the same
+    coefficients with the component-to-table map the other way round: stream A reads Y with
+    (DC 0, AC 0) and chroma with (DC 1, AC 1), stream B Y with (DC 0, AC 1) and chroma with
+    (DC 1, AC 0).  The DC tables' codes are short enough that DC + AC pairs fit one K1 table
+    entry, and the two AC tables assign different codes, so a DC pair read with the other
+    stream's AC table decodes garbage (tests/jpeg_craft.py baseline_420)."""
+    import io
+    from PIL import Image
+    from tests import jpeg_craft as J
+    rng = np.random.default_rng(11)
+    yy, xx = np.mgrid[0:h, 0:w]
+    a = np.stack([96 + 0.6 * xx, 80 + 0.9 * yy, 140 - 0.3 * xx], -1) + rng.normal(0, 9, (h, w, 3))
+    b = io.BytesIO()
+    Image.fromarray(np.clip(a, 0, 255).astype(np.uint8)).save(b, "JPEG", quality=92, subsampling=2)
+    st, coefs, dims = O.decode_coefs(b.getvalue())
+    assert st == 0
+    blocks = [coefs[i:i + 64].astype(int) for i in range(0, coefs.size, 64)]
+    _, acs = J.baseline_symbols(blocks)
+    acs = sorted(acs | {0x00, 0xF0})
+    dc_len = {0: 2, 1: 2, 2: 3, 3: 3, 4: 4, 5: 5, 6: 6, 7: 7, 8: 8, 9: 9, 10: 10, 11: 11}
+    ac0 = {s: 8 for s in acs}
+    ac1 = {s: (7 if k == 0 else 8) for k, s in enumerate(acs)}
+    qz = [[2] * 64, [3] * 64]
+    A = J.baseline_420(w, h, coefs, dims, qz, [dc_len, dc_len], [ac0, ac1], [(0, 0), (1, 1), (1, 1)])
+    B = J.baseline_420(w, h, coefs, dims, qz, [dc_len, dc_len], [ac0, ac1], [(0, 1), (1, 0), (1, 0)])
+    return A, B
+
+
+@pytest.mark.parametrize("order", ["AB", "BA", "ABBA"])
+def test_same_tables_other_component_map(dec, order):
+    """Streams whose DHT / DQT bytes are equal but whose components map to the tables
+    differently get table sets of their own in one batch (the K1 table image of a DC table
+    carries second symbols read with one AC table)."""
+    from tests import gpu_util as G
+    A, B = remapped_pair()
+    datas = [A if c == "A" else B for c in order]
+    for d in datas:  # the oracle decodes both to the same coefficients
+        assert O.oracle_decode(d, int(R.OutputFormat.RGB), [(64, 384)])[0] == 0
+    streams = [R.JpegStream(d) for d in datas]
+    bufs_all, imgs = [], []
+    for s in streams:
+        bufs, img = G.gpu_buffers([(64, 384)])
+        bufs_all.append(bufs)
+        imgs.append(img)
+    assert dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs) == 0
+    for k, (d, bufs) in enumerate(zip(datas, bufs_all)):
+        want = O.oracle_decode(d, int(R.OutputFormat.RGB), [(64, 384)])[1]
+        assert G.first_mismatch(G.to_host(bufs)[0], want[0]) is None, (order, k)

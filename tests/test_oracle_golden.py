@@ -107,3 +107,15 @@ def test_crafted_refine_overshoot_matches_libjpeg_turbo():
     st, planes, _ = O.decode_planes(data)
     assert st == 0
     assert np.array_equal(np.asarray(PIL.open(io.BytesIO(data))), planes[0])
+
+
+def test_remapped_pair_codes_the_same_coefficients():
+    """The crafted streams of test_decode_gpu.test_same_tables_other_component_map: equal
+    tables, other component-to-table map, same coefficients (checked by the oracle)."""
+    from tests.test_decode_gpu import remapped_pair
+    A, B = remapped_pair()
+    sa, ca, _ = O.decode_coefs(A)
+    sb, cb, _ = O.decode_coefs(B)
+    assert sa == sb == 0 and np.array_equal(ca, cb)
+    ia, ib = A.index(b"\xff\xda"), B.index(b"\xff\xda")
+    assert A[:ia] == B[:ib]  # identical headers up to the SOS (DQT, SOF, DHT)
