@@ -251,6 +251,7 @@ class BatchRun:
         if st != 0:
             raise RuntimeError(f"rocJpegAmdStreamParseDevice: {R.error_name(st)}")
         self.parse_s = time.perf_counter() - t0
+        self.parse_stages_ms = dec.last_parse_timings()
         dec.streams_to_device(self.streams)  # progressive streams are host-parsed: make them resident too
         self.shapes = []
         for s in self.streams:
@@ -625,6 +626,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--runs", type=int, default=5, help="timed runs of K steps; value = the median run (SURVEY 8d)")
     ap.add_argument("--batch", type=int, default=1024, help="images per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the other BASELINE configs at N=1")
@@ -726,7 +728,10 @@ def main():
     datas = run.datas
     n = run.n
 
-    elapsed = run.timed(args.steps, args.warmup, world, cdev)
+    # the median of >= 5 timed runs, each exactly K steps bracketed by barrier +
+    # synchronize (max over ranks); the warm-up steps precede the first run only
+    runs = [run.timed(args.steps, args.warmup if r == 0 else 0, world, cdev) for r in range(max(1, args.runs))]
+    elapsed = float(np.median(runs))
     # parity of the timed run's own output (the last step's), before anything else writes it
     parity = run.parity(parity_sample(n))
     imgs = torch.tensor([n], dtype=torch.int64, device=cdev)
@@ -774,6 +779,9 @@ def main():
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / K * 1e3, 4),
+            "runs": {"count": len(runs), "statistic": "median",
+                     "ms_per_step": [round(x / K * 1e3, 4) for x in runs],
+                     "spread": round((max(runs) - min(runs)) / elapsed, 5)},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -795,7 +803,8 @@ def main():
             "end_to_end_algorithmic_GBps": round(imgs_total * per_img / elapsed / 1e9, 2),
             "host_input_images_per_s_per_gpu": round(host_rate, 1) if host_rate else None,
             "parse_images_per_s": {"host_1_thread": round(parse_host_rate, 1),
-                                   "gpu_marker_scan": round(n / run.parse_s, 1)},
+                                   "gpu_marker_scan": round(n / run.parse_s, 1),
+                                   "gpu_marker_scan_stages_ms": getattr(run, "parse_stages_ms", None)},
             "parity_timed_output": parity,
             "parity_timed_output_images": len(parity_sample(n)),
             "work_table": {"images": int(len(table)), "bytes": int(table.nbytes),

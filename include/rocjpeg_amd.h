@@ -111,6 +111,10 @@ typedef struct {
   uint32_t chunk_k1;
   /* the call's chunk length in bytes: intervals of at least twice this are cut into chunks */
   uint32_t chunk_bytes;
+  /* lean K1 paired lanes: lanes that decoded two intervals back to back (the call's intervals
+     exceeded one round of the chip's decoder lanes) */
+  uint32_t lean_pairs;
+  uint32_t reserved0;
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);
@@ -225,11 +229,23 @@ RocJpegStatus rocJpegAmdShardDecode(RocJpegAmdShard shard, const RocJpegDecodePa
 RocJpegStatus rocJpegAmdShardGetImages(RocJpegAmdShard shard, int *num_images, int *indices, int capacity);
 RocJpegStatus rocJpegAmdShardDestroy(RocJpegAmdShard shard);
 
+/* Stage times of the handle's last rocJpegAmdStreamParseDevice call, in ms: [0] header walks
+ * (host threads), [1] the resident allocation, [2] staging copy overlapped with the upload,
+ * [3] job upload + marker-scan kernel + table read-back, [4] adopting the tables (host threads),
+ * [5] the whole call.  `count` entries are written (at most 6). */
+RocJpegStatus rocJpegAmdGetLastParseTimings(RocJpegHandle handle, double *ms, int count);
+
+/* Concurrent small calls on one device are decoded together (rj_coalesce.h): counters since the
+ * library was loaded -- calls that took part, combined calls (more than one caller's images in
+ * one decode) and the callers' calls those covered. */
+RocJpegStatus rocJpegAmdGetCoalesceStats(uint64_t *calls, uint64_t *combined, uint64_t *combined_members);
+
 /* ABI revision of this header's extensions (rocJpegAmdGetAbiVersion returns the library's).
  * 2: rocJpegAmdBuildWorkTable takes blob_bytes; RocJpegAmdTimings as above.
  * 3: the resident sharded entry points; the work-table broadcast carries a status header.
- * 4: RocJpegAmdTimings.chunk_k1.  5: RocJpegAmdTimings.chunk_bytes (the call's chunk length). */
-#define ROCJPEG_AMD_ABI_VERSION 5
+ * 4: RocJpegAmdTimings.chunk_k1.  5: RocJpegAmdTimings.chunk_bytes (the call's chunk length).
+ * 6: RocJpegAmdTimings.lean_pairs; rocJpegAmdGetCoalesceStats, rocJpegAmdGetLastParseTimings. */
+#define ROCJPEG_AMD_ABI_VERSION 6
 RocJpegStatus rocJpegAmdGetAbiVersion(int *version);
 
 #if defined(__cplusplus)

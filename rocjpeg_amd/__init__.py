@@ -18,7 +18,7 @@ API_SYMBOLS = (
     "rocJpegGetImageInfo", "rocJpegDecode", "rocJpegDecodeBatched", "rocJpegGetErrorName",
 )
 EXT_SYMBOLS = (
-    "rocJpegAmdStreamGetInfo", "rocJpegAmdStreamsToDevice", "rocJpegAmdSetProfiling", "rocJpegAmdGetLastTimings",
+    "rocJpegAmdGetCoalesceStats", "rocJpegAmdGetLastParseTimings", "rocJpegAmdStreamGetInfo", "rocJpegAmdStreamsToDevice", "rocJpegAmdSetProfiling", "rocJpegAmdGetLastTimings",
     "rocJpegAmdSetPathPolicy", "rocJpegAmdGetStream", "rocJpegAmdStreamParseDevice", "rocJpegAmdStreamGetIntervals",
     "rocJpegAmdStreamGetDestuffBlocks", "rocJpegAmdBuildWorkTable", "rocJpegAmdAssignShards",
     "rocJpegAmdCommGetUniqueId", "rocJpegAmdCommInitRank", "rocJpegAmdCommDestroy", "rocJpegAmdCommInfo",
@@ -26,7 +26,7 @@ EXT_SYMBOLS = (
     "rocJpegAmdShardCreate", "rocJpegAmdShardDecode", "rocJpegAmdShardGetImages", "rocJpegAmdShardDestroy",
     "rocJpegAmdGetAbiVersion", "rocJpegAmdStreamGetLeanTables",
 )
-ABI_VERSION = 5  # include/rocjpeg_amd.h ROCJPEG_AMD_ABI_VERSION
+ABI_VERSION = 6  # include/rocjpeg_amd.h ROCJPEG_AMD_ABI_VERSION
 
 
 class Status(enum.IntEnum):  # api/rocjpeg.h:53-67
@@ -107,7 +107,8 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("prog_kernel_bytes", ctypes.c_uint64 * 3),
                 ("routed_images", ctypes.c_uint32), ("lean_k1", ctypes.c_uint32),
                 ("wide_rows", ctypes.c_uint32), ("lean_split", ctypes.c_uint32),
-                ("chunk_k1", ctypes.c_uint32), ("chunk_bytes", ctypes.c_uint32)]
+                ("chunk_k1", ctypes.c_uint32), ("chunk_bytes", ctypes.c_uint32),
+                ("lean_pairs", ctypes.c_uint32), ("reserved0", ctypes.c_uint32)]
 
 
 class RocJpegAmdInterval(ctypes.Structure):  # include/rocjpeg_amd.h
@@ -178,6 +179,11 @@ def lib():
         L.rocJpegAmdGetAbiVersion.argtypes = [ctypes.POINTER(i32)]
         if hasattr(L, "rocJpegAmdStreamGetLeanTables"):  # (absent from same-ABI A/B builds of older commits)
             L.rocJpegAmdStreamGetLeanTables.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+        if hasattr(L, "rocJpegAmdGetLastParseTimings"):
+            L.rocJpegAmdGetLastParseTimings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i32]
+        if hasattr(L, "rocJpegAmdGetCoalesceStats"):
+            u64p = ctypes.POINTER(ctypes.c_uint64)
+            L.rocJpegAmdGetCoalesceStats.argtypes = [u64p, u64p, u64p]
         for name in API_SYMBOLS + EXT_SYMBOLS:
             if name != "rocJpegGetErrorName" and (name in API_SYMBOLS or hasattr(L, name)):
                 getattr(L, name).restype = i32
@@ -255,6 +261,14 @@ class JpegStream:
             pass
 
 
+def coalesce_stats():
+    """(calls, combined calls, member calls) of the library's coalescing of concurrent small calls
+    (include/rocjpeg_amd.h rocJpegAmdGetCoalesceStats)."""
+    c, k, m = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().rocJpegAmdGetCoalesceStats(ctypes.byref(c), ctypes.byref(k), ctypes.byref(m)), "coalesce stats")
+    return c.value, k.value, m.value
+
+
 def decode_params(fmt=OutputFormat.RGB, crop=(0, 0, 0, 0)):
     p = RocJpegDecodeParams()
     p.output_format = int(fmt)
@@ -310,6 +324,13 @@ class JpegDecoder:
         hs = (ctypes.c_void_p * n)(*[s.handle for s in streams])
         st = Status(lib().rocJpegAmdStreamParseDevice(self.handle, ptrs, lens, n, hs))
         return st, streams
+
+    def last_parse_timings(self):
+        """Stage times (ms) of this handle's last parse_device call (rocJpegAmdGetLastParseTimings)."""
+        ms = (ctypes.c_double * 6)()
+        _check(lib().rocJpegAmdGetLastParseTimings(self.handle, ms, 6), "parse timings")
+        keys = ("headers", "resident_alloc", "copy_upload", "kernel_readback", "adopt", "total")
+        return {k: round(ms[i], 3) for i, k in enumerate(keys)}
 
     def streams_to_device(self, streams):
         n = len(streams)

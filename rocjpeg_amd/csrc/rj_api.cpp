@@ -12,6 +12,7 @@
 
 #include "../../include/rocjpeg.h"
 #include "../../include/rocjpeg_amd.h"
+#include "rj_coalesce.h"
 #include "rj_common.h"
 #include "rj_decoder.h"
 #include "rj_stream.h"
@@ -103,7 +104,8 @@ RJ_EXPORT RocJpegStatus rocJpegDecode(RocJpegHandle handle, RocJpegStreamHandle 
   if (s == nullptr) return ROCJPEG_STATUS_INVALID_PARAMETER;  // rocjpeg_decoder.cpp:107-109
   return Guard([&] {
     rj::Stream *st = AsStream(s);
-    return AsDecoder(handle)->Decode(&st, 1, params, destination);
+    rj::Decoder *d = AsDecoder(handle);
+    return rj::CoalescedDecode(d, d->device(), &st, 1, params, destination);
   });
 }
 
@@ -116,7 +118,8 @@ RJ_EXPORT RocJpegStatus rocJpegDecodeBatched(RocJpegHandle handle, RocJpegStream
   return Guard([&] {
     std::vector<rj::Stream *> v(static_cast<size_t>(batch_size));
     for (int i = 0; i < batch_size; i++) v[i] = AsStream(streams[i]);
-    return AsDecoder(handle)->Decode(v.data(), batch_size, params, destinations);
+    rj::Decoder *d = AsDecoder(handle);
+    return rj::CoalescedDecode(d, d->device(), v.data(), batch_size, params, destinations);
   });
 }
 
@@ -249,4 +252,16 @@ RJ_EXPORT RocJpegStatus rocJpegAmdStreamGetLeanTables(RocJpegStreamHandle s, voi
     if (out != nullptr && bytes >= sizeof(RjLeanTables)) std::memcpy(out, st->LeanTables(), sizeof(RjLeanTables));
     return int(ROCJPEG_STATUS_SUCCESS);
   });
+}
+
+RJ_EXPORT RocJpegStatus rocJpegAmdGetCoalesceStats(uint64_t *calls, uint64_t *combined, uint64_t *combined_members) {
+  rj::CoalesceStats(calls, combined, combined_members);
+  return ROCJPEG_STATUS_SUCCESS;
+}
+
+RJ_EXPORT RocJpegStatus rocJpegAmdGetLastParseTimings(RocJpegHandle handle, double *ms, int count) {
+  if (handle == nullptr || ms == nullptr || count < 0) return ROCJPEG_STATUS_INVALID_PARAMETER;
+  const double *t = AsDecoder(handle)->last_scan_ms();
+  for (int i = 0; i < count && i < 6; i++) ms[i] = t[i];
+  return ROCJPEG_STATUS_SUCCESS;
 }

@@ -2,6 +2,7 @@
 #include "rj_decoder.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -157,6 +158,9 @@ int Decoder::Initialize() {
   if (const char *m = getenv("RJ_PIPE_MIN")) pipe_min_ = uint32_t(std::max(1, atoi(m)));
   if (const char *o = getenv("RJ_SORT_LANES")) sort_lanes_ = atoi(o) != 0;
   if (const char *l = getenv("RJ_LPT")) lpt_ = atoi(l) != 0;
+  if (const char *l = getenv("RJ_K1_PAIR")) pair_lanes_ = atoi(l) != 0;
+  // tests: the lane count of one round (a multiple of 256) the pairing plans for, instead of the chip's
+  if (const char *l = getenv("RJ_K1_PAIR_ROUND")) pair_round_ = uint32_t(std::max(0, atoi(l))) & ~255u;
   if (const char *l = getenv("RJ_K1_SOLO")) k1_solo_lds_ = uint32_t(std::max(0, atoi(l)));
   if (const char *so = getenv("RJ_SPLIT_OUTLIERS")) outlier_split_ = atoi(so) != 0;
   if (const char *kc = getenv("RJ_K1_CHUNK")) k1_chunk_ = atoi(kc) != 0;
@@ -252,17 +256,34 @@ int Decoder::ParseOnDevice(Stream *const *streams, const uint8_t *const *data, c
 int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *data, const size_t *len, int n) {
   RJ_HIP(hipSetDevice(device_));
   const auto t0 = std::chrono::steady_clock::now();
-  // ---- host: headers only (O(header) per stream) ----
+  for (int i = 0; i < n; i++)
+    if (streams[i] == nullptr || data[i] == nullptr) return kInvalidParameter;
+  // ---- host: headers only (O(header) per stream), over the handle's host threads ----
+  std::vector<uint8_t> hdr(size_t(n), 0);  // 1: device scan pending, 2: parsed otherwise, 0: bad
+  {
+    const int nt = n >= 64 ? pool_.threads() : 1;
+    const int per = (n + nt * 4 - 1) / (nt * 4);
+    pool_.Run((n + per - 1) / per,
+              [&](int t) {
+                for (int i = t * per; i < std::min(n, (t + 1) * per); i++) {
+                  Stream *s = streams[i];
+                  if (len[i] > 0xFFFFFFFFull || !s->Parse(data[i], uint32_t(len[i]), true)) continue;
+                  if (!s->scan_pending() && !s->plan().progressive)
+                    s->Parse(data[i], uint32_t(len[i]));  // not decodable: host parse, same info
+                  hdr[size_t(i)] = s->scan_pending() ? 1 : 2;
+                }
+              },
+              nullptr);
+  }
   std::vector<int> pend;
   for (int i = 0; i < n; i++) {
-    Stream *s = streams[i];
-    if (s == nullptr || data[i] == nullptr) return kInvalidParameter;
-    if (len[i] > 0xFFFFFFFFull) return kBadJpeg;
-    if (!s->Parse(data[i], uint32_t(len[i]), true)) return kBadJpeg;
-    if (s->scan_pending()) pend.push_back(i);
-    else if (!s->plan().progressive) s->Parse(data[i], uint32_t(len[i]));  // not decodable: host parse, same info
+    if (hdr[size_t(i)] == 0) return kBadJpeg;
+    if (hdr[size_t(i)] == 1) pend.push_back(i);
   }
   timings_.scan_device_streams = timings_.scan_host_fallbacks = 0;
+  for (double &x : scan_ms_) x = 0;
+  const auto t_hdr = std::chrono::steady_clock::now();
+  scan_ms_[0] = std::chrono::duration<double, std::milli>(t_hdr - t0).count();
   if (pend.empty()) return kOk;
   // ---- layout: one upload (bytes + jobs), one kernel, one read-back (tables + results) ----
   struct Lay {
@@ -320,7 +341,10 @@ int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *dat
               AlignUp(lay[k].expected * sizeof(RjSegDev), 256) + AlignUp(lay[k].ds_cap * sizeof(RjDsBlock), 256);
   }
   uint8_t *rblock = nullptr;
+  const auto t_lay = std::chrono::steady_clock::now();
   RJ_HIP(hipMalloc(reinterpret_cast<void **>(&rblock), std::max<uint64_t>(rbytes, 256)));
+  const auto t_alloc = std::chrono::steady_clock::now();
+  scan_ms_[1] = std::chrono::duration<double, std::milli>(t_alloc - t_lay).count();
   const int dev = device_;
   std::shared_ptr<uint8_t> block(rblock, [dev](uint8_t *p) {
     int cur = 0;
@@ -331,19 +355,36 @@ int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *dat
     }
   });
   RjScanJob *jobs = reinterpret_cast<RjScanJob *>(h + off_jobs);
-  {  // the bytes into the pinned staging blob: a plain copy over the handle's host threads
-    const int nt = bytes > (32u << 20) ? pool_.threads() : 1;
-    const size_t per = (np + size_t(nt) * 4 - 1) / (size_t(nt) * 4);
-    pool_.Run(int((np + per - 1) / per),
+  {  // the bytes into the pinned staging blob over the handle's host threads, in pieces of
+     // streams; the calling thread uploads each finished prefix of pieces while the threads copy
+     // the next (HostPool::Run's in-order done callback), so the copy and the DMA overlap
+    constexpr uint64_t kPiece = 8ull << 20;
+    std::vector<size_t> piece0{0};
+    for (size_t k = 0; k < np; k++)
+      if (lay[k].src - lay[piece0.back()].src >= kPiece) piece0.push_back(k);
+    piece0.push_back(np);
+    const int npieces = int(piece0.size()) - 1;
+    uint64_t uploaded = 0;
+    int up_err = 0;
+    pool_.Run(npieces,
               [&](int t) {
-                for (size_t k = size_t(t) * per; k < std::min(np, size_t(t + 1) * per); k++) {
+                for (size_t k = piece0[size_t(t)]; k < piece0[size_t(t) + 1]; k++) {
                   const Stream *s = streams[pend[k]];
                   std::memcpy(h + lay[k].src, s->info().ecs, s->info().ecs_size);
                   std::memset(h + lay[k].src + s->info().ecs_size, 0, 16);
                 }
               },
-              nullptr);
+              [&](int t) {
+                const uint64_t end = piece0[size_t(t) + 1] < np ? lay[piece0[size_t(t) + 1]].src : bytes;
+                if (!up_err && hipMemcpyAsync(d + uploaded, h + uploaded, end - uploaded, hipMemcpyHostToDevice,
+                                              stream_) != hipSuccess)
+                  up_err = 1;
+                uploaded = end;
+              });
+    if (up_err) return kExecutionFailed;
   }
+  const auto t_copy = std::chrono::steady_clock::now();
+  scan_ms_[2] = std::chrono::duration<double, std::milli>(t_copy - t_alloc).count();
   for (size_t k = 0; k < np; k++) {
     const Stream *s = streams[pend[k]];
     const DecodePlan &p = s->plan();
@@ -379,35 +420,50 @@ int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *dat
     J.out = reinterpret_cast<RjScanOut *>(d + off_out) + k;
   }
   const auto t1 = std::chrono::steady_clock::now();
-  RJ_HIP(hipMemcpyAsync(d, h, up_bytes, hipMemcpyHostToDevice, stream_));
+  RJ_HIP(hipMemcpyAsync(d + off_jobs, h + off_jobs, up_bytes - off_jobs, hipMemcpyHostToDevice, stream_));
   RJ_HIP(hipMemsetAsync(d + off_out, 0, np * sizeof(RjScanOut), stream_));
   RJ_HIP(LaunchScan(stream_, reinterpret_cast<const RjScanJob *>(d + off_jobs), uint32_t(np), d));
   RJ_HIP(hipMemcpyAsync(h + off_out, d + off_out, down_end - off_out, hipMemcpyDeviceToHost, stream_));
   RJ_HIP(hipStreamSynchronize(stream_));
   const auto t2 = std::chrono::steady_clock::now();
-  if (Dbg(kDebugScan))
-    fprintf(stderr, "[rj scan] %zu streams: host headers+staging+alloc %.3f ms, upload+kernel+readback %.3f ms\n",
-            size_t(np), std::chrono::duration<double, std::milli>(t1 - t0).count(),
-            std::chrono::duration<double, std::milli>(t2 - t1).count());
-  // ---- host: adopt the device tables (or scan on the host where a list overflowed) ----
-  for (size_t k = 0; k < np; k++) {
-    Stream *s = streams[pend[k]];
-    const RjScanOut &o = reinterpret_cast<const RjScanOut *>(h + off_out)[k];
-    const Lay &L = lay[k];
-    Stream::Resident &r = res[k];
-    if (o.flags) {
-      r = Stream::Resident();  // this stream keeps no share of the block
-      RJ_INFO("marker scan list overflow on stream %d: host scan", pend[k]);
-      s->Parse(data[pend[k]], uint32_t(len[pend[k]]));
-      timings_.scan_host_fallbacks++;
-      continue;
-    }
-    timings_.scan_device_streams++;
-    std::lock_guard<std::mutex> sl(s->mutex());
-    s->CompleteFromDevice(o.ecs_end, reinterpret_cast<const RjSegDev *>(h + off_segs) + L.segs, L.expected,
-                          reinterpret_cast<const RjDsBlock *>(h + off_ds) + L.ds, o.nds);
-    s->resident = r;
+  scan_ms_[3] = std::chrono::duration<double, std::milli>(t2 - t1).count();
+  // ---- host: adopt the device tables (or scan on the host where a list overflowed), over the
+  // handle's host threads (each stream under its own lock) ----
+  std::atomic<uint32_t> ndev{0}, nfall{0};
+  {
+    const int nt = np >= 64 ? pool_.threads() : 1;
+    const size_t per = (np + size_t(nt) * 4 - 1) / (size_t(nt) * 4);
+    pool_.Run(int((np + per - 1) / per),
+              [&](int t) {
+                for (size_t k = size_t(t) * per; k < std::min(np, size_t(t + 1) * per); k++) {
+                  Stream *s = streams[pend[k]];
+                  const RjScanOut &o = reinterpret_cast<const RjScanOut *>(h + off_out)[k];
+                  const Lay &L = lay[k];
+                  Stream::Resident &r = res[k];
+                  if (o.flags) {
+                    r = Stream::Resident();  // this stream keeps no share of the block
+                    s->Parse(data[pend[k]], uint32_t(len[pend[k]]));
+                    nfall++;
+                    continue;
+                  }
+                  ndev++;
+                  std::lock_guard<std::mutex> sl(s->mutex());
+                  s->CompleteFromDevice(o.ecs_end, reinterpret_cast<const RjSegDev *>(h + off_segs) + L.segs,
+                                        L.expected, reinterpret_cast<const RjDsBlock *>(h + off_ds) + L.ds, o.nds);
+                  s->resident = r;
+                }
+              },
+              nullptr);
   }
+  timings_.scan_device_streams = ndev.load();
+  timings_.scan_host_fallbacks = nfall.load();
+  if (timings_.scan_host_fallbacks) RJ_INFO("marker scan list overflow on %u streams: host scan", timings_.scan_host_fallbacks);
+  const auto t3 = std::chrono::steady_clock::now();
+  scan_ms_[4] = std::chrono::duration<double, std::milli>(t3 - t2).count();
+  scan_ms_[5] = std::chrono::duration<double, std::milli>(t3 - t0).count();
+  if (Dbg(kDebugScan))
+    fprintf(stderr, "[rj scan] %zu streams: headers %.3f alloc %.3f copy+upload %.3f kernel+readback %.3f adopt %.3f total %.3f ms\n",
+            size_t(np), scan_ms_[0], scan_ms_[1], scan_ms_[2], scan_ms_[3], scan_ms_[4], scan_ms_[5]);
   return kOk;
 }
 
@@ -1185,6 +1241,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // idle, an eighth once they fill it (profiles/r4_experiments/k1_chunk_warmup_ab.txt)
   cbuf.warm_shift = 2ull * lanes_all <= uint64_t(cu_count_) * RJ_K1_WG ? 1u : 3u;
   cbuf.seg_ent = nullptr;  // set with the split layout below
+  cbuf.lane_seg2 = nullptr;  // set with the paired lean layout below
+  cbuf.pair_lane0 = 0;
   if (profiling_) {
     RJ_CHECK(d_count_.Ensure(256));
     cbuf.count = d_count_.as<unsigned long long>();
@@ -1666,6 +1724,34 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
   }
   timings_.lean_split = nsplit;
+  // ---- lean paired lanes: a call whose intervals exceed one round of the chip's decoder lanes
+  // by a few (C2: 69,632 intervals, 65,536 lanes) would run its LPT tail as a second round; the
+  // 2 x excess shortest intervals are paired instead (the longest of them with the shortest), one
+  // lane decoding both back to back (rj_huff.hip RJ_HL_SWITCH), when no pair is longer than the
+  // longest interval by more than 1/16 (C2: the worst pair is 1.5 % longer).  One table set per
+  // call (the lane's LDS tables serve both intervals).  RJ_K1_PAIR=0 turns it off. ----
+  uint32_t npair = 0;
+  const uint32_t lanes_round = pair_round_ ? pair_round_ : uint32_t(cu_count_) * 256u;
+  if (lean && sorted && lanes_desc && ngroups == 1 && !any_split && nsplit == 0 && pair_lanes_ && tabs.size() == 1 &&
+      seg_total > lanes_round && seg_total - lanes_round <= lanes_round / 4) {
+    const uint32_t excess = seg_total - lanes_round;
+    std::vector<uint16_t> &gb = sc_.seg_bkt;
+    gb.resize(seg_total);
+    uint32_t gi = 0;
+    for (int i = 0; i < n; i++)
+      for (const uint16_t b : streams[i]->plan().seg_bucket) gb[gi++] = b;
+    const uint32_t top = gb[lane_seg[0]] + 1u;  // 32-B buckets
+    bool ok = true;
+    for (uint32_t i = 0; i < excess && ok; i++)
+      ok = uint32_t(gb[lane_seg[lanes_round - excess + i]]) + gb[lane_seg[seg_total - 1 - i]] <= top + top / 16u;
+    if (ok) {
+      npair = excess;
+      std::reverse(lane_seg.begin() + lanes_round, lane_seg.end());  // lane_seg2[i]: the partner of lane round - excess + i
+      cbuf.lane_seg2 = d_lane_seg + lanes_round;
+      cbuf.pair_lane0 = lanes_round - excess;
+    }
+  }
+  timings_.lean_pairs = npair;
   if (any_split) {
     std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(lane_seg.size()) * 4);
     std::memcpy(h + off_seg_lane0, seg_lane0.data(), uint64_t(seg_lane0.size()) * 4);
@@ -1735,8 +1821,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     for (int g = 0; g + 1 < ngroups; g++) RJ_HIP(hipStreamWaitEvent(stream_, pev_[g], 0));
   } else {
     if (lean) {  // no split interval: one pass, no resolution / serial stages
-      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, nsplit ? nl_split : seg_total, k1_src, d_tabs,
-                             d_lean, cbuf, k1_solo_lds_, nsplit ? &hsplit : nullptr));
+      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, nsplit ? nl_split : (npair ? lanes_round : seg_total), k1_src,
+                             d_tabs, d_lean, cbuf, k1_solo_lds_, nsplit ? &hsplit : nullptr));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
     } else {

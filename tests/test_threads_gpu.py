@@ -121,3 +121,50 @@ def test_threads_share_one_handle():
         _run_threads(4, work)
     finally:
         dec.close()
+
+
+def test_eight_handles_batch1_coalesced():
+    """jpegdecodeperf's default shape: 8 threads, a handle each, one image per call
+    (jpegdecodeperf.cpp:201-202,228-257).  Concurrent small calls on one device are decoded
+    together (rj_coalesce.h); every caller still gets its own images and its own status: threads
+    use three output formats (calls with other parameters are not combined), and one thread's
+    every third call is an unsupported 4:1:1 stream, which must fail alone while the calls
+    combined with it succeed."""
+    G.torch()
+    import torch
+    fmts = [R.OutputFormat.RGB, R.OutputFormat.YUV_PLANAR, R.OutputFormat.NATIVE]
+    datas = _fixtures()
+    wants = {f: _want(datas, f) for f in fmts}
+    by = {f["name"]: f for f in O.manifest()}
+    bad = O.fixture_bytes(by["c411_q90_128x64"])
+    c0 = R.coalesce_stats()
+
+    def work(t):
+        fmt = fmts[t % 3]
+        dec = R.JpegDecoder(R.Backend.HARDWARE, 0)
+        try:
+            for rnd in range(12):
+                k = (t + rnd) % len(datas)
+                if t == 7 and rnd % 3 == 0:
+                    s = R.JpegStream(bad)
+                    b = torch.full((64, 384), 0xA5, dtype=torch.uint8, device="cuda:0")
+                    torch.cuda.synchronize()
+                    st = dec.decode(s, R.decode_params(fmt), R.make_image([b.data_ptr()], [384]))
+                    assert st == R.Status.JPEG_NOT_SUPPORTED, R.error_name(st)
+                    s.close()
+                    continue
+                s = R.JpegStream(datas[k])
+                shapes = wants[fmt][k][0]
+                b = [torch.full(x, 0xA5, dtype=torch.uint8, device="cuda:0") for x in shapes]
+                torch.cuda.synchronize()
+                st = dec.decode(s, R.decode_params(fmt), R.make_image([x.data_ptr() for x in b], [x[1] for x in shapes]))
+                assert st == 0, R.error_name(st)
+                for c, (g, w) in enumerate(zip(b, wants[fmt][k][1])):
+                    assert np.array_equal(g.cpu().numpy(), w), (NAMES[k], fmt.name, rnd, c)
+                s.close()
+        finally:
+            dec.close()
+
+    _run_threads(8, work)
+    c1 = R.coalesce_stats()
+    assert c1[0] - c0[0] == 8 * 12  # every call took part

@@ -5,9 +5,10 @@
 set -e
 ROOT=$(git rev-parse --show-toplevel)
 TMP=$(mktemp -d /tmp/rjflags.XXXXXX)
-cp -r "$ROOT/rocjpeg_amd" "$ROOT/include" "$TMP/"
-rm -f "$TMP"/rocjpeg_amd/csrc/*.o "$TMP"/rocjpeg_amd/*.so
-make -C "$TMP/rocjpeg_amd" -j8 EXTRA="$2" >/dev/null
+mkdir -p "$TMP/rocjpeg_amd"
+cp -r "$ROOT/rocjpeg_amd/csrc" "$ROOT/rocjpeg_amd/Makefile" "$TMP/rocjpeg_amd/"
+cp -r "$ROOT/include" "$TMP/"
+make -C "$TMP/rocjpeg_amd" -j8 EXTRA="$2" librocjpeg_amd.so >/dev/null
 cp "$TMP/rocjpeg_amd/librocjpeg_amd.so" "$ROOT/rocjpeg_amd/librocjpeg_amd_$1.so"
 rm -rf "$TMP"
 echo "built rocjpeg_amd/librocjpeg_amd_$1.so ($2)"
