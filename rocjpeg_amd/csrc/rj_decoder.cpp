@@ -120,6 +120,7 @@ Decoder::~Decoder() {
       if (e) (void)hipEventDestroy(e);
     for (auto &e : prog_lev_ev_) (void)hipEventDestroy(e);
     for (auto &e : pk_ev_) (void)hipEventDestroy(e);
+    for (auto &e : scan_ev_) (void)hipEventDestroy(e);
     for (auto *arr : {k1s_, k2s_, k2e_})
       for (int q = 0; q < kMaxPipe; q++)
         if (arr[q]) (void)hipEventDestroy(arr[q]);
@@ -355,37 +356,7 @@ int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *dat
     }
   });
   RjScanJob *jobs = reinterpret_cast<RjScanJob *>(h + off_jobs);
-  {  // the bytes into the pinned staging blob over the handle's host threads, in pieces of
-     // streams; the calling thread uploads each finished prefix of pieces while the threads copy
-     // the next (HostPool::Run's in-order done callback), so the copy and the DMA overlap
-    constexpr uint64_t kPiece = 8ull << 20;
-    std::vector<size_t> piece0{0};
-    for (size_t k = 0; k < np; k++)
-      if (lay[k].src - lay[piece0.back()].src >= kPiece) piece0.push_back(k);
-    piece0.push_back(np);
-    const int npieces = int(piece0.size()) - 1;
-    uint64_t uploaded = 0;
-    int up_err = 0;
-    pool_.Run(npieces,
-              [&](int t) {
-                for (size_t k = piece0[size_t(t)]; k < piece0[size_t(t) + 1]; k++) {
-                  const Stream *s = streams[pend[k]];
-                  std::memcpy(h + lay[k].src, s->info().ecs, s->info().ecs_size);
-                  std::memset(h + lay[k].src + s->info().ecs_size, 0, 16);
-                }
-              },
-              [&](int t) {
-                const uint64_t end = piece0[size_t(t) + 1] < np ? lay[piece0[size_t(t) + 1]].src : bytes;
-                if (!up_err && hipMemcpyAsync(d + uploaded, h + uploaded, end - uploaded, hipMemcpyHostToDevice,
-                                              stream_) != hipSuccess)
-                  up_err = 1;
-                uploaded = end;
-              });
-    if (up_err) return kExecutionFailed;
-  }
-  const auto t_copy = std::chrono::steady_clock::now();
-  scan_ms_[2] = std::chrono::duration<double, std::milli>(t_copy - t_alloc).count();
-  for (size_t k = 0; k < np; k++) {
+  for (size_t k = 0; k < np; k++) {  // the jobs (they need only the layout), uploaded first
     const Stream *s = streams[pend[k]];
     const DecodePlan &p = s->plan();
     const Lay &L = lay[k];
@@ -419,10 +390,57 @@ int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *dat
     J.drop = reinterpret_cast<uint32_t *>(d + off_drop) + L.drop;
     J.out = reinterpret_cast<RjScanOut *>(d + off_out) + k;
   }
-  const auto t1 = std::chrono::steady_clock::now();
   RJ_HIP(hipMemcpyAsync(d + off_jobs, h + off_jobs, up_bytes - off_jobs, hipMemcpyHostToDevice, stream_));
   RJ_HIP(hipMemsetAsync(d + off_out, 0, np * sizeof(RjScanOut), stream_));
-  RJ_HIP(LaunchScan(stream_, reinterpret_cast<const RjScanJob *>(d + off_jobs), uint32_t(np), d));
+  {  // the bytes into the pinned staging blob over the handle's host threads, in pieces of
+     // streams; the calling thread uploads each finished prefix of pieces while the threads copy
+     // the next (HostPool::Run's in-order done callback), so the copy and the DMA overlap, and
+     // each uploaded piece's streams are scanned on a second stream while the next piece uploads
+    constexpr uint64_t kPiece = 8ull << 20;
+    std::vector<size_t> piece0{0};
+    for (size_t k = 0; k < np; k++)
+      if (lay[k].src - lay[piece0.back()].src >= kPiece) piece0.push_back(k);
+    piece0.push_back(np);
+    const int npieces = int(piece0.size()) - 1;
+    while (scan_ev_.size() < size_t(npieces) + 1) {
+      hipEvent_t e;
+      RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      scan_ev_.push_back(e);
+    }
+    hipStream_t kst = pstream_[0];
+    uint64_t uploaded = 0;
+    int up_err = 0;
+    pool_.Run(npieces,
+              [&](int t) {
+                for (size_t k = piece0[size_t(t)]; k < piece0[size_t(t) + 1]; k++) {
+                  const Stream *s = streams[pend[k]];
+                  std::memcpy(h + lay[k].src, s->info().ecs, s->info().ecs_size);
+                  std::memset(h + lay[k].src + s->info().ecs_size, 0, 16);
+                }
+              },
+              [&](int t) {
+                const size_t k0 = piece0[size_t(t)], k1 = piece0[size_t(t) + 1];
+                const uint64_t end = k1 < np ? lay[k1].src : bytes;
+                if (up_err) return;
+                if (hipMemcpyAsync(d + uploaded, h + uploaded, end - uploaded, hipMemcpyHostToDevice, stream_) !=
+                        hipSuccess ||
+                    hipEventRecord(scan_ev_[size_t(t)], stream_) != hipSuccess ||
+                    hipStreamWaitEvent(kst, scan_ev_[size_t(t)], 0) != hipSuccess ||
+                    LaunchScan(kst, reinterpret_cast<const RjScanJob *>(d + off_jobs) + k0, uint32_t(k1 - k0), d) !=
+                        hipSuccess)
+                  up_err = 1;
+                uploaded = end;
+              });
+    if (up_err) {
+      (void)hipStreamSynchronize(kst);
+      return kExecutionFailed;
+    }
+    RJ_HIP(hipEventRecord(scan_ev_[size_t(npieces)], kst));
+    RJ_HIP(hipStreamWaitEvent(stream_, scan_ev_[size_t(npieces)], 0));
+  }
+  const auto t_copy = std::chrono::steady_clock::now();
+  scan_ms_[2] = std::chrono::duration<double, std::milli>(t_copy - t_alloc).count();
+  const auto t1 = std::chrono::steady_clock::now();
   RJ_HIP(hipMemcpyAsync(h + off_out, d + off_out, down_end - off_out, hipMemcpyDeviceToHost, stream_));
   RJ_HIP(hipStreamSynchronize(stream_));
   const auto t2 = std::chrono::steady_clock::now();
@@ -513,7 +531,12 @@ int Decoder::Decode(Stream *const *streams, int n, const RocJpegDecodeParams *pa
   uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
   locks.reserve(uniq.size());
   for (Stream *s : uniq) locks.emplace_back(s->mutex());
-  return DecodeLocked(streams, n, params, dst);
+  const int r = DecodeLocked(streams, n, params, dst);
+  // an error return may leave copies in flight on the stream (from the parse-time pinned arena
+  // or the staging buffers): they finish before the streams' locks are released, so a
+  // re-parse or destroy cannot recycle memory a DMA is still reading
+  if (r != kOk) (void)hipStreamSynchronize(stream_);
+  return r;
 }
 
 // progressive images per call up to which every scan goes to the wave grid (see prog_wave_all)
@@ -1745,10 +1768,26 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     for (uint32_t i = 0; i < excess && ok; i++)
       ok = uint32_t(gb[lane_seg[lanes_round - excess + i]]) + gb[lane_seg[seg_total - 1 - i]] <= top + top / 16u;
     if (ok) {
+      // every wave gets its share of the pairs in its last lanes (a lane switching to its second
+      // interval stalls its wave until the mover has that interval's first chunks: spread, the
+      // stalls cost each wave a few round trips instead of one per lane); the singles keep the
+      // LPT order across the waves
       npair = excess;
-      std::reverse(lane_seg.begin() + lanes_round, lane_seg.end());  // lane_seg2[i]: the partner of lane round - excess + i
+      const uint32_t nwaves = lanes_round / 64u;
+      std::vector<uint32_t> &l2 = sc_.lane_split;  // [0, round): first intervals, [round, 2 round): second
+      l2.assign(2ull * lanes_round, UINT32_MAX);
+      uint32_t single = 0;
+      for (uint32_t w = 0; w < nwaves; w++) {
+        const uint32_t pw = excess / nwaves + (w < excess % nwaves ? 1u : 0u);
+        for (uint32_t j = 0; j < 64u - pw; j++) l2[w * 64u + j] = lane_seg[single++];
+      }
+      for (uint32_t i = 0; i < excess; i++) {  // pair i: the i-th longest of the tail's longer half + its partner
+        const uint32_t w = i % nwaves, slot = 63u - i / nwaves;
+        l2[w * 64u + slot] = lane_seg[lanes_round - excess + i];
+        l2[lanes_round + w * 64u + slot] = lane_seg[seg_total - 1 - i];
+      }
       cbuf.lane_seg2 = d_lane_seg + lanes_round;
-      cbuf.pair_lane0 = lanes_round - excess;
+      cbuf.pair_lane0 = 0;
     }
   }
   timings_.lean_pairs = npair;
@@ -1761,6 +1800,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     cbuf.seg_ent = reinterpret_cast<const unsigned long long *>(dbase + off_seg_ent);
   } else if (sorted) {  // lanes in length order; pieces stay at the interval's own slot
     if (nsplit) std::memcpy(h + off_lane_seg, sc_.lane_split.data(), uint64_t(nl_split) * 4);
+    else if (npair) std::memcpy(h + off_lane_seg, sc_.lane_split.data(), 2ull * lanes_round * 4);
     else std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(seg_total) * 4);
     cbuf.lane_seg = d_lane_seg;
     cbuf.seg_lane0 = nullptr;
@@ -1770,7 +1810,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   }
   // part B: everything up to the row lists, or only the lane list actually used
   const uint64_t blob_b = (!any_split && sorted && ngroups == 1)
-                              ? std::min<uint64_t>(blob, AlignUp(off_lane_seg + uint64_t(nsplit ? nl_split : seg_total) * 4, 256))
+                              ? std::min<uint64_t>(blob, AlignUp(off_lane_seg + uint64_t(nsplit ? nl_split : (npair ? 2ull * lanes_round : seg_total)) * 4, 256))
                               : blob;
   if (blob_b > blob_a) RJ_HIP(hipMemcpyAsync(dbase + blob_a, h + blob_a, blob_b - blob_a, hipMemcpyHostToDevice, stream_));
 

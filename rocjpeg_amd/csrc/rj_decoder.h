@@ -97,6 +97,7 @@ class Decoder {
   int path_policy_ = 0;
   RocJpegAmdTimings timings_ = {};
   double scan_ms_[6] = {};
+  std::vector<hipEvent_t> scan_ev_;  // ParseOnDevice: one per uploaded piece (its scan waits on it)
   hipEvent_t ev_[8] = {};  // 0..5 stage boundaries, 6..7 inside K1
   // pipelined launch (rj_decoder.cpp): interval length classes 0..pipe_groups_-2 on pstream_,
   // the last class on stream_; pev_ joins them (no timing), pk1_ times each class's K1

@@ -88,9 +88,13 @@ __device__ __forceinline__ void store_bytes(uint8_t *d, uint32_t n, const uint32
 #ifndef RJ_WIN_ROWS
 #define RJ_WIN_ROWS 8
 #endif
+#ifdef RJ_PROBE_SYNTH_LOAD
+__shared__ uint32_t rj_probe_sink[64];  // probe: the LDS row the never-waited window loads land in
+#endif
 struct EntWin {
   uint32_t w[RJ_WIN_ROWS];
   uint32_t base_lo, base_hi;
+
   __device__ __forceinline__ void load(const uint32_t *__restrict__ ent, uint64_t at, uint32_t lane) {
     base_lo = U(uint32_t(at));
     base_hi = U(uint32_t(at >> 32));
@@ -100,6 +104,19 @@ struct EntWin {
 #pragma unroll
     for (int r = 0; r < RJ_WIN_ROWS; r++) w[r] = (q << 16) | (q ? 1u : 0u);
     asm volatile("" : "+v"(w[0]));
+#ifdef RJ_PROBE_SYNTH_LOAD  // ... but the real window's loads issued (LDS-DMA into a scratch row nothing reads), never waited for
+    {
+      const uint32_t *pp = ent + at;
+      const uint32_t sink = uint32_t(uintptr_t((__attribute__((address_space(3))) uint32_t *)(rj_probe_sink)));
+#pragma unroll
+      for (int r = 0; r < RJ_WIN_ROWS; r++) {
+        const uint32_t *a = pp + r * 64u + lane;
+        uint32_t m0s;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(m0s) : "v"(a), "s"(sink) : "memory");
+      }
+    }
+#endif
 #else
     const uint32_t *p = ent + at;
 #pragma unroll
@@ -978,6 +995,9 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
   RJ_STAMP(te);
   RJ_STAMP_ADD(2, te - tc);
   }  // strips
+#ifdef RJ_PROBE_SYNTH_LOAD
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   if constexpr (!kWide)
     if (row_wide && tid == 0) {
       const uint32_t k = atomicAdd(wide_cnt, 1u);

@@ -26,6 +26,8 @@ struct Arena {
   size_t used = 0;
   std::vector<uint8_t *> free_chunks;  // buffers of released kChunkBytes chunks
   int state = 0;                        // 0 unprobed, 1 usable, -1 disabled
+  size_t pinned = 0;                    // bytes held from hipHostMalloc (live chunks + free_chunks)
+  size_t cap = 0;                       // at most this many (ROCJPEG_AMD_PARSE_PIN_MAX_MB, default 4 GB)
 };
 
 Arena &TheArena() {
@@ -41,6 +43,7 @@ void ReturnBuffer(uint8_t *p, size_t size) {
       a.free_chunks.push_back(p);
       return;
     }
+    a.pinned -= size;
   }
   (void)hipHostFree(p);
 }
@@ -51,9 +54,13 @@ std::shared_ptr<PinnedChunk> NewChunk(Arena &a, size_t size) {
   if (size == kChunkBytes && !a.free_chunks.empty()) {
     p = a.free_chunks.back();
     a.free_chunks.pop_back();
+  } else if (a.pinned + size > a.cap) {
+    return nullptr;  // over the cap: the stream borrows the caller's bytes (staged by the decode call)
   } else if (hipHostMalloc(reinterpret_cast<void **>(&p), size, hipHostMallocNonCoherent) != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
+  } else {
+    a.pinned += size;
   }
   return std::shared_ptr<PinnedChunk>(new PinnedChunk{p, size}, [](PinnedChunk *c) {
     ReturnBuffer(c->base, c->size);
@@ -75,6 +82,8 @@ PinnedSlot PinnedAlloc(size_t bytes) {
     const bool off = v != nullptr && v[0] == '0';
     a.state = (!off && hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0) ? 1 : -1;
     (void)hipGetLastError();
+    const char *m = std::getenv("ROCJPEG_AMD_PARSE_PIN_MAX_MB");
+    a.cap = (m != nullptr ? size_t(std::strtoull(m, nullptr, 10)) : size_t(4096)) << 20;
   }
   if (a.state < 0 || bytes == 0) return s;
   std::shared_ptr<PinnedChunk> c;

@@ -37,7 +37,7 @@ CTESTS = [
     ("jpeg-decode-crop-batch-fmt-native", "jpegdecodebatched", ["-crop", CROP]),
 ]
 FMT = {"native": 0, "yuv_planar": 1, "y": 2, "rgb": 3, "rgb_planar": 4}
-CSS = {0: "444", 1: "440", 2: "422", 3: "420", 4: "400"}  # RocJpegChromaSubsampling
+CSS = {0: "444", 1: "440", 2: "422", 3: "420", 5: "400"}  # RocJpegChromaSubsampling (api/rocjpeg.h:86-94)
 
 
 @pytest.fixture(scope="module")
