@@ -111,10 +111,6 @@ typedef struct {
   uint32_t chunk_k1;
   /* the call's chunk length in bytes: intervals of at least twice this are cut into chunks */
   uint32_t chunk_bytes;
-  /* lean K1 paired lanes: lanes that decoded two intervals back to back (the call's intervals
-     exceeded one round of the chip's decoder lanes) */
-  uint32_t lean_pairs;
-  uint32_t reserved0;
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);
@@ -244,7 +240,7 @@ RocJpegStatus rocJpegAmdGetCoalesceStats(uint64_t *calls, uint64_t *combined, ui
  * 2: rocJpegAmdBuildWorkTable takes blob_bytes; RocJpegAmdTimings as above.
  * 3: the resident sharded entry points; the work-table broadcast carries a status header.
  * 4: RocJpegAmdTimings.chunk_k1.  5: RocJpegAmdTimings.chunk_bytes (the call's chunk length).
- * 6: RocJpegAmdTimings.lean_pairs; rocJpegAmdGetCoalesceStats, rocJpegAmdGetLastParseTimings. */
+ * 6: rocJpegAmdGetCoalesceStats, rocJpegAmdGetLastParseTimings. */
 #define ROCJPEG_AMD_ABI_VERSION 6
 RocJpegStatus rocJpegAmdGetAbiVersion(int *version);
 

@@ -120,7 +120,6 @@ Decoder::~Decoder() {
       if (e) (void)hipEventDestroy(e);
     for (auto &e : prog_lev_ev_) (void)hipEventDestroy(e);
     for (auto &e : pk_ev_) (void)hipEventDestroy(e);
-    for (auto &e : scan_ev_) (void)hipEventDestroy(e);
     for (auto *arr : {k1s_, k2s_, k2e_})
       for (int q = 0; q < kMaxPipe; q++)
         if (arr[q]) (void)hipEventDestroy(arr[q]);
@@ -159,9 +158,6 @@ int Decoder::Initialize() {
   if (const char *m = getenv("RJ_PIPE_MIN")) pipe_min_ = uint32_t(std::max(1, atoi(m)));
   if (const char *o = getenv("RJ_SORT_LANES")) sort_lanes_ = atoi(o) != 0;
   if (const char *l = getenv("RJ_LPT")) lpt_ = atoi(l) != 0;
-  if (const char *l = getenv("RJ_K1_PAIR")) pair_lanes_ = atoi(l) != 0;
-  // tests: the lane count of one round (a multiple of 256) the pairing plans for, instead of the chip's
-  if (const char *l = getenv("RJ_K1_PAIR_ROUND")) pair_round_ = uint32_t(std::max(0, atoi(l))) & ~255u;
   if (const char *l = getenv("RJ_K1_SOLO")) k1_solo_lds_ = uint32_t(std::max(0, atoi(l)));
   if (const char *so = getenv("RJ_SPLIT_OUTLIERS")) outlier_split_ = atoi(so) != 0;
   if (const char *kc = getenv("RJ_K1_CHUNK")) k1_chunk_ = atoi(kc) != 0;
@@ -394,20 +390,15 @@ int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *dat
   RJ_HIP(hipMemsetAsync(d + off_out, 0, np * sizeof(RjScanOut), stream_));
   {  // the bytes into the pinned staging blob over the handle's host threads, in pieces of
      // streams; the calling thread uploads each finished prefix of pieces while the threads copy
-     // the next (HostPool::Run's in-order done callback), so the copy and the DMA overlap, and
-     // each uploaded piece's streams are scanned on a second stream while the next piece uploads
+     // the next (HostPool::Run's in-order done callback), so the copy and the DMA overlap.  (Per
+     // piece scan launches were measured: k_scan runs one wave per stream, so a piece's launch
+     // occupies only its streams' CUs and the serialised launches took 10x the one launch.)
     constexpr uint64_t kPiece = 8ull << 20;
     std::vector<size_t> piece0{0};
     for (size_t k = 0; k < np; k++)
       if (lay[k].src - lay[piece0.back()].src >= kPiece) piece0.push_back(k);
     piece0.push_back(np);
     const int npieces = int(piece0.size()) - 1;
-    while (scan_ev_.size() < size_t(npieces) + 1) {
-      hipEvent_t e;
-      RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      scan_ev_.push_back(e);
-    }
-    hipStream_t kst = pstream_[0];
     uint64_t uploaded = 0;
     int up_err = 0;
     pool_.Run(npieces,
@@ -419,24 +410,14 @@ int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *dat
                 }
               },
               [&](int t) {
-                const size_t k0 = piece0[size_t(t)], k1 = piece0[size_t(t) + 1];
-                const uint64_t end = k1 < np ? lay[k1].src : bytes;
-                if (up_err) return;
-                if (hipMemcpyAsync(d + uploaded, h + uploaded, end - uploaded, hipMemcpyHostToDevice, stream_) !=
-                        hipSuccess ||
-                    hipEventRecord(scan_ev_[size_t(t)], stream_) != hipSuccess ||
-                    hipStreamWaitEvent(kst, scan_ev_[size_t(t)], 0) != hipSuccess ||
-                    LaunchScan(kst, reinterpret_cast<const RjScanJob *>(d + off_jobs) + k0, uint32_t(k1 - k0), d) !=
-                        hipSuccess)
+                const uint64_t end = piece0[size_t(t) + 1] < np ? lay[piece0[size_t(t) + 1]].src : bytes;
+                if (!up_err && hipMemcpyAsync(d + uploaded, h + uploaded, end - uploaded, hipMemcpyHostToDevice,
+                                              stream_) != hipSuccess)
                   up_err = 1;
                 uploaded = end;
               });
-    if (up_err) {
-      (void)hipStreamSynchronize(kst);
-      return kExecutionFailed;
-    }
-    RJ_HIP(hipEventRecord(scan_ev_[size_t(npieces)], kst));
-    RJ_HIP(hipStreamWaitEvent(stream_, scan_ev_[size_t(npieces)], 0));
+    if (up_err) return kExecutionFailed;
+    RJ_HIP(LaunchScan(stream_, reinterpret_cast<const RjScanJob *>(d + off_jobs), uint32_t(np), d));
   }
   const auto t_copy = std::chrono::steady_clock::now();
   scan_ms_[2] = std::chrono::duration<double, std::milli>(t_copy - t_alloc).count();
@@ -1264,8 +1245,6 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // idle, an eighth once they fill it (profiles/r4_experiments/k1_chunk_warmup_ab.txt)
   cbuf.warm_shift = 2ull * lanes_all <= uint64_t(cu_count_) * RJ_K1_WG ? 1u : 3u;
   cbuf.seg_ent = nullptr;  // set with the split layout below
-  cbuf.lane_seg2 = nullptr;  // set with the paired lean layout below
-  cbuf.pair_lane0 = 0;
   if (profiling_) {
     RJ_CHECK(d_count_.Ensure(256));
     cbuf.count = d_count_.as<unsigned long long>();
@@ -1747,50 +1726,6 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
   }
   timings_.lean_split = nsplit;
-  // ---- lean paired lanes: a call whose intervals exceed one round of the chip's decoder lanes
-  // by a few (C2: 69,632 intervals, 65,536 lanes) would run its LPT tail as a second round; the
-  // 2 x excess shortest intervals are paired instead (the longest of them with the shortest), one
-  // lane decoding both back to back (rj_huff.hip RJ_HL_SWITCH), when no pair is longer than the
-  // longest interval by more than 1/16 (C2: the worst pair is 1.5 % longer).  One table set per
-  // call (the lane's LDS tables serve both intervals).  RJ_K1_PAIR=0 turns it off. ----
-  uint32_t npair = 0;
-  const uint32_t lanes_round = pair_round_ ? pair_round_ : uint32_t(cu_count_) * 256u;
-  if (lean && sorted && lanes_desc && ngroups == 1 && !any_split && nsplit == 0 && pair_lanes_ && tabs.size() == 1 &&
-      seg_total > lanes_round && seg_total - lanes_round <= lanes_round / 4) {
-    const uint32_t excess = seg_total - lanes_round;
-    std::vector<uint16_t> &gb = sc_.seg_bkt;
-    gb.resize(seg_total);
-    uint32_t gi = 0;
-    for (int i = 0; i < n; i++)
-      for (const uint16_t b : streams[i]->plan().seg_bucket) gb[gi++] = b;
-    const uint32_t top = gb[lane_seg[0]] + 1u;  // 32-B buckets
-    bool ok = true;
-    for (uint32_t i = 0; i < excess && ok; i++)
-      ok = uint32_t(gb[lane_seg[lanes_round - excess + i]]) + gb[lane_seg[seg_total - 1 - i]] <= top + top / 16u;
-    if (ok) {
-      // every wave gets its share of the pairs in its last lanes (a lane switching to its second
-      // interval stalls its wave until the mover has that interval's first chunks: spread, the
-      // stalls cost each wave a few round trips instead of one per lane); the singles keep the
-      // LPT order across the waves
-      npair = excess;
-      const uint32_t nwaves = lanes_round / 64u;
-      std::vector<uint32_t> &l2 = sc_.lane_split;  // [0, round): first intervals, [round, 2 round): second
-      l2.assign(2ull * lanes_round, UINT32_MAX);
-      uint32_t single = 0;
-      for (uint32_t w = 0; w < nwaves; w++) {
-        const uint32_t pw = excess / nwaves + (w < excess % nwaves ? 1u : 0u);
-        for (uint32_t j = 0; j < 64u - pw; j++) l2[w * 64u + j] = lane_seg[single++];
-      }
-      for (uint32_t i = 0; i < excess; i++) {  // pair i: the i-th longest of the tail's longer half + its partner
-        const uint32_t w = i % nwaves, slot = 63u - i / nwaves;
-        l2[w * 64u + slot] = lane_seg[lanes_round - excess + i];
-        l2[lanes_round + w * 64u + slot] = lane_seg[seg_total - 1 - i];
-      }
-      cbuf.lane_seg2 = d_lane_seg + lanes_round;
-      cbuf.pair_lane0 = 0;
-    }
-  }
-  timings_.lean_pairs = npair;
   if (any_split) {
     std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(lane_seg.size()) * 4);
     std::memcpy(h + off_seg_lane0, seg_lane0.data(), uint64_t(seg_lane0.size()) * 4);
@@ -1800,7 +1735,6 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     cbuf.seg_ent = reinterpret_cast<const unsigned long long *>(dbase + off_seg_ent);
   } else if (sorted) {  // lanes in length order; pieces stay at the interval's own slot
     if (nsplit) std::memcpy(h + off_lane_seg, sc_.lane_split.data(), uint64_t(nl_split) * 4);
-    else if (npair) std::memcpy(h + off_lane_seg, sc_.lane_split.data(), 2ull * lanes_round * 4);
     else std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(seg_total) * 4);
     cbuf.lane_seg = d_lane_seg;
     cbuf.seg_lane0 = nullptr;
@@ -1810,7 +1744,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   }
   // part B: everything up to the row lists, or only the lane list actually used
   const uint64_t blob_b = (!any_split && sorted && ngroups == 1)
-                              ? std::min<uint64_t>(blob, AlignUp(off_lane_seg + uint64_t(nsplit ? nl_split : (npair ? 2ull * lanes_round : seg_total)) * 4, 256))
+                              ? std::min<uint64_t>(blob, AlignUp(off_lane_seg + uint64_t(nsplit ? nl_split : seg_total) * 4, 256))
                               : blob;
   if (blob_b > blob_a) RJ_HIP(hipMemcpyAsync(dbase + blob_a, h + blob_a, blob_b - blob_a, hipMemcpyHostToDevice, stream_));
 
@@ -1861,8 +1795,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     for (int g = 0; g + 1 < ngroups; g++) RJ_HIP(hipStreamWaitEvent(stream_, pev_[g], 0));
   } else {
     if (lean) {  // no split interval: one pass, no resolution / serial stages
-      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, nsplit ? nl_split : (npair ? lanes_round : seg_total), k1_src,
-                             d_tabs, d_lean, cbuf, k1_solo_lds_, nsplit ? &hsplit : nullptr));
+      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, nsplit ? nl_split : seg_total, k1_src, d_tabs,
+                             d_lean, cbuf, k1_solo_lds_, nsplit ? &hsplit : nullptr));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
     } else {

@@ -97,7 +97,6 @@ class Decoder {
   int path_policy_ = 0;
   RocJpegAmdTimings timings_ = {};
   double scan_ms_[6] = {};
-  std::vector<hipEvent_t> scan_ev_;  // ParseOnDevice: one per uploaded piece (its scan waits on it)
   hipEvent_t ev_[8] = {};  // 0..5 stage boundaries, 6..7 inside K1
   // pipelined launch (rj_decoder.cpp): interval length classes 0..pipe_groups_-2 on pstream_,
   // the last class on stream_; pev_ joins them (no timing), pk1_ times each class's K1
@@ -115,8 +114,6 @@ class Decoder {
   bool pipe_groups_set_ = false;
   uint32_t pipe_min_ = 2048;       // env RJ_PIPE_MIN: fewest intervals worth pipelining
   bool sort_lanes_ = true;         // env RJ_SORT_LANES=0: K1 lanes in interval order
-  bool pair_lanes_ = true;         // env RJ_K1_PAIR=0: no paired lean lanes (the LPT tail runs as a second round)
-  uint32_t pair_round_ = 0;        // env RJ_K1_PAIR_ROUND (tests): lanes of one round, 0 = the chip's
   bool lpt_ = true;                 // env RJ_LPT=0: one K1 launch takes the shortest intervals first
   // env RJ_K1_SOLO=<bytes>: extra dynamic LDS per lean K1 workgroup, so that one fits per CU: the
   // workgroups past the first round (LPT order: the shortest) then wait for the CUs that finish

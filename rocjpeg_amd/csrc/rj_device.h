@@ -79,10 +79,6 @@ struct RjCoefBuf {
   uint32_t chunk_bytes;       // the call's chunk length (rj_chunks_cb; 0: no interval split)
   uint32_t warm_shift;        // k_huff_chunk warm-up: min(RJ_CHUNK_WARM_BYTES, chunk length >> warm_shift)
   const unsigned long long *seg_ent;  // per interval: first entry of its chunk regions (split ones)
-  // lean launch, paired lanes (rj_huff.hip): lane g >= pair_lane0 decodes a second interval,
-  // lane_seg2[g - pair_lane0], right after its first one (null: no pairs)
-  const uint32_t *lane_seg2;
-  uint32_t pair_lane0;
 };
 // Lean K1 split launch (rj_huff.hip): an interval decoded by a head lane from its start and a
 // tail lane from rj_split_byte(dst_len); lane_seg entries carry the role in their top bits.

@@ -870,8 +870,13 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
     (void)wmax;
     (void)rows;
     (void)quads_x;
+#ifdef RJ_PROBE_L2STORE  // timing probe: every row's strips stored into one 7.5-KB slot of a 7.5-MB scratch (L2-resident)
+    rgb_strip_420_full(s_buf + toff[0], s_buf + toff[1], s_buf + toff[2], tid,
+                       imgs[0].dst[0] + (blockIdx.x & 1023u) * 7680u, 480u);
+#else
     rgb_strip_420_full(s_buf + toff[0], s_buf + toff[1], s_buf + toff[2], tid,
                        dst0 + (__umul24(py0, pitch0) + px0 * 3), pitch0);
+#endif
     __builtin_amdgcn_s_waitcnt(0x0F70 | 10);
     win.settle();
   } else if (fmt == 3 && ncomp == 3 && al_y && wmax == strip_w && rows == mcu_h) {

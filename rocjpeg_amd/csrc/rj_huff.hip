@@ -255,14 +255,6 @@ typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
 __device__ __forceinline__ uint32_t lds_ld(const uint32_t *p) { return *(const lds_vu32 *)(p); }
 __device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) { *(lds_vu32 *)(p) = v; }
 #define RJ_HL_FIN 0xFFFFFFFFu  // decoder -> mover: the lane's decode is over
-// paired lanes (RjCoefBuf.lane_seg2): decoder -> mover: the first interval is done, stream the
-// second one as chunks RJ_HL_C0, RJ_HL_C0 + 1, ... (past any chunk index of the first); the
-// mover's commits from then on carry RJ_HL_SW, so the decoder never takes the first interval's
-// commit count for the second's
-#define RJ_HL_SWITCH 0xFFFFFFFEu
-#define RJ_HL_C0 (1u << 20)
-#define RJ_HL_SW 0x40000000u
-__device__ __forceinline__ uint32_t hl_mov(uint32_t v, bool sw) { return sw ? ((v & RJ_HL_SW) ? v & ~RJ_HL_SW : 0u) : v; }
 
 // Workgroup = DEC decoder lanes + one mover wave per decoder wave.  Lane `g` of
 // [lane0, lane0 + nlanes): the interval rj_lane_seg(g), decoded by decoder lane g % DEC; mover
@@ -314,11 +306,6 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
   }
   const bool head = kSplit && role == RJ_LANE_HEAD;
   const bool tail = kSplit && role == RJ_LANE_TAIL;
-  // paired lane: a second interval decoded right after the first (same table set: the host pairs
-  // only within a call of one table set)
-  uint32_t gseg2 = 0xFFFFFFFFu;
-  if (!kSplit && pending && coefs.lane_seg2 != nullptr && g >= coefs.pair_lane0)
-    gseg2 = *gp(coefs.lane_seg2 + (g - coefs.pair_lane0));
   const uint32_t pair = (L >> 6) * 32u + (L & 31u);  // a head lane and its tail share the record column
   int i = 0;
   if (pending) i = upper_index(nimg, gseg, [&](int qq) { return imgs[qq].seg_prefix; });
@@ -356,32 +343,17 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
       // ---- mover: keep the ring's free chunk slots filled (past the data: zero chunks, the
       // zero bits libjpeg inserts), up to 4 chunks per round; a round's loads are committed at
       // the start of the next round, so each round waits for loads issued one round earlier ----
-      uint32_t cm = 0, na = 0, c0 = 0, sw = 0;
-      const uint4 *msrc = src;
-      uint32_t mch = nchunks;
+      uint32_t cm = 0, na = 0;
       uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0, p2 = p0, p3 = p0;
       for (;;) {
-        uint32_t rd = lds_ld(&s_dec[L]);
-        if (!kSplit && rd == RJ_HL_SWITCH) {  // paired lane: on to the second interval
-          if (sw == 0) {
-            const RjImageDev &im2 = imgs[upper_index(nimg, gseg2, [&](int qq) { return imgs[qq].seg_prefix; })];
-            const RjSegDev sg2 = gp(im2.segs)[gseg2 - im2.seg_prefix];
-            msrc = reinterpret_cast<const uint4 *>(destuffed + im2.destuff_off + sg2.dst_off);
-            mch = (sg2.dst_len + 15) / 16;
-            na = 0;  // loads of the first interval's chunks in flight: not committed
-            cm = c0 = RJ_HL_C0;
-            sw = RJ_HL_SW;
-            lds_st(&s_mov[L], cm | sw);
-          }
-          rd = 4u * RJ_HL_C0 - 1u;  // nothing of the second interval consumed yet
-        }
+        const uint32_t rd = lds_ld(&s_dec[L]);
         if (na > 0) {
           hl_put(ring, cm & (RJ_HL_CHUNKS - 1), p0);
           if (na > 1) hl_put(ring, (cm + 1) & (RJ_HL_CHUNKS - 1), p1);
           if (na > 2) hl_put(ring, (cm + 2) & (RJ_HL_CHUNKS - 1), p2);
           if (na > 3) hl_put(ring, (cm + 3) & (RJ_HL_CHUNKS - 1), p3);
           cm += na;
-          lds_st(&s_mov[L], cm | sw);  // after the ring words (same wave, in order)
+          lds_st(&s_mov[L], cm);  // after the ring words (same wave, in order)
           na = 0;
         }
         const bool fin = rd == RJ_HL_FIN;
@@ -389,11 +361,10 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
         const uint32_t live = fin ? RJ_HL_CHUNKS : cm - (rd >> 2);
         const uint32_t n = min(RJ_HL_CHUNKS - live, 4u);
         if (n > 0) {
-          const uint32_t c = cm - c0;
-          p0 = *gp(c < mch ? msrc + c : rj_hl_zero);
-          if (n > 1) p1 = *gp(c + 1 < mch ? msrc + c + 1 : rj_hl_zero);
-          if (n > 2) p2 = *gp(c + 2 < mch ? msrc + c + 2 : rj_hl_zero);
-          if (n > 3) p3 = *gp(c + 3 < mch ? msrc + c + 3 : rj_hl_zero);
+          p0 = *gp(cm < nchunks ? src + cm : rj_hl_zero);
+          if (n > 1) p1 = *gp(cm + 1 < nchunks ? src + cm + 1 : rj_hl_zero);
+          if (n > 2) p2 = *gp(cm + 2 < nchunks ? src + cm + 2 : rj_hl_zero);
+          if (n > 3) p3 = *gp(cm + 3 < nchunks ? src + cm + 3 : rj_hl_zero);
           na = n;
         }
         if (__builtin_amdgcn_ballot_w64(!fin) == 0) break;
@@ -403,27 +374,25 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     }
 
     // ---- decoder ----
-    // per block b of the MCU: bit 2b its DC table, bit 2b + 1 its AC table
-    auto block_pattern = [](const RjImageDev &m) {
-      uint32_t pt = 0;
-      for (uint32_t bb = 0; bb < m.nblk_mcu; bb++) {
-        const uint32_t cc = m.blk_comp[bb] & 3;
-        pt |= ((m.comp_td[cc] & 1u) | ((m.comp_ta[cc] & 1u) << 1)) << (2 * bb);
-      }
-      return pt;
-    };
-    uint32_t nblk = im.nblk_mcu;
-    uint32_t pat = block_pattern(im);
-    uint32_t nb2 = 2 * nblk;
-    uint32_t nbits = nbytes * 8u;  // the interval's end, in bits of the lane's stream
-    uint32_t blocks = sg.mcu_count * nblk;
+    const uint32_t nblk = im.nblk_mcu;
+    uint32_t pat = 0;  // per block b: bit 2b its DC table, bit 2b + 1 its AC table
+    for (uint32_t bb = 0; bb < nblk; bb++) {
+      const uint32_t cc = im.blk_comp[bb] & 3;
+      pat |= ((im.comp_td[cc] & 1u) | ((im.comp_ta[cc] & 1u) << 1)) << (2 * bb);
+    }
+    const uint32_t nb2 = 2 * nblk;
+    const uint32_t nbits = nbytes * 8u;
+    const uint32_t blocks = sg.mcu_count * nblk;
     // entry regions: the interval's own; a tail lane writes its pair's slot of the split region
     const uint64_t tail_abs = kSplit ? split.ent + uint64_t((g >> 6) * 32u + (g & 31u)) * split.cap : 0u;
-    uint64_t ent_abs = tail ? tail_abs : im.ent_off + sg.ent_off;
+    const uint64_t ent_abs = tail ? tail_abs : im.ent_off + sg.ent_off;
     uint32_t *ent = coefs.ent + ent_abs;
+#ifdef RJ_EXP_E16
+#define RJ_HL_DST(f) reinterpret_cast<uint32_t *>(reinterpret_cast<uint16_t *>(coefs.ent) + ent_abs + (f))
+#else
 #define RJ_HL_DST(f) (ent + (f))
+#endif
     RjPiece *piece = coefs.piece + rj_seg_lane0_k<kSplit>(coefs, gseg);
-    bool sw_exp = false;  // paired lane on its second interval: the mover's commits carry RJ_HL_SW
     const RjTableSet *tset = tabsets + T;  // canonical search (escape path)
     const HCol<DEC> stage{&s_stage[0][L]};
     // split state: records (tail), the last MCU start seen (head), the head's scan over the records
@@ -438,10 +407,10 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
 // lane's next phase could read past them)
 #define RJ_HL_WAIT_RING(upto)                                                                     \
   {                                                                                               \
-    uint32_t cmv = hl_mov(lds_ld(&s_mov[L]), sw_exp);                                             \
+    uint32_t cmv = lds_ld(&s_mov[L]);                                                             \
     while (__builtin_amdgcn_ballot_w64(4u * cmv < (upto)) != 0) {                                 \
       __builtin_amdgcn_s_sleep(2);                                                                \
-      cmv = hl_mov(lds_ld(&s_mov[L]), sw_exp);                                                    \
+      cmv = lds_ld(&s_mov[L]);                                                                    \
     }                                                                                             \
     avail = 4u * cmv;                                                                             \
     asm volatile("" ::: "memory");                                                                \
@@ -533,43 +502,6 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
         }
         mseen = false;
       }
-      // paired lane: its first interval is done -- finish it (terminator, piece) and start the
-      // second from its first bit, at chunk RJ_HL_C0 of the ring's numbering (the mover switches
-      // sources when it reads RJ_HL_SWITCH)
-      bool fresh = false;
-      if (!kSplit && blocks_left == 0 && gseg2 != 0xFFFFFFFFu) {
-        stage[ne & (kStage - 1)] = RJ_RE_TERM;
-        while (fl < ne + 1) {
-          hl_flush<DEC, GROUP>(stage, fl, RJ_HL_DST(fl));
-          fl += GROUP;
-        }
-        *gp(piece) = RjPiece{ent_abs, 0u, blocks, 1u, {0, 0, 0}};
-        if (coefs.count) atomicAdd(&s_ne, ne + 1);
-        const RjImageDev &im2 = imgs[upper_index(nimg, gseg2, [&](int qq) { return imgs[qq].seg_prefix; })];
-        const RjSegDev sg2 = gp(im2.segs)[gseg2 - im2.seg_prefix];
-        nblk = im2.nblk_mcu;
-        pat = block_pattern(im2);
-        nb2 = 2 * nblk;
-        nbits = 128u * RJ_HL_C0 + sg2.dst_len * 8u;
-        blocks = sg2.mcu_count * nblk;
-        blocks_left = blocks;
-        skip = (sg2.flags & RJ_SEG_MISSING) != 0;
-        ent_abs = im2.ent_off + sg2.ent_off;
-        ent = coefs.ent + ent_abs;
-        piece = coefs.piece + rj_seg_lane0_k<false>(coefs, gseg2);
-        ne = fl = 0;
-        b = k = 0;
-        acb = ((pat >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES);
-        tb = RJ_HL_DC0 + ((pat & 1u) << (RJ_HL_DC_BITS + 2));
-        tsh = 32 - RJ_HL_DC_BITS;
-        q = 0u - 128u * RJ_HL_C0;  // bit 0 of chunk RJ_HL_C0 (a word boundary: peek = wb)
-        rr = 4u * RJ_HL_C0 + 1u;   // the ring index of wc
-        lds_st(&s_dec[L], RJ_HL_SWITCH);
-        sw_exp = true;
-        avail = 0;
-        gseg2 = 0xFFFFFFFFu;
-        fresh = true;
-      }
 #ifdef RJ_HL_EAGER_RING
       if (true) {
 #else
@@ -577,12 +509,6 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
 #endif
         RJ_HL_WAIT_RING(rr + PHASE + 1u);
         wc = ring[rr & (RJ_HL_WORDS - 1)];  // the last step's read-ahead may predate the commit
-      }
-      if (!kSplit && fresh) {  // the second interval's first words, peek and table entry
-        wa = 0;
-        wb = ring[(rr - 1u) & (RJ_HL_WORDS - 1)];
-        peek = __builtin_amdgcn_alignbit(wa, wb, q);
-        e = s_lut[(tb >> 2) + (peek >> tsh)];
       }
       RJ_HL_T2;
     }

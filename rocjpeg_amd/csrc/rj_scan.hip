@@ -54,55 +54,77 @@ __global__ __launch_bounds__(64) void k_scan(const RjScanJob *__restrict__ jobs,
   const uint8_t *src = arena + J.src_off;
   const uint32_t n = J.avail;
   RjScanOut *out = J.out;
-  // ---- copy into the resident ECS buffer (+16 B of zero slack) ----
-  {
-    const uint32_t n4 = (n + 15) / 16;
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);  // 16-B aligned in the arena
-    uint4 *d4 = reinterpret_cast<uint4 *>(J.ecs);
-    for (uint32_t q = lane; q <= n4; q += 64) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (q < n4) v = *gp(s4 + q);
-      *gp(d4 + q) = v;
-    }
-  }
+  // ---- pass A, one sweep of 1 KB per step (a 16-B chunk per lane, the next step's chunk loaded
+  // one step ahead): the bytes copied into the resident ECS buffer (+16 B of zero slack), the end
+  // (the first FF D9: the reference's ParseEOI), and every FF in [0, end) whose next byte lies in
+  // [0, end), classified and compacted by ballot + prefix sums into per-stream lists in byte
+  // order.  The arena holds 16 zero bytes after each stream, so chunk n4 (the slack) is readable. ----
   auto byte = [&](uint32_t p) -> uint32_t { return *gp(src + p); };
-  // ---- pass A1: the end = first FF D9 (the reference's ParseEOI) ----
-  uint32_t end = n;
-  for (uint32_t base = 0; base < n; base += 256) {
-    uint32_t hit = 0xFFFFFFFFu;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-      const uint32_t p = base + lane * 4 + j;
-      if (p + 1 < n && byte(p) == 0xFFu && byte(p + 1) == 0xD9u && hit == 0xFFFFFFFFu) hit = p;
-    }
-    uint32_t m = hit;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) m = min(m, __shfl_xor(m, off, 64));
-    if (m != 0xFFFFFFFFu) {
-      end = m;
-      break;
-    }
-  }
-  // ---- pass A2: classify every FF in [0, end) with its next byte inside [0, end) ----
+  const uint32_t n4 = (n + 15) / 16;
+  const uint4 *s4 = reinterpret_cast<const uint4 *>(src);  // 16-B aligned in the arena
+  uint4 *d4 = reinterpret_cast<uint4 *>(J.ecs);
   const uint32_t ri = J.ri;
+  uint32_t end = n;
   uint32_t nrst = 0, noth = 0, ndrop = 0;
   bool overflow = false;
-  for (uint32_t base = 0; base < end; base += 256) {
-    uint32_t rst_m = 0, oth_m = 0, drop_m = 0;  // per lane: bits j of its 4 bytes
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-      const uint32_t p = base + lane * 4 + j;
-      if (p + 1 < end) {
-        const uint32_t b = byte(p), nx = byte(p + 1);
-        if (b == 0xFFu) {
-          if (nx == 0xFFu) drop_m |= 1u << j;
-          else if (nx == 0x00u) drop_m |= 1u << (j + 4);  // the 00 at p + 1
-          else if (ri && nx >= 0xD0u && nx <= 0xD7u) rst_m |= 1u << j;
-          else oth_m |= 1u << j;
-        }
-      }
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  uint4 cur = z4;
+  if (lane <= n4) cur = *gp(s4 + lane);
+  uint32_t step = 0;
+  for (;; step++) {
+    const uint32_t q = step * 64u + lane;  // this lane's chunk
+    if (step * 64u > n4) break;
+    uint4 nxt = z4;
+    if (q + 64u <= n4) nxt = *gp(s4 + q + 64u);
+    if (q <= n4) *gp(d4 + q) = q < n4 ? cur : z4;
+    // the byte after this lane's 16: the next lane's first (lane 63: the next step's lane 0)
+    const uint32_t nb_lane = __shfl_down(cur.x & 0xFFu, 1, 64);
+    const uint32_t nb_next = __shfl(nxt.x & 0xFFu, 0, 64);
+    const uint32_t nb = lane == 63 ? nb_next : nb_lane;
+    // bytes equal to 0xFF: zero bytes of ~w (exact per byte)
+    auto ffb = [](uint32_t w) {
+      const uint32_t t = ~w;
+      return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);  // 0x80 in each 0xFF byte of w
+    };
+    const bool any_ff = (ffb(cur.x) | ffb(cur.y) | ffb(cur.z) | ffb(cur.w)) != 0;
+    if (__builtin_amdgcn_ballot_w64(any_ff) == 0) {
+      cur = nxt;
+      continue;
     }
-    // compaction in byte order: lane-major over the 4 (drops: up to 8 incl. the 00 after)
+    const uint32_t w[5] = {cur.x, cur.y, cur.z, cur.w, nb};
+    const uint32_t p0 = q * 16u;
+    // FF at p counts when p + 1 < n (and < end, applied below once the end is known)
+    // drops: an FF FF's first FF (bit j), an FF 00's 00 (bit j + 1; 16: the next lane's byte 0)
+    uint32_t rst_m = 0, oth_m = 0, dff_m = 0, d00_m = 0, d9 = 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; j++) {
+      const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+      const uint32_t nx = (w[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 0xFFu;
+      const bool ff = b == 0xFFu && p0 + j + 1 < n;
+      dff_m |= (ff && nx == 0xFFu) ? 1u << j : 0u;
+      d00_m |= (ff && nx == 0x00u) ? 1u << (j + 1) : 0u;
+      const bool rst = ff && ri != 0 && nx >= 0xD0u && nx <= 0xD7u;
+      rst_m |= rst ? 1u << j : 0u;
+      oth_m |= (ff && nx != 0xFFu && nx != 0x00u && !rst) ? 1u << j : 0u;
+      d9 = (ff && nx == 0xD9u && d9 == 0xFFFFFFFFu) ? p0 + j : d9;
+    }
+    bool last = false;
+    if (__builtin_amdgcn_ballot_w64(d9 != 0xFFFFFFFFu) != 0) {
+      uint32_t m = d9;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) m = min(m, __shfl_xor(m, off, 64));
+      end = m;
+      last = true;
+      // only FFs at p with p + 1 < end; the 00 drop of an FF at p sits at p + 1
+      const uint32_t lim = end > p0 ? end - p0 : 0u;  // positions j < lim - 1 count
+      const uint32_t keep = lim >= 17u ? 0xFFFFFFFFu : (lim >= 1u ? (1u << (lim - 1u)) - 1u : 0u);
+      rst_m &= keep;
+      oth_m &= keep;
+      dff_m &= keep;
+      d00_m &= keep << 1;
+    }
+    const uint32_t drop_m = dff_m | d00_m;  // disjoint: a byte is not both FF and 00
+    // compaction in byte order: lane-major, ascending positions within a lane
     uint32_t t;
     const uint32_t nr = __popc(rst_m), no = __popc(oth_m), nd = __popc(drop_m);
     const uint32_t pr = wave_prefix(nr, lane, t);
@@ -112,32 +134,31 @@ __global__ __launch_bounds__(64) void k_scan(const RjScanJob *__restrict__ jobs,
     const uint32_t pd = wave_prefix(nd, lane, t);
     const uint32_t td = t;
     uint32_t k = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++)
-      if (rst_m & (1u << j)) {
-        const uint32_t idx = nrst + pr + k++;
-        if (idx < J.rst_cap) *gp(J.rst + idx) = base + lane * 4 + j;
-      }
+    for (uint32_t m = rst_m; m; m &= m - 1, k++) {
+      const uint32_t idx = nrst + pr + k;
+      if (idx < J.rst_cap) *gp(J.rst + idx) = p0 + __builtin_ctz(m);
+    }
     k = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++)
-      if (oth_m & (1u << j)) {
-        const uint32_t idx = noth + po + k++;
-        if (idx < J.oth_cap) *gp(J.oth + idx) = base + lane * 4 + j;
-      }
+    for (uint32_t m = oth_m; m; m &= m - 1, k++) {
+      const uint32_t idx = noth + po + k;
+      if (idx < J.oth_cap) *gp(J.oth + idx) = p0 + __builtin_ctz(m);
+    }
     k = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; j++) {  // ascending byte positions: FF drops at p, 00 drops at p + 1
-      const uint32_t jj = (j & 1) ? (j >> 1) + 4 : (j >> 1);  // p_j (FF) then p_j + 1 (00)
-      if (drop_m & (1u << jj)) {
-        const uint32_t idx = ndrop + pd + k++;
-        const uint32_t pos = base + lane * 4 + (jj & 3) + (jj >> 2);
-        if (idx < J.drop_cap) *gp(J.drop + idx) = pos;
-      }
+    for (uint32_t m = drop_m; m; m &= m - 1, k++) {
+      const uint32_t idx = ndrop + pd + k;
+      if (idx < J.drop_cap) *gp(J.drop + idx) = p0 + __builtin_ctz(m);
     }
     nrst += tr;
     noth += to;
     ndrop += td;
+    if (last) break;
+    cur = nxt;
+  }
+  // the rest of the copy, past the step that found the end
+  for (uint32_t q = (step + 1) * 64u + lane; q <= n4; q += 64u) {
+    uint4 v = z4;
+    if (q < n4) v = *gp(s4 + q);
+    *gp(d4 + q) = v;
   }
   if (noth > J.oth_cap || ndrop > J.drop_cap) overflow = true;
   // the drop list must be sorted: a 00 drop (p + 1) of lane l's last byte may exceed lane l+1's

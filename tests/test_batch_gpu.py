@@ -105,9 +105,6 @@ def test_c2_1024_default_pipelined_layout(dec):
     assert tm["images"] == 1024 and tm["intervals"] == 1024 * 68
     # the layout the bench runs: lean K1, one launch, longest intervals first
     assert tm["lean_k1"] == 1 and tm["pipe_groups"] == 1 and tm["split_intervals"] == 0
-    # 69,632 intervals against one round of 256 lanes per CU: the excess is decoded in paired lanes
-    cus = t.cuda.get_device_properties(0).multi_processor_count
-    assert tm["lean_pairs"] == max(0, 1024 * 68 - 256 * cus), (tm["lean_pairs"], cus)
     ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
     bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
     assert not bad, f"{len(bad)} images differ, first {bad[:8]}"

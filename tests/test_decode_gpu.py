@@ -426,55 +426,3 @@ def test_same_tables_other_component_map(dec, order):
     for k, (d, bufs) in enumerate(zip(datas, bufs_all)):
         want = O.oracle_decode(d, int(R.OutputFormat.RGB), [(64, 384)])[1]
         assert G.first_mismatch(G.to_host(bufs)[0], want[0]) is None, (order, k)
-
-
-# ---- lean K1 paired lanes (rj_huff.hip RJ_HL_SWITCH): the LPT tail decoded two intervals per lane ----
-@pytest.fixture(scope="module")
-def pair_dec():
-    """A handle whose pairing plans for a round of 512 decoder lanes (RJ_K1_PAIR_ROUND, read at
-    handle creation) instead of the chip's 65,536, so that small batches pair their shortest
-    intervals; no call-time interval split (RJ_CHUNK_MIN), so the calls stay on the lean K1."""
-    import os
-    from tests import gpu_util as G
-    G.torch()
-    env = {"RJ_K1_PAIR_ROUND": "512", "RJ_CHUNK_MIN": str(1 << 30)}
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        d = R.JpegDecoder(R.Backend.HARDWARE, 0)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
-    d.set_profiling(True)
-    yield d
-    d.close()
-
-
-@pytest.mark.parametrize("fmt", [R.OutputFormat.RGB, R.OutputFormat.YUV_PLANAR])
-def test_paired_lean_lanes_match_oracle(pair_dec, fmt):
-    """540 row intervals against a 512-lane round: the 56 shortest (the small images' rows,
-    truncated ones among them) are decoded two per lane; every image equal to the oracle."""
-    from tests import gpu_util as G
-    by = {f["name"]: f for f in FIX}
-    big = O.fixture_bytes(by["p420_q90_ri_1920x1080"])
-    datas = [big] * 7 + [O.fixture_bytes(by["p420_q90_ri_256x128"])] * 6 + [O.fixture_bytes(by["p420_trunc_192x128"])] * 2
-    streams = [R.JpegStream(d) for d in datas]
-    shapes_all, bufs_all, imgs = [], [], []
-    for s in streams:
-        nc, css, w, h = pair_dec.image_info(s)
-        shapes = G.channel_shapes(fmt, css, w, h)
-        bufs, img = G.gpu_buffers(shapes)
-        shapes_all.append(shapes)
-        bufs_all.append(bufs)
-        imgs.append(img)
-    assert pair_dec.decode_batched(streams, R.decode_params(fmt), imgs) == 0
-    t = pair_dec.last_timings()
-    assert t["lean_k1"] == 1 and t["intervals"] == 540 and t["lean_pairs"] == 28, (t["lean_k1"], t["intervals"], t["lean_pairs"])
-    for k, (d, shapes, bufs) in enumerate(zip(datas, shapes_all, bufs_all)):
-        ost, want = O.oracle_decode(d, int(fmt), shapes)
-        assert ost == 0
-        for c, (g, w) in enumerate(zip(G.to_host(bufs), want)):
-            assert G.first_mismatch(g, w) is None, (k, c, G.first_mismatch(g, w))
