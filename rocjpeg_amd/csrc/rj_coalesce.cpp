@@ -1,13 +1,17 @@
 // rj_coalesce.cpp -- see rj_coalesce.h.
 #include "rj_coalesce.h"
 
+#include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
 #include <mutex>
+#include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "rj_decoder.h"
@@ -26,6 +30,7 @@ struct Request {
   const RocJpegDecodeParams *params;
   RocJpegImage *dst;
   int status = 0;
+  bool taken = false;  // in a leader's group (decoding)
   bool done = false;
 };
 
@@ -35,13 +40,38 @@ bool SameParams(const RocJpegDecodeParams &a, const RocJpegDecodeParams &b) {
          a.crop_rectangle.bottom == b.crop_rectangle.bottom;
 }
 
-// One device's queue of waiting calls and whether a leader is decoding.
+using Clock = std::chrono::steady_clock;
+
+// One device's queue of waiting calls and how many leaders are decoding.
 struct DeviceQueue {
   std::mutex mu;
-  std::condition_variable cv;
+  std::condition_variable cv;      // a group finished
+  std::condition_variable arrive;  // a call was queued (a gathering leader waits on it)
   std::deque<Request *> pending;
-  bool busy = false;
+  int busy = 0;
+  // threads that called on this device recently, and the last group's decode time: a leader
+  // waits briefly for the recent callers that are not queued yet (they return from the previous
+  // group together and call again within microseconds), so that they form one group instead of
+  // two alternating half groups
+  std::unordered_map<std::thread::id, Clock::time_point> seen;
+  double group_us = 0;
 };
+
+int EnvInt(const char *name, int dflt) {
+  const char *e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+// at most this many combined calls decode at once per device (each on its leader's handle)
+int Inflight() {
+  static const int v = std::max(1, EnvInt("RJ_COALESCE_INFLIGHT", 1));
+  return v;
+}
+// the longest a leader waits for recent callers to arrive (microseconds; 0: no wait)
+int GatherUs() {
+  static const int v = std::max(0, EnvInt("RJ_COALESCE_WAIT_US", 300));
+  return v;
+}
+constexpr auto kRecent = std::chrono::milliseconds(10);  // a caller counts as active this long
 
 DeviceQueue &QueueFor(int device) {
   static std::mutex mu;
@@ -94,20 +124,38 @@ int CoalescedDecode(Decoder *dec, int device, Stream *const *streams, int n, con
   DeviceQueue &q = QueueFor(device);
   Request me{dec, streams, n, params, dst};
   std::unique_lock<std::mutex> lk(q.mu);
+  const Clock::time_point now = Clock::now();
+  q.seen[std::this_thread::get_id()] = now;
+  if (q.seen.size() > 256)
+    for (auto it = q.seen.begin(); it != q.seen.end();) it = now - it->second > kRecent ? q.seen.erase(it) : ++it;
   q.pending.push_back(&me);
+  q.arrive.notify_all();
   while (!me.done) {
-    if (q.busy) {
+    // a call already in another leader's group only waits for it; a queued call leads when a
+    // decode slot is free
+    if (me.taken || q.busy >= Inflight()) {
       q.cv.wait(lk);
       continue;
     }
-    // leader: the oldest waiting call and every other with the same parameters, up to kMaxImages
-    q.busy = true;
+    // leader.  First the gathering window: while fewer calls are queued than threads called
+    // recently, wait for them up to min(GatherUs, a quarter of the last group's time)
+    q.busy++;
+    if (GatherUs() > 0) {
+      const Clock::time_point t0 = Clock::now();
+      size_t recent = 0;
+      for (const auto &kv : q.seen) recent += t0 - kv.second <= kRecent ? 1 : 0;
+      const double wait_us = std::min(double(GatherUs()), std::max(30.0, 0.25 * q.group_us));
+      const Clock::time_point deadline = t0 + std::chrono::microseconds(int64_t(wait_us));
+      while (q.pending.size() < recent && Clock::now() < deadline) q.arrive.wait_until(lk, deadline);
+    }
+    // the oldest waiting call and every other with the same parameters, up to kMaxImages
     std::vector<Request *> group;
     int images = 0;
     const RocJpegDecodeParams p0 = *q.pending.front()->params;
     for (auto it = q.pending.begin(); it != q.pending.end();) {
       Request *r = *it;
       if (SameParams(*r->params, p0) && (group.empty() || images + r->n <= kMaxImages)) {
+        r->taken = true;
         group.push_back(r);
         images += r->n;
         it = q.pending.erase(it);
@@ -116,14 +164,17 @@ int CoalescedDecode(Decoder *dec, int device, Stream *const *streams, int n, con
       }
     }
     lk.unlock();
+    const Clock::time_point g0 = Clock::now();
     try {
       RunGroup(dec, group);
     } catch (...) {
       for (Request *r : group) r->status = ROCJPEG_STATUS_RUNTIME_ERROR;
     }
+    const double us = std::chrono::duration<double, std::micro>(Clock::now() - g0).count();
     lk.lock();
+    q.group_us = us;
     for (Request *r : group) r->done = true;
-    q.busy = false;
+    q.busy--;
     q.cv.notify_all();
   }
   return me.status;

@@ -11,9 +11,13 @@
 // every queued call with the same decode parameters (up to kMaxImages images) and decodes them
 // in ONE call on its own handle.  Each caller still returns only after its own images are
 // written, with its own status, so the API stays synchronous (rocjpeg_decoder.cpp:183,290).
-// A call that meets an idle device is decoded at once on its own handle: a lone caller sees no
-// change.  If a combined call fails, its member calls are decoded one by one, so every caller gets
-// the status of its own images.  RJ_COALESCE=0 turns it off (each call on its own handle).
+// The leader first waits briefly (at most RJ_COALESCE_WAIT_US = 300 us, and a quarter of the last
+// group's decode time) while fewer calls are queued than threads called on the device in the last
+// 10 ms: callers returning from one group call again together, and without the wait they split
+// into two half groups that alternate on the device.  A lone caller (one recent thread) never
+// waits.  If a combined call fails, its member calls are decoded one by one, so every caller gets
+// the status of its own images.  RJ_COALESCE=0 turns it off (each call on its own handle);
+// RJ_COALESCE_INFLIGHT=k lets k combined calls decode at once (default 1).
 #pragma once
 #include <stdint.h>
 

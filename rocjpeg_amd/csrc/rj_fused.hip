@@ -30,12 +30,6 @@
 namespace rj {
 
 #define RJ_BLK_STRIDE 144  // bytes per staged block in LDS (128 + 16 pad)
-#ifndef RJ_K2_FAST
-#define RJ_K2_FAST 1  // the fast-row instance of K2 (row_is_fast420)
-#endif
-#ifndef RJ_K2_CONT
-#define RJ_K2_CONT 1  // fast rows: the continuation window loaded before the walk when the strip needs it
-#endif
 #ifndef RJ_K2_OCC
 #define RJ_K2_OCC 4  // K2 waves per SIMD the register budget is set for (128 VGPRs)
 #endif
@@ -88,9 +82,6 @@ __device__ __forceinline__ void store_bytes(uint8_t *d, uint32_t n, const uint32
 #ifndef RJ_WIN_ROWS
 #define RJ_WIN_ROWS 8
 #endif
-#ifdef RJ_PROBE_SYNTH_LOAD
-__shared__ uint32_t rj_probe_sink[64];  // probe: the LDS row the never-waited window loads land in
-#endif
 struct EntWin {
   uint32_t w[RJ_WIN_ROWS];
   uint32_t base_lo, base_hi;
@@ -98,30 +89,9 @@ struct EntWin {
   __device__ __forceinline__ void load(const uint32_t *__restrict__ ent, uint64_t at, uint32_t lane) {
     base_lo = U(uint32_t(at));
     base_hi = U(uint32_t(at >> 32));
-#ifdef RJ_PROBE_SYNTH_WIN  // timing probe: no window loads; every 8th entry starts a block (DC 0, AC 1..7 = 1)
-    (void)ent;
-    const uint32_t q = lane & 7u;
-#pragma unroll
-    for (int r = 0; r < RJ_WIN_ROWS; r++) w[r] = (q << 16) | (q ? 1u : 0u);
-    asm volatile("" : "+v"(w[0]));
-#ifdef RJ_PROBE_SYNTH_LOAD  // ... but the real window's loads issued (LDS-DMA into a scratch row nothing reads), never waited for
-    {
-      const uint32_t *pp = ent + at;
-      const uint32_t sink = uint32_t(uintptr_t((__attribute__((address_space(3))) uint32_t *)(rj_probe_sink)));
-#pragma unroll
-      for (int r = 0; r < RJ_WIN_ROWS; r++) {
-        const uint32_t *a = pp + r * 64u + lane;
-        uint32_t m0s;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(m0s) : "v"(a), "s"(sink) : "memory");
-      }
-    }
-#endif
-#else
     const uint32_t *p = ent + at;
 #pragma unroll
     for (int r = 0; r < RJ_WIN_ROWS; r++) w[r] = gp(p)[r * 64u + lane];
-#endif
   }
   // wait here for the window's loads.  vmcnt is in order on gfx9: a wait for a window row issued
   // after the previous strip's pixel stores waits for those stores too.  parse_blocks' walk over a
@@ -186,10 +156,7 @@ __device__ __forceinline__ uint64_t mask_start(uint32_t p) {
 // component's quantisers apply; s_qw[3 p + c] = quantiser | pair-layout byte offset << 16.
 // !kPairs (the fix-up instances): raw coefficients in zigzag order, checked against the int32
 // IDCT's domain (thr, on the raw value) -- the layout idct_pass1_wide reads.
-// kCont (the fast rows): before the walk, count the block starts the settled window holds; when
-// the strip's end is not among them (a strip of more than 512 entries: ~26 % of C2's strips), the
-// window that follows is loaded right away, so that it lands while the walk scatters the first.
-template <bool kRaw, bool kSplit, bool kPairs, bool kCont = false>
+template <bool kRaw, bool kSplit, bool kPairs>
 __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefBuf &coefs,
                                              const uint32_t *__restrict__ ent, uint32_t lane, uint32_t nb,
                                              uint32_t drop, uint32_t nblk, uint32_t cbits, EntWin &win, Nav &nv,
@@ -198,17 +165,6 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
   uint32_t done = 0;
   const uint32_t need = nb + drop;
   uint32_t bad_l = 0;  // this lane stored a coefficient outside the IDCT's exact domain (one ballot at the end)
-  EntWin cont;
-  bool have_cont = false;
-  if constexpr (kCont) {
-    uint32_t starts = 0;
-#pragma unroll
-    for (int r = 0; r < RJ_WIN_ROWS; r++) starts += __popcll(mask_start((win.w[r] >> 16) & 127u));
-    if (nv.bleft != 0 && starts <= need) {
-      cont.load(ent, (uint64_t(win.base_hi) << 32 | win.base_lo) + RJ_WIN_ROWS * 64u, lane);
-      have_cont = true;
-    }
-  }
   for (uint32_t moves = 0; done < need && moves < (1u << 16); moves++) {  // bounded on corrupt pieces
     if (nv.bleft == 0) {  // next piece, or the first piece of the next interval (synchronous reload)
       if (nv.seg >= im.nseg) break;
@@ -332,16 +288,7 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
     bool found = false;
     for (uint32_t guard = 0; !found && guard < (1u << 20); guard++) {  // bounded even on a corrupt stream
       if (guard) {  // the next window, settled: walk() then has no waits on any path (see EntWin::settle)
-        const uint64_t nxt = (uint64_t(win.base_hi) << 32 | win.base_lo) + RJ_WIN_ROWS * 64u;
-        if (kCont && have_cont && nxt == (uint64_t(cont.base_hi) << 32 | cont.base_lo)) {
-#pragma unroll
-          for (int r = 0; r < RJ_WIN_ROWS; r++) win.w[r] = cont.w[r];
-          win.base_lo = cont.base_lo;
-          win.base_hi = cont.base_hi;
-          have_cont = false;
-        } else {
-          win.load(ent, nxt, lane);
-        }
+        win.load(ent, (uint64_t(win.base_hi) << 32 | win.base_lo) + RJ_WIN_ROWS * 64u, lane);
         win.settle();
       }
       found = walk();
@@ -569,14 +516,8 @@ __device__ __forceinline__ void rgb_strip_420_full(const uint8_t *ty, const uint
     const rj_f2 ua = {uu.x, uu.x}, ub = {uu.y, uu.y}, va = {vv.x, vv.x}, vb = {vv.y, vv.y};
     uint32_t w0, w1, w2;
     csc4_pk(y4, ua, ub, va, vb, w0, w1, w2);
-#ifdef RJ_PROBE_NOSTORE  // timing probe: pixels computed, not stored (runtime-false guard)
-    if (pitch == 0x7FFFFFF1u)
-#endif
     *reinterpret_cast<RJ_GLOBAL uint3 *>(d + 96 * i) = make_uint3(w0, w1, w2);
     csc4_pk(y4b, ua, ub, va, vb, w0, w1, w2);
-#ifdef RJ_PROBE_NOSTORE
-    if (pitch == 0x7FFFFFF1u)
-#endif
     *reinterpret_cast<RJ_GLOBAL uint3 *>(d + pitch + 96 * i) = make_uint3(w0, w1, w2);
   }
 }
@@ -618,7 +559,7 @@ struct ImBytes {
 };
 #define RJ_OFF(f) uint32_t(offsetof(RjImageDev, f))
 
-template <bool kPlanes, bool kDense, bool kWide = false, bool kSplit = false, bool kFast = false>
+template <bool kPlanes, bool kDense, bool kWide = false, bool kSplit = false>
 __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, int i, uint32_t my, RjCoefBuf coefs,
                                          const RjTableSet *__restrict__ tabsets, uint8_t *__restrict__ planes,
                                          uint8_t *s_buf, uint32_t *s_qw, uint32_t *wide_cnt, uint2 *wide_list) {
@@ -773,7 +714,7 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
       if (has_blk) load_dense_block(im, coefs.dense, lane_blk, mx0, my, inter, s_buf + tid * RJ_BLK_STRIDE);
     } else {
       if (dc_diff)
-        parse_blocks<true, kSplit, kPairs, kFast && RJ_K2_CONT>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, s_qw, lane_info, thr, wide);
+        parse_blocks<true, kSplit, kPairs>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, s_qw, lane_info, thr, wide);
       else
         parse_blocks<false, false, kPairs>(im, coefs, ent, tid, nb, drop, nblk, cbits, win, nv, s_buf, s_qw, lane_info, thr, wide);
       drop = 0;
@@ -806,8 +747,8 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
       row_wide = row_wide || wide;
       if constexpr (!kPlanes) __syncthreads();  // every block is in registers: the staging area becomes the sample tiles
       if (has_blk) idct_dot2_block(w, o);
-      // the next strip's window, before this strip's pixel stores (kFast: after them, below)
-      if constexpr (!kDense && !kFast) win.settle();
+      // the next strip's window, before this strip's pixel stores
+      if constexpr (!kDense) win.settle();
     } else {
       int32_t v[64];
       const int16_t *zz = reinterpret_cast<const int16_t *>(s_buf + tid * RJ_BLK_STRIDE);
@@ -861,25 +802,7 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
   const uint32_t rows = min(mcu_h, H > py0 ? H - py0 : 0u);
 
   // destination offsets are 32-bit (the host only fuses when pitch * height < 2^31, pitch < 2^24)
-  if constexpr (kFast) {
-    // every strip of a fast row is a full 4:2:0 strip to RGB (row_is_fast420): the strip loop is
-    // straight-line here, so the next strip's window -- loaded at the end of phase A, before
-    // these 10 pixel stores -- is waited for after them and not with them (vmcnt counts loads
-    // and stores in issue order; gfx9 s_waitcnt simm16: vmcnt [3:0] + [15:14], expcnt [6:4]
-    // and lgkmcnt [11:8] left at their maxima).  It lands behind phases B and C.
-    (void)wmax;
-    (void)rows;
-    (void)quads_x;
-#ifdef RJ_PROBE_L2STORE  // timing probe: every row's strips stored into one 7.5-KB slot of a 7.5-MB scratch (L2-resident)
-    rgb_strip_420_full(s_buf + toff[0], s_buf + toff[1], s_buf + toff[2], tid,
-                       imgs[0].dst[0] + (blockIdx.x & 1023u) * 7680u, 480u);
-#else
-    rgb_strip_420_full(s_buf + toff[0], s_buf + toff[1], s_buf + toff[2], tid,
-                       dst0 + (__umul24(py0, pitch0) + px0 * 3), pitch0);
-#endif
-    __builtin_amdgcn_s_waitcnt(0x0F70 | 10);
-    win.settle();
-  } else if (fmt == 3 && ncomp == 3 && al_y && wmax == strip_w && rows == mcu_h) {
+  if (fmt == 3 && ncomp == 3 && al_y && wmax == strip_w && rows == mcu_h) {
     const uint8_t *ty = s_buf + toff[0], *tu = s_buf + toff[1], *tv = s_buf + toff[2];
     uint8_t *d = dst0 + (__umul24(py0, pitch0) + px0 * 3);
     if (hs1) {
@@ -964,7 +887,7 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
       }
     }
   }
-  if (!kFast && fmt == 1 && ncomp == 3) {  // YUV_PLANAR chroma planes at native resolution; U and V share pitch[1]
+  if (fmt == 1 && ncomp == 3) {  // YUV_PLANAR chroma planes at native resolution; U and V share pitch[1]
     const bool a4 = al_uv;
     const uint32_t cW = hs1 ? (W >> 1) : W, cH = vs1 ? (H >> 1) : H;
     const uint32_t cw = strip_w >> hs1, ch = mcu_h >> vs1;
@@ -1000,9 +923,6 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
   RJ_STAMP(te);
   RJ_STAMP_ADD(2, te - tc);
   }  // strips
-#ifdef RJ_PROBE_SYNTH_LOAD
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
   if constexpr (!kWide)
     if (row_wide && tid == 0) {
       const uint32_t k = atomicAdd(wide_cnt, 1u);
@@ -1017,21 +937,6 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
 #endif
 }
 
-// A row every strip of which is a full 4:2:0 strip to interleaved RGB (row_body's kFast
-// instance): 3 interleaved components Y 2x2 / Cb 1x1 / Cr 1x1 (strips of 10 MCUs = 160 x 16 px,
-// 60 blocks), lean raw entries, the image width a multiple of 160 and the row not the image's
-// partial last one, a 4-byte aligned destination.  Wave-uniform.
-__device__ __forceinline__ bool row_is_fast420(const RjImageDev &im, uint32_t my) {
-  const ImBytes ib(im);
-  const bool geom = ib.at(RJ_OFF(fmt)) == 3 && ib.at(RJ_OFF(ncomp)) == 3 && ib.at(RJ_OFF(interleaved)) != 0 &&
-                    ib.at(RJ_OFF(hmax)) == 2 && ib.at(RJ_OFF(vmax)) == 2 && ib.at(RJ_OFF(nblk_mcu)) == 6 &&
-                    ib.at(RJ_OFF(comp_h) + 1) == 1 && ib.at(RJ_OFF(comp_v) + 1) == 1 &&
-                    ib.at(RJ_OFF(comp_h) + 2) == 1 && ib.at(RJ_OFF(comp_v) + 2) == 1;
-  const uint32_t W = U(im.width), H = U(im.height), mcux = U(im.mcux);
-  const uint32_t al = U(uint32_t(reinterpret_cast<uintptr_t>(im.dst[0])) | im.dst_pitch[0]) & 3u;
-  return geom && U(im.dc_diff) != 0 && mcux % 10u == 0 && W == mcux * 16u && (my + 1) * 16u <= H && al == 0;
-}
-
 // K2: one wavefront (workgroup) per MCU row.
 template <bool kPlanes, bool kDense = false, bool kSplit = false>
 __global__ __launch_bounds__(64, RJ_K2_OCC) void k_rows(const RjImageDev *__restrict__ imgs, int nimg,
@@ -1042,22 +947,10 @@ __global__ __launch_bounds__(64, RJ_K2_OCC) void k_rows(const RjImageDev *__rest
                                              uint8_t *__restrict__ planes, uint32_t *wide_cnt, uint2 *wide_list) {
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];  // A/B, then tiles
   __shared__ __attribute__((aligned(16))) uint32_t s_qw[3 * 64];
-#ifdef RJ_K2_LDS_PAD  // occupancy probe: LDS per workgroup raised by this many bytes
-  __shared__ uint32_t s_pad[RJ_K2_LDS_PAD / 4];
-  asm volatile("" ::"v"(s_pad));
-  if (threadIdx.x == 4096) s_pad[gridDim.x & 7] = 0;
-#endif
   int i;
   uint32_t my;
-#ifdef RJ_K2_STAGGER  // probe: the first dispatch round's odd workgroups start RJ_K2_STAGGER x 8k cycles late
-  if ((blockIdx.x & 1) && blockIdx.x < 8192)
-    for (int z = 0; z < RJ_K2_STAGGER; z++) __builtin_amdgcn_s_sleep(127);
-#endif
   row_of_block(imgs, nimg, row_prefix, row_list, blockIdx.x, i, my);
-  if (RJ_K2_FAST && !kPlanes && !kDense && !kSplit && row_is_fast420(imgs[i], my))
-    row_body<kPlanes, kDense, false, kSplit, true>(imgs, i, my, coefs, tabsets, planes, s_buf, s_qw, wide_cnt, wide_list);
-  else
-    row_body<kPlanes, kDense, false, kSplit>(imgs, i, my, coefs, tabsets, planes, s_buf, s_qw, wide_cnt, wide_list);
+  row_body<kPlanes, kDense, false, kSplit>(imgs, i, my, coefs, tabsets, planes, s_buf, s_qw, wide_cnt, wide_list);
 }
 
 // K2 fix-up: the rows a K2 launch recorded (a strip outside the int32 IDCT's exact domain --

@@ -15,8 +15,9 @@
 // tables (into the stream's resident buffers and a compact copy for the host plan) and a copy
 // of the bytes into the stream's resident ECS buffer.
 //
-// Pass A (all lanes, 256 B per step): FF D9 end; then RST / other-marker / drop positions,
-// compacted by ballot + mbcnt into per-stream lists.  Pass B (lane per interval): interval
+// Pass A (all lanes, 1 KB per step: 16 B per lane, the next step's chunk in flight): the copy
+// into the resident ECS buffer, the FF D9 end, and the RST / other-marker / drop positions,
+// compacted by wave prefix sums into per-stream lists (a step with no FF byte only copies).  Pass B (lane per interval): interval
 // bounds, drops by binary search, K0 blocks, prefix sums for the destuffed / entry / chunk
 // offsets.
 #include <hip/hip_runtime.h>
