@@ -146,7 +146,12 @@ int CoalescedDecode(Decoder *dec, int device, Stream *const *streams, int n, con
       for (const auto &kv : q.seen) recent += t0 - kv.second <= kRecent ? 1 : 0;
       const double wait_us = std::min(double(GatherUs()), std::max(30.0, 0.25 * q.group_us));
       const Clock::time_point deadline = t0 + std::chrono::microseconds(int64_t(wait_us));
-      while (q.pending.size() < recent && Clock::now() < deadline) q.arrive.wait_until(lk, deadline);
+      while (!me.taken && q.pending.size() < recent && Clock::now() < deadline) q.arrive.wait_until(lk, deadline);
+      if (me.taken) {  // another leader took this call while the lock was released: it only waits now
+        q.busy--;
+        q.cv.notify_all();
+        continue;
+      }
     }
     // the oldest waiting call and every other with the same parameters, up to kMaxImages
     std::vector<Request *> group;

@@ -1,9 +1,11 @@
 // rj_pinned.cpp -- the pinned host arena of parsed bitstreams (rj_pinned.h).
 #include "rj_pinned.h"
 
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -109,6 +111,33 @@ PinnedSlot PinnedAlloc(size_t bytes) {
     s.chunk = std::move(c);
   }
   return s;
+}
+
+void CopyToStaging(void *dst, const void *src, size_t n) {
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+  if (n < 4096) {
+    std::memcpy(d, s, n);
+    return;
+  }
+  const size_t head = (16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15;
+  std::memcpy(d, s, head);
+  d += head;
+  s += head;
+  n -= head;
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(s + i));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i *>(s + i + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i *>(s + i + 32));
+    const __m128i e = _mm_loadu_si128(reinterpret_cast<const __m128i *>(s + i + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i *>(d + i), a);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(d + i + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(d + i + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(d + i + 48), e);
+  }
+  std::memcpy(d + i, s + i, n - i);
+  _mm_sfence();
 }
 
 }  // namespace rj

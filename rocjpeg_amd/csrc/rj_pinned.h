@@ -31,4 +31,11 @@ struct PinnedSlot {
 // (no device, allocation failure, or ROCJPEG_AMD_PARSE_PIN=0).
 PinnedSlot PinnedAlloc(size_t bytes);
 
+// memcpy into pinned staging memory that only a DMA or the GPU reads next: non-temporal stores
+// for the bulk, so the destination lines are neither read for ownership nor kept in the host's
+// caches (a plain copy of a few hundred KB uses cached stores: the host's memory then carries the
+// source read, the destination's ownership read, the write and the DMA's read).  Ends with a store
+// fence, so the bytes are visible before whatever the caller publishes next.
+void CopyToStaging(void *dst, const void *src, size_t n);
+
 }  // namespace rj

@@ -331,7 +331,7 @@ void Stream::PinEcs() {
   if (plan_.status != 0 || info_.ecs_size == 0) return;
   pin_ = PinnedAlloc(size_t(info_.ecs_size) + 16);
   if (pin_.ptr == nullptr) return;
-  std::memcpy(pin_.ptr, info_.ecs, info_.ecs_size);
+  CopyToStaging(pin_.ptr, info_.ecs, info_.ecs_size);
   std::memset(pin_.ptr + info_.ecs_size, 0, 16);  // K0 reads <= 8 B past the end
 }
 
