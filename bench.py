@@ -24,6 +24,7 @@ import ctypes
 import io
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -469,6 +470,31 @@ def call_shapes(dec, datas, fmt, dev, threads=8):
                 "per_thread_images_per_s": [round(r, 1) for r in rates],
                 "spread_max_over_min": round(max(rates) / min(rates), 3) if min(rates) > 0 else None}
 
+    def perf_sample(passes=4, count=256):
+        """The same shape from C, without the Python interpreter lock between the threads: the
+        restated jpegdecodeperf (tests/c/rj_samples.cpp, linked -lrocjpeg) over `count` of the
+        images written to a directory, -t threads -b 1 -fmt rgb, `passes` passes per thread."""
+        import shutil
+        import tempfile
+        exe = os.path.join(ROOT, "tests", "c", "jpegdecodeperf_rj")
+        if not os.access(exe, os.X_OK):
+            return {"error": f"{exe} not built"}
+        d = tempfile.mkdtemp(prefix="rj_perf_")
+        try:
+            for k, x in enumerate(datas[:count]):
+                with open(os.path.join(d, f"img{k:04d}.jpg"), "wb") as f:
+                    f.write(x)
+            r = subprocess.run([exe, "-i", d, "-t", str(threads), "-b", "1", "-fmt", "rgb", "-n", str(passes)],
+                               capture_output=True, text=True, timeout=300)
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+        m = re.search(r"images/s summed ([0-9.]+)", r.stdout)
+        if r.returncode != 0 or not m:
+            return {"error": (r.stdout + r.stderr)[-500:]}
+        return {"images_per_s_summed": float(m.group(1)), "threads": threads, "images": min(count, len(datas)),
+                "passes": passes, "command": f"jpegdecodeperf_rj -t {threads} -b 1 -fmt rgb -n {passes}"}
+
+    res[f"perf_threads{threads}_batch1_c_sample"] = perf_sample()
     res[f"perf_threads{threads}_batch1_host_streams"] = perf_threads(False)
     res[f"perf_threads{threads}_batch1_resident"] = perf_threads(True)
     c0 = R.coalesce_stats()

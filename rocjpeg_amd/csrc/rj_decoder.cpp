@@ -162,7 +162,6 @@ int Decoder::Initialize() {
   if (const char *so = getenv("RJ_SPLIT_OUTLIERS")) outlier_split_ = atoi(so) != 0;
   if (const char *kc = getenv("RJ_K1_CHUNK")) k1_chunk_ = atoi(kc) != 0;
   if (const char *cm = getenv("RJ_CHUNK_MIN")) chunk_min_ = uint32_t(std::max(16, atoi(cm)));
-  if (const char *us = getenv("RJ_SCAN_UPLOAD_STREAMS")) scan_up_streams_ = atoi(us) > 1 ? 2 : 1;
   if (const char *sf = getenv("RJ_SPLIT_OUTLIER_FRAC")) outlier_frac_ = atof(sf);
   if (const char *st = getenv("RJ_SPLIT_OUTLIER_T")) outlier_t_ = std::max(0.5, std::min(1.0, atof(st)));
   cu_count_ = std::max(1, prop.multiProcessorCount);
@@ -401,10 +400,7 @@ int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *dat
     piece0.push_back(np);
     const int npieces = int(piece0.size()) - 1;
     uint64_t uploaded = 0;
-    int up_err = 0, nup = 0;
-    // the pieces' DMAs alternate over two streams (two DMA engines: 54.7 vs 47.9 GB/s for 8-MB
-    // pieces, profiles/r5_experiments/h2d_rates.txt); the kernel waits for both
-    const int up_streams = scan_up_streams_;
+    int up_err = 0;
     pool_.Run(npieces,
               [&](int t) {
                 for (size_t k = piece0[size_t(t)]; k < piece0[size_t(t) + 1]; k++) {
@@ -415,21 +411,12 @@ int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *dat
               },
               [&](int t) {
                 const uint64_t end = piece0[size_t(t) + 1] < np ? lay[piece0[size_t(t) + 1]].src : bytes;
-                hipStream_t us = (up_streams > 1 && (nup & 1)) ? pstream_[0] : stream_;
                 if (!up_err && hipMemcpyAsync(d + uploaded, h + uploaded, end - uploaded, hipMemcpyHostToDevice,
-                                              us) != hipSuccess)
+                                              stream_) != hipSuccess)
                   up_err = 1;
-                nup++;
                 uploaded = end;
               });
-    if (up_streams > 1 && nup > 1) {
-      RJ_HIP(hipEventRecord(pev_[0], pstream_[0]));
-      RJ_HIP(hipStreamWaitEvent(stream_, pev_[0], 0));
-    }
-    if (up_err) {
-      (void)hipStreamSynchronize(pstream_[0]);
-      return kExecutionFailed;
-    }
+    if (up_err) return kExecutionFailed;
     RJ_HIP(LaunchScan(stream_, reinterpret_cast<const RjScanJob *>(d + off_jobs), uint32_t(np), d));
   }
   const auto t_copy = std::chrono::steady_clock::now();

@@ -192,7 +192,6 @@ class Decoder {
   // host threads of the per-call staging copies: RJ_HOST_THREADS, else up to 8 (the caller's
   // thread counts as one)
   HostPool pool_{HostThreads()};
-  int scan_up_streams_ = 2;  // env RJ_SCAN_UPLOAD_STREAMS: DMA streams of the marker scan's upload (1 or 2)
   static int HostThreads();
 };
 

@@ -45,13 +45,14 @@ struct Args {
   std::string in, out;
   bool save = false;
   int device = 0, threads = 1, batch = 1;
+  int passes = 1;  // jpegdecodeperf_rj only (not a reference option): timed passes over the thread's images
   RocJpegBackend backend = ROCJPEG_BACKEND_HARDWARE;
   RocJpegDecodeParams params{};
 };
 
 [[noreturn]] void Usage(const char *bad) {
   std::fprintf(stderr, "bad or incomplete option: %s\nusage: -i <file|dir> [-o out] [-d dev] [-be backend] "
-                       "[-fmt native|yuv_planar|y|rgb|rgb_planar] [-crop l,t,r,b] [-b batch] [-t threads]\n",
+                       "[-fmt native|yuv_planar|y|rgb|rgb_planar] [-crop l,t,r,b] [-b batch] [-t threads] [-n passes]\n",
                bad ? bad : "");
   std::exit(1);
 }
@@ -74,6 +75,7 @@ Args Parse(int argc, char **argv) {
       a.threads = std::atoi(val());
       if (a.threads <= 0 || a.threads > 32) Usage(argv[i]);
     } else if (o == "-b") a.batch = std::max(1, std::atoi(val()));
+    else if (o == "-n") a.passes = std::max(1, std::atoi(val()));
     else if (o == "-fmt") {
       const std::string f = val();
       if (f == "native") a.params.output_format = ROCJPEG_OUTPUT_NATIVE;
@@ -375,6 +377,7 @@ int RunPerf(const Args &a) {
       }
       double ms = 0;
       size_t n = 0;
+      for (int pass = 0; pass < a.passes; pass++)
       for (size_t i = 0; i < items.size(); i += size_t(a.batch)) {
         std::vector<RocJpegStreamHandle> hs;
         std::vector<RocJpegImage> imgs;

@@ -22,7 +22,7 @@ def main():
     for m in mins:
         os.environ["RJ_CHUNK_MIN"] = m
         dec = R.JpegDecoder(R.Backend.HARDWARE, 0)
-        for bs in (1, 4, 8, 16, 128):
+        for bs in [int(x) for x in os.environ.get("SHAPES", "1,4,8,16,128").split(",")]:
             streams = [R.JpegStream(d) for d in datas[:bs]]
             dec.streams_to_device(streams)
             outs = [t.empty((1080, 5760), dtype=t.uint8, device="cuda") for _ in range(bs)]
