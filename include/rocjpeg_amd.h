@@ -111,6 +111,10 @@ typedef struct {
   uint32_t chunk_k1;
   /* the call's chunk length in bytes: intervals of at least twice this are cut into chunks */
   uint32_t chunk_bytes;
+  /* MCU-phase hypotheses per speculative chunk (1: one lane per chunk; small calls: the MCU's
+     block count, each speculative chunk decoded from every phase it may start in) */
+  uint32_t chunk_hyp;
+  uint32_t reserved0;
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);
@@ -240,7 +244,7 @@ RocJpegStatus rocJpegAmdGetCoalesceStats(uint64_t *calls, uint64_t *combined, ui
  * 2: rocJpegAmdBuildWorkTable takes blob_bytes; RocJpegAmdTimings as above.
  * 3: the resident sharded entry points; the work-table broadcast carries a status header.
  * 4: RocJpegAmdTimings.chunk_k1.  5: RocJpegAmdTimings.chunk_bytes (the call's chunk length).
- * 6: rocJpegAmdGetCoalesceStats, rocJpegAmdGetLastParseTimings. */
+ * 6: rocJpegAmdGetCoalesceStats, rocJpegAmdGetLastParseTimings, RocJpegAmdTimings.chunk_hyp. */
 #define ROCJPEG_AMD_ABI_VERSION 6
 RocJpegStatus rocJpegAmdGetAbiVersion(int *version);
 

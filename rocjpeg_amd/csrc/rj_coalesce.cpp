@@ -144,6 +144,8 @@ int CoalescedDecode(Decoder *dec, int device, Stream *const *streams, int n, con
       const Clock::time_point t0 = Clock::now();
       size_t recent = 0;
       for (const auto &kv : q.seen) recent += t0 - kv.second <= kRecent ? 1 : 0;
+      // with k groups in flight the recent callers form k cohorts, each led by one leader
+      recent = (recent + size_t(Inflight()) - 1) / size_t(Inflight());
       const double wait_us = std::min(double(GatherUs()), std::max(30.0, 0.25 * q.group_us));
       const Clock::time_point deadline = t0 + std::chrono::microseconds(int64_t(wait_us));
       while (!me.taken && q.pending.size() < recent && Clock::now() < deadline) q.arrive.wait_until(lk, deadline);

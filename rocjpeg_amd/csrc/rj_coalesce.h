@@ -17,7 +17,8 @@
 // into two half groups that alternate on the device.  A lone caller (one recent thread) never
 // waits.  If a combined call fails, its member calls are decoded one by one, so every caller gets
 // the status of its own images.  RJ_COALESCE=0 turns it off (each call on its own handle);
-// RJ_COALESCE_INFLIGHT=k lets k combined calls decode at once (default 1).
+// RJ_COALESCE_INFLIGHT=k lets k combined calls decode at once, each gathering 1/k of the recent
+// callers (default 1).
 #pragma once
 #include <stdint.h>
 

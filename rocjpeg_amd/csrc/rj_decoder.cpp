@@ -162,6 +162,8 @@ int Decoder::Initialize() {
   if (const char *so = getenv("RJ_SPLIT_OUTLIERS")) outlier_split_ = atoi(so) != 0;
   if (const char *kc = getenv("RJ_K1_CHUNK")) k1_chunk_ = atoi(kc) != 0;
   if (const char *cm = getenv("RJ_CHUNK_MIN")) chunk_min_ = uint32_t(std::max(16, atoi(cm)));
+  if (const char *hy = getenv("RJ_K1_HYP")) hyp_max_ = uint32_t(std::max(1, atoi(hy)));
+  if (const char *hw = getenv("RJ_K1_HYP_WARM")) hyp_warm_ = atoi(hw) != 0;
   if (const char *sf = getenv("RJ_SPLIT_OUTLIER_FRAC")) outlier_frac_ = atof(sf);
   if (const char *st = getenv("RJ_SPLIT_OUTLIER_T")) outlier_t_ = std::max(0.5, std::min(1.0, atof(st)));
   cu_count_ = std::max(1, prop.multiProcessorCount);
@@ -1063,6 +1065,34 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // RJ_K1_WG chunks never straddles a workgroup (padding lanes), longer ones go after them.
   // Common case -- no interval split -- is the identity (lane = interval), nothing uploaded. ----
   const bool any_split = rj_chunks_cb(src_max, chunk_bytes) > 1;
+  // MCU-phase hypotheses per speculative chunk (rj_device.h rj_chunk_lanes): as many as the
+  // call's largest MCU has blocks (at most RJ_MAX_HYP), when the chunk lanes times that still fit
+  // one round of the chip's decoder lanes with the workgroup padding; 1 otherwise, and always on
+  // the round-3 chunk path (k_entropy, RJ_K1_CHUNK=0)
+  uint32_t hyp = 1;
+  if (any_split && k1_chunk_ && hyp_max_ > 1) {
+    uint32_t nblk_max = 1;
+    for (int i = 0; i < n; i++) nblk_max = std::max(nblk_max, uint32_t(streams[i]->plan().nblk_mcu));
+    for (uint32_t H = std::min<uint32_t>({uint32_t(RJ_MAX_HYP), nblk_max, hyp_max_}); H > 1; H--) {
+      uint64_t lanes = 0, dev = 0;
+      for (int i = 0; i < n; i++)
+        for (const RjSegDev &sg : streams[i]->plan().segs) {
+          const uint32_t nl = rj_chunk_lanes(rj_chunks_cb(sg.src_len, chunk_bytes), H);
+          if (nl > RJ_K1_WG) {
+            dev += nl;
+          } else {
+            if (lanes % RJ_K1_WG + nl > RJ_K1_WG) lanes = AlignUp(lanes, RJ_K1_WG);
+            lanes += nl;
+          }
+        }
+      const uint64_t wgs = (lanes + RJ_K1_WG - 1) / RJ_K1_WG + (dev + RJ_K1_WG - 1) / RJ_K1_WG;
+      if (wgs <= uint64_t(cu_count_)) {
+        hyp = H;
+        break;
+      }
+    }
+  }
+  timings_.chunk_hyp = hyp;
   std::vector<uint32_t> &seg_lane0 = sc_.seg_lane0, &lane_seg = sc_.lane_seg;
   seg_lane0.clear();
   lane_seg.clear();
@@ -1073,12 +1103,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     uint32_t gs = 0;
     for (int i = 0; i < n; i++)
       for (const RjSegDev &sg : streams[i]->plan().segs) {
-        const uint32_t nch = rj_chunks_cb(sg.src_len, chunk_bytes);
+        const uint32_t nch = rj_chunks_cb(sg.src_len, chunk_bytes), nl = rj_chunk_lanes(nch, hyp);
         split_intervals += nch > 1 ? 1u : 0u;
-        if (nch <= RJ_K1_WG) {
-          if (lanes_wg % RJ_K1_WG + nch > RJ_K1_WG) lanes_wg = uint32_t(AlignUp(lanes_wg, RJ_K1_WG));
+        if (nl <= RJ_K1_WG) {
+          if (lanes_wg % RJ_K1_WG + nl > RJ_K1_WG) lanes_wg = uint32_t(AlignUp(lanes_wg, RJ_K1_WG));
           seg_lane0[gs] = lanes_wg;
-          lanes_wg += nch;
+          lanes_wg += nl;
         } else {
           seg_lane0[gs] = UINT32_MAX;
         }
@@ -1093,7 +1123,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       for (const RjSegDev &sg : streams[i]->plan().segs) {
         if (seg_lane0[gs] == UINT32_MAX) {
           seg_lane0[gs] = lanes_all;
-          lanes_all += rj_chunks_cb(sg.src_len, chunk_bytes);
+          lanes_all += rj_chunk_lanes(rj_chunks_cb(sg.src_len, chunk_bytes), hyp);
         }
         gs++;
       }
@@ -1101,8 +1131,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     gs = 0;
     for (int i = 0; i < n; i++)
       for (const RjSegDev &sg : streams[i]->plan().segs) {
-        const uint32_t nch = rj_chunks_cb(sg.src_len, chunk_bytes);
-        for (uint32_t q = 0; q < nch; q++) lane_seg[seg_lane0[gs] + q] = gs;
+        const uint32_t nl = rj_chunk_lanes(rj_chunks_cb(sg.src_len, chunk_bytes), hyp);
+        for (uint32_t q = 0; q < nl; q++) lane_seg[seg_lane0[gs] + q] = gs;
         gs++;
       }
   }
@@ -1119,7 +1149,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         const uint32_t nch = rj_chunks_cb(sg.src_len, chunk_bytes);
         if (nch > 1) {
           seg_ent[gs] = at;
-          at += rj_chunk_regions(sg.src_len, nch);
+          at += rj_chunk_regions(sg.src_len, nch, hyp);
         }
         gs++;
       }
@@ -1241,9 +1271,14 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   cbuf.wide_flag = d_wide_flag_;
   cbuf.piece_shift = 0;
   cbuf.chunk_bytes = chunk_bytes;
+  cbuf.hyp = hyp;
   // chunk warm-up (k_huff_chunk): up to half a chunk while the call's lanes leave the chip half
   // idle, an eighth once they fill it (profiles/r4_experiments/k1_chunk_warmup_ab.txt)
   cbuf.warm_shift = 2ull * lanes_all <= uint64_t(cu_count_) * RJ_K1_WG ? 1u : 3u;
+  // (RJ_K1_HYP_WARM=0: no warm-up under phase hypotheses -- measured slower: the in-phase
+  // hypothesis still needs the warm-up to align its symbols before its records begin,
+  // profiles/r5_experiments/k1_hyp_small_calls_warm.txt)
+  if (hyp > 1 && !hyp_warm_) cbuf.warm_shift = 31u;
   cbuf.seg_ent = nullptr;  // set with the split layout below
   if (profiling_) {
     RJ_CHECK(d_count_.Ensure(256));
@@ -2029,7 +2064,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       for (int h = 0; h < 8; h++) fprintf(stderr, " %u", hist[h]);
       fprintf(stderr, " | iters mean %.0f max %u\n", (nsync + ndone) ? sum_it / (nsync + ndone) : 0.0, max_it);
       if (n == 1 && Dbg(kDebugK1Pieces)) {  // one image: its first interval's pieces and chunks
-        const uint32_t l0 = seg_lane0[0], nch = rj_chunks_cb(streams[0]->plan().segs[0].src_len, timings_.chunk_bytes);
+        const uint32_t l0 = seg_lane0[0], nch = rj_chunks_cb(streams[0]->plan().segs[0].src_len, timings_.chunk_bytes),
+                       H = timings_.chunk_hyp;
         std::vector<RjPiece> pc(nch);
         RJ_HIP(hipMemcpy(pc.data(), d_piece_.as<RjPiece>() + l0, nch * sizeof(RjPiece), hipMemcpyDeviceToHost));
         fprintf(stderr, "[K1] seg0 lanes %u.. nch %u npieces %u\n", l0, nch, pc[0].npieces);
@@ -2037,7 +2073,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
           fprintf(stderr, "  piece %u: ent %llu first %u n %u dcd %d %d %d\n", q, (unsigned long long)pc[q].ent,
                   pc[q].first_blk, pc[q].nblk, pc[q].dcd[0], pc[q].dcd[1], pc[q].dcd[2]);
         for (uint32_t c = 0; c < nch; c++) {
-          const RjChunkRes &r = cr[l0 + nch - 1 - c];
+          const RjChunkRes &r = cr[l0 + rj_chunk_lane(nch, H, c, 0)];
           fprintf(stderr, "  chunk %u: st %u tgt %u rec %u rb %u ne %u stop %u end %u\n", c, r.status, r.tgt, r.rec,
                   r.rb, r.ne, r.pad[0], r.pad[1]);
         }

@@ -192,6 +192,8 @@ class Decoder {
   // host threads of the per-call staging copies: RJ_HOST_THREADS, else up to 8 (the caller's
   // thread counts as one)
   HostPool pool_{HostThreads()};
+  uint32_t hyp_max_ = RJ_MAX_HYP;  // env RJ_K1_HYP: most MCU-phase hypotheses per speculative chunk (1: off)
+  bool hyp_warm_ = true;           // env RJ_K1_HYP_WARM=0: no speculative warm-up under hypotheses
   static int HostThreads();
 };
 

@@ -50,7 +50,7 @@ struct RjRecord {
 // what a chunk's lane found when it stopped
 struct RjChunkRes {
   uint32_t status;           // RJ_CHUNK_*
-  uint32_t tgt, rec;         // SYNC: later chunk (interval-relative) and its record index
+  uint32_t tgt, rec;         // SYNC: later chunk (chunks ahead, bits [15:0]; its hypothesis, [31:16]) and its record index
   uint32_t rb, ne;           // blocks / entries this lane produced before the stop point
   int32_t pred[3];           // its (chunk-relative) DC predictors at the stop point
   uint32_t rb_over;          // first block that read past the data (UINT32_MAX: none)
@@ -79,6 +79,7 @@ struct RjCoefBuf {
   uint32_t chunk_bytes;       // the call's chunk length (rj_chunks_cb; 0: no interval split)
   uint32_t warm_shift;        // k_huff_chunk warm-up: min(RJ_CHUNK_WARM_BYTES, chunk length >> warm_shift)
   const unsigned long long *seg_ent;  // per interval: first entry of its chunk regions (split ones)
+  uint32_t hyp;               // MCU-phase hypotheses per speculative chunk (rj_chunk_lanes; 1: one lane per chunk)
 };
 // Lean K1 split launch (rj_huff.hip): an interval decoded by a head lane from its start and a
 // tail lane from rj_split_byte(dst_len); lane_seg entries carry the role in their top bits.
@@ -96,6 +97,7 @@ struct RjHuffSplit {
 #define RJ_ENT_TERM (127u << 16)  // end-of-stream marker
 #define RJ_ENT_SLACK 1024         // entries of read slack after the last region (K2 reads 512-entry windows)
 #define RJ_MAX_RECORDS 64         // chunk-start records per speculative chunk
+#define RJ_MAX_HYP 6              // MCU-phase hypotheses per speculative chunk at most (4:2:0's 6 blocks)
 #ifndef RJ_RECORD_EVERY
 #define RJ_RECORD_EVERY 8         // one record every 8th block start of a chunk's head
 #endif
@@ -138,6 +140,19 @@ __host__ __device__ inline uint32_t rj_chunks_cb(uint32_t bytes, uint32_t cb) {
 __host__ __device__ inline uint32_t rj_nch(const RjCoefBuf &c, uint32_t src_len) {
   return rj_chunks_cb(src_len, c.chunk_bytes);
 }
+// Lanes of an interval cut into nch chunks when each speculative chunk (c > 0) is decoded under
+// `hyp` hypotheses of the MCU phase at its start (hypothesis h assumes block h of an MCU begins
+// there): chunk 0 has one lane, every other chunk `hyp`.  A speculative decode that starts in the
+// wrong phase keeps decoding a chroma block with the luma tables (or the reverse) until it slips
+// into step by chance, which makes the resynchronisation long-tailed; one of the hypotheses starts
+// in step and meets the true decode as soon as the symbols align.  Small calls, whose lanes leave
+// the chip idle, take hyp = the MCU's block count (rj_decoder.cpp); large ones keep 1.
+// Lane offsets inside the interval, reverse chunk order: chunk nch-1's hypotheses at [0, hyp), ...,
+// chunk 1's at [(nch-2) hyp, (nch-1) hyp), chunk 0 at (nch-1) hyp.
+__host__ __device__ inline uint32_t rj_chunk_lanes(uint32_t nch, uint32_t hyp) { return nch > 1 ? 1u + (nch - 1) * hyp : 1u; }
+__host__ __device__ inline uint32_t rj_chunk_lane(uint32_t nch, uint32_t hyp, uint32_t c, uint32_t h) {
+  return c == 0 ? (nch - 1) * hyp : (nch - 1 - c) * hyp + h;
+}
 // chunk length in bytes (16-B multiple); chunk c covers [c*len, min((c+1)*len, bytes))
 __host__ __device__ inline uint32_t rj_chunk_len(uint32_t bytes, uint32_t nch) {
   return ((bytes + nch - 1) / nch + 15u) & ~15u;
@@ -159,10 +174,10 @@ __host__ __device__ inline uint64_t rj_chunk_cap(uint32_t clen) {
 __host__ __device__ inline uint64_t rj_interval_entries(uint32_t bytes, uint64_t blocks, uint32_t nblk_mcu) {
   return rj_group(8ull * bytes + blocks + uint64_t(nblk_mcu) * RJ_ENT_PER_BLOCK + 1);
 }
-// the chunk regions of an interval a call cuts into nch chunks (RjCoefBuf.seg_ent: placed by
-// the call after the images' serial regions)
-__host__ __device__ inline uint64_t rj_chunk_regions(uint32_t bytes, uint32_t nch) {
-  return uint64_t(nch) * rj_chunk_cap(rj_chunk_len(bytes, nch));
+// the chunk regions of an interval a call cuts into nch chunks, one per lane (RjCoefBuf.seg_ent:
+// placed by the call after the images' serial regions; lane offset o's region at o x cap)
+__host__ __device__ inline uint64_t rj_chunk_regions(uint32_t bytes, uint32_t nch, uint32_t hyp) {
+  return uint64_t(rj_chunk_lanes(nch, hyp)) * rj_chunk_cap(rj_chunk_len(bytes, nch));
 }
 
 // One restart interval of one image (host parser rj_stream.cpp builds these).

@@ -732,14 +732,16 @@ __global__ __launch_bounds__(256) void k_resolve(const RjImageDev *__restrict__ 
   bool ok = true;
   if (nch > 1) {
     const uint32_t total = sg.mcu_count * im.nblk_mcu;
-    const uint32_t lane_first = rj_seg_lane0(coefs, g);  // lane of chunk c: lane_first + nch-1-c
+    // lane of chunk c under phase hypothesis h: lane_first + rj_chunk_lane(nch, hyp, c, h)
+    const uint32_t lane_first = rj_seg_lane0(coefs, g), H = coefs.hyp;
     const uint64_t rcap = rj_chunk_cap(rj_chunk_len(sg.src_len, nch));
-    const uint64_t ent0 = gp(coefs.seg_ent)[g];  // the call's chunk regions of this interval
+    const uint64_t ent0 = gp(coefs.seg_ent)[g];  // the call's chunk regions of this interval (one per lane)
     RjPiece *pieces = coefs.piece + lane_first;
-    uint32_t c = 0, vs_rb = 0, vs_ne = 0, T = 0, np = 0;
+    uint32_t c = 0, h = 0, vs_rb = 0, vs_ne = 0, T = 0, np = 0;
     int32_t D[3] = {0, 0, 0};
     while (true) {
-      const RjChunkRes r = gp(coefs.res)[lane_first + nch - 1 - c];
+      const uint32_t o = rj_chunk_lane(nch, H, c, h);
+      const RjChunkRes r = gp(coefs.res)[lane_first + o];
       if (r.status != RJ_CHUNK_SYNC && r.status != RJ_CHUNK_DONE) { ok = false; break; }
       if (r.rb < vs_rb) { ok = false; break; }
       uint32_t nb = r.rb - vs_rb;
@@ -750,15 +752,16 @@ __global__ __launch_bounds__(256) void k_resolve(const RjImageDev *__restrict__ 
         if (T + nb < total) { ok = false; break; }
       }
       if (T + nb > total) nb = total - T;
-      gp(pieces)[np] = RjPiece{ent0 + uint64_t(c) * rcap + vs_ne, T, nb, 0u, {D[0], D[1], D[2]}};
+      gp(pieces)[np] = RjPiece{ent0 + uint64_t(o) * rcap + vs_ne, T, nb, 0u, {D[0], D[1], D[2]}};
       np++;
       T += nb;
       if (r.status == RJ_CHUNK_DONE || T >= total) break;
-      const uint32_t t = c + r.tgt;
-      if (t >= nch || r.rec >= RJ_MAX_RECORDS) { ok = false; break; }
-      const RjRecord rec = gp(coefs.rec)[uint64_t(lane_first + nch - 1 - t) * RJ_MAX_RECORDS + r.rec];
+      const uint32_t t = c + (r.tgt & 0xFFFFu), th = r.tgt >> 16;
+      if (t >= nch || t <= c || th >= H || r.rec >= RJ_MAX_RECORDS || np >= nch) { ok = false; break; }
+      const RjRecord rec = gp(coefs.rec)[uint64_t(lane_first + rj_chunk_lane(nch, H, t, th)) * RJ_MAX_RECORDS + r.rec];
       for (int q = 0; q < 3; q++) D[q] = r.pred[q] + D[q] - rec.pred[q];
       c = t;
+      h = th;
       vs_rb = rec.rb;
       vs_ne = rec.ne;
     }

@@ -666,17 +666,21 @@ __device__ __forceinline__ void hc_put_record(RjRecord *r, uint32_t pos, uint32_
       if (SAFE) {                                                                                         \
         if (pos >= next_tgt_bit && tgt < next_chunks) { /* entered the next later chunk */              \
           tgt++;                                                                                          \
-          j = 0;                                                                                          \
+          _Pragma("unroll") for (int hh = 0; hh < NH; hh++) j[hh] = 0;                                     \
           next_tgt_bit += clen_bits;                                                                      \
         }                                                                                                 \
-        if (tgt && cache_tj == (tgt << 16 | j) && uint32_t(cache >> 36) == (epoch & 0x0FFFFFFFu)) {      \
-          const uint32_t cpos = uint32_t(cache);                                                          \
-          if (cpos == pos && uint32_t(cache >> 32 & 15u) == (b >> 1)) {                                   \
-            status = RJ_CHUNK_SYNC; /* identical state from here on: the later chunk owns the rest */     \
-            s_tgt = tgt;                                                                                  \
-            s_rec = j;                                                                                    \
-          } else if (cpos < pos) {                                                                        \
-            j++;                                                                                          \
+        /* against each phase hypothesis of that chunk (rj_chunk_lanes) */                                \
+        _Pragma("unroll") for (int hh = 0; hh < NH; hh++) {                                               \
+          if (uint32_t(hh) < H && status == 0 && tgt && cache_tj[hh] == (tgt << 16 | j[hh]) &&             \
+              uint32_t(cache[hh] >> 36) == (epoch & 0x0FFFFFFFu)) {                                       \
+            const uint32_t cpos = uint32_t(cache[hh]);                                                    \
+            if (cpos == pos && uint32_t(cache[hh] >> 32 & 15u) == (b >> 1)) {                             \
+              status = RJ_CHUNK_SYNC; /* identical state from here on: the later chunk owns the rest */   \
+              s_tgt = tgt | uint32_t(hh) << 16;                                                           \
+              s_rec = j[hh];                                                                              \
+            } else if (cpos < pos) {                                                                      \
+              j[hh]++;                                                                                    \
+            }                                                                                             \
           }                                                                                               \
         }                                                                                                 \
         if (status == 0 && pos >= nbits_abs) {                                                            \
@@ -692,7 +696,33 @@ __device__ __forceinline__ void hc_put_record(RjRecord *r, uint32_t pos, uint32_
     tsh = tshn;                                                                                           \
   } while (0)
 
-template <int kScope>
+// kHyp chain propagation inside a workgroup (k_huff_chunk): lane X is on its interval's true
+// chain; follow the links of the lanes it reaches, marking each on the chain and its chunk decided
+// (and the chunks a link jumps over passed by).  Lanes are workgroup-relative; i0 is the interval's
+// first lane.  A lane that syncs stores its link, then reads its own mark; the walk sets a mark,
+// then reads the link: with sequentially consistent LDS atomics one of the two sees the other, so
+// no link is lost (a lane may be walked twice, which only repeats idempotent stores).
+template <typename U32>
+__device__ __forceinline__ void hc_chain_walk(uint32_t X, uint32_t i0, uint32_t nch, uint32_t H, U32 *s_link, U32 *s_onc,
+                                              U32 *s_conf) {
+  for (uint32_t guard = 0; guard < 2u * RJ_K1_WG; guard++) {
+    const uint32_t T = __hip_atomic_load(&s_link[X], __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (T == 0xFFFFFFFFu) break;
+    const uint32_t oT = T - i0, oX = X - i0, c0 = (nch - 1) * H;
+    const uint32_t cT = nch - 1 - oT / H, hT = oT - (oT / H) * H;
+    const uint32_t cX = oX >= c0 ? 0u : nch - 1 - oX / H;
+    for (uint32_t cc = cX + 1; cc < cT; cc++)  // chunks the link jumps over: no hypothesis of theirs is needed
+      __hip_atomic_store(&s_conf[i0 + (nch - 1 - cc) * H], 0xFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&s_conf[T - hT], hT + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (__hip_atomic_fetch_or(&s_onc[T], 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP) != 0) break;
+    X = T;
+  }
+}
+
+// kHyp: the layout with MCU-phase hypotheses (RjCoefBuf.hyp > 1, small calls); the instance
+// without keeps one lane per chunk and none of the per-hypothesis state (its registers and
+// compares cost a restart-less 1024-image call 8 % of K1 when compiled in).
+template <int kScope, bool kHyp>
 __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0,
                                                       uint32_t nlanes, const uint8_t *__restrict__ destuffed,
                                                       const RjTableSet *__restrict__ tabsets,
@@ -707,6 +737,14 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
   __shared__ __attribute__((aligned(16))) uint32_t s_lut[RJ_HL_LUT_WORDS];
   __shared__ uint32_t s_dec[DEC];
   __shared__ uint32_t s_mov[DEC];
+  // kHyp, workgroup-scope layout (an interval's lanes in this workgroup): the chain of pieces as
+  // the lanes find it.  s_link[l]: the lane (in the workgroup) lane l synced into; s_onc[l]: lane l
+  // is on the interval's true chain (chunk 0's lane from the start, then every lane an on-chain
+  // lane synced into); s_conf[first lane of a chunk]: 0 unknown, h + 1 when hypothesis h of that
+  // chunk is on the chain, 0xFFFF when the chain passed the chunk by.  A speculative lane past its
+  // own end whose chunk is decided for another hypothesis stops: nothing will read its pieces,
+  // and a hypothesis that started out of phase may take a long time to fall into step.
+  __shared__ uint32_t s_link[kHyp ? DEC : 1], s_onc[kHyp ? DEC : 1], s_conf[kHyp ? DEC : 1];
   __shared__ uint32_t s_T, s_ne;
   const uint32_t tid = threadIdx.x;
   const bool mover = tid >= uint32_t(DEC);
@@ -714,7 +752,9 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
   if (tid == 0) s_ne = 0;
   const uint32_t g = lane0 + blockIdx.x * DEC + L;
   bool pending = g < lane0 + nlanes;
-  uint32_t gseg = 0, c = 0, nch = 1;
+  uint32_t gseg = 0, c = 0, h = 0, nch = 1, l_first = 0;
+  constexpr int NH = kHyp ? RJ_MAX_HYP : 1;  // hypothesis state slots
+  const uint32_t H = kHyp ? coefs.hyp : 1u;
   int i = 0;
   if (pending) {
     gseg = rj_lane_seg(coefs, g);
@@ -723,7 +763,14 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
   if (pending) {
     i = upper_index(nimg, gseg, [&](int qq) { return imgs[qq].seg_prefix; });
     nch = rj_nch(coefs, gp(imgs[i].segs)[gseg - imgs[i].seg_prefix].src_len);
-    c = nch - 1 - (g - rj_seg_lane0(coefs, gseg));  // reverse order: later chunks on earlier lanes
+    // reverse order, later chunks on earlier lanes; each chunk c > 0 under H phase hypotheses
+    // (rj_device.h rj_chunk_lane)
+    l_first = rj_seg_lane0(coefs, gseg);
+    const uint32_t o = g - l_first;
+    if (nch > 1 && o < (nch - 1) * H) {
+      c = nch - 1 - o / H;
+      h = o - (o / H) * H;
+    }
   }
   const RjImageDev &im = imgs[i];
   const uint32_t my_ts = im.tabset;
@@ -734,6 +781,11 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     if (!mover) {
       s_dec[L] = 0;
       s_mov[L] = 0;
+      if constexpr (kHyp) {
+        s_link[L] = 0xFFFFFFFFu;
+        s_onc[L] = c == 0 ? 1u : 0u;
+        s_conf[L] = 0u;
+      }
     }
     __syncthreads();
     const uint32_t T = s_T;
@@ -751,7 +803,8 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     const uint32_t nbytes = sg.dst_len;
     const uint32_t clen = chunk ? rj_chunk_len(nbytes, nch) : nbytes;
     const uint32_t b0 = chunk ? min(c * clen, nbytes) : 0u, b1 = chunk ? min(b0 + clen, nbytes) : nbytes;
-    const bool empty = chunk && c > 0 && b0 >= nbytes;  // no data left for this chunk (16-B rounding)
+    // no data left for this chunk (16-B rounding), or a phase hypothesis the image's MCU does not have
+    const bool empty = chunk && c > 0 && (b0 >= nbytes || h >= uint32_t(im.nblk_mcu));
     // a speculative lane starts `warm` bytes before its chunk, so that its decode has usually
     // resynchronised with the true one by the chunk start, where its records begin: the lane
     // before then meets a record right after it crosses, instead of running on through the
@@ -812,7 +865,7 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     const uint32_t blocks = sg.mcu_count * nblk;
     const uint64_t ent_abs = im.ent_off + sg.ent_off;
     const uint32_t rcap = chunk ? uint32_t(rj_chunk_cap(rj_chunk_len(sg.src_len, nch))) : 0u;
-    const uint64_t ent_lane = chunk ? gp(coefs.seg_ent)[gseg] + uint64_t(c) * rcap : ent_abs;
+    const uint64_t ent_lane = chunk ? gp(coefs.seg_ent)[gseg] + uint64_t(rj_chunk_lane(nch, H, c, h)) * rcap : ent_abs;
     uint32_t *ent = coefs.ent + ent_lane;
     const RjTableSet *tset = tabsets + T;
     const HCol<DEC> stage{&s_stage[0][L]};
@@ -822,16 +875,27 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     const uint32_t cap = rcap, next_chunks = chunk ? nch - 1 - c : 0u;
     const bool spec = chunk && c > 0;
     RjRecord *const rec_mine = coefs.rec + uint64_t(g) * RJ_MAX_RECORDS;
-    const RjRecord *const rec_next = rec_mine - RJ_MAX_RECORDS;  // chunk c + 1 sits on lane g - 1
-    uint32_t rb = 0, nrec = 0, tgt = 0, j = 0, status = 0, rb_over = 0xFFFFFFFFu, s_tgt = 0, s_rec = 0;
+    // the records of chunk t, hypothesis hh: lane l_first + rj_chunk_lane(nch, H, t, hh)
+    const RjRecord *const rec_int = coefs.rec + uint64_t(l_first) * RJ_MAX_RECORDS;
+    uint32_t rb = 0, nrec = 0, tgt = 0, status = 0, rb_over = 0xFFFFFFFFu, s_tgt = 0, s_rec = 0;
     uint32_t next_tgt_bit = end_bit;
     uint32_t rec_rb = 0;  // blocks before the next record may be taken (its first: at the chunk start)
-    uint64_t cache = 0;
-    uint32_t cache_tj = 0xFFFFFFFFu;
+    // per hypothesis of the chunk being sought: the record looked at next, and the one loaded
+    // at the phase start (key {pos, phase | epoch}, tagged with its (chunk, record))
+    uint32_t j[NH], cache_tj[NH];
+    uint64_t cache[NH];
+#pragma unroll
+    for (int hh = 0; hh < NH; hh++) {
+      j[hh] = 0;
+      cache_tj[hh] = 0xFFFFFFFFu;
+      cache[hh] = 0;
+    }
     bool rp = false;
     uint32_t rp_pos = 0, rp_b = 0, rp_ne = 0, rp_rb = 0;
     int rp_p0 = 0, rp_p1 = 0, rp_p2 = 0;
     int pred0 = 0, pred1 = 0, pred2 = 0;
+    bool linked = false;  // kHyp: this lane's sync was published (s_link)
+    const uint32_t wg_base = lane0 + blockIdx.x * DEC;
     if (empty) {
       RjChunkRes o = {};
       o.status = RJ_CHUNK_DONE;
@@ -841,8 +905,8 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
       lds_st(&s_dec[L], RJ_HL_FIN);
       continue;
     }
-    if (spec && warm == 0) {  // no warm-up: the chunk's first bit is a block start by assumption
-      hc_put_record<kScope>(rec_mine, start_bit, 0u, epoch, 0u, 0u, 0, 0, 0);
+    if (spec && warm == 0) {  // no warm-up: the chunk's first bit is a block start by assumption (block h)
+      hc_put_record<kScope>(rec_mine, start_bit, h, epoch, 0u, 0u, 0, 0, 0);
       nrec = 1;
       rec_rb = RJ_RECORD_EVERY;
     }
@@ -864,9 +928,9 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     uint32_t ne = 0, fl = 0;
     bool skip = !chunk && (sg.flags & RJ_SEG_MISSING) != 0;
     uint32_t blocks_left = chunk ? 0x7FFFFFFFu : blocks;
-    uint32_t b = 0, k = 0;
-    uint32_t acb = ((pat >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES);
-    uint32_t tb = RJ_HL_DC0 + ((pat & 1u) << (RJ_HL_DC_BITS + 2));
+    uint32_t b = 2u * h, k = 0;  // a speculative lane starts in its hypothesis' phase (block h of an MCU)
+    uint32_t acb = ((pat >> b >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES);
+    uint32_t tb = RJ_HL_DC0 + (((pat >> b) & 1u) << (RJ_HL_DC_BITS + 2));
     uint32_t tsh = 32 - RJ_HL_DC_BITS;
     uint32_t peek = __builtin_amdgcn_alignbit(wa, wb, q);
     uint32_t e = s_lut[(tb >> 2) + (peek >> tsh)];
@@ -883,15 +947,26 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
       const bool safe = __builtin_amdgcn_ballot_w64(
                             chunk ? pos0 + PHASE * 31u >= end_bit
                                   : !(blocks_left >= PHASE && !skip && (0u - q) + PHASE * 31u < nbits)) != 0;
-      uint64_t rec_ld = 0;
-      uint32_t rec_ld_tj = 0xFFFFFFFFu;
+      uint64_t rec_ld[NH];
+      uint32_t rec_ld_tj[NH];
+#pragma unroll
+      for (int hh = 0; hh < NH; hh++) {
+        rec_ld[hh] = 0;
+        rec_ld_tj[hh] = 0xFFFFFFFFu;
+      }
       const bool seek = chunk && pos0 + PHASE * 31u >= end_bit;
       if (__builtin_amdgcn_ballot_w64(seek) != 0) {
         const uint32_t t = tgt ? tgt : 1u;
-        const bool have = seek && t <= next_chunks && j < RJ_MAX_RECORDS;
-        const RjRecord *r = have ? rec_next - int64_t(t - 1) * RJ_MAX_RECORDS + j : rec_mine;
-        rec_ld = __hip_atomic_load(reinterpret_cast<const uint64_t *>(r), __ATOMIC_RELAXED, kScope);
-        rec_ld_tj = have ? (t << 16 | j) : 0xFFFFFFFFu;
+#pragma unroll
+        for (int hh = 0; hh < NH; hh++) {
+          if (uint32_t(hh) < H) {
+            const bool have = seek && t <= next_chunks && j[hh] < RJ_MAX_RECORDS;
+            const RjRecord *r = have ? rec_int + uint64_t(rj_chunk_lane(nch, H, c + t, uint32_t(hh))) * RJ_MAX_RECORDS + j[hh]
+                                     : rec_mine;
+            rec_ld[hh] = __hip_atomic_load(reinterpret_cast<const uint64_t *>(r), __ATOMIC_RELAXED, kScope);
+            rec_ld_tj[hh] = have ? (t << 16 | j[hh]) : 0xFFFFFFFFu;
+          }
+        }
       }
       if (!safe) {
 #pragma unroll
@@ -901,12 +976,31 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
         for (uint32_t s_ = 0; s_ < PHASE; s_++) RJ_HC_STEP(true);
       }
       lds_st(&s_dec[L], max(rr, 2u) - 2u);
+      if constexpr (kHyp && kScope == __HIP_MEMORY_SCOPE_WORKGROUP) {
+        if (chunk && status == RJ_CHUNK_SYNC && !linked) {  // synced this phase: link, and pass the chain on
+          linked = true;
+          const uint32_t tl = l_first + rj_chunk_lane(nch, H, c + (s_tgt & 0xFFFFu), s_tgt >> 16) - wg_base;
+          __hip_atomic_store(&s_link[L], tl, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (__hip_atomic_load(&s_onc[L], __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
+            hc_chain_walk(L, l_first - wg_base, nch, H, s_link, s_onc, s_conf);
+        }
+        if (chunk && c > 0 && status == 0 && start_bit + (0u - q) >= end_bit) {
+          const uint32_t cf = __hip_atomic_load(&s_conf[L - h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (cf != 0u && cf != h + 1u) {  // another hypothesis of this chunk is on the chain
+            status = RJ_CHUNK_FAIL;
+            blocks_left = 0;
+          }
+        }
+      }
       if (ne - fl >= GROUP) {
         hl_flush<DEC, GROUP>(stage, fl, ent + fl);
         fl += GROUP;
       }
-      cache = rec_ld;
-      cache_tj = rec_ld_tj;
+#pragma unroll
+      for (int hh = 0; hh < NH; hh++) {
+        cache[hh] = rec_ld[hh];
+        cache_tj[hh] = rec_ld_tj[hh];
+      }
       if (__builtin_amdgcn_ballot_w64(avail < rr + PHASE + 1u) != 0) {
         RJ_HC_WAIT_RING(rr + PHASE + 1u);
         wc = ring[rr & (RJ_HL_WORDS - 1)];
@@ -923,7 +1017,7 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     if (chunk) {
       RjChunkRes o;
       o.status = status;
-      o.tgt = s_tgt;
+      o.tgt = s_tgt;  // chunks ahead | hypothesis << 16
       o.rec = s_rec;
       o.rb = rb;
       o.ne = ne;
@@ -946,13 +1040,25 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
 hipError_t LaunchHuffChunks(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t lanes_wg,
                             uint32_t lanes_dev, const uint8_t *destuffed, const RjTableSet *tabsets,
                             const RjLeanTables *lean, RjCoefBuf coefs, uint32_t epoch) {
-  if (lanes_wg)
-    hipLaunchKernelGGL((k_huff_chunk<__HIP_MEMORY_SCOPE_WORKGROUP>), dim3((lanes_wg + RJ_K1_WG - 1) / RJ_K1_WG),
-                       dim3(2 * RJ_K1_WG), 0, st, imgs, nimg, lane0, lanes_wg, destuffed, tabsets, lean, coefs, epoch);
-  if (lanes_dev)
-    hipLaunchKernelGGL((k_huff_chunk<__HIP_MEMORY_SCOPE_AGENT>), dim3((lanes_dev + RJ_K1_WG - 1) / RJ_K1_WG),
-                       dim3(2 * RJ_K1_WG), 0, st, imgs, nimg, lane0 + lanes_wg, lanes_dev, destuffed, tabsets, lean,
-                       coefs, epoch);
+  const bool hyp = coefs.hyp > 1;
+  if (lanes_wg) {
+    const dim3 grid((lanes_wg + RJ_K1_WG - 1) / RJ_K1_WG), block(2 * RJ_K1_WG);
+    if (hyp)
+      hipLaunchKernelGGL((k_huff_chunk<__HIP_MEMORY_SCOPE_WORKGROUP, true>), grid, block, 0, st, imgs, nimg, lane0,
+                         lanes_wg, destuffed, tabsets, lean, coefs, epoch);
+    else
+      hipLaunchKernelGGL((k_huff_chunk<__HIP_MEMORY_SCOPE_WORKGROUP, false>), grid, block, 0, st, imgs, nimg, lane0,
+                         lanes_wg, destuffed, tabsets, lean, coefs, epoch);
+  }
+  if (lanes_dev) {
+    const dim3 grid((lanes_dev + RJ_K1_WG - 1) / RJ_K1_WG), block(2 * RJ_K1_WG);
+    if (hyp)
+      hipLaunchKernelGGL((k_huff_chunk<__HIP_MEMORY_SCOPE_AGENT, true>), grid, block, 0, st, imgs, nimg,
+                         lane0 + lanes_wg, lanes_dev, destuffed, tabsets, lean, coefs, epoch);
+    else
+      hipLaunchKernelGGL((k_huff_chunk<__HIP_MEMORY_SCOPE_AGENT, false>), grid, block, 0, st, imgs, nimg,
+                         lane0 + lanes_wg, lanes_dev, destuffed, tabsets, lean, coefs, epoch);
+  }
   return hipGetLastError();
 }
 

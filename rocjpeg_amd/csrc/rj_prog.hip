@@ -203,6 +203,26 @@ template <bool kRefine>
 __device__ __forceinline__ void lane_dc(const PLaneIn &L, PGeo &g, PBits &br, const HRow &lut, const VRow &vals, uint16_t *coef16,
                         unsigned long long *rec) {
   const RjProgScanDev &sc = L.sc;
+  if constexpr (kRefine) {
+    // DC refinement has no Huffman codes: block i of the interval (decode order) takes stream bit
+    // i, and libjpeg reads zeros past the data.  The record words are therefore the stream's bits
+    // in order -- word w = bit-reversed big-endian bytes [8w, 8w + 8) -- cut at min(data bits,
+    // blocks): a copy, not a walk (the block-by-block loop below took ~30 ms per 1080p image).
+    if (!L.active) return;
+    uint32_t per = 0;
+    for (uint32_t q = 0; q < g.ns && q < 3; q++) per += g.hs[q] * g.vs[q];
+    const uint32_t lim = min(g.nunits * per, L.iv.dst_len * 8u);
+    const uint2 *src = reinterpret_cast<const uint2 *>(br.src);  // the interval start is 16-B aligned
+    for (uint32_t w = 0; w * 64u < lim; w++) {
+      const uint2 v = gp(src)[w];  // the destuffed interval has >= 16 zero bytes of slack after its data
+      const uint64_t x = (uint64_t(__builtin_bswap32(v.x)) << 32) | __builtin_bswap32(v.y);
+      uint64_t bits = __builtin_bitreverse64(x);
+      const uint32_t left = lim - w * 64u;
+      if (left < 64u) bits &= (1ull << left) - 1ull;
+      *gp(rec + w) = bits;
+    }
+    return;
+  }
   const RjHuffDev *gt0 = nullptr, *gt1 = nullptr;
   if (!kRefine && L.active) {
     gt0 = L.im->ptabs + sc.tab[0];

@@ -82,7 +82,7 @@ def test_one_row_image_is_split_at_the_floor(dec, fmt):
     data = O.fixture_bytes(RI_1080)
     st, tm, bufs, shapes = _decode_batch(dec, [data], fmt)
     assert st == 0
-    assert tm["chunk_bytes"] == 384 and tm["lean_k1"] == 0 and tm["chunk_k1"] == 1
+    assert tm["chunk_bytes"] == 384 and tm["lean_k1"] == 0 and tm["chunk_k1"] == 1 and tm["chunk_hyp"] == 6
     assert tm["split_intervals"] > 0 and tm["chunks"] > tm["intervals"]
     _check([data], bufs, shapes, fmt)
 
@@ -111,3 +111,46 @@ def test_floor_above_every_interval_keeps_the_lean_k1(dec, lean_dec):
         for x, y in zip(G.to_host(a), G.to_host(b)):
             assert np.array_equal(x, y)
     _check([data, data], bufs_c, shapes)
+
+
+@pytest.fixture(scope="module")
+def hyp_decs():
+    out = {}
+    for h in (1, 2):
+        out[h] = _handle({"RJ_K1_HYP": str(h)})
+        out[h].set_profiling(True)
+    yield out
+    for d in out.values():
+        d.close()
+
+
+def test_phase_hypotheses_match_the_oracle(dec, hyp_decs):
+    """Small calls decode every speculative chunk under several MCU-phase hypotheses
+    (rj_device.h rj_chunk_lanes): up to the call's largest MCU's 6 blocks (4:2:0), as many as
+    fit one round of lanes; a 2-hypothesis handle leaves the phases 2..5 void, and 1 is the
+    round-4 layout.  4:2:0, 4:2:2 and gray images with intervals of several chunks, in one call (the
+    gray image's MCU has one block: its extra hypothesis lanes stay empty), must equal the oracle
+    under each, with the same bytes."""
+    by = {f["name"]: f for f in O.manifest()}
+    datas = [O.fixture_bytes(by[n]) for n in ("mug_420", "mug_422", "mug_400")] + [O.fixture_bytes(RI_1080)]
+    st, tm, bufs, shapes = _decode_batch(dec, datas)
+    # (three 4K restart-less images cut at the 384-B floor: as many hypotheses as fit one round)
+    assert st == 0 and tm["chunk_k1"] == 1 and 2 <= tm["chunk_hyp"] <= 6, tm
+    _check(datas, bufs, shapes)
+    for h, d in hyp_decs.items():
+        st, tm_h, bufs_h, _ = _decode_batch(d, datas)
+        assert st == 0 and tm_h["chunk_hyp"] == h, (h, tm_h["chunk_hyp"])
+        for a, b in zip(bufs, bufs_h):
+            for x, y in zip(G.to_host(a), G.to_host(b)):
+                assert np.array_equal(x, y), h
+
+
+def test_phase_hypotheses_on_damaged_rows(dec):
+    """Truncated and bit-flipped variants under 6 hypotheses: a speculative lane of any phase
+    that meets damaged data must still hand the interval to the resolution or the serial
+    fallback exactly as the single-hypothesis layout does (the oracle decides)."""
+    data = O.fixture_bytes(RI_1080)
+    datas = [data] + list(_variants(data).values())
+    st, tm, bufs, shapes = _decode_batch(dec, datas)
+    assert st == 0 and tm["chunk_hyp"] == 6
+    _check(datas, bufs, shapes)
