@@ -164,6 +164,7 @@ int Decoder::Initialize() {
   if (const char *cm = getenv("RJ_CHUNK_MIN")) chunk_min_ = uint32_t(std::max(16, atoi(cm)));
   if (const char *hy = getenv("RJ_K1_HYP")) hyp_max_ = uint32_t(std::max(1, atoi(hy)));
   if (const char *hw = getenv("RJ_K1_HYP_WARM")) hyp_warm_ = atoi(hw) != 0;
+  if (const char *hc = getenv("RJ_K1_HYP_CHUNK_MIN")) hyp_chunk_min_ = uint32_t(std::max(16, atoi(hc))) & ~15u;
   if (const char *sf = getenv("RJ_SPLIT_OUTLIER_FRAC")) outlier_frac_ = atof(sf);
   if (const char *st = getenv("RJ_SPLIT_OUTLIER_T")) outlier_t_ = std::max(0.5, std::min(1.0, atof(st)));
   cu_count_ = std::max(1, prop.multiProcessorCount);
@@ -1059,25 +1060,27 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       cb_fill = cb_fill * wgs / uint64_t(cu_count_) + 16;
     }
   }
-  const uint32_t chunk_bytes = uint32_t(std::min<uint64_t>(1u << 30, cb_fill));
-  timings_.chunk_bytes = chunk_bytes;
+  uint32_t chunk_bytes = uint32_t(std::min<uint64_t>(1u << 30, cb_fill));
   // ---- K1 lane layout (rj_device.h RjCoefBuf): one lane per chunk; an interval of at most
   // RJ_K1_WG chunks never straddles a workgroup (padding lanes), longer ones go after them.
   // Common case -- no interval split -- is the identity (lane = interval), nothing uploaded. ----
-  const bool any_split = rj_chunks_cb(src_max, chunk_bytes) > 1;
-  // MCU-phase hypotheses per speculative chunk (rj_device.h rj_chunk_lanes): as many as the
-  // call's largest MCU has blocks (at most RJ_MAX_HYP), when the chunk lanes times that still fit
-  // one round of the chip's decoder lanes with the workgroup padding; 1 otherwise, and always on
-  // the round-3 chunk path (k_entropy, RJ_K1_CHUNK=0)
+  // MCU-phase hypotheses per speculative chunk (rj_device.h rj_chunk_lanes) and the chunk length
+  // they go with: the most hypotheses (up to the call's largest MCU's block count, RJ_MAX_HYP)
+  // for which some chunk length from hyp_chunk_min_ (192 B) up to the call's length above fits
+  // one round of the chip's decoder lanes with the workgroup padding, at the shortest such
+  // length; 1 otherwise (the length above), and always on the round-3 chunk path (k_entropy,
+  // RJ_K1_CHUNK=0).  Measured (profiles/r5_experiments/k1_hyp_chunk_floor_sweep.txt): with six
+  // hypotheses one image is fastest at 192 B (the lane's chain is its warm-up, its chunk and a
+  // short overlap), sixteen at 384 B (shorter chunks would cost hypotheses)
   uint32_t hyp = 1;
-  if (any_split && k1_chunk_ && hyp_max_ > 1) {
+  if (rj_chunks_cb(src_max, chunk_bytes) > 1 && k1_chunk_ && hyp_max_ > 1) {
     uint32_t nblk_max = 1;
     for (int i = 0; i < n; i++) nblk_max = std::max(nblk_max, uint32_t(streams[i]->plan().nblk_mcu));
-    for (uint32_t H = std::min<uint32_t>({uint32_t(RJ_MAX_HYP), nblk_max, hyp_max_}); H > 1; H--) {
+    auto fits = [&](uint32_t cb, uint32_t H) {
       uint64_t lanes = 0, dev = 0;
       for (int i = 0; i < n; i++)
         for (const RjSegDev &sg : streams[i]->plan().segs) {
-          const uint32_t nl = rj_chunk_lanes(rj_chunks_cb(sg.src_len, chunk_bytes), H);
+          const uint32_t nl = rj_chunk_lanes(rj_chunks_cb(sg.src_len, cb), H);
           if (nl > RJ_K1_WG) {
             dev += nl;
           } else {
@@ -1085,13 +1088,24 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
             lanes += nl;
           }
         }
-      const uint64_t wgs = (lanes + RJ_K1_WG - 1) / RJ_K1_WG + (dev + RJ_K1_WG - 1) / RJ_K1_WG;
-      if (wgs <= uint64_t(cu_count_)) {
+      return (lanes + RJ_K1_WG - 1) / RJ_K1_WG + (dev + RJ_K1_WG - 1) / RJ_K1_WG <= uint64_t(cu_count_);
+    };
+    // lanes only grow with H and shrink with the chunk length: a call that fills the chip with one
+    // hypothesis at its own length (every large call) is rejected by the first test
+    if (fits(chunk_bytes, 2))
+      for (uint32_t H = std::min<uint32_t>({uint32_t(RJ_MAX_HYP), nblk_max, hyp_max_}); H > 1; H--) {
+        if (!fits(chunk_bytes, H)) continue;
         hyp = H;
+        for (uint32_t cb = std::min(hyp_chunk_min_, chunk_bytes); cb < chunk_bytes; cb += 64)
+          if (fits(cb, H)) {
+            chunk_bytes = cb;
+            break;
+          }
         break;
       }
-    }
   }
+  timings_.chunk_bytes = chunk_bytes;
+  const bool any_split = rj_chunks_cb(src_max, chunk_bytes) > 1;
   timings_.chunk_hyp = hyp;
   std::vector<uint32_t> &seg_lane0 = sc_.seg_lane0, &lane_seg = sc_.lane_seg;
   seg_lane0.clear();

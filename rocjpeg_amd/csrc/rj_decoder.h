@@ -194,6 +194,7 @@ class Decoder {
   HostPool pool_{HostThreads()};
   uint32_t hyp_max_ = RJ_MAX_HYP;  // env RJ_K1_HYP: most MCU-phase hypotheses per speculative chunk (1: off)
   bool hyp_warm_ = true;           // env RJ_K1_HYP_WARM=0: no speculative warm-up under hypotheses
+  uint32_t hyp_chunk_min_ = 192;   // env RJ_K1_HYP_CHUNK_MIN: shortest chunk under phase hypotheses
   static int HostThreads();
 };
 

@@ -77,12 +77,14 @@ def _check(datas, bufs_all, shapes_all, fmt=R.OutputFormat.RGB):
 @pytest.mark.parametrize("fmt", [R.OutputFormat.RGB, R.OutputFormat.YUV_PLANAR], ids=["RGB", "YUV_PLANAR"])
 def test_one_row_image_is_split_at_the_floor(dec, fmt):
     """One 1080p image with one MCU row per interval (68 intervals of ~4 KB): the call cuts
-    every interval into chunks of the floor (384 B, rj_device.h RJ_CHUNK_MIN_BYTES) and decodes it
-    like the oracle."""
+    every interval into chunks, decodes each speculative chunk under its MCU's 6 phase
+    hypotheses, which fit the chip down to the 192-B hypothesis floor (rj_decoder.cpp; without
+    hypotheses the floor is 384 B, rj_device.h RJ_CHUNK_MIN_BYTES), and decodes it like the
+    oracle."""
     data = O.fixture_bytes(RI_1080)
     st, tm, bufs, shapes = _decode_batch(dec, [data], fmt)
     assert st == 0
-    assert tm["chunk_bytes"] == 384 and tm["lean_k1"] == 0 and tm["chunk_k1"] == 1 and tm["chunk_hyp"] == 6
+    assert tm["chunk_bytes"] == 192 and tm["lean_k1"] == 0 and tm["chunk_k1"] == 1 and tm["chunk_hyp"] == 6
     assert tm["split_intervals"] > 0 and tm["chunks"] > tm["intervals"]
     _check([data], bufs, shapes, fmt)
 
@@ -122,6 +124,14 @@ def hyp_decs():
     yield out
     for d in out.values():
         d.close()
+
+
+def test_without_hypotheses_the_floor_is_384(hyp_decs):
+    """RJ_K1_HYP=1: the same image at the handle's floor, one lane per chunk."""
+    data = O.fixture_bytes(RI_1080)
+    st, tm, bufs, shapes = _decode_batch(hyp_decs[1], [data])
+    assert st == 0 and tm["chunk_bytes"] == 384 and tm["chunk_hyp"] == 1
+    _check([data], bufs, shapes)
 
 
 def test_phase_hypotheses_match_the_oracle(dec, hyp_decs):
