@@ -1092,15 +1092,16 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     };
     // lanes only grow with H and shrink with the chunk length: a call that fills the chip with one
     // hypothesis at its own length (every large call) is rejected by the first test
-    if (fits(chunk_bytes, 2))
+    // (chunks longer than the length above, for more hypotheses, measured slower from 16 images up:
+    // profiles/r5_experiments/k1_hyp_longer_chunks.txt)
+    const uint32_t cb_hi = chunk_bytes;
+    if (fits(cb_hi, 2))
       for (uint32_t H = std::min<uint32_t>({uint32_t(RJ_MAX_HYP), nblk_max, hyp_max_}); H > 1; H--) {
-        if (!fits(chunk_bytes, H)) continue;
+        if (!fits(cb_hi, H)) continue;
         hyp = H;
-        for (uint32_t cb = std::min(hyp_chunk_min_, chunk_bytes); cb < chunk_bytes; cb += 64)
-          if (fits(cb, H)) {
-            chunk_bytes = cb;
-            break;
-          }
+        uint32_t cb = std::min(hyp_chunk_min_, chunk_bytes);
+        while (cb < cb_hi && !fits(cb, H)) cb += 64;
+        chunk_bytes = std::min(cb, cb_hi);
         break;
       }
   }

@@ -573,6 +573,9 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
     if (threadIdx.x == 0) __hip_atomic_store(progress + gi, units_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   const RjProgScanDev &sc = *gp(im.pscans + iv.scan);
+#ifdef RJ_PROG_PRIO  // A/B probe: the luma AC refinements (the longest chains) issue first on their SIMD
+  if (rfl(uint32_t(sc.kind)) == RJ_PK_AC_REFINE && (rfl(uint32_t(sc.comp[0])) & 3u) == 0) __builtin_amdgcn_s_setprio(RJ_PROG_PRIO);
+#endif
   const uint32_t ss = rfl(sc.ss), se = rfl(sc.se);
   const uint64_t band = (se >= 63 ? ~0ull : ((1ull << (se + 1)) - 1)) & ~((1ull << ss) - 1);
   const uint32_t nunits = rfl(iv.nunits), dst_len = rfl(iv.dst_len);

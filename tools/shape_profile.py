@@ -18,11 +18,12 @@ def main():
     t = G.torch()
     bench._init_gen()
     gen = bench.WORKLOADS["c2nori" if nori else "c2"]["gen"]
-    datas = [bench._make_jpeg((s, gen)) for s in range(1234, 1234 + 128)]
+    shapes = [int(x) for x in os.environ.get("SHAPES", "1,4,8,16,128").split(",")]
+    datas = [bench._make_jpeg((s, gen)) for s in range(1234, 1234 + max(shapes))]
     for m in mins:
         os.environ["RJ_CHUNK_MIN"] = m
         dec = R.JpegDecoder(R.Backend.HARDWARE, 0)
-        for bs in [int(x) for x in os.environ.get("SHAPES", "1,4,8,16,128").split(",")]:
+        for bs in shapes:
             streams = [R.JpegStream(d) for d in datas[:bs]]
             dec.streams_to_device(streams)
             outs = [t.empty((1080, 5760), dtype=t.uint8, device="cuda") for _ in range(bs)]
