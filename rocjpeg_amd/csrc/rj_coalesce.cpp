@@ -118,7 +118,7 @@ void RunGroup(Decoder *dec, std::vector<Request *> &group) {
 int CoalescedDecode(Decoder *dec, int device, Stream *const *streams, int n, const RocJpegDecodeParams *params,
                     RocJpegImage *dst) {
   if (!Enabled() || n > kSmallCall || n <= 0 || device < 0 || streams == nullptr || params == nullptr ||
-      dst == nullptr)
+      dst == nullptr || !dec->Coalescable())
     return dec->Decode(streams, n, params, dst);
   g_calls.fetch_add(1, std::memory_order_relaxed);
   DeviceQueue &q = QueueFor(device);

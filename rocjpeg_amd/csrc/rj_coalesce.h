@@ -18,7 +18,8 @@
 // waits.  If a combined call fails, its member calls are decoded one by one, so every caller gets
 // the status of its own images.  RJ_COALESCE=0 turns it off (each call on its own handle);
 // RJ_COALESCE_INFLIGHT=k lets k combined calls decode at once, each gathering 1/k of the recent
-// callers (default 1).
+// callers (default 1).  Calls on a handle with profiling on or a forced output path are never
+// combined (Decoder::Coalescable: their timings and path belong to that handle).
 #pragma once
 #include <stdint.h>
 

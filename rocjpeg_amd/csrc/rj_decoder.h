@@ -64,6 +64,9 @@ class Decoder {
   const double *last_scan_ms() const { return scan_ms_; }
   hipStream_t stream() const { return stream_; }
   int device() const { return device_; }
+  // a call on this handle may be decoded inside another handle's combined call (rj_coalesce.h):
+  // not while the caller profiles (its timings are per handle) or forces the general output path
+  bool Coalescable() const { return !profiling_ && path_policy_ == 0; }
 
  private:
   int DecodeLocked(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);

@@ -21,6 +21,7 @@ class Decoder {
  public:
   std::atomic<int> active{0};
   std::atomic<long> images{0};
+  bool Coalescable() const { return true; }
   int Decode(Stream *const *s, int n, const RocJpegDecodeParams *p, RocJpegImage *d) {
     if (active.fetch_add(1) != 0) {
       std::fprintf(stderr, "handle used by two threads at once\n");
