@@ -573,9 +573,29 @@ __global__ __launch_bounds__(64) void k_prog_wave(const RjImageDev *__restrict__
     if (threadIdx.x == 0) __hip_atomic_store(progress + gi, units_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   const RjProgScanDev &sc = *gp(im.pscans + iv.scan);
-#ifdef RJ_PROG_PRIO  // A/B probe: the luma AC refinements (the longest chains) issue first on their SIMD
-  if (rfl(uint32_t(sc.kind)) == RJ_PK_AC_REFINE && (rfl(uint32_t(sc.comp[0])) & 3u) == 0) __builtin_amdgcn_s_setprio(RJ_PROG_PRIO);
+  // The luma AC refinements are the grid's longest chains (one image's final one alone ~43 ms):
+  // they issue first on a SIMD they share with other scans' waves (s_setprio; C5 +2.6-3.4 %
+  // same-box, profiles/r5_experiments/c5_prio_ab.txt).  RJ_PROG_PRIO_MODE (A/B builds): 0 none,
+  // 1 luma refinements, 2 every refinement, 3 graded (luma refinements 3, chroma refinements 2,
+  // luma first scans 1), 4 luma refinements 3 and luma first scans 2, 5 every luma scan 3
+#ifndef RJ_PROG_PRIO_MODE
+#define RJ_PROG_PRIO_MODE 1
 #endif
+  {
+    const uint32_t kind = rfl(uint32_t(sc.kind)), luma = (rfl(uint32_t(sc.comp[0])) & 3u) == 0;
+    if (RJ_PROG_PRIO_MODE == 1 && kind == RJ_PK_AC_REFINE && luma) __builtin_amdgcn_s_setprio(3);
+    if (RJ_PROG_PRIO_MODE == 2 && kind == RJ_PK_AC_REFINE) __builtin_amdgcn_s_setprio(3);
+    if (RJ_PROG_PRIO_MODE == 3) {
+      if (kind == RJ_PK_AC_REFINE && luma) __builtin_amdgcn_s_setprio(3);
+      else if (kind == RJ_PK_AC_REFINE) __builtin_amdgcn_s_setprio(2);
+      else if (luma) __builtin_amdgcn_s_setprio(1);
+    }
+    if (RJ_PROG_PRIO_MODE == 4 && luma) {
+      if (kind == RJ_PK_AC_REFINE) __builtin_amdgcn_s_setprio(3);
+      else __builtin_amdgcn_s_setprio(2);
+    }
+    if (RJ_PROG_PRIO_MODE == 5 && luma) __builtin_amdgcn_s_setprio(3);
+  }
   const uint32_t ss = rfl(sc.ss), se = rfl(sc.se);
   const uint64_t band = (se >= 63 ? ~0ull : ((1ull << (se + 1)) - 1)) & ~((1ull << ss) - 1);
   const uint32_t nunits = rfl(iv.nunits), dst_len = rfl(iv.dst_len);
