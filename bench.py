@@ -470,7 +470,7 @@ def call_shapes(dec, datas, fmt, dev, threads=8):
                 "per_thread_images_per_s": [round(r, 1) for r in rates],
                 "spread_max_over_min": round(max(rates) / min(rates), 3) if min(rates) > 0 else None}
 
-    def perf_sample(passes=4, count=256):
+    def perf_sample(passes=12, count=256):
         """The same shape from C, without the Python interpreter lock between the threads: the
         restated jpegdecodeperf (tests/c/rj_samples.cpp, linked -lrocjpeg) over `count` of the
         images written to a directory, -t threads -b 1 -fmt rgb, `passes` passes per thread."""
