@@ -466,9 +466,6 @@ __global__ __launch_bounds__(RJ_PW) __attribute__((amdgpu_waves_per_eu(1, 1))) v
   const VRow vals{s_vals + lane};
   switch (kind) {
     case RJ_PK_DC_FIRST:
-#ifdef RJ_PROG_DC_PRIO  // A/B probe: the DC-first lanes (one image's whole DC scan per lane) at top priority
-      __builtin_amdgcn_s_setprio(3);
-#endif
       lane_dc<false>(L, g, br, lut, vals, coef16, rec);
       break;
     case RJ_PK_DC_REFINE:
