@@ -1939,7 +1939,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (Dbg(kDebugStamps)) DumpRowStamps();
 #endif
 #ifdef RJ_HL_STAMPS
-  if (Dbg(kDebugStamps) && lean) DumpHuffStamps();
+  if (Dbg(kDebugStamps)) DumpHuffStamps();
 #endif
 
   if (nsplit && n == 1 && Dbg(kDebugK1Pieces)) {  // development: every interval's pieces (split launch)

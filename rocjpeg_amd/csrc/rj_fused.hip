@@ -90,13 +90,8 @@ struct EntWin {
     base_lo = U(uint32_t(at));
     base_hi = U(uint32_t(at >> 32));
     const uint32_t *p = ent + at;
-#ifdef RJ_K2_NT_WIN  // A/B probe: the window read as streaming (non-temporal) loads
-#pragma unroll
-    for (int r = 0; r < RJ_WIN_ROWS; r++) w[r] = __builtin_nontemporal_load(gp(p) + r * 64u + lane);
-#else
 #pragma unroll
     for (int r = 0; r < RJ_WIN_ROWS; r++) w[r] = gp(p)[r * 64u + lane];
-#endif
   }
   // wait here for the window's loads.  vmcnt is in order on gfx9: a wait for a window row issued
   // after the previous strip's pixel stores waits for those stores too.  parse_blocks' walk over a

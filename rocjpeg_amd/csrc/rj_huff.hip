@@ -52,6 +52,9 @@ __device__ const uint4 rj_hl_zero[2] = {};
 
 #ifdef RJ_HL_STAMPS  // diagnostic build: cycles in the symbol steps / the phase ends, summed over waves
 __device__ unsigned long long rj_hl_stamp[8];
+// k_huff_chunk: per decoder wave, summed: setup cycles (entry to the first phase), loop cycles,
+// phases, safe phases, waves; max loop cycles; ring-wait cycles
+__device__ unsigned long long rj_hc_stamp[8];
 #define RJ_HL_COUNT_ESC st_esc++
 #else
 #define RJ_HL_COUNT_ESC
@@ -748,6 +751,10 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
   __shared__ uint32_t s_T, s_ne;
   const uint32_t tid = threadIdx.x;
   const bool mover = tid >= uint32_t(DEC);
+#ifdef RJ_HL_STAMPS
+  const uint64_t hc_t_entry = __builtin_amdgcn_s_memtime();
+  uint64_t hc_loop = 0, hc_ph = 0, hc_safe = 0, hc_wait = 0, hc_setup = 0;
+#endif
   const uint32_t L = mover ? tid - DEC : tid;
   if (tid == 0) s_ne = 0;
   const uint32_t g = lane0 + blockIdx.x * DEC + L;
@@ -922,6 +929,10 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
   }
     uint32_t avail = 0;
     RJ_HC_WAIT_RING(uint32_t(PHASE) + 2u);
+#ifdef RJ_HL_STAMPS
+    const uint64_t hc_t_loop = __builtin_amdgcn_s_memtime();
+    hc_setup += hc_t_loop - hc_t_entry;
+#endif
     uint32_t q = 0;
     uint32_t wa = 0, wb = ring[0], wc = ring[1];
     uint32_t rr = 1;
@@ -975,6 +986,10 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
 #pragma unroll
         for (uint32_t s_ = 0; s_ < PHASE; s_++) RJ_HC_STEP(true);
       }
+#ifdef RJ_HL_STAMPS
+      hc_ph++;
+      hc_safe += safe ? 1u : 0u;
+#endif
       lds_st(&s_dec[L], max(rr, 2u) - 2u);
       if constexpr (kHyp && kScope == __HIP_MEMORY_SCOPE_WORKGROUP) {
         if (chunk && status == RJ_CHUNK_SYNC && !linked) {  // synced this phase: link, and pass the chain on
@@ -1002,10 +1017,19 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
         cache_tj[hh] = rec_ld_tj[hh];
       }
       if (__builtin_amdgcn_ballot_w64(avail < rr + PHASE + 1u) != 0) {
+#ifdef RJ_HL_STAMPS
+        const uint64_t hw0 = __builtin_amdgcn_s_memtime();
+#endif
         RJ_HC_WAIT_RING(rr + PHASE + 1u);
         wc = ring[rr & (RJ_HL_WORDS - 1)];
+#ifdef RJ_HL_STAMPS
+        hc_wait += __builtin_amdgcn_s_memtime() - hw0;
+#endif
       }
     }
+#ifdef RJ_HL_STAMPS
+    hc_loop += __builtin_amdgcn_s_memtime() - hc_t_loop;
+#endif
 #undef RJ_HC_WAIT_RING
     lds_st(&s_dec[L], RJ_HL_FIN);
     if (rp) hc_put_record<kScope>(rec_mine + nrec, rp_pos, rp_b, epoch, rp_ne, rp_rb, rp_p0, rp_p1, rp_p2);
@@ -1035,6 +1059,18 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     if (coefs.count) atomicAdd(&s_ne, ne + 1);
   }
   if (tid == 0 && coefs.count != nullptr && s_ne != 0) atomicAdd(coefs.count, (unsigned long long)s_ne);
+#ifdef RJ_HL_STAMPS
+  if (!mover && (tid & 63) == 0 && hc_ph) {
+    atomicAdd(&rj_hc_stamp[0], (unsigned long long)hc_setup);
+    atomicAdd(&rj_hc_stamp[1], (unsigned long long)hc_loop);
+    atomicAdd(&rj_hc_stamp[2], (unsigned long long)hc_ph);
+    atomicAdd(&rj_hc_stamp[3], (unsigned long long)hc_safe);
+    atomicAdd(&rj_hc_stamp[4], 1ull);
+    atomicMax(&rj_hc_stamp[5], (unsigned long long)hc_loop);
+    atomicAdd(&rj_hc_stamp[6], (unsigned long long)hc_wait);
+    atomicMax(&rj_hc_stamp[7], (unsigned long long)(__builtin_amdgcn_s_memtime() - hc_t_entry));
+  }
+#endif
 }
 
 hipError_t LaunchHuffChunks(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t lanes_wg,
@@ -1072,6 +1108,15 @@ void DumpHuffStamps() {
           h[4], ph / w, h[3] / w, h[5] / w, h[0] / ph, h[1] / ph);
   unsigned long long z[8] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(rj_hl_stamp), z, sizeof(z));
+  unsigned long long c[8];
+  (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(rj_hc_stamp), sizeof(c));
+  if (c[4]) {
+    const double wv = double(c[4]), pp = c[2] ? double(c[2]) : 1.0;
+    fprintf(stderr, "[rj k_huff_chunk] decoder waves %llu: per wave setup %.0f cycles, loop %.0f (max %llu, wave max %llu from entry), "
+            "%.0f phases (%.0f safe), %.0f cycles per phase, ring waits %.0f per wave\n",
+            c[4], c[0] / wv, c[1] / wv, c[5], c[7], c[2] / wv, c[3] / wv, c[1] / pp, c[6] / wv);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(rj_hc_stamp), z, sizeof(z));
+  }
 }
 #endif
 
