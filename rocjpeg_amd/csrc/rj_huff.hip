@@ -54,7 +54,7 @@ __device__ const uint4 rj_hl_zero[2] = {};
 __device__ unsigned long long rj_hl_stamp[8];
 // k_huff_chunk: per decoder wave, summed: setup cycles (entry to the first phase), loop cycles,
 // phases, safe phases, waves; max loop cycles; ring-wait cycles
-__device__ unsigned long long rj_hc_stamp[8];
+__device__ unsigned long long rj_hc_stamp[10];
 #define RJ_HL_COUNT_ESC st_esc++
 #else
 #define RJ_HL_COUNT_ESC
@@ -672,17 +672,20 @@ __device__ __forceinline__ void hc_put_record(RjRecord *r, uint32_t pos, uint32_
           _Pragma("unroll") for (int hh = 0; hh < NH; hh++) j[hh] = 0;                                     \
           next_tgt_bit += clen_bits;                                                                      \
         }                                                                                                 \
-        /* against each phase hypothesis of that chunk (rj_chunk_lanes) */                                \
-        _Pragma("unroll") for (int hh = 0; hh < NH; hh++) {                                               \
-          if (uint32_t(hh) < H && status == 0 && tgt && cache_tj[hh] == (tgt << 16 | j[hh]) &&             \
-              uint32_t(cache[hh] >> 36) == (epoch & 0x0FFFFFFFu)) {                                       \
-            const uint32_t cpos = uint32_t(cache[hh]);                                                    \
-            if (cpos == pos && uint32_t(cache[hh] >> 32 & 15u) == (b >> 1)) {                             \
-              status = RJ_CHUNK_SYNC; /* identical state from here on: the later chunk owns the rest */   \
-              s_tgt = tgt | uint32_t(hh) << 16;                                                           \
-              s_rec = j[hh];                                                                              \
-            } else if (cpos < pos) {                                                                      \
-              j[hh]++;                                                                                    \
+        /* against each phase hypothesis of that chunk (rj_chunk_lanes); lanes still inside their */    \
+        /* own chunk (tgt 0) skip the compares */                                                         \
+        if (tgt != 0u && status == 0u) {                                                                  \
+          _Pragma("unroll") for (int hh = 0; hh < NH; hh++) {                                             \
+            if (uint32_t(hh) < H && status == 0 && cache_tj[hh] == (tgt << 16 | j[hh]) &&                  \
+                uint32_t(cache[hh] >> 36) == (epoch & 0x0FFFFFFFu)) {                                     \
+              const uint32_t cpos = uint32_t(cache[hh]);                                                  \
+              if (cpos == pos && uint32_t(cache[hh] >> 32 & 15u) == (b >> 1)) {                           \
+                status = RJ_CHUNK_SYNC; /* identical state from here on: the later chunk owns the rest */ \
+                s_tgt = tgt | uint32_t(hh) << 16;                                                         \
+                s_rec = j[hh];                                                                            \
+              } else if (cpos < pos) {                                                                    \
+                j[hh]++;                                                                                  \
+              }                                                                                           \
             }                                                                                             \
           }                                                                                               \
         }                                                                                                 \
@@ -753,7 +756,7 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
   const bool mover = tid >= uint32_t(DEC);
 #ifdef RJ_HL_STAMPS
   const uint64_t hc_t_entry = __builtin_amdgcn_s_memtime();
-  uint64_t hc_loop = 0, hc_ph = 0, hc_safe = 0, hc_wait = 0, hc_setup = 0;
+  uint64_t hc_loop = 0, hc_ph = 0, hc_safe = 0, hc_wait = 0, hc_setup = 0, hc_safe_cyc = 0, hc_uns_cyc = 0;
 #endif
   const uint32_t L = mover ? tid - DEC : tid;
   if (tid == 0) s_ne = 0;
@@ -979,6 +982,9 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
           }
         }
       }
+#ifdef RJ_HL_STAMPS
+      const uint64_t hs0 = __builtin_amdgcn_s_memtime();
+#endif
       if (!safe) {
 #pragma unroll
         for (uint32_t s_ = 0; s_ < PHASE; s_++) RJ_HC_STEP(false);
@@ -987,6 +993,11 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
         for (uint32_t s_ = 0; s_ < PHASE; s_++) RJ_HC_STEP(true);
       }
 #ifdef RJ_HL_STAMPS
+      {
+        const uint64_t hs1 = __builtin_amdgcn_s_memtime();
+        if (safe) hc_safe_cyc += hs1 - hs0;
+        else hc_uns_cyc += hs1 - hs0;
+      }
       hc_ph++;
       hc_safe += safe ? 1u : 0u;
 #endif
@@ -1007,14 +1018,19 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
           }
         }
       }
+      // the records loaded at the phase start land here, before this phase's entry flush: a wait
+      // for them placed after the flush would also wait for its stores (vmcnt counts loads and
+      // stores in issue order)
+#pragma unroll
+      for (int hh = 0; hh < NH; hh++) {
+        uint32_t lo = uint32_t(rec_ld[hh]), hi = uint32_t(rec_ld[hh] >> 32);
+        asm volatile("" : "+v"(lo), "+v"(hi));
+        cache[hh] = uint64_t(hi) << 32 | lo;
+        cache_tj[hh] = rec_ld_tj[hh];
+      }
       if (ne - fl >= GROUP) {
         hl_flush<DEC, GROUP>(stage, fl, ent + fl);
         fl += GROUP;
-      }
-#pragma unroll
-      for (int hh = 0; hh < NH; hh++) {
-        cache[hh] = rec_ld[hh];
-        cache_tj[hh] = rec_ld_tj[hh];
       }
       if (__builtin_amdgcn_ballot_w64(avail < rr + PHASE + 1u) != 0) {
 #ifdef RJ_HL_STAMPS
@@ -1069,6 +1085,8 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     atomicMax(&rj_hc_stamp[5], (unsigned long long)hc_loop);
     atomicAdd(&rj_hc_stamp[6], (unsigned long long)hc_wait);
     atomicMax(&rj_hc_stamp[7], (unsigned long long)(__builtin_amdgcn_s_memtime() - hc_t_entry));
+    atomicAdd(&rj_hc_stamp[8], (unsigned long long)hc_safe_cyc);
+    atomicAdd(&rj_hc_stamp[9], (unsigned long long)hc_uns_cyc);
   }
 #endif
 }
@@ -1108,14 +1126,17 @@ void DumpHuffStamps() {
           h[4], ph / w, h[3] / w, h[5] / w, h[0] / ph, h[1] / ph);
   unsigned long long z[8] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(rj_hl_stamp), z, sizeof(z));
-  unsigned long long c[8];
+  unsigned long long c[10];
   (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(rj_hc_stamp), sizeof(c));
   if (c[4]) {
     const double wv = double(c[4]), pp = c[2] ? double(c[2]) : 1.0;
     fprintf(stderr, "[rj k_huff_chunk] decoder waves %llu: per wave setup %.0f cycles, loop %.0f (max %llu, wave max %llu from entry), "
-            "%.0f phases (%.0f safe), %.0f cycles per phase, ring waits %.0f per wave\n",
-            c[4], c[0] / wv, c[1] / wv, c[5], c[7], c[2] / wv, c[3] / wv, c[1] / pp, c[6] / wv);
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(rj_hc_stamp), z, sizeof(z));
+            "%.0f phases (%.0f safe), %.0f cycles per phase, ring waits %.0f per wave; step cycles per safe phase %.0f, "
+            "per other phase %.0f\n",
+            c[4], c[0] / wv, c[1] / wv, c[5], c[7], c[2] / wv, c[3] / wv, c[1] / pp, c[6] / wv,
+            c[3] ? double(c[8]) / double(c[3]) : 0.0, c[2] > c[3] ? double(c[9]) / double(c[2] - c[3]) : 0.0);
+    unsigned long long z2[10] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(rj_hc_stamp), z2, sizeof(z2));
   }
 }
 #endif
