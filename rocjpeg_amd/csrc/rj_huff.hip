@@ -54,7 +54,7 @@ __device__ const uint4 rj_hl_zero[2] = {};
 __device__ unsigned long long rj_hl_stamp[8];
 // k_huff_chunk: per decoder wave, summed: setup cycles (entry to the first phase), loop cycles,
 // phases, safe phases, waves; max loop cycles; ring-wait cycles
-__device__ unsigned long long rj_hc_stamp[10];
+__device__ unsigned long long rj_hc_stamp[14];
 #define RJ_HL_COUNT_ESC st_esc++
 #else
 #define RJ_HL_COUNT_ESC
@@ -757,6 +757,7 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
 #ifdef RJ_HL_STAMPS
   const uint64_t hc_t_entry = __builtin_amdgcn_s_memtime();
   uint64_t hc_loop = 0, hc_ph = 0, hc_safe = 0, hc_wait = 0, hc_setup = 0, hc_safe_cyc = 0, hc_uns_cyc = 0;
+  uint64_t hc_end[4] = {0, 0, 0, 0};  // phase end: s_dec + chain block, record settle, flush; phase start
 #endif
   const uint32_t L = mover ? tid - DEC : tid;
   if (tid == 0) s_ne = 0;
@@ -950,6 +951,9 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     uint32_t e = s_lut[(tb >> 2) + (peek >> tsh)];
     while (__builtin_amdgcn_ballot_w64(blocks_left > 0) != 0) {
       if (blocks_left == 0) continue;
+#ifdef RJ_HL_STAMPS
+      const uint64_t hp0 = __builtin_amdgcn_s_memtime();
+#endif
       // ---- phase start: the captured record leaves; the record being sought is loaded ----
       if (rp) {
         hc_put_record<kScope>(rec_mine + nrec, rp_pos, rp_b, epoch, rp_ne, rp_rb, rp_p0, rp_p1, rp_p2);
@@ -984,6 +988,7 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
       }
 #ifdef RJ_HL_STAMPS
       const uint64_t hs0 = __builtin_amdgcn_s_memtime();
+      hc_end[3] += hs0 - hp0;
 #endif
       if (!safe) {
 #pragma unroll
@@ -993,11 +998,9 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
         for (uint32_t s_ = 0; s_ < PHASE; s_++) RJ_HC_STEP(true);
       }
 #ifdef RJ_HL_STAMPS
-      {
-        const uint64_t hs1 = __builtin_amdgcn_s_memtime();
-        if (safe) hc_safe_cyc += hs1 - hs0;
-        else hc_uns_cyc += hs1 - hs0;
-      }
+      const uint64_t hs1 = __builtin_amdgcn_s_memtime();
+      if (safe) hc_safe_cyc += hs1 - hs0;
+      else hc_uns_cyc += hs1 - hs0;
       hc_ph++;
       hc_safe += safe ? 1u : 0u;
 #endif
@@ -1018,6 +1021,10 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
           }
         }
       }
+#ifdef RJ_HL_STAMPS
+      const uint64_t he1 = __builtin_amdgcn_s_memtime();
+      hc_end[0] += he1 - hs1;
+#endif
       // the records loaded at the phase start land here, before this phase's entry flush: a wait
       // for them placed after the flush would also wait for its stores (vmcnt counts loads and
       // stores in issue order)
@@ -1028,10 +1035,17 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
         cache[hh] = uint64_t(hi) << 32 | lo;
         cache_tj[hh] = rec_ld_tj[hh];
       }
+#ifdef RJ_HL_STAMPS
+      const uint64_t he2 = __builtin_amdgcn_s_memtime();
+      hc_end[1] += he2 - he1;
+#endif
       if (ne - fl >= GROUP) {
         hl_flush<DEC, GROUP>(stage, fl, ent + fl);
         fl += GROUP;
       }
+#ifdef RJ_HL_STAMPS
+      hc_end[2] += __builtin_amdgcn_s_memtime() - he2;
+#endif
       if (__builtin_amdgcn_ballot_w64(avail < rr + PHASE + 1u) != 0) {
 #ifdef RJ_HL_STAMPS
         const uint64_t hw0 = __builtin_amdgcn_s_memtime();
@@ -1087,6 +1101,7 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     atomicMax(&rj_hc_stamp[7], (unsigned long long)(__builtin_amdgcn_s_memtime() - hc_t_entry));
     atomicAdd(&rj_hc_stamp[8], (unsigned long long)hc_safe_cyc);
     atomicAdd(&rj_hc_stamp[9], (unsigned long long)hc_uns_cyc);
+    for (int q = 0; q < 4; q++) atomicAdd(&rj_hc_stamp[10 + q], (unsigned long long)hc_end[q]);
   }
 #endif
 }
@@ -1126,7 +1141,7 @@ void DumpHuffStamps() {
           h[4], ph / w, h[3] / w, h[5] / w, h[0] / ph, h[1] / ph);
   unsigned long long z[8] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(rj_hl_stamp), z, sizeof(z));
-  unsigned long long c[10];
+  unsigned long long c[14];
   (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(rj_hc_stamp), sizeof(c));
   if (c[4]) {
     const double wv = double(c[4]), pp = c[2] ? double(c[2]) : 1.0;
@@ -1135,7 +1150,9 @@ void DumpHuffStamps() {
             "per other phase %.0f\n",
             c[4], c[0] / wv, c[1] / wv, c[5], c[7], c[2] / wv, c[3] / wv, c[1] / pp, c[6] / wv,
             c[3] ? double(c[8]) / double(c[3]) : 0.0, c[2] > c[3] ? double(c[9]) / double(c[2] - c[3]) : 0.0);
-    unsigned long long z2[10] = {};
+    fprintf(stderr, "[rj k_huff_chunk] per phase: s_dec + chain %.0f, record settle %.0f, flush %.0f, phase start %.0f cycles\n",
+            c[10] / pp, c[11] / pp, c[12] / pp, c[13] / pp);
+    unsigned long long z2[14] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(rj_hc_stamp), z2, sizeof(z2));
   }
 }
