@@ -16,6 +16,9 @@
 //   * bits: the two stream words holding the bit position in registers, the next one read one
 //     step ahead from the lane's LDS ring, which a mover wave beside each decoder wave keeps
 //     filled; a 32-bit peek is one v_alignbit_b32 (q = -pos);
+//   * addresses: table bases are LDS byte addresses (a lookup is a shift and a shift-add), the
+//     stage and the ring are aligned to their own size (a word's address is one v_and_or_b32),
+//     extra bits and their mask are v_bfe_u32s;
 //   * block / MCU bookkeeping: the block index inside the MCU selects the tables through a
 //     2-bit-per-block pattern; the step is software-pipelined (the next lookup is issued before
 //     this symbol's entry is written).
@@ -165,7 +168,8 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
   do {                                                                                                    \
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(e >= RJ_HL_ESC) != 0, 0)) {                          \
       RJ_HL_COUNT_ESC;                                                                                    \
-      if (e >= RJ_HL_ESC) e = hl_escape(e, peek, tsh != 21u, acb, s_lut, tset, pat >> b);                 \
+      if (e >= RJ_HL_ESC) e = hl_escape(e, peek, tsh != 21u, acb - lut_a, s_lut, tset, pat >> b);         \
+      asm volatile("" : "+v"(e)); /* settled here: the join needs no wait for the LDS writes */          \
     }                                                                                                     \
     /* ---- the chain: bit position, block / table state, the next lookup ---- */                      \
     const uint32_t qold = q;                                                                              \
@@ -190,21 +194,20 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
     const uint32_t bn = b + 2u == nb2 ? 0u : b + 2u;                                                      \
     b = bend ? bn : b;                                                                                    \
     /* next symbol's table: the new block's DC table, or the current block's AC table */                 \
-    const uint32_t ids = pat >> b;                                                                        \
-    acb = bend ? ((ids >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES) : acb;                                      \
-    const uint32_t dcb = RJ_HL_DC0 + ((ids & 1u) << (RJ_HL_DC_BITS + 2));                                 \
+    /* (table bases are LDS byte addresses: a lookup is one shift and one shift-add) */                 \
+    acb = bend ? __umul24(__builtin_amdgcn_ubfe(pat_ac, b, 1u), uint32_t(RJ_HL_AC_BYTES)) + lut_a : acb;  \
+    const uint32_t dcb = (__builtin_amdgcn_ubfe(pat, b, 1u) << (RJ_HL_DC_BITS + 2)) + lut_dc;              \
     const uint32_t tbn = bend ? dcb : acb;                                                                \
     const uint32_t tshn = bend ? uint32_t(32 - RJ_HL_DC_BITS) : uint32_t(32 - RJ_HL_AC_BITS);            \
     const uint32_t peekn = __builtin_amdgcn_alignbit(wa, wb, q);                                          \
-    const uint32_t en = s_lut[(tbn >> 2) + (peekn >> tshn)];                                              \
-    wc = ring[rr & (RJ_HL_WORDS - 1)];                                                                    \
+    const uint32_t en = lds_rd(((peekn >> tshn) << 2) + tbn);                                             \
+    wc = lds_rd(((rr << kColShift) & kRingMask) | ring_a);                                                  \
     /* ---- this step's entries, while the lookup is in flight ---- */                                  \
     /* a coefficient: HUFF_EXTEND of the s extra bits (the low s of the symbol's n bits,            \
        right-aligned), and its position clamped to 63 (libjpeg's natural-order table) */            \
     const uint32_t s1 = (e >> 21) & 15u;                                                                  \
-    const uint32_t raw = peek >> (32u - n1);                                                              \
-    const uint32_t xm = (1u << s1) - 1u; /* v_bfm */                                                     \
-    const uint32_t xb = raw & xm;                                                                         \
+    const uint32_t xb = __builtin_amdgcn_ubfe(peek, 32u - n1, s1); /* the low s of the top n bits */    \
+    const uint32_t xm = __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0u, s1);                                       \
     const uint32_t xv = xb > xm - xb ? xb : xb - xm; /* top extra bit clear: negative */               \
     const uint32_t xp = min(kcur + R1, 63u);                                                              \
     uint32_t entry = __builtin_amdgcn_perm(xp, xv, 0x05040100u); /* value's low half | position << 16 */ \
@@ -214,18 +217,17 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
       emit = skip ? 1u : emit;                                                                            \
       emit = blocks_left > 0 ? emit : 0u;                                                                 \
     }                                                                                                     \
-    stage[ne & (kStage - 1)] = entry; /* a non-emitted write lands in the next free slot */                \
+    lds_wr(((ne << kColShift) & kStageMask) | stage_a, entry); /* a non-emitted write: the next free slot */ \
     ne += emit;                                                                                           \
     {                                                                                                     \
       const uint32_t s2 = (e >> 5) & 15u;                                                                 \
-      const uint32_t raw2 = peek >> ((32u - n1 - n2) & 31u);                                              \
-      const uint32_t xm2 = (1u << s2) - 1u;                                                               \
-      const uint32_t xb2 = raw2 & xm2;                                                                    \
+      const uint32_t xb2 = __builtin_amdgcn_ubfe(peek, 32u - n1 - n2, s2);                                \
+      const uint32_t xm2 = __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0u, s2);                                    \
       const uint32_t xv2 = xb2 > xm2 - xb2 ? xb2 : xb2 - xm2;                                             \
       const uint32_t xp2 = min(k1 + R2, 63u);                                                             \
       uint32_t emit2 = (use2 && s2 != 0u) ? 1u : 0u;                                                      \
       if (SAFE) emit2 = blocks_left > 0 ? emit2 : 0u;                                                     \
-      stage[ne & (kStage - 1)] = __builtin_amdgcn_perm(xp2, xv2, 0x05040100u);                            \
+      lds_wr(((ne << kColShift) & kStageMask) | stage_a, __builtin_amdgcn_perm(xp2, xv2, 0x05040100u));   \
       ne += emit2;                                                                                        \
     }                                                                                                     \
     if (SAFE) {                                                                                           \
@@ -257,6 +259,13 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
 typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
 __device__ __forceinline__ uint32_t lds_ld(const uint32_t *p) { return *(const lds_vu32 *)(p); }
 __device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) { *(lds_vu32 *)(p) = v; }
+// plain LDS words by byte address (RJ_HL_STEP: the address arithmetic stays two VALU operations)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(p);
+}
+__device__ __forceinline__ uint32_t lds_rd(uint32_t a) { return *(const lds_u32 *)(uintptr_t)(a); }
+__device__ __forceinline__ void lds_wr(uint32_t a, uint32_t v) { *(lds_u32 *)(uintptr_t)(a) = v; }
 #define RJ_HL_FIN 0xFFFFFFFFu  // decoder -> mover: the lane's decode is over
 
 // Workgroup = DEC decoder lanes + one mover wave per decoder wave.  Lane `g` of
@@ -282,11 +291,17 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0, uint32_t nlanes, const uint8_t *__restrict__ destuffed,
     const RjTableSet *__restrict__ tabsets, const RjLeanTables *__restrict__ lean, RjCoefBuf coefs, RjHuffSplit split) {
   constexpr uint32_t kStage = 2 * GROUP;
+  constexpr uint32_t kColShift = __builtin_ctz(DEC * 4u);  // bytes between a lane column's words
+  // the stage and the ring are aligned to their own size: a word's LDS address is its lane
+  // column's address OR its row bits (one v_and_or_b32)
+  constexpr uint32_t kStageMask = (kStage << kColShift) - (1u << kColShift);
+  constexpr uint32_t kRingMask = (RJ_HL_WORDS << kColShift) - (1u << kColShift);
+  static_assert((DEC & (DEC - 1)) == 0, "lane columns: DEC a power of two");
   // a phase adds <= 2 PHASE entries to < GROUP pending ones: the stage must hold them
   static_assert(2 * PHASE <= GROUP + 1, "stage too small for a phase of two-symbol steps");
   constexpr uint32_t kPairs = kSplit ? DEC / 2 : 1;
-  __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_HL_WORDS][DEC];
-  __shared__ __attribute__((aligned(16))) uint32_t s_stage[kStage][DEC];
+  __shared__ __attribute__((aligned(RJ_HL_WORDS * DEC * 4))) uint32_t s_ring[RJ_HL_WORDS][DEC];
+  __shared__ __attribute__((aligned(kStage * DEC * 4))) uint32_t s_stage[kStage][DEC];
   __shared__ __attribute__((aligned(16))) uint32_t s_lut[RJ_HL_LUT_WORDS];
   __shared__ uint32_t s_dec[DEC];  // decoder -> mover: ring words fully consumed (RJ_HL_FIN: done)
   __shared__ uint32_t s_mov[DEC];  // mover -> decoder: 16-B chunks committed to the ring
@@ -384,6 +399,7 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
       pat |= ((im.comp_td[cc] & 1u) | ((im.comp_ta[cc] & 1u) << 1)) << (2 * bb);
     }
     const uint32_t nb2 = 2 * nblk;
+    const uint32_t pat_ac = pat >> 1;  // bit 2b: block b's AC table
     const uint32_t nbits = nbytes * 8u;
     const uint32_t blocks = sg.mcu_count * nblk;
     // entry regions: the interval's own; a tail lane writes its pair's slot of the split region
@@ -398,6 +414,8 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     RjPiece *piece = coefs.piece + rj_seg_lane0_k<kSplit>(coefs, gseg);
     const RjTableSet *tset = tabsets + T;  // canonical search (escape path)
     const HCol<DEC> stage{&s_stage[0][L]};
+    const uint32_t stage_a = lds_addr(&s_stage[0][L]), ring_a = lds_addr(&s_ring[0][L]);
+    const uint32_t lut_a = lds_addr(s_lut), lut_dc = lut_a + RJ_HL_DC0;
     // split state: records (tail), the last MCU start seen (head), the head's scan over the records
     uint16_t *const recs = &s_rec[0][kSplit ? pair : 0u];
     uint32_t nr = tail ? 0u : kRec;
@@ -429,7 +447,7 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     bool skip = (sg.flags & RJ_SEG_MISSING) != 0;
     uint32_t blocks_left = blocks;
     uint32_t b = 0, k = 0;
-    uint32_t acb = ((pat >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES);
+    uint32_t acb = ((pat >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES) + lut_a;  // LDS byte address
     uint32_t tb = RJ_HL_DC0 + ((pat & 1u) << (RJ_HL_DC_BITS + 2));
     uint32_t tsh = 32 - RJ_HL_DC_BITS;
     // the first symbol's peek and table entry (RJ_HL_STEP is software-pipelined)
@@ -437,6 +455,7 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     uint32_t e = s_lut[(tb >> 2) + (peek >> tsh)];
 #ifdef RJ_HL_STAMPS
     uint64_t st_steps = 0, st_end = 0, st_fast = 0, st_safe = 0, st_esc = 0;
+    const uint64_t st_begin = __builtin_amdgcn_s_memtime();
 #define RJ_HL_T0 const uint64_t t0 = __builtin_amdgcn_s_memtime()
 #define RJ_HL_T1(fast)                                  \
   const uint64_t t1 = __builtin_amdgcn_s_memtime();     \
@@ -524,6 +543,9 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
       atomicAdd(&rj_hl_stamp[3], (unsigned long long)st_safe);
       atomicAdd(&rj_hl_stamp[4], 1ull);
       atomicAdd(&rj_hl_stamp[5], (unsigned long long)st_esc);
+      const unsigned long long st_loop = __builtin_amdgcn_s_memtime() - st_begin;
+      atomicAdd(&rj_hl_stamp[6], st_loop);
+      atomicMax(&rj_hl_stamp[7], st_loop);
     }
 #endif
     stage[ne & (kStage - 1)] = RJ_RE_TERM;
@@ -578,7 +600,8 @@ __device__ __forceinline__ void hc_put_record(RjRecord *r, uint32_t pos, uint32_
 #define RJ_HC_STEP(SAFE)                                                                                        \
   do {                                                                                                    \
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(e >= RJ_HL_ESC) != 0, 0)) {                          \
-      if (e >= RJ_HL_ESC) e = hl_escape(e, peek, tsh != 21u, acb, s_lut, tset, pat >> b);                 \
+      if (e >= RJ_HL_ESC) e = hl_escape(e, peek, tsh != 21u, acb - lut_a, s_lut, tset, pat >> b);         \
+      asm volatile("" : "+v"(e)); /* settled here: the join needs no wait for the LDS writes */          \
     }                                                                                                     \
     const uint32_t qold = q;                                                                              \
     const uint32_t R1 = (e >> 25) & 63u, n1 = (e >> 16) & 31u;                                            \
@@ -600,19 +623,18 @@ __device__ __forceinline__ void hc_put_record(RjRecord *r, uint32_t pos, uint32_
     k = bend ? 0u : kn;                                                                                   \
     const uint32_t bn = b + 2u == nb2 ? 0u : b + 2u;                                                      \
     b = bend ? bn : b;                                                                                    \
-    const uint32_t ids = pat >> b;                                                                        \
-    acb = bend ? ((ids >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES) : acb;                                      \
-    const uint32_t dcb = RJ_HL_DC0 + ((ids & 1u) << (RJ_HL_DC_BITS + 2));                                 \
+    /* (table bases are LDS byte addresses: a lookup is one shift and one shift-add) */                 \
+    acb = bend ? __umul24(__builtin_amdgcn_ubfe(pat_ac, b, 1u), uint32_t(RJ_HL_AC_BYTES)) + lut_a : acb;  \
+    const uint32_t dcb = (__builtin_amdgcn_ubfe(pat, b, 1u) << (RJ_HL_DC_BITS + 2)) + lut_dc;              \
     const uint32_t tbn = bend ? dcb : acb;                                                                \
     const uint32_t tshn = bend ? uint32_t(32 - RJ_HL_DC_BITS) : uint32_t(32 - RJ_HL_AC_BITS);            \
     const uint32_t peekn = __builtin_amdgcn_alignbit(wa, wb, q);                                          \
-    const uint32_t en = s_lut[(tbn >> 2) + (peekn >> tshn)];                                              \
-    wc = ring[rr & (RJ_HL_WORDS - 1)];                                                                    \
+    const uint32_t en = lds_rd(((peekn >> tshn) << 2) + tbn);                                             \
+    wc = lds_rd(((rr << kColShift) & kRingMask) | ring_a);                                                  \
     /* ---- entries; a DC symbol's value is the predictor of its block's component + the difference */ \
     const uint32_t s1 = (e >> 21) & 15u;                                                                  \
-    const uint32_t raw = peek >> (32u - n1);                                                              \
-    const uint32_t xm = (1u << s1) - 1u;                                                                  \
-    const uint32_t xb = raw & xm;                                                                         \
+    const uint32_t xb = __builtin_amdgcn_ubfe(peek, 32u - n1, s1);                                        \
+    const uint32_t xm = __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0u, s1);                                       \
     const uint32_t xv = xb > xm - xb ? xb : xb - xm;                                                      \
     const bool isdc = kcur == 0u;                                                                         \
     const uint32_t cc = (cpat >> bcur) & 3u;                                                              \
@@ -632,18 +654,17 @@ __device__ __forceinline__ void hc_put_record(RjRecord *r, uint32_t pos, uint32_
       pred1 = (upd && cc == 1u) ? pdc : pred1;                                                            \
       pred2 = (upd && cc == 2u) ? pdc : pred2;                                                            \
     }                                                                                                     \
-    stage[ne & (kStage - 1)] = entry;                                                                     \
+    lds_wr(((ne << kColShift) & kStageMask) | stage_a, entry);                                          \
     ne += emit;                                                                                           \
     {                                                                                                     \
       const uint32_t s2 = (e >> 5) & 15u;                                                                 \
-      const uint32_t raw2 = peek >> ((32u - n1 - n2) & 31u);                                              \
-      const uint32_t xm2 = (1u << s2) - 1u;                                                               \
-      const uint32_t xb2 = raw2 & xm2;                                                                    \
+      const uint32_t xb2 = __builtin_amdgcn_ubfe(peek, 32u - n1 - n2, s2);                                \
+      const uint32_t xm2 = __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0u, s2);                                    \
       const uint32_t xv2 = xb2 > xm2 - xb2 ? xb2 : xb2 - xm2;                                             \
       const uint32_t xp2 = min(k1 + R2, 63u);                                                             \
       uint32_t emit2 = (use2 && s2 != 0u) ? 1u : 0u;                                                      \
       if (SAFE) emit2 = act ? emit2 : 0u;                                                                 \
-      stage[ne & (kStage - 1)] = __builtin_amdgcn_perm(xp2, xv2, 0x05040100u);                             \
+      lds_wr(((ne << kColShift) & kStageMask) | stage_a, __builtin_amdgcn_perm(xp2, xv2, 0x05040100u));   \
       ne += emit2;                                                                                        \
     }                                                                                                     \
     if (SAFE) {                                                                                           \
@@ -737,9 +758,15 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
   constexpr int DEC = RJ_K1_WG;  // the chunk layout's granule (an interval of <= DEC chunks in one workgroup)
   constexpr int GROUP = RJ_HL_GROUP, PHASE = RJ_HL_PHASE;
   constexpr uint32_t kStage = 2 * GROUP;
+  constexpr uint32_t kColShift = __builtin_ctz(DEC * 4u);  // bytes between a lane column's words
+  // the stage and the ring are aligned to their own size: a word's LDS address is its lane
+  // column's address OR its row bits (one v_and_or_b32)
+  constexpr uint32_t kStageMask = (kStage << kColShift) - (1u << kColShift);
+  constexpr uint32_t kRingMask = (RJ_HL_WORDS << kColShift) - (1u << kColShift);
+  static_assert((DEC & (DEC - 1)) == 0, "lane columns: DEC a power of two");
   static_assert(2 * PHASE <= GROUP + 1, "stage too small for a phase of two-symbol steps");
-  __shared__ __attribute__((aligned(16))) uint32_t s_ring[RJ_HL_WORDS][DEC];
-  __shared__ __attribute__((aligned(16))) uint32_t s_stage[kStage][DEC];
+  __shared__ __attribute__((aligned(RJ_HL_WORDS * DEC * 4))) uint32_t s_ring[RJ_HL_WORDS][DEC];
+  __shared__ __attribute__((aligned(kStage * DEC * 4))) uint32_t s_stage[kStage][DEC];
   __shared__ __attribute__((aligned(16))) uint32_t s_lut[RJ_HL_LUT_WORDS];
   __shared__ uint32_t s_dec[DEC];
   __shared__ uint32_t s_mov[DEC];
@@ -871,6 +898,7 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
       cpat |= cc << (2 * bb);
     }
     const uint32_t nb2 = 2 * nblk;
+    const uint32_t pat_ac = pat >> 1;  // bit 2b: block b's AC table
     const uint32_t nbits = lane_bytes * 8u;  // data bits from the lane's first bit
     const uint32_t nbits_skip = chunk ? 0xFFFFFFFFu : nbits;  // chunk lanes never zero-fill (DONE instead)
     const uint32_t blocks = sg.mcu_count * nblk;
@@ -880,6 +908,8 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     uint32_t *ent = coefs.ent + ent_lane;
     const RjTableSet *tset = tabsets + T;
     const HCol<DEC> stage{&s_stage[0][L]};
+    const uint32_t stage_a = lds_addr(&s_stage[0][L]), ring_a = lds_addr(&s_ring[0][L]);
+    const uint32_t lut_a = lds_addr(s_lut), lut_dc = lut_a + RJ_HL_DC0;
     // chunk-lane state (rj_entropy.hip decode_lane)
     const uint32_t start_bit = bs * 8u, own_bit = b0 * 8u, end_bit = b1 * 8u, nbits_abs = nbytes * 8u;
     const uint32_t clen_bits = clen * 8u, ov_bit = end_bit + rj_chunk_reach(clen) * 8u;
@@ -944,7 +974,7 @@ __global__ __launch_bounds__(512, 1) void k_huff_chunk(const RjImageDev *__restr
     bool skip = !chunk && (sg.flags & RJ_SEG_MISSING) != 0;
     uint32_t blocks_left = chunk ? 0x7FFFFFFFu : blocks;
     uint32_t b = 2u * h, k = 0;  // a speculative lane starts in its hypothesis' phase (block h of an MCU)
-    uint32_t acb = ((pat >> b >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES);
+    uint32_t acb = ((pat >> b >> 1) & 1u) * uint32_t(RJ_HL_AC_BYTES) + lut_a;  // LDS byte address
     uint32_t tb = RJ_HL_DC0 + (((pat >> b) & 1u) << (RJ_HL_DC_BITS + 2));
     uint32_t tsh = 32 - RJ_HL_DC_BITS;
     uint32_t peek = __builtin_amdgcn_alignbit(wa, wb, q);
@@ -1137,8 +1167,9 @@ void DumpHuffStamps() {
   (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(rj_hl_stamp), sizeof(h));
   const double w = h[4] ? double(h[4]) : 1.0;
   const double ph = double(h[2] + h[3]) ? double(h[2] + h[3]) : 1.0;
-  fprintf(stderr, "[rj k_huff] waves %llu: per wave %.0f phases (%.0f safe), %.0f escape steps; cycles per phase: steps %.0f, end %.0f\n",
-          h[4], ph / w, h[3] / w, h[5] / w, h[0] / ph, h[1] / ph);
+  fprintf(stderr, "[rj k_huff] waves %llu: per wave %.0f phases (%.0f safe), %.0f escape steps; cycles per phase: steps %.0f, end %.0f; "
+          "decode cycles per wave %.0f (max %llu)\n",
+          h[4], ph / w, h[3] / w, h[5] / w, h[0] / ph, h[1] / ph, h[6] / w, h[7]);
   unsigned long long z[8] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(rj_hl_stamp), z, sizeof(z));
   unsigned long long c[14];
