@@ -114,7 +114,9 @@ typedef struct {
   /* MCU-phase hypotheses per speculative chunk (1: one lane per chunk; small calls: the MCU's
      block count, each speculative chunk decoded from every phase it may start in) */
   uint32_t chunk_hyp;
-  uint32_t reserved0;
+  /* 1: the lean K1 ran five decoder waves per CU (the overflow past one round of four as fifth
+     waves, rj_huff.hip k_huff<RJ_HL_DEC5>) */
+  uint32_t lean_five;
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);

@@ -108,7 +108,7 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("routed_images", ctypes.c_uint32), ("lean_k1", ctypes.c_uint32),
                 ("wide_rows", ctypes.c_uint32), ("lean_split", ctypes.c_uint32),
                 ("chunk_k1", ctypes.c_uint32), ("chunk_bytes", ctypes.c_uint32),
-                ("chunk_hyp", ctypes.c_uint32), ("reserved0", ctypes.c_uint32)]
+                ("chunk_hyp", ctypes.c_uint32), ("lean_five", ctypes.c_uint32)]
 
 
 class RocJpegAmdInterval(ctypes.Structure):  # include/rocjpeg_amd.h

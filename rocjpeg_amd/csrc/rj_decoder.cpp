@@ -160,6 +160,7 @@ int Decoder::Initialize() {
   if (const char *l = getenv("RJ_LPT")) lpt_ = atoi(l) != 0;
   if (const char *l = getenv("RJ_K1_SOLO")) k1_solo_lds_ = uint32_t(std::max(0, atoi(l)));
   if (const char *so = getenv("RJ_SPLIT_OUTLIERS")) outlier_split_ = atoi(so) != 0;
+  if (const char *f5 = getenv("RJ_K1_FIVE")) five_waves_ = atoi(f5);
   if (const char *kc = getenv("RJ_K1_CHUNK")) k1_chunk_ = atoi(kc) != 0;
   if (const char *cm = getenv("RJ_CHUNK_MIN")) chunk_min_ = uint32_t(std::max(16, atoi(cm)));
   if (const char *hy = getenv("RJ_K1_HYP")) hyp_max_ = uint32_t(std::max(1, atoi(hy)));
@@ -1776,6 +1777,34 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
   }
   timings_.lean_split = nsplit;
+  // ---- five decoder waves per CU (rj_huff.hip k_huff<RJ_HL_DEC5>): a lean call whose intervals
+  // overflow one round of four decoder waves per CU by at most one wave per CU (C2: 69,632
+  // intervals on 65,536 lanes) gives the last workgroups -- the shortest intervals of the round --
+  // a fifth decoder wave with the overflow (the longest overflow wave beside the shortest round)
+  // instead of a second round that starts only when the first workgroups finish ----
+  static_assert(RJ_HL_DEC5 == 256 + 64, "five-wave layout: one overflow wave per workgroup");
+  uint32_t nl_five = 0;
+  if (lean && sorted && lanes_desc && ngroups == 1 && !any_split && nsplit == 0 && five_waves_) {
+    const uint64_t round = uint64_t(cu_count_) * 256;
+    if (seg_total > round && seg_total - round <= uint64_t(cu_count_) * 64) {
+      const uint32_t cu = uint32_t(cu_count_), ntail = uint32_t((seg_total - round + 63) / 64);
+      nl_five = cu * RJ_HL_DEC5;
+      std::vector<uint32_t> &l5 = sc_.lane_split;
+      l5.assign(nl_five, UINT32_MAX);
+      for (uint32_t w = 0; w < cu; w++) {
+        // a workgroup that takes a fifth wave lists its four in reverse (shortest first): the
+        // fifth decoder wave shares a SIMD with the first (waves go to the SIMDs in order)
+        const bool rev = five_waves_ == 2 && w >= cu - ntail;
+        for (uint32_t q = 0; q < 4; q++)
+          std::memcpy(&l5[uint64_t(w) * RJ_HL_DEC5 + q * 64], &lane_seg[uint64_t(w) * 256 + (rev ? 3 - q : q) * 64], 64 * 4);
+      }
+      for (uint32_t t = 0; t < ntail; t++) {
+        const uint32_t w = cu - 1 - t, g0 = uint32_t(round) + t * 64, cnt = std::min<uint32_t>(64, seg_total - g0);
+        std::memcpy(&l5[uint64_t(w) * RJ_HL_DEC5 + 256], &lane_seg[g0], uint64_t(cnt) * 4);
+      }
+    }
+  }
+  timings_.lean_five = nl_five ? 1u : 0u;
   if (any_split) {
     std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(lane_seg.size()) * 4);
     std::memcpy(h + off_seg_lane0, seg_lane0.data(), uint64_t(seg_lane0.size()) * 4);
@@ -1785,6 +1814,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     cbuf.seg_ent = reinterpret_cast<const unsigned long long *>(dbase + off_seg_ent);
   } else if (sorted) {  // lanes in length order; pieces stay at the interval's own slot
     if (nsplit) std::memcpy(h + off_lane_seg, sc_.lane_split.data(), uint64_t(nl_split) * 4);
+    else if (nl_five) std::memcpy(h + off_lane_seg, sc_.lane_split.data(), uint64_t(nl_five) * 4);
     else std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(seg_total) * 4);
     cbuf.lane_seg = d_lane_seg;
     cbuf.seg_lane0 = nullptr;
@@ -1794,7 +1824,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   }
   // part B: everything up to the row lists, or only the lane list actually used
   const uint64_t blob_b = (!any_split && sorted && ngroups == 1)
-                              ? std::min<uint64_t>(blob, AlignUp(off_lane_seg + uint64_t(nsplit ? nl_split : seg_total) * 4, 256))
+                              ? std::min<uint64_t>(blob, AlignUp(off_lane_seg + uint64_t(nsplit ? nl_split : (nl_five ? nl_five : seg_total)) * 4, 256))
                               : blob;
   if (blob_b > blob_a) RJ_HIP(hipMemcpyAsync(dbase + blob_a, h + blob_a, blob_b - blob_a, hipMemcpyHostToDevice, stream_));
 
@@ -1845,8 +1875,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     for (int g = 0; g + 1 < ngroups; g++) RJ_HIP(hipStreamWaitEvent(stream_, pev_[g], 0));
   } else {
     if (lean) {  // no split interval: one pass, no resolution / serial stages
-      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, nsplit ? nl_split : seg_total, k1_src, d_tabs,
-                             d_lean, cbuf, k1_solo_lds_, nsplit ? &hsplit : nullptr));
+      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, nsplit ? nl_split : (nl_five ? nl_five : seg_total), k1_src,
+                             d_tabs, d_lean, cbuf, k1_solo_lds_, nsplit ? &hsplit : nullptr, nl_five != 0));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
     } else {

@@ -124,6 +124,8 @@ class Decoder {
   uint32_t k1_solo_lds_ = 16384;
   uint32_t chunk_min_ = RJ_CHUNK_MIN_BYTES;  // env RJ_CHUNK_MIN: floor of the call's chunk length (bytes)
   bool k1_chunk_ = true;           // env RJ_K1_CHUNK=0: chunk-layout calls take k_entropy's K1 (A/B)
+  int five_waves_ = 2;             // env RJ_K1_FIVE: 0 a lean call's overflow past one round of lanes runs as a second round;
+                                   // 1 fifth waves; 2 fifth waves beside their workgroup's shortest wave
   bool outlier_split_ = true;      // env RJ_SPLIT_OUTLIERS=0: never split the outlier intervals (one decoder wave per SIMD)
   double outlier_t_ = 9.0 / 16;    // env RJ_SPLIT_OUTLIER_T: outliers are longer than this share of the longest interval
   double outlier_frac_ = 0.7;      // env RJ_SPLIT_OUTLIER_FRAC: at most this share of the intervals split in that mode

@@ -86,6 +86,7 @@ struct RjCoefBuf {
 #define RJ_LANE_HEAD 0x40000000u
 #define RJ_LANE_TAIL 0x80000000u
 #define RJ_HL_SPLIT_DEC 256          // decoder lanes per workgroup of the split launch (two workgroups per CU)
+#define RJ_HL_DEC5 320               // decoder lanes per workgroup of the five-wave lean launch
 #define RJ_SPLIT_MIN_BYTES 1024u     // shorter intervals stay whole
 __host__ __device__ inline uint32_t rj_split_byte(uint32_t dst_len) { return (dst_len * 29u / 64u) & ~15u; }
 struct RjHuffSplit {

@@ -164,6 +164,11 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
 // block / table state -- the chain the next lookup depends on -- and issues the next symbol's
 // LDS lookup, then does this step's remaining work (its entries into the stage, the counters)
 // while that lookup is in flight.
+// row `i` (mod `rows`) of a lane column's LDS array (rows x DEC words): with DEC a power of two the
+// array is aligned to its size and the address is one v_and_or_b32, otherwise a v_mad_u32_u24
+#define RJ_HL_COLW(i, rows, mask, base) \
+  (kPow2 ? ((((i) << kColShift) & (mask)) | (base)) : (__umul24((i) & ((rows) - 1u), DEC * 4u) + (base)))
+__host__ __device__ constexpr uint32_t hl_align(uint32_t bytes) { return (bytes & (bytes - 1)) == 0 ? bytes : 16u; }
 #define RJ_HL_STEP(SAFE, SYNC)                                                                                  \
   do {                                                                                                    \
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(e >= RJ_HL_ESC) != 0, 0)) {                          \
@@ -201,7 +206,7 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
     const uint32_t tshn = bend ? uint32_t(32 - RJ_HL_DC_BITS) : uint32_t(32 - RJ_HL_AC_BITS);            \
     const uint32_t peekn = __builtin_amdgcn_alignbit(wa, wb, q);                                          \
     const uint32_t en = lds_rd(((peekn >> tshn) << 2) + tbn);                                             \
-    wc = lds_rd(((rr << kColShift) & kRingMask) | ring_a);                                                  \
+    wc = lds_rd(RJ_HL_COLW(rr, RJ_HL_WORDS, kRingMask, ring_a));                                                  \
     /* ---- this step's entries, while the lookup is in flight ---- */                                  \
     /* a coefficient: HUFF_EXTEND of the s extra bits (the low s of the symbol's n bits,            \
        right-aligned), and its position clamped to 63 (libjpeg's natural-order table) */            \
@@ -217,7 +222,7 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
       emit = skip ? 1u : emit;                                                                            \
       emit = blocks_left > 0 ? emit : 0u;                                                                 \
     }                                                                                                     \
-    lds_wr(((ne << kColShift) & kStageMask) | stage_a, entry); /* a non-emitted write: the next free slot */ \
+    lds_wr(RJ_HL_COLW(ne, kStage, kStageMask, stage_a), entry); /* a non-emitted write: the next free slot */ \
     ne += emit;                                                                                           \
     {                                                                                                     \
       const uint32_t s2 = (e >> 5) & 15u;                                                                 \
@@ -227,7 +232,7 @@ __device__ __forceinline__ uint32_t hl_escape(uint32_t e, uint32_t peek, bool is
       const uint32_t xp2 = min(k1 + R2, 63u);                                                             \
       uint32_t emit2 = (use2 && s2 != 0u) ? 1u : 0u;                                                      \
       if (SAFE) emit2 = blocks_left > 0 ? emit2 : 0u;                                                     \
-      lds_wr(((ne << kColShift) & kStageMask) | stage_a, __builtin_amdgcn_perm(xp2, xv2, 0x05040100u));   \
+      lds_wr(RJ_HL_COLW(ne, kStage, kStageMask, stage_a), __builtin_amdgcn_perm(xp2, xv2, 0x05040100u));   \
       ne += emit2;                                                                                        \
     }                                                                                                     \
     if (SAFE) {                                                                                           \
@@ -291,17 +296,18 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0, uint32_t nlanes, const uint8_t *__restrict__ destuffed,
     const RjTableSet *__restrict__ tabsets, const RjLeanTables *__restrict__ lean, RjCoefBuf coefs, RjHuffSplit split) {
   constexpr uint32_t kStage = 2 * GROUP;
-  constexpr uint32_t kColShift = __builtin_ctz(DEC * 4u);  // bytes between a lane column's words
+  constexpr bool kPow2 = (DEC & (DEC - 1)) == 0;
+  constexpr uint32_t kColShift = kPow2 ? __builtin_ctz(DEC * 4u) : 0u;  // bytes between a lane column's words
   // the stage and the ring are aligned to their own size: a word's LDS address is its lane
   // column's address OR its row bits (one v_and_or_b32)
   constexpr uint32_t kStageMask = (kStage << kColShift) - (1u << kColShift);
   constexpr uint32_t kRingMask = (RJ_HL_WORDS << kColShift) - (1u << kColShift);
-  static_assert((DEC & (DEC - 1)) == 0, "lane columns: DEC a power of two");
+  static_assert(DEC % 64 == 0, "whole decoder waves");
   // a phase adds <= 2 PHASE entries to < GROUP pending ones: the stage must hold them
   static_assert(2 * PHASE <= GROUP + 1, "stage too small for a phase of two-symbol steps");
   constexpr uint32_t kPairs = kSplit ? DEC / 2 : 1;
-  __shared__ __attribute__((aligned(RJ_HL_WORDS * DEC * 4))) uint32_t s_ring[RJ_HL_WORDS][DEC];
-  __shared__ __attribute__((aligned(kStage * DEC * 4))) uint32_t s_stage[kStage][DEC];
+  __shared__ __attribute__((aligned(hl_align(RJ_HL_WORDS * DEC * 4)))) uint32_t s_ring[RJ_HL_WORDS][DEC];
+  __shared__ __attribute__((aligned(hl_align(kStage * DEC * 4)))) uint32_t s_stage[kStage][DEC];
   __shared__ __attribute__((aligned(16))) uint32_t s_lut[RJ_HL_LUT_WORDS];
   __shared__ uint32_t s_dec[DEC];  // decoder -> mover: ring words fully consumed (RJ_HL_FIN: done)
   __shared__ uint32_t s_mov[DEC];  // mover -> decoder: 16-B chunks committed to the ring
@@ -1191,15 +1197,20 @@ void DumpHuffStamps() {
 
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
-                           RjCoefBuf coefs, uint32_t extra_lds, const RjHuffSplit *split) {
+                           RjCoefBuf coefs, uint32_t extra_lds, const RjHuffSplit *split, bool five_waves) {
   if (nlanes == 0) return hipSuccess;
   if (split != nullptr) {  // outliers split: one decoder wave per SIMD, two workgroups per CU
     hipLaunchKernelGGL((k_huff<RJ_HL_SPLIT_DEC, 8, true, 4>), dim3((nlanes + RJ_HL_SPLIT_DEC - 1) / RJ_HL_SPLIT_DEC),
                        dim3(2 * RJ_HL_SPLIT_DEC), 0, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs,
                        *split);
   } else {
-    hipLaunchKernelGGL((k_huff<256, RJ_HL_GROUP, false, RJ_HL_PHASE>), dim3((nlanes + 255) / 256), dim3(512), extra_lds,
-                       st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs, RjHuffSplit{0, 0});
+    if (five_waves)  // one workgroup per CU by its LDS (~105 KB)
+      hipLaunchKernelGGL((k_huff<RJ_HL_DEC5, RJ_HL_GROUP, false, RJ_HL_PHASE>),
+                         dim3((nlanes + RJ_HL_DEC5 - 1) / RJ_HL_DEC5), dim3(2 * RJ_HL_DEC5), 0, st, imgs, nimg, lane0,
+                         nlanes, destuffed, tabsets, lean, coefs, RjHuffSplit{0, 0});
+    else
+      hipLaunchKernelGGL((k_huff<256, RJ_HL_GROUP, false, RJ_HL_PHASE>), dim3((nlanes + 255) / 256), dim3(512),
+                         extra_lds, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs, RjHuffSplit{0, 0});
   }
   return hipGetLastError();
 }

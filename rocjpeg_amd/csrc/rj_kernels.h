@@ -30,9 +30,13 @@ hipError_t LaunchEntropyLanes(hipStream_t st, const RjImageDev *imgs, int nimg, 
 // tail lanes (RJ_LANE_HEAD / RJ_LANE_TAIL), split waves first, then whole intervals 64 per wave;
 // pieces at interval << 1 (coefs.piece_shift = 1); 512-thread workgroups, two per CU (one
 // decoder wave per SIMD, as in the unsplit launch).
+// five_waves: RJ_HL_DEC5 lanes per workgroup (five decoder waves, one workgroup per CU): a call
+// whose intervals overflow one round of four waves per CU by at most one wave per CU lists the
+// overflow as fifth waves (lane_seg laid out per workgroup, empty lanes 0xFFFFFFFF).
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
-                           RjCoefBuf coefs, uint32_t extra_lds = 0, const RjHuffSplit *split = nullptr);
+                           RjCoefBuf coefs, uint32_t extra_lds = 0, const RjHuffSplit *split = nullptr,
+                           bool five_waves = false);
 // K1 chunk lanes on the lean machinery (rj_huff.hip k_huff_chunk): stage 0 of LaunchEntropy's
 // layout (from lane0: lanes_wg lanes with workgroup-scope records, then lanes_dev), absolute DC entries.
 hipError_t LaunchHuffChunks(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t lanes_wg,

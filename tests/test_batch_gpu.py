@@ -86,6 +86,47 @@ def test_c2_1024_split_launch(split_dec):
     assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
 
 
+@pytest.fixture(scope="module")
+def two_round_dec():
+    """A handle with the five-wave lean layout off (RJ_K1_FIVE=0, read at handle creation): the
+    intervals past one round of lanes run as a second round."""
+    torch()
+    old = os.environ.get("RJ_K1_FIVE")
+    os.environ["RJ_K1_FIVE"] = "0"
+    try:
+        d = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    finally:
+        if old is None:
+            del os.environ["RJ_K1_FIVE"]
+        else:
+            os.environ["RJ_K1_FIVE"] = old
+    yield d
+    d.close()
+
+
+def test_c2_1024_two_round_layout(two_round_dec):
+    """The C2 call with the overflow intervals as a second round of lean lanes (the layout
+    before the fifth waves, still the one for batches past five waves per CU): every image
+    equal to the oracle."""
+    t = torch()
+    distinct, copies = 64, 16
+    datas = _c2_images(distinct, seed0=777)
+    with ThreadPoolExecutor(16) as ex:
+        want = list(ex.map(lambda d: O.oracle_decode(d, int(R.OutputFormat.RGB), [(1080, 5760)]), datas))
+    streams = [R.JpegStream(datas[i % distinct]) for i in range(distinct * copies)]
+    out = t.full((len(streams), 1080, 5760), 0xA5, dtype=t.uint8, device="cuda")
+    imgs = [R.make_image([out[i].data_ptr()], [5760]) for i in range(len(streams))]
+    two_round_dec.set_profiling(True)
+    st = two_round_dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs)
+    tm = two_round_dec.last_timings()
+    two_round_dec.set_profiling(False)
+    assert st == 0, R.error_name(st)
+    assert tm["lean_k1"] == 1 and tm["lean_five"] == 0 and tm["lean_split"] == 0
+    ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
+    bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
+    assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
+
+
 def test_c2_1024_default_pipelined_layout(dec):
     t = torch()
     distinct, copies = 256, 4
@@ -103,8 +144,11 @@ def test_c2_1024_default_pipelined_layout(dec):
     dec.set_profiling(False)
     assert st == 0, R.error_name(st)
     assert tm["images"] == 1024 and tm["intervals"] == 1024 * 68
-    # the layout the bench runs: lean K1, one launch, longest intervals first
+    # the layout the bench runs: lean K1, one launch, longest intervals first; the 4,096 intervals
+    # past one round of four decoder waves per CU run as fifth waves (rj_huff.hip k_huff<RJ_HL_DEC5>)
     assert tm["lean_k1"] == 1 and tm["pipe_groups"] == 1 and tm["split_intervals"] == 0
+    cu = t.cuda.get_device_properties(0).multi_processor_count
+    assert tm["lean_five"] == int(256 * cu < 1024 * 68 <= 320 * cu)
     ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
     bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
     assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
