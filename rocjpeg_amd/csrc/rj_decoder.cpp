@@ -161,6 +161,7 @@ int Decoder::Initialize() {
   if (const char *l = getenv("RJ_K1_SOLO")) k1_solo_lds_ = uint32_t(std::max(0, atoi(l)));
   if (const char *so = getenv("RJ_SPLIT_OUTLIERS")) outlier_split_ = atoi(so) != 0;
   if (const char *f5 = getenv("RJ_K1_FIVE")) five_waves_ = atoi(f5);
+  if (const char *t5 = getenv("RJ_K1_SPLIT5_T")) split5_t_ = atof(t5);
   if (const char *kc = getenv("RJ_K1_CHUNK")) k1_chunk_ = atoi(kc) != 0;
   if (const char *cm = getenv("RJ_CHUNK_MIN")) chunk_min_ = uint32_t(std::max(16, atoi(cm)));
   if (const char *hy = getenv("RJ_K1_HYP")) hyp_max_ = uint32_t(std::max(1, atoi(hy)));
@@ -1781,26 +1782,77 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // overflow one round of four decoder waves per CU by at most one wave per CU (C2: 69,632
   // intervals on 65,536 lanes) gives the last workgroups -- the shortest intervals of the round --
   // a fifth decoder wave with the overflow (the longest overflow wave beside the shortest round)
-  // instead of a second round that starts only when the first workgroups finish ----
+  // instead of a second round that starts only when the first workgroups finish.  The longest
+  // intervals (above split5_t_ of the longest, while the waves still fit) are decoded by a head and
+  // a tail lane in the same launch (32 pairs per wave, first): the chain that sets K1's time is
+  // then the longest interval left whole ----
   static_assert(RJ_HL_DEC5 == 256 + 64, "five-wave layout: one overflow wave per workgroup");
-  uint32_t nl_five = 0;
+  uint32_t nl_five = 0, nsplit5 = 0;
   if (lean && sorted && lanes_desc && ngroups == 1 && !any_split && nsplit == 0 && five_waves_) {
-    const uint64_t round = uint64_t(cu_count_) * 256;
-    if (seg_total > round && seg_total - round <= uint64_t(cu_count_) * 64) {
-      const uint32_t cu = uint32_t(cu_count_), ntail = uint32_t((seg_total - round + 63) / 64);
+    const uint32_t cu = uint32_t(cu_count_);
+    const uint64_t round = uint64_t(cu) * 256;
+    if (seg_total > round && seg_total <= uint64_t(cu) * RJ_HL_DEC5) {
+      uint32_t ns = 0;
+      uint64_t cap = 0;
+      if (split5_t_ > 0.0) {
+        std::vector<uint2> &sl = sc_.seg_len;
+        sl.resize(seg_total);
+        uint32_t g = 0;
+        for (int i = 0; i < n; i++)
+          for (const uint64_t v : streams[i]->plan().seg_lenblk) sl[g++] = uint2{uint32_t(v), uint32_t(v >> 32)};
+        const double lim = double(sl[lane_seg[0]].x) * split5_t_;
+        while (ns < seg_total) {
+          const uint32_t len = sl[lane_seg[ns]].x;
+          if (len < RJ_SPLIT_MIN_BYTES || double(len) <= lim) break;
+          ns++;
+        }
+        while (ns > 0 && (ns + 31) / 32 + (seg_total - ns + 63) / 64 > 5ull * cu) ns = ns > 32 ? ns - 32 : 0;
+        for (uint32_t j = 0; j < ns; j++) {
+          const uint2 v = sl[lane_seg[j]];
+          cap = std::max<uint64_t>(cap, rj_group(8ull * (v.x - rj_split_byte(v.x)) + v.y +
+                                                 uint64_t(RJ_MAX_BLK_MCU) * RJ_ENT_PER_BLOCK + 1));
+        }
+      }
+      const uint32_t wsp = (ns + 31) / 32, wav = wsp + uint32_t((seg_total - ns + 63) / 64);
+      const uint32_t host = wav > 4 * cu ? wav - 4 * cu : 0u;  // workgroups that take a fifth wave
       nl_five = cu * RJ_HL_DEC5;
       std::vector<uint32_t> &l5 = sc_.lane_split;
       l5.assign(nl_five, UINT32_MAX);
-      for (uint32_t w = 0; w < cu; w++) {
+      uint32_t top = 0;  // global waves holding split pairs: [0, top)
+      for (uint32_t k = 0; k < wav; k++) {
         // a workgroup that takes a fifth wave lists its four in reverse (shortest first): the
         // fifth decoder wave shares a SIMD with the first (waves go to the SIMDs in order)
-        const bool rev = five_waves_ == 2 && w >= cu - ntail;
-        for (uint32_t q = 0; q < 4; q++)
-          std::memcpy(&l5[uint64_t(w) * RJ_HL_DEC5 + q * 64], &lane_seg[uint64_t(w) * 256 + (rev ? 3 - q : q) * 64], 64 * 4);
+        uint32_t w, q;
+        if (k < 4 * cu) {
+          w = k / 4;
+          q = k % 4;
+          if (five_waves_ == 2 && w >= cu - host) q = 3 - q;
+        } else {
+          w = cu - 1 - (k - 4 * cu);
+          q = 4;
+        }
+        uint32_t *dst = &l5[uint64_t(w) * RJ_HL_DEC5 + q * 64];
+        if (k < wsp) {  // 32 heads, then their 32 tails
+          for (uint32_t i = 0; i < 32 && k * 32 + i < ns; i++) {
+            dst[i] = lane_seg[k * 32 + i] | RJ_LANE_HEAD;
+            dst[32 + i] = lane_seg[k * 32 + i] | RJ_LANE_TAIL;
+          }
+          top = std::max(top, w * 5 + q + 1);
+        } else {
+          const uint64_t j0 = ns + uint64_t(k - wsp) * 64;
+          std::memcpy(dst, &lane_seg[j0], std::min<uint64_t>(64, seg_total - j0) * 4);
+        }
       }
-      for (uint32_t t = 0; t < ntail; t++) {
-        const uint32_t w = cu - 1 - t, g0 = uint32_t(round) + t * 64, cnt = std::min<uint32_t>(64, seg_total - g0);
-        std::memcpy(&l5[uint64_t(w) * RJ_HL_DEC5 + 256], &lane_seg[g0], uint64_t(cnt) * 4);
+      if (ns > 0) {  // tail regions by global wave (rj_huff.hip: pair slot (g >> 6) * 32 + (g & 31))
+        nsplit5 = ns;
+        hsplit.ent = AlignUp(ent_total, RJ_ENT_GROUP);
+        hsplit.cap = cap;
+        RJ_CHECK(d_entries_.Ensure((hsplit.ent + uint64_t(top) * 32 * cap + RJ_ENT_SLACK) * 4));
+        RJ_CHECK(d_piece_.Ensure(2ull * seg_total * sizeof(RjPiece)));
+        cbuf.ent = d_entries_.as<uint32_t>();
+        cbuf.piece = d_piece_.as<RjPiece>();
+        cbuf.piece_shift = 1;  // interval s: pieces 2s (head) and 2s + 1 (tail)
+        timings_.lean_split = ns;
       }
     }
   }
@@ -1876,7 +1928,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   } else {
     if (lean) {  // no split interval: one pass, no resolution / serial stages
       RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, nsplit ? nl_split : (nl_five ? nl_five : seg_total), k1_src,
-                             d_tabs, d_lean, cbuf, k1_solo_lds_, nsplit ? &hsplit : nullptr, nl_five != 0));
+                             d_tabs, d_lean, cbuf, k1_solo_lds_, (nsplit || nsplit5) ? &hsplit : nullptr, nl_five != 0));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
     } else {

@@ -126,6 +126,8 @@ class Decoder {
   bool k1_chunk_ = true;           // env RJ_K1_CHUNK=0: chunk-layout calls take k_entropy's K1 (A/B)
   int five_waves_ = 2;             // env RJ_K1_FIVE: 0 a lean call's overflow past one round of lanes runs as a second round;
                                    // 1 fifth waves; 2 fifth waves beside their workgroup's shortest wave
+  double split5_t_ = 0.8;          // env RJ_K1_SPLIT5_T (0: off): five-wave lean calls split the intervals above this share of
+                                   // the longest, as many as the five waves per CU hold
   bool outlier_split_ = true;      // env RJ_SPLIT_OUTLIERS=0: never split the outlier intervals (one decoder wave per SIMD)
   double outlier_t_ = 9.0 / 16;    // env RJ_SPLIT_OUTLIER_T: outliers are longer than this share of the longest interval
   double outlier_frac_ = 0.7;      // env RJ_SPLIT_OUTLIER_FRAC: at most this share of the intervals split in that mode

@@ -112,6 +112,7 @@ struct Nav {
   uint32_t seg, pj;         // interval (image-relative) and piece within it
   int32_t dcd[3];           // DC correction of the current piece, per component
   uint32_t skip;            // blocks at cur() to pass over before the piece (lean split tails)
+  uint32_t term;            // 1: a lean split tail that may end before its blocks (terminator check)
   __device__ __forceinline__ uint64_t cur() const { return uint64_t(cur_hi) << 32 | cur_lo; }
   __device__ __forceinline__ void set_cur(uint64_t v) {
     cur_lo = U(uint32_t(v));
@@ -125,7 +126,12 @@ struct Nav {
     dcd[1] = int32_t(U(uint32_t(p.dcd[1])));
     dcd[2] = int32_t(U(uint32_t(p.dcd[2])));
     skip = 0;
+    term = 0;
   }
+};
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
 };
 
 // Expand the next `nb` blocks of the entry streams into the zeroed LDS blocks [0, nb) (block j
@@ -181,7 +187,11 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
         pb = coefs.piece + U(rj_seg_lane0_k<kSplit>(coefs, im.seg_prefix + nv.seg));
       }
       nv.take(pb + nv.pj);
-      if (kRaw && kSplit && nv.pj > 0) nv.skip = U(gp(pb + nv.pj)->npieces);  // a split interval's tail
+      if (kRaw && kSplit && nv.pj > 0) {  // a split interval's tail: skip count, bit 31 may end early
+        const uint32_t f = U(gp(pb + nv.pj)->npieces);
+        nv.skip = f & 0x7FFFFFFFu;
+        nv.term = f >> 31;
+      }
       win.load(ent, nv.cur(), lane);
       win.settle();
     }
@@ -196,7 +206,9 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
     const uint32_t st_lim4 = (pass || lim_s < 0) ? 0u : uint32_t(lim_s) * 4u;
     const uint32_t end4 = uint32_t(lim_s) * 4u;  // rel4 of the block past the piece
     // one pass over the window in registers; true when the piece ends inside it
-    auto walk = [&]() __attribute__((always_inline)) -> bool {
+    // kT: the terminator check of a lean split tail that may end early (only those pay for it)
+    auto walk = [&](auto kT) __attribute__((always_inline)) -> bool {
+      constexpr bool kTerm = kRaw && kSplit && decltype(kT)::value;
 #pragma unroll
       for (int r = 0; r < RJ_WIN_ROWS; r++) {
         const uint32_t e = win.w[r];
@@ -218,12 +230,12 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
         // a split interval's tail piece may end early (its lane stopped at libjpeg's
         // insufficient-data point): the piece's remaining blocks are zero blocks, and nothing
         // after its terminator belongs to the stream
-        const uint64_t term = (kRaw && kSplit) ? __ballot(p == 127 && ord < piece) : 0ull;
+        const uint64_t term = kTerm ? __ballot(p == 127 && ord < piece) : 0ull;
         const int tl = term ? __ffsll((long long)term) - 1 : 64;
         // the entry's block in the strip, and from its lane: LDS base, quantiser row (whole wave)
         // (ds_bpermute takes the source lane from address bits [7:2]: rel mod 64, no masking)
         const uint32_t info = kPairs ? uint32_t(__builtin_amdgcn_ds_bpermute(int(rel4), int(lane_info))) : 0u;
-        if (rel4 < st_lim4 && p < 64u && (!(kRaw && kSplit) || int(lane) < tl)) {
+        if (rel4 < st_lim4 && p < 64u && (!kTerm || int(lane) < tl)) {
           int v = int(int16_t(e & 0xFFFFu));  // lean entries: K1 applied HUFF_EXTEND
           if constexpr (kPairs) {
             // component-interleaved s_qw[3 p + c]: (a/4) mod 32 banks; info >> 16 = 4 c (bytes)
@@ -291,7 +303,7 @@ __device__ __forceinline__ void parse_blocks(const RjImageDev &im, const RjCoefB
         win.load(ent, (uint64_t(win.base_hi) << 32 | win.base_lo) + RJ_WIN_ROWS * 64u, lane);
         win.settle();
       }
-      found = walk();
+      found = (kRaw && kSplit && nv.term) ? walk(BoolC<true>{}) : walk(BoolC<false>{});
     }
     if (pass) {
       nv.skip = 0;

@@ -239,7 +239,10 @@ __host__ __device__ constexpr uint32_t hl_align(uint32_t bytes) { return (bytes 
       const bool act = blocks_left > 0;                                                                   \
       blocks_left -= (bend && act) ? 1u : 0u;                                                             \
       skip = skip || (bend && bn == 0u && (0u - q) > nbits);                                              \
-      if (kSplit) blocks_left = (skip && tail) ? 0u : blocks_left; /* K2 zero-fills a short tail */       \
+      if (kSplit) { /* a tail stops at libjpeg's insufficient-data point (K2 zero-fills a short tail) */ \
+        tdone = (skip && tail && blocks_left != 0u) ? blocks - blocks_left : tdone;                         \
+        blocks_left = (skip && tail) ? 0u : blocks_left;                                                    \
+      }                                                                                                   \
     } else {                                                                                              \
       blocks_left -= bend ? 1u : 0u;                                                                      \
     }                                                                                                     \
@@ -249,6 +252,7 @@ __host__ __device__ constexpr uint32_t hl_align(uint32_t bytes) { return (bytes 
       mleft = ms ? blocks_left : mleft;                                                                   \
       mseen = mseen || ms;                                                                                \
       recs[min(nr, kRec) * kPairs] = uint16_t(0u - q);                                                     \
+      if (kRecNe) rnes[min(nr, kRec) * kPairs] = uint16_t(ne); /* the tail's entries before that MCU */   \
       nr += (ms && nr < kRec) ? 1u : 0u;                                                                  \
     }                                                                                                     \
     e = en;                                                                                               \
@@ -287,9 +291,9 @@ __device__ __forceinline__ void lds_wr(uint32_t a, uint32_t v) { *(lds_u32 *)(ui
 // head decodes from the interval start; past the split it compares each MCU start with the
 // tail's records.  Huffman codes resynchronise: at the first equal MCU start both decoders are in
 // the same state, so the head stops there and the interval becomes two pieces -- the head's
-// blocks before that MCU, and the tail's blocks after its first (record + 1) MCUs (the skip, in
-// the tail piece's npieces field; lean raw entries carry DC differences, so no DC correction is
-// needed).  With no equal MCU start the head decodes the whole interval.  A tail that reaches libjpeg's insufficient-data point stops: K2 zero-fills
+// blocks before that MCU, and the tail's blocks after its first (record + 1) MCUs: the tail notes
+// its entry count with each record, so its piece starts at that entry and K2 walks no skipped
+// blocks (lean raw entries carry DC differences, so no DC correction is needed).  With no equal MCU start the head decodes the whole interval.  A tail that reaches libjpeg's insufficient-data point stops: K2 zero-fills
 // the piece's missing blocks exactly as libjpeg's zero blocks.
 template <int DEC, int GROUP, bool kSplit, int PHASE>
 __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
@@ -312,8 +316,14 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
   __shared__ uint32_t s_dec[DEC];  // decoder -> mover: ring words fully consumed (RJ_HL_FIN: done)
   __shared__ uint32_t s_mov[DEC];  // mover -> decoder: 16-B chunks committed to the ring
   constexpr uint32_t kRec = RJ_HL_REC;  // MCU-start records per tail lane
+  // the tail's entry count with each record, so its piece starts past the skipped MCUs (not in
+  // the two-workgroups-per-CU instance: two workgroups must fit in LDS; its tail pieces carry the
+  // skip, which K2 walks)
+  constexpr bool kRecNe = kSplit && GROUP >= RJ_HL_GROUP;
   __shared__ uint16_t s_rec[kSplit ? kRec + 1 : 1][kPairs];  // tail lanes' MCU-start records (+ scratch)
+  __shared__ uint16_t s_rne[kRecNe ? kRec + 1 : 1][kRecNe ? kPairs : 1];  // ... and the tail's entry count at each
   __shared__ uint32_t s_nrec[kPairs];  // records published by the tail (bit 31: no more will come)
+  __shared__ uint32_t s_tdone[kPairs];  // blocks a tail decoded before it stopped (0xFFFFFFFF: never stopped)
   __shared__ uint32_t s_T, s_ne;
   const uint32_t tid = threadIdx.x;
   const bool mover = tid >= uint32_t(DEC);
@@ -424,8 +434,9 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     const uint32_t lut_a = lds_addr(s_lut), lut_dc = lut_a + RJ_HL_DC0;
     // split state: records (tail), the last MCU start seen (head), the head's scan over the records
     uint16_t *const recs = &s_rec[0][kSplit ? pair : 0u];
+    uint16_t *const rnes = &s_rne[0][kRecNe ? pair : 0u];
     uint32_t nr = tail ? 0u : kRec;
-    uint32_t mpos = 0, mleft = 0, jrec = 0, blk_head = 0, skip_tail = 0;
+    uint32_t mpos = 0, mleft = 0, jrec = 0, blk_head = 0, ne_tail = 0, skip_tail = 0, tdone = 0xFFFFFFFFu;
     bool mseen = false, synced = false, checking = head;
     const uint32_t sp_bits = sp_byte * 8u;
     if (tail) lds_st(&s_nrec[pair], 0u);
@@ -522,7 +533,9 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
             synced = true;  // same state from here on: the rest is the tail's
             checking = false;
             blk_head = blocks - mleft;
-            skip_tail = (jrec + 1) * nblk;  // record j: after the tail's first j + 1 MCUs
+            // record j: after the tail's first j + 1 MCUs, whose entries the tail piece starts past
+            if (kRecNe) ne_tail = *(const __attribute__((address_space(3))) volatile uint16_t *)(&rnes[jrec * kPairs]);
+            else skip_tail = (jrec + 1) * nblk;
             blocks_left = 0;
           } else if (jrec >= nrec && (pub >> 31) != 0) {
             checking = false;  // no record left to meet: the head decodes the whole interval
@@ -541,6 +554,7 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
       RJ_HL_T2;
     }
     lds_st(&s_dec[L], RJ_HL_FIN);
+    if (kSplit && tail) lds_st(&s_tdone[pair], tdone);  // before its head (same wave) writes the pieces
 #ifdef RJ_HL_STAMPS
     if ((tid & 63) == 0) {
       atomicAdd(&rj_hl_stamp[0], (unsigned long long)st_steps);
@@ -562,7 +576,12 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     if (!tail) {
       if (synced) {
         gp(piece)[0] = RjPiece{ent_abs, 0u, blk_head, 2u, {0, 0, 0}};
-        gp(piece)[1] = RjPiece{tail_abs, blk_head, blocks - blk_head, skip_tail, {0, 0, 0}};  // npieces: skip
+        // the tail piece's npieces: the blocks K2 passes over first (0 when the piece starts at
+        // the recorded entry), bit 31 when the tail stopped short of its blocks (K2 then checks
+        // for its terminator and zero-fills the rest)
+        const uint32_t need = (jrec + 1) * nblk + (blocks - blk_head);
+        const uint32_t early = lds_ld(&s_tdone[pair]) < need ? 0x80000000u : 0u;
+        gp(piece)[1] = RjPiece{tail_abs + ne_tail, blk_head, blocks - blk_head, skip_tail | early, {0, 0, 0}};
       } else {
         *gp(piece) = RjPiece{ent_abs, 0u, blocks, 1u, {0, 0, 0}};
       }
@@ -1199,7 +1218,10 @@ hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uin
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
                            RjCoefBuf coefs, uint32_t extra_lds, const RjHuffSplit *split, bool five_waves) {
   if (nlanes == 0) return hipSuccess;
-  if (split != nullptr) {  // outliers split: one decoder wave per SIMD, two workgroups per CU
+  if (split != nullptr && five_waves) {  // five-wave layout with split pairs first
+    hipLaunchKernelGGL((k_huff<RJ_HL_DEC5, RJ_HL_GROUP, true, RJ_HL_PHASE>), dim3((nlanes + RJ_HL_DEC5 - 1) / RJ_HL_DEC5),
+                       dim3(2 * RJ_HL_DEC5), 0, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs, *split);
+  } else if (split != nullptr) {  // outliers split: one decoder wave per SIMD, two workgroups per CU
     hipLaunchKernelGGL((k_huff<RJ_HL_SPLIT_DEC, 8, true, 4>), dim3((nlanes + RJ_HL_SPLIT_DEC - 1) / RJ_HL_SPLIT_DEC),
                        dim3(2 * RJ_HL_SPLIT_DEC), 0, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs,
                        *split);

@@ -148,7 +148,10 @@ def test_c2_1024_default_pipelined_layout(dec):
     # past one round of four decoder waves per CU run as fifth waves (rj_huff.hip k_huff<RJ_HL_DEC5>)
     assert tm["lean_k1"] == 1 and tm["pipe_groups"] == 1 and tm["split_intervals"] == 0
     cu = t.cuda.get_device_properties(0).multi_processor_count
-    assert tm["lean_five"] == int(256 * cu < 1024 * 68 <= 320 * cu)
+    five = 256 * cu < 1024 * 68 <= 320 * cu
+    assert tm["lean_five"] == int(five)
+    # ... with the longest intervals as head + tail lanes in the same launch (RJ_K1_SPLIT5_T)
+    assert (tm["lean_split"] > 0) == five
     ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
     bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
     assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
