@@ -127,6 +127,72 @@ def test_c2_1024_two_round_layout(two_round_dec):
     assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
 
 
+@pytest.fixture(scope="module")
+def split5_dec():
+    """A handle whose five-wave lean calls split as many of their longest intervals as the five
+    waves per CU hold (RJ_K1_SPLIT5_T near 0, read at handle creation)."""
+    torch()
+    old = os.environ.get("RJ_K1_SPLIT5_T")
+    os.environ["RJ_K1_SPLIT5_T"] = "0.05"
+    try:
+        d = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    finally:
+        if old is None:
+            del os.environ["RJ_K1_SPLIT5_T"]
+        else:
+            os.environ["RJ_K1_SPLIT5_T"] = old
+    yield d
+    d.close()
+
+
+def _damaged(data, seed):
+    """A C2 stream with bytes flipped inside its entropy-coded data (corrupt codes, desynchronised
+    intervals), or truncated mid-scan (libjpeg's insufficient-data path)."""
+    s = data.index(b"\xff\xda")
+    s += 2 + int.from_bytes(data[s + 2:s + 4], "big")
+    e = len(data) - 2
+    rng = np.random.default_rng(seed)
+    if seed % 2:
+        cut = s + int((e - s) * (0.3 + 0.6 * rng.random()))
+        if data[cut - 1] == 0xFF:
+            cut -= 1
+        return data[:cut] + b"\xff\xd9"
+    buf = bytearray(data)
+    for pos in rng.integers(s + 64, e - 64, 40):
+        if buf[pos] != 0xFF and buf[pos - 1] != 0xFF and buf[pos + 1] != 0x00:
+            nb = buf[pos] ^ (1 << int(rng.integers(0, 8)))
+            if nb != 0xFF:
+                buf[pos] = nb
+    return bytes(buf)
+
+
+def test_c2_1024_split5_damaged(split5_dec):
+    """The five-wave lean launch with its longest intervals split (head + tail lanes in the same
+    launch) over a C2 batch with damaged streams: a tail that runs out of data short of its piece
+    writes libjpeg's zero blocks itself; every image equal to the oracle."""
+    t = torch()
+    distinct, copies = 64, 16
+    datas = _c2_images(48, seed0=2024)
+    datas += [_damaged(datas[k], k) for k in range(16)]
+    with ThreadPoolExecutor(16) as ex:
+        want = list(ex.map(lambda d: O.oracle_decode(d, int(R.OutputFormat.RGB), [(1080, 5760)]), datas))
+    assert all(st == 0 for st, _ in want)
+    streams = [R.JpegStream(datas[i % distinct]) for i in range(distinct * copies)]
+    out = t.full((len(streams), 1080, 5760), 0xA5, dtype=t.uint8, device="cuda")
+    imgs = [R.make_image([out[i].data_ptr()], [5760]) for i in range(len(streams))]
+    split5_dec.set_profiling(True)
+    st = split5_dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs)
+    tm = split5_dec.last_timings()
+    split5_dec.set_profiling(False)
+    assert st == 0, R.error_name(st)
+    cu = t.cuda.get_device_properties(0).multi_processor_count
+    if 256 * cu < tm["intervals"] <= 320 * cu:
+        assert tm["lean_five"] == 1 and tm["lean_split"] > 0
+    ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
+    bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
+    assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
+
+
 def test_c2_1024_default_pipelined_layout(dec):
     t = torch()
     distinct, copies = 256, 4
