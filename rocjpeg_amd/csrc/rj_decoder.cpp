@@ -1787,7 +1787,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // a tail lane in the same launch (32 pairs per wave, first): the chain that sets K1's time is
   // then the longest interval left whole ----
   static_assert(RJ_HL_DEC5 == 256 + 64, "five-wave layout: one overflow wave per workgroup");
-  uint32_t nl_five = 0, nsplit5 = 0;
+  uint32_t nl_five = 0, nsplit5 = 0, nsplit_rows = 0;
   if (lean && sorted && lanes_desc && ngroups == 1 && !any_split && nsplit == 0 && five_waves_) {
     const uint32_t cu = uint32_t(cu_count_);
     const uint64_t round = uint64_t(cu) * 256;
@@ -1845,6 +1845,22 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       }
       if (ns > 0) {  // tail regions by global wave (rj_huff.hip: pair slot (g >> 6) * 32 + (g & 31))
         nsplit5 = ns;
+        // every interval one MCU row: the split intervals' rows go to the split-aware K2 instance
+        // as an explicit (image, row) list after the lane list, the rest to the plain instance
+        bool row_ivals = true;
+        for (int i = 0; i < n && row_ivals; i++) row_ivals = imgs[i].ri_mcus == imgs[i].mcux;
+        if (row_ivals && nl_five + 2ull * ns <= n_lane_seg) {
+          std::vector<uint8_t> &mark = sc_.split_mark;  // split intervals, then a pass in image order
+          mark.assign(seg_total, 0);
+          for (uint32_t j = 0; j < ns; j++) mark[lane_seg[j]] = 1;
+          l5.resize(nl_five + 2ull * ns);
+          uint2 *sr = reinterpret_cast<uint2 *>(l5.data() + nl_five);
+          uint32_t k = 0;
+          for (int i = 0; i < n; i++)
+            for (uint32_t r = 0; r < imgs[i].nseg; r++)
+              if (mark[imgs[i].seg_prefix + r]) sr[k++] = uint2{uint32_t(i), r};
+          nsplit_rows = k;
+        }
         hsplit.ent = AlignUp(ent_total, RJ_ENT_GROUP);
         hsplit.cap = cap;
         RJ_CHECK(d_entries_.Ensure((hsplit.ent + uint64_t(top) * 32 * cap + RJ_ENT_SLACK) * 4));
@@ -1866,7 +1882,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     cbuf.seg_ent = reinterpret_cast<const unsigned long long *>(dbase + off_seg_ent);
   } else if (sorted) {  // lanes in length order; pieces stay at the interval's own slot
     if (nsplit) std::memcpy(h + off_lane_seg, sc_.lane_split.data(), uint64_t(nl_split) * 4);
-    else if (nl_five) std::memcpy(h + off_lane_seg, sc_.lane_split.data(), uint64_t(nl_five) * 4);
+    else if (nl_five) std::memcpy(h + off_lane_seg, sc_.lane_split.data(), uint64_t(sc_.lane_split.size()) * 4);
     else std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(seg_total) * 4);
     cbuf.lane_seg = d_lane_seg;
     cbuf.seg_lane0 = nullptr;
@@ -1876,7 +1892,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   }
   // part B: everything up to the row lists, or only the lane list actually used
   const uint64_t blob_b = (!any_split && sorted && ngroups == 1)
-                              ? std::min<uint64_t>(blob, AlignUp(off_lane_seg + uint64_t(nsplit ? nl_split : (nl_five ? nl_five : seg_total)) * 4, 256))
+                              ? std::min<uint64_t>(blob, AlignUp(off_lane_seg + uint64_t(nsplit ? nl_split : (nl_five ? nl_five + 2 * nsplit_rows : seg_total)) * 4, 256))
                               : blob;
   if (blob_b > blob_a) RJ_HIP(hipMemcpyAsync(dbase + blob_a, h + blob_a, blob_b - blob_a, hipMemcpyHostToDevice, stream_));
 
@@ -1945,7 +1961,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
     wide(fused_rows, wcnt, wlist, false, false);
 #ifndef RJ_EXP_SKIP_K2  // timing build: K0 + K1 only (the output is not written)
-    RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr, wcnt, wlist));
+    RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr, wcnt, wlist,
+                      nsplit_rows ? reinterpret_cast<const uint2 *>(dbase + off_lane_seg + uint64_t(nl_five) * 4) : nullptr,
+                      nsplit_rows));
 #endif
     wide(general_rows, wcnt, wlist, true, false);
     RJ_HIP(LaunchRows(stream_, true, d_imgs, n, d_grows, nullptr, general_rows, cbuf, d_tabs,
@@ -2101,6 +2119,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       timings_.k1_launch_ms_sum = timings_.entropy_chunks_ms;
       timings_.k1_launches = (lanes_wg ? 1u : 0u) + (lanes_dev ? 1u : 0u);
       timings_.k2_launch_ms_sum = ms[3];
+      // (a split call's fused rows run as two launches, plain then split-aware, counted as one:
+      // together they are the K2 of the batch, and their rocprofv3 averages add up to it)
       timings_.k2_launches = (fused_rows ? 1u : 0u) + (general_rows ? 1u : 0u);
       if (!lean) {  // (the lean launch has no resolution: the flags are another call's)
         std::vector<uint32_t> fb(seg_total);

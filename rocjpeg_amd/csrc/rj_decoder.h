@@ -167,7 +167,7 @@ class Decoder {
     std::vector<uint32_t> tab_of, row_prefix, grow_prefix, seg_lane0, lane_seg, bucket_pos, seg_pos, lane_split;
     std::vector<uint2> seg_len;  // per interval: destuffed bytes, blocks (outlier split planning)
     std::vector<uint16_t> seg_bkt;  // per interval: 32-B length bucket (outlier split planning)
-    std::vector<uint8_t> is_fused, row_group, routed;
+    std::vector<uint8_t> is_fused, row_group, routed, split_mark;
     std::vector<uint2> row_list;
     std::vector<uint32_t> prow_prefix, pgrow_prefix, prog_lanes, prog_bucket;  // progressive images
     std::vector<RjFoldJob> fold_jobs;

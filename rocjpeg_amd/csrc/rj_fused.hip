@@ -671,7 +671,11 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
       // every load of the row's start is then one dependent step from the row record)
       nv.seg = my;
       nv.pj = 0;
-      nv.take(coefs.piece + rj_seg_lane0_k<kSplit>(coefs, U(im.seg_prefix) + my));
+      const RjPiece *p0 = coefs.piece + rj_seg_lane0_k<kSplit>(coefs, U(im.seg_prefix) + my);
+      // plain instance in a lean split call (LaunchRows split_rows): a split interval's row is
+      // the split-aware launch's
+      if (!kSplit && !kWide && coefs.piece_shift != 0 && U(gp(p0)->npieces) == 2u) return;
+      nv.take(p0);
     } else {
       nv.seg = U(ri ? (my * mcux) / ri : 0);
       const RjSegDev sg = gp(im.segs)[nv.seg];
@@ -1013,9 +1017,25 @@ hipError_t LaunchRowsFix(hipStream_t st, bool to_planes, bool dense, const RjIma
 
 hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
                       const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
-                      uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list) {
+                      uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list, const uint2 *split_rows,
+                      uint32_t nsplit_rows) {
   if (nrows == 0) return hipSuccess;
-  if (coefs.piece_shift != 0) {  // lean split launch: pieces with skips / early terminators
+  if (coefs.piece_shift != 0 && split_rows != nullptr) {  // plain rows, then the split intervals' rows
+    const uint32_t *no_prefix = nullptr;
+    if (to_planes) {
+      hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs, tabsets,
+                         planes, wide_cnt, wide_list);
+      if (nsplit_rows)
+        hipLaunchKernelGGL((k_rows<true, false, true>), dim3(nsplit_rows), dim3(64), 0, st, imgs, nimg, no_prefix,
+                           split_rows, coefs, tabsets, planes, wide_cnt, wide_list);
+    } else {
+      hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs, tabsets,
+                         planes, wide_cnt, wide_list);
+      if (nsplit_rows)
+        hipLaunchKernelGGL((k_rows<false, false, true>), dim3(nsplit_rows), dim3(64), 0, st, imgs, nimg, no_prefix,
+                           split_rows, coefs, tabsets, planes, wide_cnt, wide_list);
+    }
+  } else if (coefs.piece_shift != 0) {  // lean split launch: pieces with skips / early terminators
     if (to_planes)
       hipLaunchKernelGGL((k_rows<true, false, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list,
                          coefs, tabsets, planes, wide_cnt, wide_list);

@@ -55,9 +55,13 @@ hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobD
 // wide_cnt (zero on entry) / wide_list (nrows slots): this launch's fix-up list; rows with
 // coefficients outside the int32 IDCT's exact domain are recorded there (and coefs.wide_flag
 // raised) for the host to issue LaunchRowsFix after the call's kernels.
+// split_rows (a lean split call whose every interval is one MCU row): the rows of the split
+// intervals, decoded by the split-aware instance; every other row by the plain instance, whose
+// waves leave at once on a split interval's row (two launches).
 hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
                       const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
-                      uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list);
+                      uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list, const uint2 *split_rows = nullptr,
+                      uint32_t nsplit_rows = 0);
 // The fix-up launch of one K2 launch's list (same variant; cap = that launch's rows).
 hipError_t LaunchRowsFix(hipStream_t st, bool to_planes, bool dense, const RjImageDev *imgs, int nimg, RjCoefBuf coefs,
                          const RjTableSet *tabsets, uint8_t *planes, const uint32_t *wide_cnt, const uint2 *wide_list,

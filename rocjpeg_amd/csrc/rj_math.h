@@ -57,7 +57,7 @@ __device__ __forceinline__ uint32_t rj_seg_lane0(const RjCoefBuf &c, uint32_t se
 // the same where the kernel instance knows the layout (kSplit: a lean split launch, piece_shift 1)
 template <bool kSplit>
 __device__ __forceinline__ uint32_t rj_seg_lane0_k(const RjCoefBuf &c, uint32_t seg) {
-  return c.seg_lane0 ? *gp(c.seg_lane0 + seg) : (kSplit ? seg << 1 : seg);
+  return c.seg_lane0 ? *gp(c.seg_lane0 + seg) : (kSplit ? seg << 1 : seg << c.piece_shift);
 }
 
 // Inclusive prefix sum over the wave's 64 lanes (DPP: row shifts, then row broadcasts; gfx9).
