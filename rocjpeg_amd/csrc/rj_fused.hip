@@ -33,6 +33,9 @@ namespace rj {
 #ifndef RJ_K2_OCC
 #define RJ_K2_OCC 4  // K2 waves per SIMD the register budget is set for (128 VGPRs)
 #endif
+#ifndef RJ_K2_DENSE_OCC
+#define RJ_K2_DENSE_OCC 3  // the progressive (dense, int32 IDCT) K2: 168 VGPRs, no spills
+#endif
 
 #ifdef RJ_EXP_STAMPS  // diagnostic build: cycles per K2 phase, summed over waves (rj_decoder.cpp prints)
 __device__ unsigned long long rj_stamp[8];
@@ -969,6 +972,22 @@ __global__ __launch_bounds__(64, RJ_K2_OCC) void k_rows(const RjImageDev *__rest
   row_body<kPlanes, kDense, false, kSplit>(imgs, i, my, coefs, tabsets, planes, s_buf, s_qw, wide_cnt, wide_list);
 }
 
+// K2 of progressive images (dense coefficients, int32 IDCT) with its own register budget
+template <bool kPlanes>
+__global__ __launch_bounds__(64, RJ_K2_DENSE_OCC) void k_rows_dense(const RjImageDev *__restrict__ imgs, int nimg,
+                                                                   const uint32_t *__restrict__ row_prefix,
+                                                                   const uint2 *__restrict__ row_list, RjCoefBuf coefs,
+                                                                   const RjTableSet *__restrict__ tabsets,
+                                                                   uint8_t *__restrict__ planes, uint32_t *wide_cnt,
+                                                                   uint2 *wide_list) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];
+  __shared__ __attribute__((aligned(16))) uint32_t s_qw[3 * 64];
+  int i;
+  uint32_t my;
+  row_of_block(imgs, nimg, row_prefix, row_list, blockIdx.x, i, my);
+  row_body<kPlanes, true, false, false>(imgs, i, my, coefs, tabsets, planes, s_buf, s_qw, wide_cnt, wide_list);
+}
+
 // K2 fix-up: the rows a K2 launch recorded (a strip outside the int32 IDCT's exact domain --
 // corrupt data with large quantisers), decoded again with the 64-bit IDCT for those strips.
 // Issued by the host only when a K2 launch of the call raised the host-mapped flag
@@ -1058,11 +1077,11 @@ hipError_t LaunchRowsDense(hipStream_t st, bool to_planes, const RjImageDev *img
   if (nrows == 0) return hipSuccess;
   const uint2 *no_list = nullptr;
   if (to_planes)
-    hipLaunchKernelGGL((k_rows<true, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, no_list,
-                       coefs, tabsets, planes, wide_cnt, wide_list);
+    hipLaunchKernelGGL(k_rows_dense<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, no_list, coefs,
+                       tabsets, planes, wide_cnt, wide_list);
   else
-    hipLaunchKernelGGL((k_rows<false, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, no_list,
-                       coefs, tabsets, planes, wide_cnt, wide_list);
+    hipLaunchKernelGGL(k_rows_dense<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, no_list, coefs,
+                       tabsets, planes, wide_cnt, wide_list);
   return hipGetLastError();
 }
 
