@@ -33,6 +33,9 @@ namespace rj {
 #ifndef RJ_K2_OCC
 #define RJ_K2_OCC 4  // K2 waves per SIMD the register budget is set for (128 VGPRs)
 #endif
+#ifndef RJ_K2_SPLIT_OCC
+#define RJ_K2_SPLIT_OCC 3  // the split-aware instance (lean split calls): 133 VGPRs, no spills
+#endif
 #ifndef RJ_K2_DENSE_OCC
 #define RJ_K2_DENSE_OCC 3  // the progressive (dense, int32 IDCT) K2: 168 VGPRs, no spills
 #endif
@@ -972,6 +975,22 @@ __global__ __launch_bounds__(64, RJ_K2_OCC) void k_rows(const RjImageDev *__rest
   row_body<kPlanes, kDense, false, kSplit>(imgs, i, my, coefs, tabsets, planes, s_buf, s_qw, wide_cnt, wide_list);
 }
 
+// K2 of lean split calls' rows (pieces, skips, early-ending tails) with its own register budget
+template <bool kPlanes>
+__global__ __launch_bounds__(64, RJ_K2_SPLIT_OCC) void k_rows_split(const RjImageDev *__restrict__ imgs, int nimg,
+                                                                   const uint32_t *__restrict__ row_prefix,
+                                                                   const uint2 *__restrict__ row_list, RjCoefBuf coefs,
+                                                                   const RjTableSet *__restrict__ tabsets,
+                                                                   uint8_t *__restrict__ planes, uint32_t *wide_cnt,
+                                                                   uint2 *wide_list) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];
+  __shared__ __attribute__((aligned(16))) uint32_t s_qw[3 * 64];
+  int i;
+  uint32_t my;
+  row_of_block(imgs, nimg, row_prefix, row_list, blockIdx.x, i, my);
+  row_body<kPlanes, false, false, true>(imgs, i, my, coefs, tabsets, planes, s_buf, s_qw, wide_cnt, wide_list);
+}
+
 // K2 of progressive images (dense coefficients, int32 IDCT) with its own register budget
 template <bool kPlanes>
 __global__ __launch_bounds__(64, RJ_K2_DENSE_OCC) void k_rows_dense(const RjImageDev *__restrict__ imgs, int nimg,
@@ -1045,21 +1064,21 @@ hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, in
       hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs, tabsets,
                          planes, wide_cnt, wide_list);
       if (nsplit_rows)
-        hipLaunchKernelGGL((k_rows<true, false, true>), dim3(nsplit_rows), dim3(64), 0, st, imgs, nimg, no_prefix,
+        hipLaunchKernelGGL(k_rows_split<true>, dim3(nsplit_rows), dim3(64), 0, st, imgs, nimg, no_prefix,
                            split_rows, coefs, tabsets, planes, wide_cnt, wide_list);
     } else {
       hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs, tabsets,
                          planes, wide_cnt, wide_list);
       if (nsplit_rows)
-        hipLaunchKernelGGL((k_rows<false, false, true>), dim3(nsplit_rows), dim3(64), 0, st, imgs, nimg, no_prefix,
+        hipLaunchKernelGGL(k_rows_split<false>, dim3(nsplit_rows), dim3(64), 0, st, imgs, nimg, no_prefix,
                            split_rows, coefs, tabsets, planes, wide_cnt, wide_list);
     }
   } else if (coefs.piece_shift != 0) {  // lean split launch: pieces with skips / early terminators
     if (to_planes)
-      hipLaunchKernelGGL((k_rows<true, false, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list,
+      hipLaunchKernelGGL(k_rows_split<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list,
                          coefs, tabsets, planes, wide_cnt, wide_list);
     else
-      hipLaunchKernelGGL((k_rows<false, false, true>), dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list,
+      hipLaunchKernelGGL(k_rows_split<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list,
                          coefs, tabsets, planes, wide_cnt, wide_list);
   } else if (to_planes) {
     hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs,
