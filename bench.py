@@ -225,8 +225,11 @@ def pmc_traffic(kernel, batch, launches, workload="c2"):
     try:
         with open(path) as f:
             prof = json.load(f)
-        k = prof["kernels"][kernel]
-        return int(k["hbm_bytes_per_image"] * batch / max(1, launches)), f"profiles/{name} ({prof.get('commit', '?')})"
+        ks = prof["kernels"]
+        per_image = ks[kernel]["hbm_bytes_per_image"]
+        if kernel == "k_rows":  # a lean split call's K2: the plain and split-aware launches together
+            per_image += ks.get("k_rows_split", {}).get("hbm_bytes_per_image", 0.0)
+        return int(per_image * batch / max(1, launches)), f"profiles/{name} ({prof.get('commit', '?')})"
     except (OSError, KeyError, ValueError):
         return None
 
