@@ -198,7 +198,9 @@ struct RjSegDev {
 // K0 work unit: up to RJ_DS_BLOCK raw bytes of one interval.  The host parser knows where every
 // stuffed byte is (its marker scan visits each FF), so each block's output offset is known up
 // front and the blocks are independent.
+#ifndef RJ_DS_BLOCK
 #define RJ_DS_BLOCK 2048u
+#endif
 struct RjDsBlock {
   uint32_t src_off;   // ECS-relative raw offset
   uint32_t len;       // raw bytes

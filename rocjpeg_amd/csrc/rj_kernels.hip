@@ -38,7 +38,7 @@ __device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v, uint32_t &to
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ imgs, int nimg,
                                                 uint8_t *__restrict__ destuffed, const uint32_t *__restrict__ ds_map) {
-  static_assert(RJ_DS_BLOCK == 2048u, "8 chunks of 256 B per block");
+  static_assert(RJ_DS_BLOCK % 256u == 0 && RJ_DS_BLOCK <= 4096u, "256-B chunks, all loads issued up front");
   constexpr int kIt = RJ_DS_BLOCK / 256;
   const uint32_t g = blockIdx.x;
   const uint32_t lane = threadIdx.x;
