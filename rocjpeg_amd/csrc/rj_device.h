@@ -172,8 +172,11 @@ __host__ __device__ inline uint64_t rj_chunk_cap(uint32_t clen) {
 // entries reserved for an interval at parse time: one serial stream (zero-bit decode of the
 // last MCU after the data ends, then one zero DC entry per skipped block) -- an exact lane's
 // output, or the serial re-decode of a split interval the resolution failed
+#ifndef RJ_EXP_ENT_PER_BYTE
+#define RJ_EXP_ENT_PER_BYTE 8ull  // (timing probes only: a smaller reservation is unsafe for arbitrary tables)
+#endif
 __host__ __device__ inline uint64_t rj_interval_entries(uint32_t bytes, uint64_t blocks, uint32_t nblk_mcu) {
-  return rj_group(8ull * bytes + blocks + uint64_t(nblk_mcu) * RJ_ENT_PER_BLOCK + 1);
+  return rj_group(RJ_EXP_ENT_PER_BYTE * bytes + blocks + uint64_t(nblk_mcu) * RJ_ENT_PER_BLOCK + 1);
 }
 // the chunk regions of an interval a call cuts into nch chunks, one per lane (RjCoefBuf.seg_ent:
 // placed by the call after the images' serial regions; lane offset o's region at o x cap)
