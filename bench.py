@@ -859,6 +859,9 @@ def main():
                                "split_intervals": t["split_intervals"], "serial_fallbacks": t["serial_fallbacks"],
                                "entry_bytes_per_image": round(t["entry_bytes"] / n), "lean_k1": t["lean_k1"],
                                "lean_split": t["lean_split"], "lean_five": t.get("lean_five", 0), "chunk_k1": t["chunk_k1"]},
+            "live_rows": {"live": t["live"], "rows_beside_k1": t["live_rows"], "rows_after_k1": t["rest_rows"],
+                          "gave_up": t["live_pad"], "live_span_ms": round(t["live_ms"], 4),
+                          "after_k1_span_ms": round(t["rest_ms"], 4)},
             "end_to_end_algorithmic_GBps": round(imgs_total * per_img / elapsed / 1e9, 2),
             "host_input_images_per_s_per_gpu": round(host_rate, 1) if host_rate else None,
             "parse_images_per_s": {"host_1_thread": round(parse_host_rate, 1),

@@ -117,6 +117,12 @@ typedef struct {
   /* 1: the lean K1 ran five decoder waves per CU (the overflow past one round of four as fifth
      waves, rj_huff.hip k_huff<RJ_HL_DEC5>) */
   uint32_t lean_five;
+  /* live rows (K2 beside K1 inside the call): 1 when the call ran them; the rows the live K2
+     decoded while K1 ran, the rows the stream-ordered K2 took after it; the live K2's launch span
+     (from its stream's start, when K1 starts, to its last row) and the stream-ordered K2's span
+     after K1 (rows no ticket took, synced split rows), HIP events on each launch's stream */
+  uint32_t live, live_rows, rest_rows, live_pad;
+  float live_ms, rest_ms;
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);
@@ -247,7 +253,7 @@ RocJpegStatus rocJpegAmdGetCoalesceStats(uint64_t *calls, uint64_t *combined, ui
  * 3: the resident sharded entry points; the work-table broadcast carries a status header.
  * 4: RocJpegAmdTimings.chunk_k1.  5: RocJpegAmdTimings.chunk_bytes (the call's chunk length).
  * 6: rocJpegAmdGetCoalesceStats, rocJpegAmdGetLastParseTimings, RocJpegAmdTimings.chunk_hyp. */
-#define ROCJPEG_AMD_ABI_VERSION 6
+#define ROCJPEG_AMD_ABI_VERSION 7
 RocJpegStatus rocJpegAmdGetAbiVersion(int *version);
 
 #if defined(__cplusplus)

@@ -26,7 +26,7 @@ EXT_SYMBOLS = (
     "rocJpegAmdShardCreate", "rocJpegAmdShardDecode", "rocJpegAmdShardGetImages", "rocJpegAmdShardDestroy",
     "rocJpegAmdGetAbiVersion", "rocJpegAmdStreamGetLeanTables",
 )
-ABI_VERSION = 6  # include/rocjpeg_amd.h ROCJPEG_AMD_ABI_VERSION
+ABI_VERSION = 7  # include/rocjpeg_amd.h ROCJPEG_AMD_ABI_VERSION
 
 
 class Status(enum.IntEnum):  # api/rocjpeg.h:53-67
@@ -108,7 +108,9 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("routed_images", ctypes.c_uint32), ("lean_k1", ctypes.c_uint32),
                 ("wide_rows", ctypes.c_uint32), ("lean_split", ctypes.c_uint32),
                 ("chunk_k1", ctypes.c_uint32), ("chunk_bytes", ctypes.c_uint32),
-                ("chunk_hyp", ctypes.c_uint32), ("lean_five", ctypes.c_uint32)]
+                ("chunk_hyp", ctypes.c_uint32), ("lean_five", ctypes.c_uint32),
+                ("live", ctypes.c_uint32), ("live_rows", ctypes.c_uint32), ("rest_rows", ctypes.c_uint32),
+                ("live_pad", ctypes.c_uint32), ("live_ms", ctypes.c_float), ("rest_ms", ctypes.c_float)]
 
 
 class RocJpegAmdInterval(ctypes.Structure):  # include/rocjpeg_amd.h

@@ -261,7 +261,8 @@ RJ_EXPORT RocJpegStatus rocJpegAmdGetCoalesceStats(uint64_t *calls, uint64_t *co
 
 RJ_EXPORT RocJpegStatus rocJpegAmdGetLastParseTimings(RocJpegHandle handle, double *ms, int count) {
   if (handle == nullptr || ms == nullptr || count < 0) return ROCJPEG_STATUS_INVALID_PARAMETER;
-  const double *t = AsDecoder(handle)->last_scan_ms();
+  double t[6];
+  AsDecoder(handle)->last_scan_ms(t);
   for (int i = 0; i < count && i < 6; i++) ms[i] = t[i];
   return ROCJPEG_STATUS_SUCCESS;
 }

@@ -90,27 +90,39 @@ bool Enabled() {
   return on;
 }
 
-// The group's calls as one call on `dec`; on failure each call alone (its own status).
+// The group's calls as one call on `dec`.  Each member is first checked as its own call would
+// be (Decoder::Check: the host validation a decode runs before any device work); a member that
+// fails there gets that status at once and stays out of the combined call, so one caller's bad
+// stream or destination costs the others nothing.  Should the combined call still fail (a device
+// error), each remaining call is decoded alone and gets its own status.
 void RunGroup(Decoder *dec, std::vector<Request *> &group) {
   if (group.size() == 1) {
     Request *r = group[0];
     r->status = dec->Decode(r->streams, r->n, r->params, r->dst);
     return;
   }
+  std::vector<Request *> ok;
+  ok.reserve(group.size());
+  for (Request *r : group) {
+    r->status = dec->Check(r->streams, r->n, r->params, r->dst);
+    if (r->status == 0) ok.push_back(r);
+  }
+  if (ok.empty()) return;
+  if (ok.size() == 1) {
+    ok[0]->status = dec->Decode(ok[0]->streams, ok[0]->n, ok[0]->params, ok[0]->dst);
+    return;
+  }
   g_combined.fetch_add(1, std::memory_order_relaxed);
-  g_members.fetch_add(group.size(), std::memory_order_relaxed);
+  g_members.fetch_add(ok.size(), std::memory_order_relaxed);
   std::vector<Stream *> streams;
   std::vector<RocJpegImage> dst;
-  for (Request *r : group) {
+  for (Request *r : ok) {
     streams.insert(streams.end(), r->streams, r->streams + r->n);
     dst.insert(dst.end(), r->dst, r->dst + r->n);
   }
-  const int st = dec->Decode(streams.data(), int(streams.size()), group[0]->params, dst.data());
-  if (st == 0) {
-    for (Request *r : group) r->status = 0;
-    return;
-  }
-  for (Request *r : group) r->status = dec->Decode(r->streams, r->n, r->params, r->dst);
+  const int st = dec->Decode(streams.data(), int(streams.size()), ok[0]->params, dst.data());
+  if (st == 0) return;
+  for (Request *r : ok) r->status = dec->Decode(r->streams, r->n, r->params, r->dst);
 }
 
 }  // namespace
@@ -125,10 +137,21 @@ int CoalescedDecode(Decoder *dec, int device, Stream *const *streams, int n, con
   Request me{dec, streams, n, params, dst};
   std::unique_lock<std::mutex> lk(q.mu);
   const Clock::time_point now = Clock::now();
-  q.seen[std::this_thread::get_id()] = now;
+  q.seen[std::this_thread::get_id()] = now;  // (may throw: nothing is queued yet)
   if (q.seen.size() > 256)
     for (auto it = q.seen.begin(); it != q.seen.end();) it = now - it->second > kRecent ? q.seen.erase(it) : ++it;
   q.pending.push_back(&me);
+  // `me` lives on this stack: should anything below throw while it is still queued (not yet in a
+  // group), it leaves the queue before the unwind (the lock is held wherever that can happen)
+  struct Unqueue {
+    DeviceQueue &q;
+    Request &me;
+    ~Unqueue() {
+      if (me.taken) return;
+      auto it = std::find(q.pending.begin(), q.pending.end(), &me);
+      if (it != q.pending.end()) q.pending.erase(it);
+    }
+  } unqueue{q, me};
   q.arrive.notify_all();
   while (!me.done) {
     // a call already in another leader's group only waits for it; a queued call leads when a
@@ -155,8 +178,10 @@ int CoalescedDecode(Decoder *dec, int device, Stream *const *streams, int n, con
         continue;
       }
     }
-    // the oldest waiting call and every other with the same parameters, up to kMaxImages
+    // the oldest waiting call and every other with the same parameters, up to kMaxImages (the
+    // group's storage first: no allocation may fail once a member is marked taken)
     std::vector<Request *> group;
+    group.reserve(q.pending.size());
     int images = 0;
     const RocJpegDecodeParams p0 = *q.pending.front()->params;
     for (auto it = q.pending.begin(); it != q.pending.end();) {

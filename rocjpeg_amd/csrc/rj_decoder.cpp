@@ -125,6 +125,11 @@ Decoder::~Decoder() {
         if (arr[q]) (void)hipEventDestroy(arr[q]);
     for (auto &q : pstream_)
       if (q) (void)hipStreamDestroy(q);
+    for (auto &e : live_ev_)
+      if (e) (void)hipEventDestroy(e);
+    for (auto &e : live_t_)
+      if (e) (void)hipEventDestroy(e);
+    if (lstream_) (void)hipStreamDestroy(lstream_);
     (void)hipStreamDestroy(stream_);
   }
   if (h_wide_flag_) (void)hipHostFree(h_wide_flag_);
@@ -174,6 +179,17 @@ int Decoder::Initialize() {
   RJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_wide_flag_), h_wide_flag_, 0));
   *reinterpret_cast<volatile uint32_t *>(h_wide_flag_) = 0;
   for (auto &q : pstream_) RJ_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+  {
+    int lo = 0, hi = 0;  // "least" is the numerically greatest
+    RJ_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    RJ_HIP(hipStreamCreateWithPriority(&lstream_, hipStreamNonBlocking, lo));
+  }
+  for (auto &e : live_ev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto &e : live_t_) RJ_HIP(hipEventCreate(&e));
+  if (const char *lk = getenv("RJ_K2_LIVE")) {  // 0 off; 2 (test): the live launch always gives up
+    live_k2_ = atoi(lk) != 0;  // 1: on
+    live_test_giveup_ = atoi(lk) == 2;
+  }
   for (auto &e : pev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : pk1_) RJ_HIP(hipEventCreate(&e));
   for (auto &e : kev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -245,25 +261,37 @@ int Decoder::StreamsToDevice(Stream *const *streams, int n) {
 int Decoder::ParseOnDevice(Stream *const *streams, const uint8_t *const *data, const size_t *len, int n) {
   std::lock_guard<std::mutex> lock(mu_);
   if (streams == nullptr || data == nullptr || len == nullptr || n < 0) return kInvalidParameter;
-  const int st = ParseOnDeviceImpl(streams, data, len, n);
-  // Whatever ended the call (a header that failed to parse, a HIP error), no stream is left
-  // half-parsed: a stream whose header walk deferred its marker scan gets the host scan.
-  for (int i = 0; i < n; i++) {
-    Stream *s = streams[i];
-    if (s != nullptr && s->scan_pending() && data[i] != nullptr) s->Parse(data[i], uint32_t(len[i]));
+  // Whatever ended the call (a header that failed to parse, a HIP error, an exception from a
+  // host worker), no stream is left half-parsed: a stream whose header walk deferred its marker
+  // scan gets the host scan.
+  auto settle = [&] {
+    for (int i = 0; i < n; i++) {
+      Stream *s = streams[i];
+      if (s != nullptr && s->scan_pending() && data[i] != nullptr) s->Parse(data[i], uint32_t(len[i]));
+    }
+  };
+  int st;
+  try {
+    st = ParseOnDeviceImpl(streams, data, len, n);
+  } catch (...) {
+    settle();
+    throw;
   }
+  settle();
   return st;
 }
 
 int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *data, const size_t *len, int n) {
   RJ_HIP(hipSetDevice(device_));
   const auto t0 = std::chrono::steady_clock::now();
+  for (double &x : scan_ms_) x = 0;  // a call that fails early reports no stages of an earlier one
+  timings_.scan_device_streams = timings_.scan_host_fallbacks = 0;
   for (int i = 0; i < n; i++)
     if (streams[i] == nullptr || data[i] == nullptr) return kInvalidParameter;
   // ---- host: headers only (O(header) per stream), over the handle's host threads ----
   std::vector<uint8_t> hdr(size_t(n), 0);  // 1: device scan pending, 2: parsed otherwise, 0: bad
   {
-    const int nt = n >= 64 ? pool_.threads() : 1;
+    const int nt = n >= 64 ? pool_.threads() : 1;  // small batches stay on the calling thread
     const int per = (n + nt * 4 - 1) / (nt * 4);
     pool_.Run((n + per - 1) / per,
               [&](int t) {
@@ -275,7 +303,7 @@ int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *dat
                   hdr[size_t(i)] = s->scan_pending() ? 1 : 2;
                 }
               },
-              nullptr);
+              nullptr, nt == 1);
   }
   std::vector<int> pend;
   for (int i = 0; i < n; i++) {
@@ -457,7 +485,7 @@ int Decoder::ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *dat
                   s->resident = r;
                 }
               },
-              nullptr);
+              nullptr, nt == 1);
   }
   timings_.scan_device_streams = ndev.load();
   timings_.scan_host_fallbacks = nfall.load();
@@ -523,6 +551,43 @@ int Decoder::Decode(Stream *const *streams, int n, const RocJpegDecodeParams *pa
   // re-parse or destroy cannot recycle memory a DMA is still reading
   if (r != kOk) (void)hipStreamSynchronize(stream_);
   return r;
+}
+
+// The destination channels an output format needs (rocjpeg_decoder.cpp:143-180; DecodeLocked's
+// job builder makes the same checks as it lays out the jobs).
+static int CheckDestination(int fmt, int css, const RocJpegImage &o) {
+  auto need = [&](int c) { return o.channel[c] != nullptr; };
+  switch (fmt) {
+    case ROCJPEG_OUTPUT_YUV_PLANAR:
+      if (!need(0)) return kInvalidParameter;
+      if ((css == kCss422 || css == kCss420 || css == kCss444 || css == kCss440) && (!need(1) || !need(2)))
+        return kInvalidParameter;
+      return kOk;
+    case ROCJPEG_OUTPUT_Y:
+    case ROCJPEG_OUTPUT_RGB:
+      return need(0) ? kOk : kInvalidParameter;
+    case ROCJPEG_OUTPUT_RGB_PLANAR:
+      return (need(0) && need(1) && need(2)) ? kOk : kInvalidParameter;
+    default:
+      return kOk;  // NATIVE writes what it has channels for; unknown formats write nothing
+  }
+}
+
+int Decoder::Check(Stream *const *streams, int n, const RocJpegDecodeParams *params, const RocJpegImage *dst) {
+  if (streams == nullptr || params == nullptr || dst == nullptr || n < 0) return kInvalidParameter;
+  for (int i = 0; i < n; i++) {
+    if (streams[i] == nullptr) return kInvalidParameter;
+    std::lock_guard<std::mutex> sl(streams[i]->mutex());
+    const DecodePlan &p = streams[i]->plan();
+    if (p.status != 0) return p.status;
+    if (streams[i]->scan_pending()) return kBadJpeg;
+  }
+  for (int i = 0; i < n; i++) {
+    std::lock_guard<std::mutex> sl(streams[i]->mutex());
+    const int st = CheckDestination(int(params->output_format), streams[i]->info().css, dst[i]);
+    if (st != kOk) return st;
+  }
+  return kOk;
 }
 
 // progressive images per call up to which every scan goes to the wave grid (see prog_wave_all)
@@ -1252,7 +1317,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t off_wide = AlignUp(off_lean + ((lean || hc) ? tabs.size() * sizeof(RjLeanTables) : 0), 256);
   // K0's block -> image map: the image holding block 64 k, for k <= ds_total / 64 (+ a sentinel)
   const uint32_t n_dsmap = ds_total / 64u + 2u;
-  const uint64_t off_dsmap = AlignUp(off_wide + kWideSites * sizeof(uint32_t), 256);
+  const uint64_t off_live = AlignUp(off_wide + kWideSites * sizeof(uint32_t), 64);
+  const uint64_t off_live_cu = AlignUp(off_live + RJ_LIVE_CTRS * sizeof(uint32_t), 256);
+  const uint64_t off_dsmap = AlignUp(off_live_cu + RJ_LIVE_CU_KEYS * sizeof(uint32_t), 256);
   const uint64_t off_stage = AlignUp(off_dsmap + n_dsmap * sizeof(uint32_t), 256);
   const uint64_t blob_a = AlignUp(off_stage + stage_bytes, 256);
   // (a lean launch may split intervals: head + tail lanes, up to 2 per interval + one wave of padding)
@@ -1297,6 +1364,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // profiles/r5_experiments/k1_hyp_small_calls_warm.txt)
   if (hyp > 1 && !hyp_warm_) cbuf.warm_shift = 31u;
   cbuf.seg_ent = nullptr;  // set with the split layout below
+  cbuf.wide_cap = 0;       // set per fix-up site (wide() below)
   if (profiling_) {
     RJ_CHECK(d_count_.Ensure(256));
     cbuf.count = d_count_.as<unsigned long long>();
@@ -1453,6 +1521,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint2 *d_row_list = reinterpret_cast<const uint2 *>(dbase + off_row_list);
   const uint32_t *d_lane_seg = reinterpret_cast<const uint32_t *>(dbase + off_lane_seg);
   std::memset(h + off_wide, 0, kWideSites * sizeof(uint32_t));
+  std::memset(h + off_live, 0, RJ_LIVE_CTRS * sizeof(uint32_t));
+  std::memset(h + off_live_cu, 0, RJ_LIVE_CU_KEYS * sizeof(uint32_t));
   {
     uint32_t *map = reinterpret_cast<uint32_t *>(h + off_dsmap);
     for (uint32_t k = 0; k < n_dsmap; k++) map[k] = uint32_t(n - 1);
@@ -1467,6 +1537,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // the next K2 launch's fix-up list: its counter and `rows` slots
   auto wide = [&](uint32_t rows, uint32_t *&cnt, uint2 *&list, bool planes, bool dense) {
     cnt = d_wide_cnt + std::min<int>(int(wide_sites_.size()), kWideSites - 1);
+    cbuf.wide_cap = rows;  // the launches that follow (until the next site) append at most this many
     list = d_wide_.as<uint2>() + wide_used;
     wide_used += rows;
     if (rows) wide_sites_.push_back({planes, dense, rows, cnt, list});
@@ -1906,6 +1977,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
             ms(t_host0, t_dedupe), ms(t_dedupe, t_layout), ms(t_layout, t_lanes), ms(t_lanes, t_k0),
             ms(t_k0, t_end));
   }
+  bool live = false;
+  RjLive lv{};
+  *reinterpret_cast<volatile uint32_t *>(h_wide_flag_ + 1) = 0;  // a lost live row (never expected)
   if (ngroups > 1) {
     RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0 and upload B done
     for (int g = 0; g < ngroups; g++) {
@@ -1943,8 +2017,40 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     for (int g = 0; g + 1 < ngroups; g++) RJ_HIP(hipStreamWaitEvent(stream_, pev_[g], 0));
   } else {
     if (lean) {  // no split interval: one pass, no resolution / serial stages
-      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, nsplit ? nl_split : (nl_five ? nl_five : seg_total), k1_src,
-                             d_tabs, d_lean, cbuf, k1_solo_lds_, (nsplit || nsplit5) ? &hsplit : nullptr, nl_five != 0));
+      const uint32_t k1_lanes = nsplit ? nl_split : (nl_five ? nl_five : seg_total);
+      // live rows (rj_device.h RjLive): K2 beside K1 when every row is one interval of a fused
+      // baseline image and the whole K1 grid is resident at once (one workgroup per CU)
+      const uint32_t k1_dec = nl_five ? uint32_t(RJ_HL_DEC5) : 256u;
+      const uint32_t k1_groups = (k1_lanes + k1_dec - 1) / k1_dec;
+      bool rows_one_ival = true;
+      for (int i = 0; i < n && rows_one_ival; i++) rows_one_ival = imgs[i].ri_mcus == imgs[i].mcux && imgs[i].mcuy < (1u << RJ_LIVE_ROW_BITS);
+      live = live_k2_ && rows_one_ival && nsplit == 0 && (nsplit5 == 0 || nsplit_rows > 0) && prog_images == 0 &&
+             general_rows == 0 && fused_rows > 0 && fused_images == uint32_t(n) && k1_groups <= uint32_t(cu_count_) &&
+             n < (1 << (32 - RJ_LIVE_ROW_BITS));
+      if (live) {
+        const size_t had = d_live_.capacity();
+        RJ_CHECK(d_live_.Ensure(uint64_t(fused_rows) * sizeof(unsigned long long)));
+        if (d_live_.capacity() != had)  // fresh slots: no tag may match an epoch by chance
+          RJ_HIP(hipMemsetAsync(d_live_.as<void>(), 0, d_live_.capacity(), stream_));
+        lv.slot = d_live_.as<unsigned long long>();
+        lv.ctr = reinterpret_cast<uint32_t *>(dbase + off_live);
+        lv.cu_busy = reinterpret_cast<uint32_t *>(dbase + off_live_cu);
+        lv.epoch = epoch_;
+        lv.k1_groups = live_test_giveup_ ? 0xFFFFFFFFu : k1_groups;
+        lv.k1_waves = k1_groups * (k1_dec / 64u);
+        lv.rows = fused_rows;
+        RJ_HIP(hipEventRecord(live_ev_[0], stream_));  // descriptors and lane lists uploaded, K0 done
+        RJ_HIP(hipStreamWaitEvent(lstream_, live_ev_[0], 0));
+      }
+      RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, k1_lanes, k1_src, d_tabs, d_lean, cbuf, k1_solo_lds_,
+                             (nsplit || nsplit5) ? &hsplit : nullptr, nl_five != 0, live ? &lv : nullptr));
+      if (live) {
+        wide(fused_rows, wcnt, wlist, false, false);  // one list: the live, rest and split launches decode disjoint rows
+        if (profiling_) RJ_HIP(hipEventRecord(live_t_[0], lstream_));
+        RJ_HIP(LaunchRowsLive(lstream_, d_imgs, n, lv, cbuf, d_tabs, wcnt, wlist));
+        if (profiling_) RJ_HIP(hipEventRecord(live_t_[1], lstream_));
+        RJ_HIP(hipEventRecord(live_ev_[1], lstream_));
+      }
       if (profiling_) RJ_HIP(hipEventRecord(ev_[6], stream_));
       if (profiling_) RJ_HIP(hipEventRecord(ev_[7], stream_));
     } else {
@@ -1959,12 +2065,20 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       }
     }
     if (profiling_) RJ_HIP(hipEventRecord(ev_[3], stream_));
-    wide(fused_rows, wcnt, wlist, false, false);
+    const uint2 *split_rows = nsplit_rows ? reinterpret_cast<const uint2 *>(dbase + off_lane_seg + uint64_t(nl_five) * 4) : nullptr;
+    if (live) {  // the published rows no live ticket took, the synced split rows, then join the live K2
+      if (profiling_) RJ_HIP(hipEventRecord(live_t_[2], stream_));
+      RJ_HIP(LaunchRowsRest(stream_, d_imgs, n, lv, cbuf, d_tabs, wcnt, wlist));
+      RJ_HIP(LaunchRowsSplit(stream_, d_imgs, n, split_rows, nsplit_rows, cbuf, d_tabs, wcnt, wlist));
+      if (profiling_) RJ_HIP(hipEventRecord(live_t_[3], stream_));
+      RJ_HIP(hipStreamWaitEvent(stream_, live_ev_[1], 0));
+    } else {
+      wide(fused_rows, wcnt, wlist, false, false);
 #ifndef RJ_EXP_SKIP_K2  // timing build: K0 + K1 only (the output is not written)
-    RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr, wcnt, wlist,
-                      nsplit_rows ? reinterpret_cast<const uint2 *>(dbase + off_lane_seg + uint64_t(nl_five) * 4) : nullptr,
-                      nsplit_rows));
+      RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr, wcnt, wlist,
+                        split_rows, nsplit_rows));
 #endif
+    }
     wide(general_rows, wcnt, wlist, true, false);
     RJ_HIP(LaunchRows(stream_, true, d_imgs, n, d_grows, nullptr, general_rows, cbuf, d_tabs,
                       d_planes_.as<uint8_t>(), wcnt, wlist));
@@ -1976,6 +2090,20 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(hipMemcpy2DAsync(rc.user, rc.pitch, d_route_.as<uint8_t>() + rc.off, rc.pitch, rc.row_bytes, rc.rows,
                             hipMemcpyDefault, stream_));
   RJ_HIP(hipStreamSynchronize(stream_));
+  if (live && *reinterpret_cast<volatile uint32_t *>(h_wide_flag_ + 1)) {
+    // a live K2 workgroup gave up on its row (never expected; rj_fused.hip live_claim): decode
+    // every row again in stream order, then redo the output stage -- all idempotent
+    *reinterpret_cast<volatile uint32_t *>(h_wide_flag_ + 1) = 0;
+    RJ_ERR("live rows: a row was not published in time; the call's rows are decoded again");
+    wide(fused_rows, wcnt, wlist, false, false);
+    RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr, wcnt, wlist,
+                      nsplit_rows ? reinterpret_cast<const uint2 *>(dbase + off_lane_seg + uint64_t(nl_five) * 4) : nullptr,
+                      nsplit_rows));
+    for (const RouteCopy &rc : routes_)
+      RJ_HIP(hipMemcpy2DAsync(rc.user, rc.pitch, d_route_.as<uint8_t>() + rc.off, rc.pitch, rc.row_bytes, rc.rows,
+                              hipMemcpyDefault, stream_));
+    RJ_HIP(hipStreamSynchronize(stream_));
+  }
   timings_.wide_rows = 0;
   if (*reinterpret_cast<volatile uint32_t *>(h_wide_flag_)) {
     // rows outside the int32 IDCT's exact domain (corrupt data, large quantisers): decode them
@@ -2145,6 +2273,19 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
           fprintf(stderr, "[rj prog] level %u: %u lanes, %.3f ms\n", L, prog_level_off[L + 1] - prog_level_off[L], t);
         }
       }
+    }
+    timings_.live = live ? 1u : 0u;
+    timings_.live_rows = timings_.rest_rows = 0;
+    timings_.live_ms = timings_.rest_ms = 0.0f;
+    if (live) {
+      uint32_t c[RJ_LIVE_CTRS];
+      RJ_HIP(hipMemcpy(c, lv.ctr, sizeof(c), hipMemcpyDeviceToHost));
+      const uint32_t pub = std::min(c[RJ_LIVE_RESERVED], lv.rows);
+      timings_.live_rows = std::min(c[RJ_LIVE_FINAL], pub);
+      timings_.rest_rows = pub - timings_.live_rows;
+      timings_.live_pad = c[RJ_LIVE_GIVEUP];
+      RJ_HIP(hipEventElapsedTime(&timings_.live_ms, live_t_[0], live_t_[1]));
+      RJ_HIP(hipEventElapsedTime(&timings_.rest_ms, live_t_[2], live_t_[3]));
     }
     unsigned long long cnt = 0;
     RJ_HIP(hipMemcpy(&cnt, cbuf.count, sizeof(cnt), hipMemcpyDeviceToHost));

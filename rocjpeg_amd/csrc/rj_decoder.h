@@ -52,16 +52,27 @@ class Decoder {
   int Initialize();
   int GetImageInfo(Stream *s, uint8_t *nc, RocJpegChromaSubsampling *css, uint32_t *w, uint32_t *h);
   int Decode(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
+  // The host-side validation Decode runs before any device work (stream status, destination
+  // channels the format needs), without decoding: the status Decode would return for these images
+  // if it fails there, else kOk (rj_coalesce.cpp pre-validates a combined call's members).
+  int Check(Stream *const *streams, int n, const RocJpegDecodeParams *params, const RocJpegImage *dst);
   int StreamsToDevice(Stream *const *streams, int n);
   // rocJpegStreamParse + rocJpegAmdStreamsToDevice for a batch, with the O(bytes) marker scan
   // (FF D9 end, restart intervals, destuffing tables) on this handle's GPU (rj_scan.hip)
   int ParseOnDevice(Stream *const *streams, const uint8_t *const *data, const size_t *len, int n);
   void SetProfiling(bool on) { profiling_ = on; }
   void SetPathPolicy(int p) { path_policy_ = p; }
-  RocJpegAmdTimings last_timings() const { return timings_; }
+  // (copies under the handle's lock: a concurrent call on the handle writes them)
+  RocJpegAmdTimings last_timings() {
+    std::lock_guard<std::mutex> lock(mu_);
+    return timings_;
+  }
   // the last ParseOnDevice call's stages, ms: headers, resident allocation, staging copy + upload,
   // jobs upload + kernel + read-back, adoption, total
-  const double *last_scan_ms() const { return scan_ms_; }
+  void last_scan_ms(double out[6]) {
+    std::lock_guard<std::mutex> lock(mu_);
+    for (int k = 0; k < 6; k++) out[k] = scan_ms_[k];
+  }
   hipStream_t stream() const { return stream_; }
   int device() const { return device_; }
   // a call on this handle may be decoded inside another handle's combined call (rj_coalesce.h):
@@ -149,6 +160,15 @@ class Decoder {
   hipEvent_t kev_[kMaxPipe] = {};  // K1 of class g done (K2 of later classes waits on it)
   hipEvent_t k1s_[kMaxPipe] = {}, k2s_[kMaxPipe] = {}, k2e_[kMaxPipe] = {};  // profiling: launch spans
   DeviceBuffer d_count_;  // profiling: entries written by K1
+  // live rows (rj_device.h RjLive): K2 beside the lean five-wave K1 on lstream_ (lowest priority,
+  // so the stream-ordered kernels win dispatch arbitration); env RJ_K2_LIVE=1 turns it on (off by
+  // default: beside K1 it slowed K1 by more than it saved)
+  bool live_k2_ = false;
+  bool live_test_giveup_ = false;
+  hipStream_t lstream_ = nullptr;
+  hipEvent_t live_ev_[2] = {};  // fork (descriptors uploaded), join (the live K2 done)
+  hipEvent_t live_t_[4] = {};   // profiling: live K2 span (its stream), rest + split span (after K1)
+  DeviceBuffer d_live_;          // published-row slots
 
   // a run of non-resident streams whose parse-time pinned copies are adjacent (one DMA)
   struct PinRun {

@@ -80,6 +80,7 @@ struct RjCoefBuf {
   uint32_t warm_shift;        // k_huff_chunk warm-up: min(RJ_CHUNK_WARM_BYTES, chunk length >> warm_shift)
   const unsigned long long *seg_ent;  // per interval: first entry of its chunk regions (split ones)
   uint32_t hyp;               // MCU-phase hypotheses per speculative chunk (rj_chunk_lanes; 1: one lane per chunk)
+  uint32_t wide_cap;          // K2: slots of the launch's fix-up list (the launches sharing one decode disjoint rows)
 };
 // Lean K1 split launch (rj_huff.hip): an interval decoded by a head lane from its start and a
 // tail lane from rj_split_byte(dst_len); lane_seg entries carry the role in their top bits.
@@ -93,6 +94,42 @@ struct RjHuffSplit {
   uint64_t ent;  // first entry of the tail lanes' regions (pair p at ent + p * cap)
   uint64_t cap;  // entries per tail region
 };
+// K1 -> K2 hand-off inside one call (the "live" rows, rj_huff.hip hl_publish -> rj_fused.hip
+// k_rows_live): a lean five-wave K1 decoder wave that has written its intervals' entries and
+// pieces publishes those MCU rows (row images, one interval per row) into `slot`; K2 workgroups
+// on a second stream take tickets in publication order and decode each row as soon as it is
+// published, on the CUs whose K1 workgroup has finished.  A stream-ordered K2 after both takes
+// the rows no ticket reached (k_rows_rest).
+struct RjLive {
+  unsigned long long *slot;  // per published row: epoch | (image << 11 | MCU row) << 32 (8-B sc1 granule)
+  uint32_t *ctr;             // RJ_LIVE_* counters, zeroed per call in upload A
+  uint32_t *cu_busy;         // per CU (rj_live_cu_key): K1 workgroups running there (zeroed in upload A)
+  uint32_t epoch;            // this call's tag (never 0)
+  uint32_t k1_groups;        // K1 workgroups (all must be resident before any K2 waits on a row)
+  uint32_t k1_waves;         // K1 decoder waves (each reports once when it is done)
+  uint32_t rows;             // rows the K1 launch may publish (the K2 grid)
+};
+#define RJ_LIVE_RESERVED 0  // slots reserved by K1 (published rows, once K1 is done)
+#define RJ_LIVE_TICKET 1    // tickets taken by k_rows_live
+#define RJ_LIVE_STARTED 2   // K1 workgroups started
+#define RJ_LIVE_DONE 3      // K1 decoder waves done
+#define RJ_LIVE_ERROR 4     // a ticket holder gave up on its row (never expected)
+#define RJ_LIVE_GIVEUP 5    // K1 was not resident in time: the live launch leaves everything to k_rows_rest
+#define RJ_LIVE_FINAL 6     // tickets taken before K1's last wave closed the counter
+#define RJ_LIVE_CLOSED 0x80000000u  // RJ_LIVE_TICKET: no ticket is valid any more
+#define RJ_LIVE_CTRS 16     // counter words (64 B)
+#define RJ_LIVE_ROW_BITS 11 // MCU rows per image < 2^11 (16384 / 8)
+#define RJ_LIVE_CU_KEYS 2048  // XCC (4 bits of HW_REG_XCC_ID) x CU / SH / SE (bits 8..15 of HW_REG_HW_ID)
+// the CU this wave runs on, as an index below RJ_LIVE_CU_KEYS
+__device__ __forceinline__ uint32_t rj_live_cu_key() {
+#ifdef __HIP_DEVICE_COMPILE__
+  const uint32_t hw = __builtin_amdgcn_s_getreg((7 << 11) | (8 << 6) | 4);   // hwreg(HW_REG_HW_ID, 8, 8)
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // hwreg(HW_REG_XCC_ID, 0, 4)
+  return ((xcc & 7u) << 8) | (hw & 255u);
+#else
+  return 0;
+#endif
+}
 #define RJ_ENT_PER_BLOCK 64       // worst case: DC + 63 AC (each position written at most once)
 #define RJ_ENT_GROUP 16           // K1 writes entries in 64-B groups; regions are group-aligned
 #define RJ_ENT_TERM (127u << 16)  // end-of-stream marker

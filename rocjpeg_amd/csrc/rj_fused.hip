@@ -580,7 +580,8 @@ struct ImBytes {
 template <bool kPlanes, bool kDense, bool kWide = false, bool kSplit = false>
 __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, int i, uint32_t my, RjCoefBuf coefs,
                                          const RjTableSet *__restrict__ tabsets, uint8_t *__restrict__ planes,
-                                         uint8_t *s_buf, uint32_t *s_qw, uint32_t *wide_cnt, uint2 *wide_list) {
+                                         uint8_t *s_buf, uint32_t *s_qw, uint32_t *wide_cnt, uint2 *wide_list,
+                                         bool only_synced = false) {
   // the main instances dequantise in the entry scatter into the dot2 IDCT's pair layout; the
   // fix-up (kWide) and progressive (kDense) instances keep raw zigzag blocks and the int32 IDCT
   constexpr bool kPairs = !kDense && !kWide;
@@ -681,6 +682,9 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
       // plain instance in a lean split call (LaunchRows split_rows): a split interval's row is
       // the split-aware launch's
       if (!kSplit && !kWide && coefs.piece_shift != 0 && U(gp(p0)->npieces) == 2u) return;
+      // split-aware instance beside it: only the rows whose head met its tail (two pieces); a
+      // head that decoded its whole interval left one plain piece, the plain instance's
+      if (kSplit && only_synced && U(gp(p0)->npieces) != 2u) return;
       nv.take(p0);
     } else {
       nv.seg = U(ri ? (my * mcux) / ri : 0);
@@ -947,8 +951,10 @@ __device__ __forceinline__ void row_body(const RjImageDev *__restrict__ imgs, in
   }  // strips
   if constexpr (!kWide)
     if (row_wide && tid == 0) {
+      // (the launches sharing one list decode disjoint rows; the bound keeps a miscount from
+      // spilling into the next list)
       const uint32_t k = atomicAdd(wide_cnt, 1u);
-      wide_list[k] = make_uint2(uint32_t(i), my);
+      if (k < coefs.wide_cap) wide_list[k] = make_uint2(uint32_t(i), my);
       // host-mapped flag: the host issues the fix-up launches after the call's kernels
       __hip_atomic_store(coefs.wide_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -982,13 +988,14 @@ __global__ __launch_bounds__(64, RJ_K2_SPLIT_OCC) void k_rows_split(const RjImag
                                                                    const uint2 *__restrict__ row_list, RjCoefBuf coefs,
                                                                    const RjTableSet *__restrict__ tabsets,
                                                                    uint8_t *__restrict__ planes, uint32_t *wide_cnt,
-                                                                   uint2 *wide_list) {
+                                                                   uint2 *wide_list, uint32_t only_synced) {
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];
   __shared__ __attribute__((aligned(16))) uint32_t s_qw[3 * 64];
   int i;
   uint32_t my;
   row_of_block(imgs, nimg, row_prefix, row_list, blockIdx.x, i, my);
-  row_body<kPlanes, false, false, true>(imgs, i, my, coefs, tabsets, planes, s_buf, s_qw, wide_cnt, wide_list);
+  row_body<kPlanes, false, false, true>(imgs, i, my, coefs, tabsets, planes, s_buf, s_qw, wide_cnt, wide_list,
+                                        only_synced != 0);
 }
 
 // K2 of progressive images (dense coefficients, int32 IDCT) with its own register budget
@@ -1005,6 +1012,127 @@ __global__ __launch_bounds__(64, RJ_K2_DENSE_OCC) void k_rows_dense(const RjImag
   uint32_t my;
   row_of_block(imgs, nimg, row_prefix, row_list, blockIdx.x, i, my);
   row_body<kPlanes, true, false, false>(imgs, i, my, coefs, tabsets, planes, s_buf, s_qw, wide_cnt, wide_list);
+}
+
+// ---- live rows (rj_device.h RjLive): K2 beside K1 ----
+#define RJ_LIVE_RESIDENT_TICKS 2000ull   // 20 us (s_memrealtime, 100 MHz): K1 must be resident by then
+#define RJ_LIVE_ROW_TICKS 400000000ull   // 4 s: a published row never takes this long (defence only)
+#ifndef RJ_LIVE_POLL
+#define RJ_LIVE_POLL 16                   // s_sleep between polls of a waiting live workgroup (x 64 cycles)
+#endif
+__device__ __forceinline__ uint32_t live_ld(uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lane 0: a ticket's published slot (epoch | row << 32), or 0 (leave: K1 not resident in time,
+// the ticket counter closed by K1's last wave, or the ticket past every published row)
+__device__ __forceinline__ unsigned long long live_claim(const RjLive &lv, uint32_t *host_flag) {
+  uint32_t *c = lv.ctr;
+  if (live_ld(c + RJ_LIVE_GIVEUP) != 0u || live_ld(c + RJ_LIVE_DONE) >= lv.k1_waves) return 0;
+  // waiting on a row is safe only once every K1 workgroup holds its CU: a K2 workgroup that
+  // arrived first would otherwise keep a K1 workgroup from its LDS
+  const uint64_t t0 = wall_clock64();
+  while (live_ld(c + RJ_LIVE_STARTED) < lv.k1_groups) {
+    if (wall_clock64() - t0 > RJ_LIVE_RESIDENT_TICKS) {
+      __hip_atomic_store(c + RJ_LIVE_GIVEUP, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return 0;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  // only on a CU whose K1 workgroup is done: beside a running one, this wave's LDS and issue
+  // traffic lengthens K1's symbol chains (measured: K1 1.7 -> 2.9 ms)
+  {
+    const uint32_t *busy = lv.cu_busy + rj_live_cu_key();
+    while (__hip_atomic_load(busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      if (live_ld(c + RJ_LIVE_DONE) >= lv.k1_waves) return 0;  // K1 is over: k_rows_rest takes the rest
+      __builtin_amdgcn_s_sleep(RJ_LIVE_POLL);
+    }
+  }
+  const uint32_t t = atomicAdd(c + RJ_LIVE_TICKET, 1u);
+  if ((t & RJ_LIVE_CLOSED) != 0u || t >= lv.rows) return 0;
+  unsigned long long *sp = lv.slot + t;
+  const uint64_t t1 = wall_clock64();
+  for (;;) {
+    unsigned long long v = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (uint32_t(v) == lv.epoch) return v;
+    if (live_ld(c + RJ_LIVE_DONE) >= lv.k1_waves) {  // every slot K1 reserved is written by now
+      v = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return uint32_t(v) == lv.epoch ? v : 0ull;
+    }
+    if (wall_clock64() - t1 > RJ_LIVE_ROW_TICKS) {  // the row is lost: the host re-decodes the call's rows
+      __hip_atomic_store(c + RJ_LIVE_ERROR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(host_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return 0;
+    }
+    __builtin_amdgcn_s_sleep(RJ_LIVE_POLL);
+  }
+}
+
+// K2 beside K1 (a second, low-priority stream): one workgroup per row K1 may publish; it decodes
+// the row its ticket names once K1 has published it (agent-scope acquire: the guide's valid
+// consumer form -- one relaxed poll, one acquire, then plain loads).
+__global__ __launch_bounds__(64, RJ_K2_OCC) void k_rows_live(const RjImageDev *__restrict__ imgs, int nimg, RjLive lv,
+                                                          RjCoefBuf coefs, const RjTableSet *__restrict__ tabsets,
+                                                          uint32_t *wide_cnt, uint2 *wide_list) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];
+  __shared__ __attribute__((aligned(16))) uint32_t s_qw[3 * 64];
+  unsigned long long v = 0;
+  if (threadIdx.x == 0) v = live_claim(lv, coefs.wide_flag + 1);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v));
+  if (lo == 0u) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int i = int(hi >> RJ_LIVE_ROW_BITS);
+  if (i >= nimg) return;
+  row_body<false, false, false, false>(imgs, i, hi & ((1u << RJ_LIVE_ROW_BITS) - 1u), coefs, tabsets, nullptr, s_buf,
+                                       s_qw, wide_cnt, wide_list);
+}
+
+// K2 after K1 (stream order): the published rows no ticket took -- [min(final tickets,
+// published), published); K1's last wave closed the ticket counter and stored its final value.
+__global__ __launch_bounds__(64, RJ_K2_OCC) void k_rows_rest(const RjImageDev *__restrict__ imgs, int nimg, RjLive lv,
+                                                          RjCoefBuf coefs, const RjTableSet *__restrict__ tabsets,
+                                                          uint32_t *wide_cnt, uint2 *wide_list) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RJ_FUSED_MAX_BLK * RJ_BLK_STRIDE];
+  __shared__ __attribute__((aligned(16))) uint32_t s_qw[3 * 64];
+  const uint32_t pub = min(U(lv.ctr[RJ_LIVE_RESERVED]), lv.rows);
+  const uint32_t pos = min(U(lv.ctr[RJ_LIVE_FINAL]), pub) + blockIdx.x;
+  if (pos >= pub) return;
+  const unsigned long long v = lv.slot[pos];
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
+  if (__builtin_amdgcn_readfirstlane(uint32_t(v)) != lv.epoch) {  // never expected: K1 published it
+    if (threadIdx.x == 0) __hip_atomic_store(coefs.wide_flag + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  const int i = int(hi >> RJ_LIVE_ROW_BITS);
+  if (i >= nimg) return;
+  row_body<false, false, false, false>(imgs, i, hi & ((1u << RJ_LIVE_ROW_BITS) - 1u), coefs, tabsets, nullptr, s_buf,
+                                       s_qw, wide_cnt, wide_list);
+}
+
+hipError_t LaunchRowsLive(hipStream_t st, const RjImageDev *imgs, int nimg, const RjLive &lv, RjCoefBuf coefs,
+                          const RjTableSet *tabsets, uint32_t *wide_cnt, uint2 *wide_list) {
+  if (lv.rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rows_live, dim3(lv.rows), dim3(64), 0, st, imgs, nimg, lv, coefs, tabsets, wide_cnt, wide_list);
+  return hipGetLastError();
+}
+
+hipError_t LaunchRowsRest(hipStream_t st, const RjImageDev *imgs, int nimg, const RjLive &lv, RjCoefBuf coefs,
+                          const RjTableSet *tabsets, uint32_t *wide_cnt, uint2 *wide_list) {
+  if (lv.rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rows_rest, dim3(lv.rows), dim3(64), 0, st, imgs, nimg, lv, coefs, tabsets, wide_cnt, wide_list);
+  return hipGetLastError();
+}
+
+hipError_t LaunchRowsSplit(hipStream_t st, const RjImageDev *imgs, int nimg, const uint2 *split_rows,
+                           uint32_t nsplit_rows, RjCoefBuf coefs, const RjTableSet *tabsets, uint32_t *wide_cnt,
+                           uint2 *wide_list) {
+  if (nsplit_rows == 0 || split_rows == nullptr) return hipSuccess;
+  const uint32_t *no_prefix = nullptr;
+  uint8_t *no_planes = nullptr;
+  hipLaunchKernelGGL(k_rows_split<false>, dim3(nsplit_rows), dim3(64), 0, st, imgs, nimg, no_prefix, split_rows, coefs,
+                     tabsets, no_planes, wide_cnt, wide_list, 1u);
+  return hipGetLastError();
 }
 
 // K2 fix-up: the rows a K2 launch recorded (a strip outside the int32 IDCT's exact domain --
@@ -1065,21 +1193,21 @@ hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, in
                          planes, wide_cnt, wide_list);
       if (nsplit_rows)
         hipLaunchKernelGGL(k_rows_split<true>, dim3(nsplit_rows), dim3(64), 0, st, imgs, nimg, no_prefix,
-                           split_rows, coefs, tabsets, planes, wide_cnt, wide_list);
+                           split_rows, coefs, tabsets, planes, wide_cnt, wide_list, 1u);
     } else {
       hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs, tabsets,
                          planes, wide_cnt, wide_list);
       if (nsplit_rows)
         hipLaunchKernelGGL(k_rows_split<false>, dim3(nsplit_rows), dim3(64), 0, st, imgs, nimg, no_prefix,
-                           split_rows, coefs, tabsets, planes, wide_cnt, wide_list);
+                           split_rows, coefs, tabsets, planes, wide_cnt, wide_list, 1u);
     }
   } else if (coefs.piece_shift != 0) {  // lean split launch: pieces with skips / early terminators
     if (to_planes)
       hipLaunchKernelGGL(k_rows_split<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list,
-                         coefs, tabsets, planes, wide_cnt, wide_list);
+                         coefs, tabsets, planes, wide_cnt, wide_list, 0u);
     else
       hipLaunchKernelGGL(k_rows_split<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list,
-                         coefs, tabsets, planes, wide_cnt, wide_list);
+                         coefs, tabsets, planes, wide_cnt, wide_list, 0u);
   } else if (to_planes) {
     hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs,
                        tabsets, planes, wide_cnt, wide_list);

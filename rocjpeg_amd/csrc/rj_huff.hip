@@ -54,7 +54,7 @@ namespace rj {
 __device__ const uint4 rj_hl_zero[2] = {};
 
 #ifdef RJ_HL_STAMPS  // diagnostic build: cycles in the symbol steps / the phase ends, summed over waves
-__device__ unsigned long long rj_hl_stamp[8];
+__device__ unsigned long long rj_hl_stamp[10];  // [8]: s_memrealtime ticks of the loops (100 MHz), [9] unused
 // k_huff_chunk: per decoder wave, summed: setup cycles (entry to the first phase), loop cycles,
 // phases, safe phases, waves; max loop cycles; ring-wait cycles
 __device__ unsigned long long rj_hc_stamp[14];
@@ -277,6 +277,30 @@ __device__ __forceinline__ uint32_t lds_rd(uint32_t a) { return *(const lds_u32 
 __device__ __forceinline__ void lds_wr(uint32_t a, uint32_t v) { *(lds_u32 *)(uintptr_t)(a) = v; }
 #define RJ_HL_FIN 0xFFFFFFFFu  // decoder -> mover: the lane's decode is over
 
+// Live rows (rj_device.h RjLive): the active lanes of one decoder wave whose `pub` is set have
+// finished their intervals (entries flushed, pieces written); publish their MCU rows.  The
+// release is the guide's valid producer form (MI355X_MICROARCH.md, inter-workgroup visibility):
+// this wave's stores drained, agent-scope release (the XCD's L2 written back), drained again,
+// then one 8-B sc1 store per row -- data and tag in one granule, polled by the consumer.
+__device__ __forceinline__ void hl_publish(const RjLive &lv, bool pub, uint32_t img, uint32_t row) {
+  const uint64_t m = __builtin_amdgcn_ballot_w64(pub);
+  if (m == 0) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifndef RJ_EXP_LIVE_NOFENCE  // timing build: the release's cost (rows may then be read stale)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  const uint32_t lane = __lane_id(), leader = uint32_t(__builtin_ctzll(m));
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(&lv.ctr[RJ_LIVE_RESERVED], uint32_t(__builtin_popcountll(m)));
+  base = __shfl(base, int(leader));
+  if (pub) {
+    const uint32_t r = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+    const uint64_t v = uint64_t(lv.epoch) | (uint64_t((img << RJ_LIVE_ROW_BITS) | row) << 32);
+    __hip_atomic_store(&lv.slot[base + r], (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Workgroup = DEC decoder lanes + one mover wave per decoder wave.  Lane `g` of
 // [lane0, lane0 + nlanes): the interval rj_lane_seg(g), decoded by decoder lane g % DEC; mover
 // lane g % DEC + DEC keeps that lane's bit ring filled.  The decoder never waits on vector
@@ -298,7 +322,8 @@ __device__ __forceinline__ void lds_wr(uint32_t a, uint32_t v) { *(lds_u32 *)(ui
 template <int DEC, int GROUP, bool kSplit, int PHASE>
 __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     const RjImageDev *__restrict__ imgs, int nimg, uint32_t lane0, uint32_t nlanes, const uint8_t *__restrict__ destuffed,
-    const RjTableSet *__restrict__ tabsets, const RjLeanTables *__restrict__ lean, RjCoefBuf coefs, RjHuffSplit split) {
+    const RjTableSet *__restrict__ tabsets, const RjLeanTables *__restrict__ lean, RjCoefBuf coefs, RjHuffSplit split,
+    RjLive live) {
   constexpr uint32_t kStage = 2 * GROUP;
   constexpr bool kPow2 = (DEC & (DEC - 1)) == 0;
   constexpr uint32_t kColShift = kPow2 ? __builtin_ctz(DEC * 4u) : 0u;  // bytes between a lane column's words
@@ -329,6 +354,10 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
   const bool mover = tid >= uint32_t(DEC);
   const uint32_t L = mover ? tid - DEC : tid;  // the decoder lane (LDS column)
   if (tid == 0) s_ne = 0;
+  if (live.slot != nullptr && tid == 0) {  // this CU runs K1 (live K2 waits there until it is done)
+    atomicAdd(&live.cu_busy[rj_live_cu_key()], 1u);
+    atomicAdd(&live.ctr[RJ_LIVE_STARTED], 1u);
+  }
   const uint32_t g = lane0 + blockIdx.x * DEC + L;
   bool pending = g < lane0 + nlanes;
   uint32_t gseg = 0, role = 0;
@@ -473,6 +502,7 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
 #ifdef RJ_HL_STAMPS
     uint64_t st_steps = 0, st_end = 0, st_fast = 0, st_safe = 0, st_esc = 0;
     const uint64_t st_begin = __builtin_amdgcn_s_memtime();
+    const uint64_t st_begin_rt = __builtin_amdgcn_s_memrealtime();
 #define RJ_HL_T0 const uint64_t t0 = __builtin_amdgcn_s_memtime()
 #define RJ_HL_T1(fast)                                  \
   const uint64_t t1 = __builtin_amdgcn_s_memtime();     \
@@ -566,6 +596,7 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
       const unsigned long long st_loop = __builtin_amdgcn_s_memtime() - st_begin;
       atomicAdd(&rj_hl_stamp[6], st_loop);
       atomicMax(&rj_hl_stamp[7], st_loop);
+      atomicAdd(&rj_hl_stamp[8], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - st_begin_rt));
     }
 #endif
     stage[ne & (kStage - 1)] = RJ_RE_TERM;
@@ -586,7 +617,20 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
         *gp(piece) = RjPiece{ent_abs, 0u, blocks, 1u, {0, 0, 0}};
       }
     }
+    // live rows: a whole interval's row (or a split head's that met no tail record) is complete;
+    // a synced split row is two pieces, left to the split-aware K2 instance
+    if (live.slot != nullptr) hl_publish(live, !tail && !synced, uint32_t(i), seg);
     if (coefs.count) atomicAdd(&s_ne, ne + 1);
+  }
+  // (every wave left the loop at its last barrier: the workgroup's decoding is over)
+  if (live.slot != nullptr && tid == 0) atomicSub(&live.cu_busy[rj_live_cu_key()], 1u);
+  if (live.slot != nullptr && !mover && (tid & 63u) == 0) {  // this decoder wave is done (after its rows)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t d = __hip_atomic_fetch_add(&live.ctr[RJ_LIVE_DONE], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (d + 1u == live.k1_waves) {  // the last one: close the tickets; k_rows_rest takes what is left
+      const uint32_t t = atomicOr(&live.ctr[RJ_LIVE_TICKET], RJ_LIVE_CLOSED);
+      __hip_atomic_store(&live.ctr[RJ_LIVE_FINAL], t & ~RJ_LIVE_CLOSED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   if (tid == 0 && coefs.count != nullptr && s_ne != 0) atomicAdd(coefs.count, (unsigned long long)s_ne);
 }
@@ -1188,14 +1232,14 @@ hipError_t LaunchHuffChunks(hipStream_t st, const RjImageDev *imgs, int nimg, ui
 
 #ifdef RJ_HL_STAMPS
 void DumpHuffStamps() {
-  unsigned long long h[8];
+  unsigned long long h[10];
   (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(rj_hl_stamp), sizeof(h));
   const double w = h[4] ? double(h[4]) : 1.0;
   const double ph = double(h[2] + h[3]) ? double(h[2] + h[3]) : 1.0;
   fprintf(stderr, "[rj k_huff] waves %llu: per wave %.0f phases (%.0f safe), %.0f escape steps; cycles per phase: steps %.0f, end %.0f; "
-          "decode cycles per wave %.0f (max %llu)\n",
-          h[4], ph / w, h[3] / w, h[5] / w, h[0] / ph, h[1] / ph, h[6] / w, h[7]);
-  unsigned long long z[8] = {};
+          "decode cycles per wave %.0f (max %llu); clock %.0f MHz\n",
+          h[4], ph / w, h[3] / w, h[5] / w, h[0] / ph, h[1] / ph, h[6] / w, h[7], h[8] ? 100.0 * double(h[6]) / double(h[8]) : 0.0);
+  unsigned long long z[10] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(rj_hl_stamp), z, sizeof(z));
   unsigned long long c[14];
   (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(rj_hc_stamp), sizeof(c));
@@ -1216,23 +1260,25 @@ void DumpHuffStamps() {
 
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
-                           RjCoefBuf coefs, uint32_t extra_lds, const RjHuffSplit *split, bool five_waves) {
+                           RjCoefBuf coefs, uint32_t extra_lds, const RjHuffSplit *split, bool five_waves,
+                           const RjLive *live) {
   if (nlanes == 0) return hipSuccess;
+  const RjLive lv = live != nullptr ? *live : RjLive{};
   if (split != nullptr && five_waves) {  // five-wave layout with split pairs first
     hipLaunchKernelGGL((k_huff<RJ_HL_DEC5, RJ_HL_GROUP, true, RJ_HL_PHASE>), dim3((nlanes + RJ_HL_DEC5 - 1) / RJ_HL_DEC5),
-                       dim3(2 * RJ_HL_DEC5), 0, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs, *split);
+                       dim3(2 * RJ_HL_DEC5), 0, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs, *split, lv);
   } else if (split != nullptr) {  // outliers split: one decoder wave per SIMD, two workgroups per CU
     hipLaunchKernelGGL((k_huff<RJ_HL_SPLIT_DEC, 8, true, 4>), dim3((nlanes + RJ_HL_SPLIT_DEC - 1) / RJ_HL_SPLIT_DEC),
                        dim3(2 * RJ_HL_SPLIT_DEC), 0, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs,
-                       *split);
+                       *split, lv);
   } else {
     if (five_waves)  // one workgroup per CU by its LDS (~105 KB)
       hipLaunchKernelGGL((k_huff<RJ_HL_DEC5, RJ_HL_GROUP, false, RJ_HL_PHASE>),
                          dim3((nlanes + RJ_HL_DEC5 - 1) / RJ_HL_DEC5), dim3(2 * RJ_HL_DEC5), 0, st, imgs, nimg, lane0,
-                         nlanes, destuffed, tabsets, lean, coefs, RjHuffSplit{0, 0});
+                         nlanes, destuffed, tabsets, lean, coefs, RjHuffSplit{0, 0}, lv);
     else
       hipLaunchKernelGGL((k_huff<256, RJ_HL_GROUP, false, RJ_HL_PHASE>), dim3((nlanes + 255) / 256), dim3(512),
-                         extra_lds, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs, RjHuffSplit{0, 0});
+                         extra_lds, st, imgs, nimg, lane0, nlanes, destuffed, tabsets, lean, coefs, RjHuffSplit{0, 0}, lv);
   }
   return hipGetLastError();
 }

@@ -36,7 +36,7 @@ hipError_t LaunchEntropyLanes(hipStream_t st, const RjImageDev *imgs, int nimg, 
 hipError_t LaunchHuffLanes(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t nlanes,
                            const uint8_t *destuffed, const RjTableSet *tabsets, const RjLeanTables *lean,
                            RjCoefBuf coefs, uint32_t extra_lds = 0, const RjHuffSplit *split = nullptr,
-                           bool five_waves = false);
+                           bool five_waves = false, const RjLive *live = nullptr);
 // K1 chunk lanes on the lean machinery (rj_huff.hip k_huff_chunk): stage 0 of LaunchEntropy's
 // layout (from lane0: lanes_wg lanes with workgroup-scope records, then lanes_dev), absolute DC entries.
 hipError_t LaunchHuffChunks(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t lane0, uint32_t lanes_wg,
@@ -62,6 +62,17 @@ hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, in
                       const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
                       uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list, const uint2 *split_rows = nullptr,
                       uint32_t nsplit_rows = 0);
+// Live rows (rj_device.h RjLive): K2 beside K1 (second stream; grid = lv.rows, one workgroup per
+// ticket), and the stream-ordered K2 after K1 over the published rows no ticket took.
+hipError_t LaunchRowsLive(hipStream_t st, const RjImageDev *imgs, int nimg, const RjLive &lv, RjCoefBuf coefs,
+                          const RjTableSet *tabsets, uint32_t *wide_cnt, uint2 *wide_list);
+hipError_t LaunchRowsRest(hipStream_t st, const RjImageDev *imgs, int nimg, const RjLive &lv, RjCoefBuf coefs,
+                          const RjTableSet *tabsets, uint32_t *wide_cnt, uint2 *wide_list);
+// The split-aware instance alone over an (image, row) list, decoding only the rows whose head met
+// its tail (the other split rows were published whole).
+hipError_t LaunchRowsSplit(hipStream_t st, const RjImageDev *imgs, int nimg, const uint2 *split_rows,
+                           uint32_t nsplit_rows, RjCoefBuf coefs, const RjTableSet *tabsets, uint32_t *wide_cnt,
+                           uint2 *wide_list);
 // The fix-up launch of one K2 launch's list (same variant; cap = that launch's rows).
 hipError_t LaunchRowsFix(hipStream_t st, bool to_planes, bool dense, const RjImageDev *imgs, int nimg, RjCoefBuf coefs,
                          const RjTableSet *tabsets, uint8_t *planes, const uint32_t *wide_cnt, const uint2 *wide_list,

@@ -7,6 +7,7 @@
 // (src/rocjpeg_vaapi_decoder.cpp:677-689, vaCreateBuffer); here one call stages a whole batch.
 #pragma once
 #include <atomic>
+#include <exception>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -30,12 +31,14 @@ class HostPool {
   }
   int threads() const { return want_; }
 
-  // Runs task(k) for k in [0, n) on the workers and the caller; the caller also runs
-  // done(k) for every k in increasing k as soon as tasks 0..k have all finished (done may be
-  // empty).  Returns after every task and every done() call.  Exceptions must not escape task.
-  void Run(int n, const std::function<void(int)> &task, const std::function<void(int)> &done) {
+  // Runs task(k) for k in [0, n) on the workers and the caller (only the caller when `serial`);
+  // the caller also runs done(k) for every k in increasing k as soon as tasks 0..k have all
+  // finished (done may be empty).  Returns after every task and every done() call.  An exception
+  // thrown by a task (on any thread) or by done() is caught, every worker is let finish this job,
+  // and the first one is rethrown on the calling thread (rj_api.cpp's Guard maps it to a status).
+  void Run(int n, const std::function<void(int)> &task, const std::function<void(int)> &done, bool serial = false) {
     if (n <= 0) return;
-    if (want_ == 1 || n == 1) {
+    if (want_ == 1 || n == 1 || serial) {
       for (int k = 0; k < n; k++) {
         task(k);
         if (done) done(k);
@@ -43,6 +46,8 @@ class HostPool {
       return;
     }
     Start();
+    first_error_ = nullptr;
+    failed_.store(false, std::memory_order_relaxed);
     flags_.reset(new std::atomic<uint8_t>[n]);
     for (int k = 0; k < n; k++) flags_[k].store(0, std::memory_order_relaxed);
     {
@@ -57,14 +62,14 @@ class HostPool {
     int flushed = 0;
     auto flush = [&] {
       while (flushed < n && flags_[flushed].load(std::memory_order_acquire)) {
-        if (done) done(flushed);
+        if (done && !failed_.load(std::memory_order_relaxed)) Guarded([&] { done(flushed); });
         flushed++;
       }
     };
     for (;;) {
       const int k = next_.fetch_add(1, std::memory_order_relaxed);
       if (k >= n) break;
-      task(k);
+      if (!failed_.load(std::memory_order_relaxed)) Guarded([&] { task(k); });
       flags_[k].store(1, std::memory_order_release);
       flush();
     }
@@ -72,9 +77,20 @@ class HostPool {
       flush();
       if (flushed < n) std::this_thread::yield();
     }
-    std::unique_lock<std::mutex> l(mu_);  // every worker has left this job (task_ stays valid until then)
-    idle_cv_.wait(l, [&] { return active_ == 0; });
-    task_ = nullptr;
+    {
+      std::unique_lock<std::mutex> l(mu_);  // every worker has left this job (task_ stays valid until then)
+      idle_cv_.wait(l, [&] { return active_ == 0; });
+      task_ = nullptr;
+    }
+    if (failed_.load(std::memory_order_acquire)) {
+      std::exception_ptr e;
+      {
+        std::lock_guard<std::mutex> l(mu_);
+        e = first_error_;
+        first_error_ = nullptr;
+      }
+      std::rethrow_exception(e);
+    }
   }
 
  private:
@@ -98,7 +114,7 @@ class HostPool {
       for (;;) {
         const int k = next_.fetch_add(1, std::memory_order_relaxed);
         if (k >= n) break;
-        (*task)(k);
+        if (!failed_.load(std::memory_order_relaxed)) Guarded([&] { (*task)(k); });  // (later tasks are skipped)
         flags_[k].store(1, std::memory_order_release);
       }
       std::lock_guard<std::mutex> l(mu_);
@@ -106,7 +122,21 @@ class HostPool {
     }
   }
 
+  // runs f, keeping the first exception of the job (a worker must never let one escape)
+  template <typename F>
+  void Guarded(F &&f) {
+    try {
+      f();
+    } catch (...) {
+      std::lock_guard<std::mutex> l(mu_);
+      if (!first_error_) first_error_ = std::current_exception();
+      failed_.store(true, std::memory_order_release);
+    }
+  }
+
   const int want_;
+  std::exception_ptr first_error_;
+  std::atomic<bool> failed_{false};
   std::vector<std::thread> workers_;
   std::mutex mu_;
   std::condition_variable cv_, idle_cv_;

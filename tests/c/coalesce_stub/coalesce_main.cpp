@@ -12,7 +12,7 @@ int main(int argc, char **argv) {
   const int T = argc > 1 ? std::atoi(argv[1]) : 8, calls = argc > 2 ? std::atoi(argv[2]) : 1000;
   std::vector<rj::Decoder> decs(T);
   std::vector<std::thread> th;
-  std::vector<int> wrong(T, 0);
+  std::vector<int> wrong(T, 0), nbad(T, 0);
   for (int t = 0; t < T; t++)
     th.emplace_back([&, t] {
       rj::Stream st;
@@ -24,18 +24,23 @@ int main(int argc, char **argv) {
       img.pitch[0] = uint32_t(t);
       for (int i = 0; i < calls; i++) {
         st.bad = t == 0 && i % 7 == 3;
+        nbad[t] += st.bad ? 1 : 0;
         const int r = rj::CoalescedDecode(&decs[t], 0, &sp, 1, &p, &img);
         if (r != (st.bad ? ROCJPEG_STATUS_BAD_JPEG : 0)) wrong[t]++;
       }
     });
   for (auto &x : th) x.join();
-  long img = 0;
-  for (auto &d : decs) img += d.images;
-  int bad = 0;
+  long img = 0, att = 0;
+  for (auto &d : decs) {
+    img += d.images;
+    att += d.attempts;
+  }
+  int bad = 0, bad_calls = 0;
   for (int w : wrong) bad += w;
+  for (int b : nbad) bad_calls += b;
   uint64_t a, b, c;
   rj::CoalesceStats(&a, &b, &c);
-  std::printf("calls %llu combined %llu members %llu images %ld wrong_status %d\n", (unsigned long long)a,
-              (unsigned long long)b, (unsigned long long)c, img, bad);
+  std::printf("calls %llu combined %llu members %llu images %ld wrong_status %d bad_calls %d attempts %ld\n", (unsigned long long)a,
+              (unsigned long long)b, (unsigned long long)c, img, bad, bad_calls, att);
   return bad ? 1 : 0;
 }

@@ -20,8 +20,15 @@ class Stream {
 class Decoder {
  public:
   std::atomic<int> active{0};
-  std::atomic<long> images{0};
+  std::atomic<long> images{0}, attempts{0};  // images decoded successfully / handed to Decode
   bool Coalescable() const { return true; }
+  // host validation without decoding (rj_decoder.h Decoder::Check): a bad stream fails its call
+  int Check(Stream *const *s, int n, const RocJpegDecodeParams *p, const RocJpegImage *d) {
+    if (s == nullptr || p == nullptr || d == nullptr) std::abort();
+    for (int i = 0; i < n; i++)
+      if (s[i]->bad) return ROCJPEG_STATUS_BAD_JPEG;
+    return 0;
+  }
   int Decode(Stream *const *s, int n, const RocJpegDecodeParams *p, RocJpegImage *d) {
     if (active.fetch_add(1) != 0) {
       std::fprintf(stderr, "handle used by two threads at once\n");
@@ -39,7 +46,8 @@ class Decoder {
       if (s[i]->bad) st = ROCJPEG_STATUS_BAD_JPEG;
     }
     std::this_thread::sleep_for(std::chrono::microseconds(200 + 20 * n));
-    images += n;
+    attempts += n;
+    if (st == 0) images += n;
     active.fetch_sub(1);
     return st;
   }

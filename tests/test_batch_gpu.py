@@ -187,7 +187,60 @@ def test_c2_1024_split5_damaged(split5_dec):
     assert st == 0, R.error_name(st)
     cu = t.cuda.get_device_properties(0).multi_processor_count
     if 256 * cu < tm["intervals"] <= 320 * cu:
-        assert tm["lean_five"] == 1 and tm["lean_split"] > 0
+        assert tm["lean_five"] == 1 and tm["lean_split"] > 0 and tm["live"] == 1
+    ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
+    bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
+    assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
+
+
+@pytest.fixture(scope="module", params=["1", "2"], ids=["live", "live_giveup"])
+def live_dec(request):
+    """A handle with K2 beside K1 (live rows, rj_device.h RjLive; RJ_K2_LIVE read at handle
+    creation): "1" the live launch as measured; "2" a test knob under which the live launch never
+    sees K1 resident, so every live workgroup leaves without a ticket and the stream-ordered K2
+    after K1 takes every published row -- the path a K2 dispatched ahead of K1 falls back to."""
+    torch()
+    old = os.environ.get("RJ_K2_LIVE")
+    os.environ["RJ_K2_LIVE"] = request.param
+    try:
+        d = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    finally:
+        if old is None:
+            del os.environ["RJ_K2_LIVE"]
+        else:
+            os.environ["RJ_K2_LIVE"] = old
+    yield request.param, d
+    d.close()
+
+
+def test_c2_1024_live_rows_damaged(live_dec):
+    """Live rows over a C2 batch with damaged streams (K1 lanes finishing out of order, split
+    heads that never meet their tails): the rows published while K1 runs decoded beside it, the
+    rest after it, the synced split rows by the split-aware instance -- every row exactly once
+    (ticket accounting below) and every image equal to the oracle."""
+    mode, dec = live_dec
+    t = torch()
+    distinct, copies = 64, 16
+    datas = _c2_images(48, seed0=3033)
+    datas += [_damaged(datas[k], k + 7) for k in range(16)]
+    with ThreadPoolExecutor(16) as ex:
+        want = list(ex.map(lambda d: O.oracle_decode(d, int(R.OutputFormat.RGB), [(1080, 5760)]), datas))
+    assert all(st == 0 for st, _ in want)
+    streams = [R.JpegStream(datas[i % distinct]) for i in range(distinct * copies)]
+    out = t.full((len(streams), 1080, 5760), 0xA5, dtype=t.uint8, device="cuda")
+    imgs = [R.make_image([out[i].data_ptr()], [5760]) for i in range(len(streams))]
+    dec.set_profiling(True)
+    st = dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs)
+    tm = dec.last_timings()
+    dec.set_profiling(False)
+    assert st == 0, R.error_name(st)
+    cu = t.cuda.get_device_properties(0).multi_processor_count
+    if 256 * cu < tm["intervals"] <= 320 * cu:
+        assert tm["live"] == 1 and tm["lean_five"] == 1
+        rows = tm["live_rows"] + tm["rest_rows"]
+        assert 0 < rows <= 1024 * 68 and rows >= 1024 * 68 - tm["lean_split"]
+        if mode == "2":
+            assert tm["live_pad"] == 1 and tm["live_rows"] == 0
     ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
     bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
     assert not bad, f"{len(bad)} images differ, first {bad[:8]}"

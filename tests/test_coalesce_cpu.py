@@ -43,12 +43,15 @@ def test_coalesced_calls_keep_their_own_status(stub_exe, env):
     e.pop("RJ_COALESCE", None)
     r = subprocess.run([stub_exe, "8", "400"], capture_output=True, text=True, timeout=300, env=e)
     assert r.returncode == 0, (r.stdout, r.stderr[-3000:])
-    m = re.search(r"calls (\d+) combined (\d+) members (\d+) images (\d+) wrong_status (\d+)", r.stdout)
-    calls, combined, members, images, wrong = map(int, m.groups())
-    assert calls == 8 * 400 and wrong == 0
+    m = re.search(r"calls (\d+) combined (\d+) members (\d+) images (\d+) wrong_status (\d+) bad_calls (\d+) "
+                  r"attempts (\d+)", r.stdout)
+    calls, combined, members, images, wrong, bad, attempts = map(int, m.groups())
+    assert calls == 8 * 400 and wrong == 0 and bad > 0
     assert combined > 0 and members > combined  # calls were decoded together
-    # every image decoded at least once (a failed combined call re-decodes its members alone)
-    assert images >= calls
+    # members are validated before the combined call: a bad stream is never decoded and costs
+    # the calls combined with it no second decode: every good image decoded once, no image
+    # handed to a decode twice
+    assert images == calls - bad and attempts <= calls
 
 
 def test_coalescing_off(stub_exe):
