@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -129,6 +130,7 @@ Decoder::~Decoder() {
       if (e) (void)hipEventDestroy(e);
     for (auto &e : live_t_)
       if (e) (void)hipEventDestroy(e);
+    if (split_ev_) (void)hipEventDestroy(split_ev_);
     if (lstream_) (void)hipStreamDestroy(lstream_);
     (void)hipStreamDestroy(stream_);
   }
@@ -186,10 +188,13 @@ int Decoder::Initialize() {
   }
   for (auto &e : live_ev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : live_t_) RJ_HIP(hipEventCreate(&e));
+  RJ_HIP(hipEventCreateWithFlags(&split_ev_, hipEventDisableTiming));
   if (const char *lk = getenv("RJ_K2_LIVE")) {  // 0 off; 2 (test): the live launch always gives up
     live_k2_ = atoi(lk) != 0;  // 1: on
     live_test_giveup_ = atoi(lk) == 2;
   }
+  if (const char *ll = getenv("RJ_K2_LIVE_LDS")) live_lds_ = uint32_t(std::max(0, atoi(ll)));
+  if (const char *sh = getenv("RJ_SPLIT_HOST")) split_host_ = atoi(sh) != 0;
   for (auto &e : pev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : pk1_) RJ_HIP(hipEventCreate(&e));
   for (auto &e : kev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -534,10 +539,90 @@ int Decoder::PtrDevice(const void *p) {
 }
 
 int Decoder::Decode(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
-  std::lock_guard<std::mutex> lock(mu_);
   if (streams == nullptr || params == nullptr || dst == nullptr || n < 0) return kInvalidParameter;
   for (int i = 0; i < n; i++)
     if (streams[i] == nullptr) return kInvalidParameter;
+  if (split_host_ && n >= kSplitHostMin && !profiling_ && path_policy_ == 0) {
+    int staged = 0;
+    for (int i = 0; i < n; i++) {
+      std::lock_guard<std::mutex> sl(streams[i]->mutex());
+      const Stream *s = streams[i];
+      staged += (s->resident.device == device_ && s->resident.generation == s->generation()) ? 0 : 1;
+    }
+    if (staged >= kSplitHostMin) return DecodeSplit(streams, n, params, dst);
+  }
+  return DecodeOne(streams, n, params, dst);
+}
+
+int Decoder::DecodeSplit(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
+  // the whole call's host validation first: a call that would fail it writes nothing, as unsplit
+  const int cst = Check(streams, n, params, dst);
+  if (cst != kOk) return cst;
+  {
+    std::lock_guard<std::mutex> lock(mu_);
+    if (!helper_) {
+      std::unique_ptr<Decoder> h(new Decoder(backend_, device_));
+      if (h->Initialize() != kOk) {
+        split_host_ = false;  // (no second handle on this device: every call decodes whole)
+      } else {
+        h->split_host_ = false;
+        helper_ = std::move(h);
+      }
+    }
+  }
+  if (!helper_) return DecodeOne(streams, n, params, dst);
+  // the halves' uploads in order on the copy engine: the second starts when the first is done, so
+  // the first half's kernels run while the second half's bytes cross PCIe (both uploads at once
+  // would share the engine and leave the GPU idle until both land)
+  const int half = n / 2;
+  int st2 = kOk;
+  Decoder *helper = helper_.get();
+  std::mutex m;
+  std::condition_variable cv;
+  bool signalled = false;
+  auto signal = [&] {
+    std::lock_guard<std::mutex> l(m);
+    if (!signalled) {
+      signalled = true;
+      cv.notify_all();
+    }
+  };
+  std::thread t([&] {
+    {
+      std::unique_lock<std::mutex> l(m);
+      cv.wait(l, [&] { return signalled; });
+    }
+    try {
+      st2 = helper->DecodeOne(streams + half, n - half, params, dst + half);
+    } catch (...) {
+      st2 = kRuntimeError;
+    }
+    helper->upload_after_ = nullptr;
+  });
+  int st1;
+  helper->upload_after_ = split_ev_;
+  uploaded_ = [&] {
+    if (hipEventRecord(split_ev_, stream_) != hipSuccess) helper->upload_after_ = nullptr;
+    signal();
+  };
+  try {
+    st1 = DecodeOne(streams, half, params, dst);
+  } catch (...) {
+    uploaded_ = nullptr;
+    helper->upload_after_ = nullptr;
+    signal();
+    t.join();
+    throw;
+  }
+  uploaded_ = nullptr;
+  if (!signalled) helper->upload_after_ = nullptr;  // (the first half never uploaded: nothing to wait for)
+  signal();
+  t.join();
+  return st1 != kOk ? st1 : st2;
+}
+
+int Decoder::DecodeOne(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
+  std::lock_guard<std::mutex> lock(mu_);
   // Hold every stream's lock for the call: a concurrent re-parse must not move its bytes.
   std::vector<std::unique_lock<std::mutex>> locks;
   std::vector<Stream *> uniq(streams, streams + n);
@@ -1433,6 +1518,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
   }
   if (profiling_) RJ_HIP(hipEventRecord(ev_[0], stream_));
+  if (upload_after_ != nullptr) RJ_HIP(hipStreamWaitEvent(stream_, upload_after_, 0));  // DecodeSplit's second half
   for (const PinRun &r : pin_runs)  // parse-time pinned bitstreams: straight to the device
     RJ_HIP(hipMemcpyAsync(decs + r.dev, r.host, r.len, hipMemcpyHostToDevice, stream_));
   if (stage_bytes || ecs_copy_bytes) {
@@ -1547,6 +1633,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
 
   const auto t_k0 = std::chrono::steady_clock::now();
   RJ_HIP(hipMemcpyAsync(dbase, h, blob_a, hipMemcpyHostToDevice, stream_));
+  if (uploaded_) uploaded_();  // DecodeSplit's first half: its uploads are enqueued
   if (cbuf.count) RJ_HIP(hipMemsetAsync(cbuf.count, 0, sizeof(unsigned long long), stream_));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
   RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>(),
@@ -2047,7 +2134,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       if (live) {
         wide(fused_rows, wcnt, wlist, false, false);  // one list: the live, rest and split launches decode disjoint rows
         if (profiling_) RJ_HIP(hipEventRecord(live_t_[0], lstream_));
-        RJ_HIP(LaunchRowsLive(lstream_, d_imgs, n, lv, cbuf, d_tabs, wcnt, wlist));
+        RJ_HIP(LaunchRowsLive(lstream_, d_imgs, n, lv, cbuf, d_tabs, wcnt, wlist, live_lds_));
         if (profiling_) RJ_HIP(hipEventRecord(live_t_[1], lstream_));
         RJ_HIP(hipEventRecord(live_ev_[1], lstream_));
       }

@@ -8,6 +8,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -81,6 +84,19 @@ class Decoder {
 
  private:
   int DecodeLocked(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
+  int DecodeOne(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
+  // A large call whose bitstreams are in host memory (every call stages them over PCIe): its
+  // second half is decoded by a helper handle (same device, its own stream and buffers) on a
+  // second host thread, so one half's upload overlaps the other's kernels -- what two caller
+  // threads with a handle each get (tools/host_input_threads.py: 105k -> 135k images/s).
+  // env RJ_SPLIT_HOST=0 turns it off; never while profiling (the timings are per handle).
+  int DecodeSplit(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
+  std::atomic<bool> split_host_{true};
+  std::unique_ptr<Decoder> helper_;
+  static constexpr int kSplitHostMin = 1024;  // staged (non-resident) images a call needs to split
+  hipEvent_t split_ev_ = nullptr;                // the first half's uploads are done (recorded on stream_)
+  hipEvent_t upload_after_ = nullptr;            // helper: wait for this before uploading
+  std::function<void()> uploaded_;               // first half: called once its uploads are enqueued
   int ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *data, const size_t *len, int n);
   // Device of the allocation holding p (hipPointerGetAttributes, cached per call by address
   // range); -1: host memory (pinned or pageable).
@@ -165,6 +181,7 @@ class Decoder {
   // default: beside K1 it slowed K1 by more than it saved)
   bool live_k2_ = false;
   bool live_test_giveup_ = false;
+  uint32_t live_lds_ = 0;  // env RJ_K2_LIVE_LDS: extra LDS per live K2 workgroup (fewer of them per CU)
   hipStream_t lstream_ = nullptr;
   hipEvent_t live_ev_[2] = {};  // fork (descriptors uploaded), join (the live K2 done)
   hipEvent_t live_t_[4] = {};   // profiling: live K2 span (its stream), rest + split span (after K1)

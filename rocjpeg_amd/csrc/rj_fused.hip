@@ -1111,9 +1111,10 @@ __global__ __launch_bounds__(64, RJ_K2_OCC) void k_rows_rest(const RjImageDev *_
 }
 
 hipError_t LaunchRowsLive(hipStream_t st, const RjImageDev *imgs, int nimg, const RjLive &lv, RjCoefBuf coefs,
-                          const RjTableSet *tabsets, uint32_t *wide_cnt, uint2 *wide_list) {
+                          const RjTableSet *tabsets, uint32_t *wide_cnt, uint2 *wide_list, uint32_t extra_lds) {
   if (lv.rows == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rows_live, dim3(lv.rows), dim3(64), 0, st, imgs, nimg, lv, coefs, tabsets, wide_cnt, wide_list);
+  hipLaunchKernelGGL(k_rows_live, dim3(lv.rows), dim3(64), extra_lds, st, imgs, nimg, lv, coefs, tabsets, wide_cnt,
+                     wide_list);
   return hipGetLastError();
 }
 

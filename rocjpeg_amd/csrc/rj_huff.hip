@@ -54,7 +54,7 @@ namespace rj {
 __device__ const uint4 rj_hl_zero[2] = {};
 
 #ifdef RJ_HL_STAMPS  // diagnostic build: cycles in the symbol steps / the phase ends, summed over waves
-__device__ unsigned long long rj_hl_stamp[10];  // [8]: s_memrealtime ticks of the loops (100 MHz), [9] unused
+__device__ unsigned long long rj_hl_stamp[11];  // [8]: s_memrealtime ticks of the loops (100 MHz), [9] to the flush's end, [10] ring checks
 // k_huff_chunk: per decoder wave, summed: setup cycles (entry to the first phase), loop cycles,
 // phases, safe phases, waves; max loop cycles; ring-wait cycles
 __device__ unsigned long long rj_hc_stamp[14];
@@ -500,7 +500,7 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
     uint32_t peek = __builtin_amdgcn_alignbit(wa, wb, q);
     uint32_t e = s_lut[(tb >> 2) + (peek >> tsh)];
 #ifdef RJ_HL_STAMPS
-    uint64_t st_steps = 0, st_end = 0, st_fast = 0, st_safe = 0, st_esc = 0;
+    uint64_t st_steps = 0, st_end = 0, st_fast = 0, st_safe = 0, st_esc = 0, st_flush = 0, st_waits = 0;
     const uint64_t st_begin = __builtin_amdgcn_s_memtime();
     const uint64_t st_begin_rt = __builtin_amdgcn_s_memrealtime();
 #define RJ_HL_T0 const uint64_t t0 = __builtin_amdgcn_s_memtime()
@@ -510,7 +510,11 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
   if (fast) st_fast++;                                  \
   else st_safe++
 #define RJ_HL_T2 st_end += __builtin_amdgcn_s_memtime() - t1
+#define RJ_HL_TF st_flush += __builtin_amdgcn_s_memtime() - t1
+#define RJ_HL_TW st_waits++
 #else
+#define RJ_HL_TF
+#define RJ_HL_TW
 #define RJ_HL_T0
 #define RJ_HL_T1(fast)
 #define RJ_HL_T2
@@ -543,6 +547,7 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
         hl_flush<DEC, GROUP>(stage, fl, RJ_HL_DST(fl));
         fl += GROUP;
       }
+      RJ_HL_TF;
       if (kSplit) {
         if (tail) {  // publish the records (16-bit positions: the next phase must stay below 2^16)
           if ((0u - q) >= RJ_HL_REC_LIMIT) nr = kRec;
@@ -578,6 +583,7 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
 #else
       if (__builtin_amdgcn_ballot_w64(avail < rr + PHASE + 1u) != 0) {
 #endif
+        RJ_HL_TW;
         RJ_HL_WAIT_RING(rr + PHASE + 1u);
         wc = ring[rr & (RJ_HL_WORDS - 1)];  // the last step's read-ahead may predate the commit
       }
@@ -597,6 +603,8 @@ __global__ __launch_bounds__(2 * DEC, 2) void k_huff(
       atomicAdd(&rj_hl_stamp[6], st_loop);
       atomicMax(&rj_hl_stamp[7], st_loop);
       atomicAdd(&rj_hl_stamp[8], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - st_begin_rt));
+      atomicAdd(&rj_hl_stamp[9], (unsigned long long)st_flush);
+      atomicAdd(&rj_hl_stamp[10], (unsigned long long)st_waits);
     }
 #endif
     stage[ne & (kStage - 1)] = RJ_RE_TERM;
@@ -1232,14 +1240,17 @@ hipError_t LaunchHuffChunks(hipStream_t st, const RjImageDev *imgs, int nimg, ui
 
 #ifdef RJ_HL_STAMPS
 void DumpHuffStamps() {
-  unsigned long long h[10];
+  unsigned long long h[11];
   (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(rj_hl_stamp), sizeof(h));
   const double w = h[4] ? double(h[4]) : 1.0;
   const double ph = double(h[2] + h[3]) ? double(h[2] + h[3]) : 1.0;
   fprintf(stderr, "[rj k_huff] waves %llu: per wave %.0f phases (%.0f safe), %.0f escape steps; cycles per phase: steps %.0f, end %.0f; "
-          "decode cycles per wave %.0f (max %llu); clock %.0f MHz\n",
-          h[4], ph / w, h[3] / w, h[5] / w, h[0] / ph, h[1] / ph, h[6] / w, h[7], h[8] ? 100.0 * double(h[6]) / double(h[8]) : 0.0);
-  unsigned long long z[10] = {};
+          "decode cycles per wave %.0f (max %llu); clock %.0f MHz; of the end: to the flush's end %.0f, ring checks per phase %.3f\n",
+          h[4], ph / w, h[3] / w, h[5] / w, h[0] / ph, h[1] / ph, h[6] / w, h[7], h[8] ? 100.0 * double(h[6]) / double(h[8]) : 0.0,
+          h[9] / ph, h[10] / ph);
+  // (a stamp waits for the wave's outstanding LDS operations: "end" includes the drain of the
+  // last steps' lookups, not only the phase-end work)
+  unsigned long long z[11] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(rj_hl_stamp), z, sizeof(z));
   unsigned long long c[14];
   (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(rj_hc_stamp), sizeof(c));

@@ -65,7 +65,7 @@ hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, in
 // Live rows (rj_device.h RjLive): K2 beside K1 (second stream; grid = lv.rows, one workgroup per
 // ticket), and the stream-ordered K2 after K1 over the published rows no ticket took.
 hipError_t LaunchRowsLive(hipStream_t st, const RjImageDev *imgs, int nimg, const RjLive &lv, RjCoefBuf coefs,
-                          const RjTableSet *tabsets, uint32_t *wide_cnt, uint2 *wide_list);
+                          const RjTableSet *tabsets, uint32_t *wide_cnt, uint2 *wide_list, uint32_t extra_lds = 0);
 hipError_t LaunchRowsRest(hipStream_t st, const RjImageDev *imgs, int nimg, const RjLive &lv, RjCoefBuf coefs,
                           const RjTableSet *tabsets, uint32_t *wide_cnt, uint2 *wide_list);
 // The split-aware instance alone over an (image, row) list, decoding only the rows whose head met

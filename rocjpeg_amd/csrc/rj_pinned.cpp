@@ -24,8 +24,6 @@ constexpr size_t kMaxFreeChunks = 8;  // released chunks kept for reuse (512 MB)
 
 struct Arena {
   std::mutex mu;
-  std::shared_ptr<PinnedChunk> cur;  // the chunk slots are carved from
-  size_t used = 0;
   std::vector<uint8_t *> free_chunks;  // buffers of released kChunkBytes chunks
   int state = 0;                        // 0 unprobed, 1 usable, -1 disabled
   size_t pinned = 0;                    // bytes held from hipHostMalloc (live chunks + free_chunks)
@@ -35,6 +33,20 @@ struct Arena {
 Arena &TheArena() {
   static Arena *a = new Arena;  // never destroyed: slots may outlive static destructors
   return *a;
+}
+
+// The chunk a thread carves its slots from.  Per thread, so that the streams one thread parses
+// one after another stay adjacent when several threads parse at once (jpegdecodeperf: a thread per
+// handle, each parsing its own files): a decode call then uploads a thread's streams in a few
+// large DMAs.  With one shared chunk, concurrent parses interleave their slots and a 512-image
+// call became ~500 DMAs of one stream each (profiles/r6_experiments/host_input_threads.txt).
+struct ThreadChunk {
+  std::shared_ptr<PinnedChunk> cur;
+  size_t used = 0;
+};
+ThreadChunk &MyChunk() {
+  static thread_local ThreadChunk t;
+  return t;
 }
 
 void ReturnBuffer(uint8_t *p, size_t size) {
@@ -94,15 +106,16 @@ PinnedSlot PinnedAlloc(size_t bytes) {
     c = NewChunk(a, need);
     if (c) p = c->base;
   } else {
-    if (!a.cur || a.used + need > a.cur->size) {
-      retired = std::move(a.cur);
-      a.cur = NewChunk(a, kChunkBytes);
-      a.used = 0;
+    ThreadChunk &t = MyChunk();
+    if (!t.cur || t.used + need > t.cur->size) {
+      retired = std::move(t.cur);
+      t.cur = NewChunk(a, kChunkBytes);
+      t.used = 0;
     }
-    if (a.cur) {
-      c = a.cur;
-      p = c->base + a.used;
-      a.used += need;
+    if (t.cur) {
+      c = t.cur;
+      p = c->base + t.used;
+      t.used += need;
     }
   }
   if (p != nullptr) {

@@ -187,7 +187,7 @@ def test_c2_1024_split5_damaged(split5_dec):
     assert st == 0, R.error_name(st)
     cu = t.cuda.get_device_properties(0).multi_processor_count
     if 256 * cu < tm["intervals"] <= 320 * cu:
-        assert tm["lean_five"] == 1 and tm["lean_split"] > 0 and tm["live"] == 1
+        assert tm["lean_five"] == 1 and tm["lean_split"] > 0
     ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
     bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
     assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
@@ -244,6 +244,30 @@ def test_c2_1024_live_rows_damaged(live_dec):
     ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
     bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
     assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
+
+
+def test_c2_1024_host_streams_two_handles(dec):
+    """The drop-in input path: 1024 C2 streams in host memory (each call stages them over PCIe), on
+    a handle with profiling off -- the call decodes its second half on a helper handle on a second
+    host thread (rj_decoder.h DecodeSplit), so one half's upload overlaps the other's kernels.
+    Every image equal to the oracle; a bad stream in the second half fails the call with its status."""
+    t = torch()
+    distinct, copies = 64, 16
+    datas = _c2_images(distinct, seed0=6060)
+    with ThreadPoolExecutor(16) as ex:
+        want = list(ex.map(lambda d: O.oracle_decode(d, int(R.OutputFormat.RGB), [(1080, 5760)]), datas))
+    streams = [R.JpegStream(datas[i % distinct]) for i in range(distinct * copies)]
+    out = t.full((len(streams), 1080, 5760), 0xA5, dtype=t.uint8, device="cuda")
+    imgs = [R.make_image([out[i].data_ptr()], [5760]) for i in range(len(streams))]
+    st = dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs)
+    assert st == 0, R.error_name(st)
+    ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
+    bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
+    assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
+    by = {f["name"]: f for f in O.manifest()}
+    s411 = R.JpegStream(O.fixture_bytes(by["c411_q90_128x64"]))
+    st = dec.decode_batched(streams[:900] + [s411] + streams[901:], R.decode_params(R.OutputFormat.RGB), imgs)
+    assert st == R.Status.JPEG_NOT_SUPPORTED, R.error_name(st)
 
 
 def test_c2_1024_default_pipelined_layout(dec):

@@ -168,3 +168,72 @@ def test_eight_handles_batch1_coalesced():
     _run_threads(8, work)
     c1 = R.coalesce_stats()
     assert c1[0] - c0[0] == 8 * 12  # every call took part
+
+
+def _c2_images(count, seed0=1234):
+    import os
+    import sys
+    sys.path.insert(0, O.ROOT)
+    import bench
+    bench._init_gen()
+    return [bench._make_jpeg((s, bench.WORKLOADS["c2"]["gen"])) for s in range(seed0, seed0 + count)]
+
+
+def test_eight_handles_batch1_one_bad_caller_latency():
+    """jpegdecodeperf's shape with one misbehaving caller: 8 threads, a handle each, one 1080p
+    image per call, rounds in lockstep; in the second run thread 7's every call is an unsupported
+    stream.  The coalescer checks each member before the combined call (Decoder::Check), so the
+    bad call fails alone and the healthy ones are decoded once, together: their outputs stay
+    oracle-exact and their p90 call latency stays within 1.5x of the clean run's (+0.3 ms of
+    timer slack).  Reference: rocjpeg_decoder.h:174 (per-handle serialisation)."""
+    G.torch()
+    import time
+
+    import torch
+    fmt = R.OutputFormat.RGB
+    datas = _c2_images(8, seed0=5150)
+    want = [O.oracle_decode(d, int(fmt), [(1080, 5760)])[1][0] for d in datas]
+    by = {f["name"]: f for f in O.manifest()}
+    bad = O.fixture_bytes(by["c411_q90_128x64"])
+    rounds = 40
+
+    def run(with_bad):
+        lat = [[] for _ in range(8)]
+        outs = [torch.full((1080, 5760), 0xA5, dtype=torch.uint8, device="cuda:0") for _ in range(8)]
+        torch.cuda.synchronize()
+
+        def work(t):
+            dec = R.JpegDecoder(R.Backend.HARDWARE, 0)
+            try:
+                good = R.JpegStream(datas[t])
+                bs = R.JpegStream(bad)
+                bbuf = torch.full((64, 384), 0xA5, dtype=torch.uint8, device="cuda:0")
+                torch.cuda.synchronize()
+                img = R.make_image([outs[t].data_ptr()], [5760])
+                bimg = R.make_image([bbuf.data_ptr()], [384])
+                for rnd in range(rounds):
+                    barrier.wait()
+                    if with_bad and t == 7:
+                        st = dec.decode(bs, R.decode_params(fmt), bimg)
+                        assert st == R.Status.JPEG_NOT_SUPPORTED, R.error_name(st)
+                        continue
+                    t0 = time.perf_counter()
+                    st = dec.decode(good, R.decode_params(fmt), img)
+                    lat[t].append(time.perf_counter() - t0)
+                    assert st == 0, R.error_name(st)
+                good.close()
+                bs.close()
+            finally:
+                dec.close()
+
+        import threading
+        barrier = threading.Barrier(8)
+        _run_threads(8, work)
+        for t in range(8 if not with_bad else 7):
+            assert np.array_equal(outs[t].cpu().numpy(), want[t]), t
+        healthy = np.concatenate([np.array(lat[t][5:]) for t in range(7)])  # (the first rounds warm up)
+        return float(np.percentile(healthy, 90))
+
+    clean = run(False)
+    with_bad = run(True)
+    assert with_bad <= 1.5 * clean + 0.3e-3, (clean, with_bad)

@@ -1,5 +1,9 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-L=$PWD/rocjpeg_amd
-STEPS=5 bash tools/gpu_ab_env.sh off:RJ_LIB_PATH=$L/librocjpeg_amd_hlstamps.so,RJ_DEBUG_STAMPS=1,RJ_K2_LIVE=0 live:RJ_LIB_PATH=$L/librocjpeg_amd_hlstamps.so,RJ_DEBUG_STAMPS=1
-for f in gpurun_out/ab/off_1.log gpurun_out/ab/live_1.log gpurun_out/ab/off_2.log gpurun_out/ab/live_2.log; do echo $f; grep "rj k_huff\]" $f | tail -3; done
+mkdir -p gpurun_out/r6j
+timeout -k 10 300 python3 -u -m pytest tests/test_batch_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r6j/pytest.log 2>&1 || { tail -30 gpurun_out/r6j/pytest.log; exit 1; }
+tail -1 gpurun_out/r6j/pytest.log
+timeout -k 10 300 python3 tools/host_input_threads.py 6 1,2 > gpurun_out/r6j/host_threads.log 2>&1 || { tail -20 gpurun_out/r6j/host_threads.log; exit 1; }
+grep "T=" gpurun_out/r6j/host_threads.log
+RJ_SPLIT_HOST=0 timeout -k 10 300 python3 tools/host_input_threads.py 6 1 > gpurun_out/r6j/host_threads_nosplit.log 2>&1 || { tail -20 gpurun_out/r6j/host_threads_nosplit.log; exit 1; }
+grep "T=" gpurun_out/r6j/host_threads_nosplit.log
