@@ -416,15 +416,34 @@ def call_shapes(dec, datas, fmt, dev, threads=8):
     shapes = b.shapes
     b.close()
 
-    def perf_threads(resident, budget_s=1.0):
-        """jpegdecodeperf: each thread its own handle, its own images, batch 1."""
+    def perf_threads(resident, budget_s=1.0, bad_caller=False):
+        """jpegdecodeperf: each thread its own handle, its own images, batch 1.  bad_caller: the
+        last thread's every call is an unsupported (4:1:1) stream, which must fail alone; the rates
+        and latencies are the healthy threads'."""
         per = max(1, min(len(datas), 256) // threads)
         rates, errs = [0.0] * threads, []
+        lats = [[] for _ in range(threads)]
         barrier = threading.Barrier(threads)
+        bad_bytes = open(os.path.join(ROOT, "tests", "golden", "img", "c411_q90_128x64.jpg"), "rb").read()
 
         def worker(t):
             try:
                 d = R.JpegDecoder(R.Backend.HARDWARE, dev.index or 0)
+                if bad_caller and t == threads - 1:
+                    bs = R.JpegStream(bad_bytes)
+                    bout = torch.empty(64 * 384, dtype=torch.uint8, device=dev)
+                    bimg = R.make_image([bout.data_ptr()], [384])
+                    bpar = R.decode_params(fmt)
+                    hb = (ctypes.c_void_p * 1)(bs.handle)
+                    barrier.wait()
+                    t_end = time.perf_counter() + budget_s
+                    while time.perf_counter() < t_end:
+                        st_ = L.rocJpegDecodeBatched(d.handle, hb, 1, ctypes.byref(bpar), ctypes.byref(bimg))
+                        if st_ != int(R.Status.JPEG_NOT_SUPPORTED):
+                            raise RuntimeError("the bad caller got " + R.error_name(st_))
+                    bs.close()
+                    d.close()
+                    return
                 mine = datas[t * per:(t + 1) * per]
                 if resident:
                     st_, streams = d.parse_device(mine)
@@ -448,6 +467,7 @@ def call_shapes(dec, datas, fmt, dev, threads=8):
                     st_ = L.rocJpegDecodeBatched(d.handle, _sub(hs, ctypes.c_void_p, j, 1), 1, ctypes.byref(par),
                                                  ctypes.byref(img))
                     tot += time.perf_counter() - t0
+                    lats[t].append(time.perf_counter() - t0)
                     if st_ != 0:
                         raise RuntimeError(R.error_name(st_))
                     cnt += 1
@@ -469,9 +489,14 @@ def call_shapes(dec, datas, fmt, dev, threads=8):
             x.join()
         if errs:
             return {"error": errs[0]}
-        return {"images_per_s_summed": round(sum(rates), 1), "threads": threads,
-                "per_thread_images_per_s": [round(r, 1) for r in rates],
-                "spread_max_over_min": round(max(rates) / min(rates), 3) if min(rates) > 0 else None}
+        healthy = [r for t, r in enumerate(rates) if not (bad_caller and t == threads - 1)]
+        lat = np.concatenate([np.array(x) for x in lats if x]) * 1e3
+        return {"images_per_s_summed": round(sum(healthy), 1), "threads": threads,
+                "per_thread_images_per_s": [round(r, 1) for r in healthy],
+                "spread_max_over_min": round(max(healthy) / min(healthy), 3) if min(healthy) > 0 else None,
+                "latency_ms": {"p50": round(float(np.median(lat)), 4), "p90": round(float(np.percentile(lat, 90)), 4)},
+                **({"bad_caller": "thread %d: an unsupported stream per call, failing alone" % (threads - 1)}
+                   if bad_caller else {})}
 
     def perf_sample(passes=12, count=256):
         """The same shape from C, without the Python interpreter lock between the threads: the
@@ -500,6 +525,8 @@ def call_shapes(dec, datas, fmt, dev, threads=8):
     res[f"perf_threads{threads}_batch1_c_sample"] = perf_sample()
     res[f"perf_threads{threads}_batch1_host_streams"] = perf_threads(False)
     res[f"perf_threads{threads}_batch1_resident"] = perf_threads(True)
+    # the coalescer with one misbehaving caller: healthy callers' p90 latency
+    res[f"perf_threads{threads}_batch1_resident_one_bad_caller"] = perf_threads(True, bad_caller=True)
     c0 = R.coalesce_stats()
     res["coalescing"] = {"calls": c0[0], "combined_calls": c0[1], "combined_members": c0[2],
                          "note": "process totals of rocJpegAmdGetCoalesceStats: concurrent small calls "
