@@ -82,6 +82,9 @@ __global__ __launch_bounds__(64) void k_scan(const RjScanJob *__restrict__ jobs,
     const uint32_t nb_lane = __shfl_down(cur.x & 0xFFu, 1, 64);
     const uint32_t nb_next = __shfl(nxt.x & 0xFFu, 0, 64);
     const uint32_t nb = lane == 63 ? nb_next : nb_lane;
+    // and the one after that, for lane 63's last byte: an FF there followed by the next step's
+    // FF D9 is a fill byte in front of the end, not a drop (the end is found only next step)
+    const uint32_t nb2_next = __shfl((nxt.x >> 8) & 0xFFu, 0, 64);
     // bytes equal to 0xFF: zero bytes of ~w (exact per byte)
     auto ffb = [](uint32_t w) {
       const uint32_t t = ~w;
@@ -109,6 +112,7 @@ __global__ __launch_bounds__(64) void k_scan(const RjScanJob *__restrict__ jobs,
       oth_m |= (ff && nx != 0xFFu && nx != 0x00u && !rst) ? 1u << j : 0u;
       d9 = (ff && nx == 0xD9u && d9 == 0xFFFFFFFFu) ? p0 + j : d9;
     }
+    if (lane == 63 && nb == 0xFFu && nb2_next == 0xD9u) dff_m &= 0x7FFFu;  // FF | FF D9 across steps
     bool last = false;
     if (__builtin_amdgcn_ballot_w64(d9 != 0xFFFFFFFFu) != 0) {
       uint32_t m = d9;

@@ -56,6 +56,14 @@ def variants(data):
     out["foreign_marker"] = data[:mid] + b"\xff\xe1" + data[mid:]
     out["fill_run"] = data[:mid] + b"\xff\xff\xff\xff\x00" + data[mid:]
     out["ff_at_end"] = data[:e] + b"\xff"
+    # a fill byte and the EOI across the scan's 1-KB step boundary (ECS bytes 1023 | 1024, 1025 =
+    # FF | FF D9): the fill byte is not a drop (an FF counts only below the end)
+    for cut in (1023, 2047):
+        if len(body) > cut + 64:
+            b = bytearray(body[:cut])
+            if b[-1] == 0xFF:
+                b[-1] = 0x12
+            out[f"fill_eoi_step_{cut + 1}"] = data[:s] + bytes(b) + b"\xff\xff\xd9"
     return out
 
 
