@@ -1,6 +1,8 @@
 // rj_decoder.cpp -- batch planner + launch sequence (see rj_decoder.h).
 #include "rj_decoder.h"
 
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -131,6 +133,8 @@ Decoder::~Decoder() {
     for (auto &e : live_t_)
       if (e) (void)hipEventDestroy(e);
     if (split_ev_) (void)hipEventDestroy(split_ev_);
+    if (bev_) (void)hipEventDestroy(bev_);
+    if (bstream_) (void)hipStreamDestroy(bstream_);
     if (lstream_) (void)hipStreamDestroy(lstream_);
     (void)hipStreamDestroy(stream_);
   }
@@ -157,6 +161,8 @@ int Decoder::Initialize() {
     return -7;  // ROCJPEG_STATUS_ARCH_MISMATCH
   }
   RJ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  // (created next to stream_: streams take the process's hardware queues round-robin)
+  RJ_HIP(hipStreamCreateWithFlags(&bstream_, hipStreamNonBlocking));
   for (auto &e : ev_) RJ_HIP(hipEventCreate(&e));
   if (const char *g = getenv("RJ_PIPE_GROUPS")) {
     pipe_groups_ = std::max(1, std::min(kMaxPipe, atoi(g)));
@@ -189,6 +195,9 @@ int Decoder::Initialize() {
   for (auto &e : live_ev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : live_t_) RJ_HIP(hipEventCreate(&e));
   RJ_HIP(hipEventCreateWithFlags(&split_ev_, hipEventDisableTiming));
+  RJ_HIP(hipEventCreateWithFlags(&bev_, hipEventDisableTiming));
+  if (const char *sp = getenv("RJ_SYNC_SPIN")) spin_sync_ = atoi(sp) != 0;
+  if (const char *ub = getenv("RJ_UPLOAD_B_SIDE")) side_b_ = atoi(ub) != 0;
   if (const char *lk = getenv("RJ_K2_LIVE")) {  // 0 off; 2 (test): the live launch always gives up
     live_k2_ = atoi(lk) != 0;  // 1: on
     live_test_giveup_ = atoi(lk) == 2;
@@ -621,20 +630,42 @@ int Decoder::DecodeSplit(Stream *const *streams, int n, const RocJpegDecodeParam
   return st1 != kOk ? st1 : st2;
 }
 
+// The end of a call: the calling thread polls the stream (yielding between polls) instead of
+// sleeping in hipStreamSynchronize when spin_sync_ is set (env RJ_SYNC_SPIN=1).
+hipError_t Decoder::WaitCall() {
+  if (spin_sync_) {
+    hipError_t e;
+    while ((e = hipStreamQuery(stream_)) == hipErrorNotReady) sched_yield();
+    if (e != hipSuccess) return e;
+  }
+  return hipStreamSynchronize(stream_);
+}
+
 int Decoder::DecodeOne(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
   std::lock_guard<std::mutex> lock(mu_);
-  // Hold every stream's lock for the call: a concurrent re-parse must not move its bytes.
+  // Hold every stream's lock for the call: a concurrent re-parse must not move its bytes.  Locks
+  // are taken in address order (no deadlock between calls sharing streams); a batch already in
+  // increasing order -- the usual one, streams created in sequence -- is not sorted again.
   std::vector<std::unique_lock<std::mutex>> locks;
-  std::vector<Stream *> uniq(streams, streams + n);
-  std::sort(uniq.begin(), uniq.end());
-  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  std::vector<Stream *> &uniq = lock_order_;
+  uniq.assign(streams, streams + n);
+  const std::less<Stream *> before;
+  bool increasing = true;
+  for (int i = 1; i < n && increasing; i++) increasing = before(uniq[i - 1], uniq[i]);
+  if (!increasing) {
+    std::sort(uniq.begin(), uniq.end(), before);
+    uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  }
   locks.reserve(uniq.size());
   for (Stream *s : uniq) locks.emplace_back(s->mutex());
   const int r = DecodeLocked(streams, n, params, dst);
   // an error return may leave copies in flight on the stream (from the parse-time pinned arena
   // or the staging buffers): they finish before the streams' locks are released, so a
   // re-parse or destroy cannot recycle memory a DMA is still reading
-  if (r != kOk) (void)hipStreamSynchronize(stream_);
+  if (r != kOk) {
+    (void)hipStreamSynchronize(stream_);
+    (void)hipStreamSynchronize(bstream_);
+  }
   return r;
 }
 
@@ -1783,6 +1814,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       aligned = aligned && p.rows_aligned;
       for (const uint16_t b : p.seg_bucket) pos[bucket(b)]++;
     }
+    sc_.bucket_cnt.assign(pos.begin(), pos.end());  // (the outlier split counts on it)
     for (uint32_t b = 0, cum = 0; b < kBuckets; b++) {
       const uint32_t c = pos[b];
       pos[b] = cum;
@@ -1801,9 +1833,19 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     uint2 *rl = rows_from_lanes ? row_list.data() : nullptr;
     uint32_t gs = 0;
     const bool want_pos = ngroups > 1;
+    // the lean splits below (longest lanes first) read the intervals' exact lengths in lane order
+    const bool want_len = lean && desc && ngroups == 1 && (outlier_split_ || (five_waves_ && split5_t_ > 0.0));
+    std::vector<uint64_t> &lane_len = sc_.lane_len;
+    if (want_len) lane_len.resize(seg_total);
     for (int i = 0; i < n; i++) {
       const DecodePlan &p = streams[i]->plan();
-      if (rl != nullptr || want_pos) {
+      if (want_len) {
+        for (size_t q = 0; q < p.segs.size(); q++) {
+          const uint32_t l = pos[bucket(p.seg_bucket[q])]++;
+          ls[l] = gs++;
+          lane_len[l] = p.seg_lenblk[q];
+        }
+      } else if (rl != nullptr || want_pos) {
         uint32_t r = 0;
         for (size_t q = 0; q < p.segs.size(); q++) {
           const uint32_t l = pos[bucket(p.seg_bucket[q])]++;
@@ -1877,38 +1919,35 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // more than outlier_frac_ of the intervals would split (near-uniform lengths, e.g. C2:
   // splitting nearly everything is slower).  C4's mixed resolutions: 42,376 of
   // 75,350 split, +12 %. ----
+  const auto t_sorted = std::chrono::steady_clock::now();
   uint32_t nsplit = 0, nl_split = 0;
   RjHuffSplit hsplit{0, 0};
+  // lane j's interval: (destuffed bytes, blocks), gathered by the lane sort
+  auto lane_len = [&](uint32_t j) {
+    const uint64_t v = sc_.lane_len[j];
+    return uint2{uint32_t(v), uint32_t(v >> 32)};
+  };
   if (lean && sorted && lanes_desc && ngroups == 1 && !any_split && outlier_split_ && seg_total > 0) {
     // one round of the split grid: two workgroups per CU of RJ_HL_SPLIT_DEC decoder lanes
     const int64_t waves = int64_t(cu_count_) * 2 * (RJ_HL_SPLIT_DEC / 64);
     const int64_t kmax = 64 * waves - int64_t(seg_total);
     uint64_t lim = 0;
     {
-      // count the outliers on the cached 32-B length buckets first; the descriptors' exact
-      // lengths are gathered only when the call does split
-      std::vector<uint16_t> &gb = sc_.seg_bkt;
-      gb.resize(seg_total);
-      uint32_t g = 0;
-      for (int i = 0; i < n; i++)
-        for (const uint16_t b : streams[i]->plan().seg_bucket) gb[g++] = b;
-      const uint32_t blim = uint32_t(double(gb[lane_seg[0]]) * outlier_t_);
+      // count the outliers on the lane sort's 32-B length histogram first (longest bucket
+      // first); exact lengths only for the lanes the call does split
+      const std::vector<uint32_t> &hist = sc_.bucket_cnt;
+      const uint32_t nb = uint32_t(hist.size());
+      uint32_t k0 = 0;
+      while (k0 < nb && hist[k0] == 0) k0++;
+      const uint32_t blim = uint32_t(double(nb - 1 - k0) * outlier_t_);
       uint32_t cnt = 0;
-      while (cnt < seg_total && gb[lane_seg[cnt]] > blim) cnt++;
-      if (cnt == 0 || double(cnt) > outlier_frac_ * double(seg_total)) {
-        lim = UINT64_MAX;  // nothing to split
-      } else {
-        std::vector<uint2> &sl = sc_.seg_len;
-        sl.resize(seg_total);
-        g = 0;
-        for (int i = 0; i < n; i++)
-          for (const uint64_t v : streams[i]->plan().seg_lenblk) sl[g++] = uint2{uint32_t(v), uint32_t(v >> 32)};
-        lim = uint64_t(double(sl[lane_seg[0]].x) * outlier_t_);
-      }
+      for (uint32_t k = k0; k < nb && nb - 1 - k > blim; k++) cnt += hist[k];
+      if (cnt == 0 || double(cnt) > outlier_frac_ * double(seg_total)) lim = UINT64_MAX;  // nothing to split
+      else lim = uint64_t(double(lane_len(0).x) * outlier_t_);
     }
     uint64_t cap = 0;
     while (int64_t(nsplit) < kmax && nsplit < seg_total && lim != UINT64_MAX) {
-      const uint2 sl = sc_.seg_len[lane_seg[nsplit]];
+      const uint2 sl = lane_len(nsplit);
       if (sl.x < RJ_SPLIT_MIN_BYTES) break;  // lanes are sorted longest first
       if (sl.x <= lim) break;
       cap = std::max<uint64_t>(cap, rj_group(8ull * (sl.x - rj_split_byte(sl.x)) + sl.y +
@@ -1953,20 +1992,15 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       uint32_t ns = 0;
       uint64_t cap = 0;
       if (split5_t_ > 0.0) {
-        std::vector<uint2> &sl = sc_.seg_len;
-        sl.resize(seg_total);
-        uint32_t g = 0;
-        for (int i = 0; i < n; i++)
-          for (const uint64_t v : streams[i]->plan().seg_lenblk) sl[g++] = uint2{uint32_t(v), uint32_t(v >> 32)};
-        const double lim = double(sl[lane_seg[0]].x) * split5_t_;
+        const double lim = double(lane_len(0).x) * split5_t_;
         while (ns < seg_total) {
-          const uint32_t len = sl[lane_seg[ns]].x;
+          const uint32_t len = lane_len(ns).x;
           if (len < RJ_SPLIT_MIN_BYTES || double(len) <= lim) break;
           ns++;
         }
         while (ns > 0 && (ns + 31) / 32 + (seg_total - ns + 63) / 64 > 5ull * cu) ns = ns > 32 ? ns - 32 : 0;
         for (uint32_t j = 0; j < ns; j++) {
-          const uint2 v = sl[lane_seg[j]];
+          const uint2 v = lane_len(j);
           cap = std::max<uint64_t>(cap, rj_group(8ull * (v.x - rj_split_byte(v.x)) + v.y +
                                                  uint64_t(RJ_MAX_BLK_MCU) * RJ_ENT_PER_BLOCK + 1));
         }
@@ -1974,8 +2008,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       const uint32_t wsp = (ns + 31) / 32, wav = wsp + uint32_t((seg_total - ns + 63) / 64);
       const uint32_t host = wav > 4 * cu ? wav - 4 * cu : 0u;  // workgroups that take a fifth wave
       nl_five = cu * RJ_HL_DEC5;
-      std::vector<uint32_t> &l5 = sc_.lane_split;
-      l5.assign(nl_five, UINT32_MAX);
+      // written in place into blob B (its lane list holds 2 x seg_total + 64 >= nl_five words)
+      uint32_t *const l5 = reinterpret_cast<uint32_t *>(h + off_lane_seg);
+      std::fill(l5, l5 + nl_five, UINT32_MAX);
       uint32_t top = 0;  // global waves holding split pairs: [0, top)
       for (uint32_t k = 0; k < wav; k++) {
         // a workgroup that takes a fifth wave lists its four in reverse (shortest first): the
@@ -2008,15 +2043,19 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         bool row_ivals = true;
         for (int i = 0; i < n && row_ivals; i++) row_ivals = imgs[i].ri_mcus == imgs[i].mcux;
         if (row_ivals && nl_five + 2ull * ns <= n_lane_seg) {
-          std::vector<uint8_t> &mark = sc_.split_mark;  // split intervals, then a pass in image order
-          mark.assign(seg_total, 0);
-          for (uint32_t j = 0; j < ns; j++) mark[lane_seg[j]] = 1;
-          l5.resize(nl_five + 2ull * ns);
-          uint2 *sr = reinterpret_cast<uint2 *>(l5.data() + nl_five);
+          // the split intervals as a bit set, read back in interval (= image, row) order
+          std::vector<uint64_t> &mark = sc_.split_bits;
+          mark.assign((uint64_t(seg_total) + 63) / 64, 0ull);
+          for (uint32_t j = 0; j < ns; j++) mark[lane_seg[j] >> 6] |= 1ull << (lane_seg[j] & 63);
+          uint2 *sr = reinterpret_cast<uint2 *>(l5 + nl_five);
           uint32_t k = 0;
-          for (int i = 0; i < n; i++)
-            for (uint32_t r = 0; r < imgs[i].nseg; r++)
-              if (mark[imgs[i].seg_prefix + r]) sr[k++] = uint2{uint32_t(i), r};
+          int i = 0;
+          for (size_t w = 0; w < mark.size(); w++)
+            for (uint64_t bits = mark[w]; bits != 0; bits &= bits - 1) {
+              const uint32_t gs = uint32_t(w * 64 + uint32_t(__builtin_ctzll(bits)));
+              while (imgs[i].seg_prefix + imgs[i].nseg <= gs) i++;
+              sr[k++] = uint2{uint32_t(i), gs - imgs[i].seg_prefix};
+            }
           nsplit_rows = k;
         }
         hsplit.ent = AlignUp(ent_total, RJ_ENT_GROUP);
@@ -2031,6 +2070,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
   }
   timings_.lean_five = nl_five ? 1u : 0u;
+  const auto t_five = std::chrono::steady_clock::now();
   if (any_split) {
     std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(lane_seg.size()) * 4);
     std::memcpy(h + off_seg_lane0, seg_lane0.data(), uint64_t(seg_lane0.size()) * 4);
@@ -2040,7 +2080,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     cbuf.seg_ent = reinterpret_cast<const unsigned long long *>(dbase + off_seg_ent);
   } else if (sorted) {  // lanes in length order; pieces stay at the interval's own slot
     if (nsplit) std::memcpy(h + off_lane_seg, sc_.lane_split.data(), uint64_t(nl_split) * 4);
-    else if (nl_five) std::memcpy(h + off_lane_seg, sc_.lane_split.data(), uint64_t(sc_.lane_split.size()) * 4);
+    else if (nl_five) {}  // written in place
     else std::memcpy(h + off_lane_seg, lane_seg.data(), uint64_t(seg_total) * 4);
     cbuf.lane_seg = d_lane_seg;
     cbuf.seg_lane0 = nullptr;
@@ -2052,7 +2092,19 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t blob_b = (!any_split && sorted && ngroups == 1)
                               ? std::min<uint64_t>(blob, AlignUp(off_lane_seg + uint64_t(nsplit ? nl_split : (nl_five ? nl_five + 2 * nsplit_rows : seg_total)) * 4, 256))
                               : blob;
-  if (blob_b > blob_a) RJ_HIP(hipMemcpyAsync(dbase + blob_a, h + blob_a, blob_b - blob_a, hipMemcpyHostToDevice, stream_));
+  if (blob_b > blob_a) {
+    if (side_b_ && stage_bytes == 0 && ecs_stage_bytes == 0) {
+      // on its own stream: the lane lists cross PCIe while K0 runs, and K1 waits for them by an
+      // event (behind K0 in the call's stream the copy ran only once K0 was done: ~25 us before K1).
+      // Only calls with nothing staged: beside staged bitstreams (DecodeSplit's two halves) the
+      // small copy queued behind the other half's upload (host input 126k -> 98-108k images/s)
+      RJ_HIP(hipMemcpyAsync(dbase + blob_a, h + blob_a, blob_b - blob_a, hipMemcpyHostToDevice, bstream_));
+      RJ_HIP(hipEventRecord(bev_, bstream_));
+      RJ_HIP(hipStreamWaitEvent(stream_, bev_, 0));
+    } else {
+      RJ_HIP(hipMemcpyAsync(dbase + blob_a, h + blob_a, blob_b - blob_a, hipMemcpyHostToDevice, stream_));
+    }
+  }
 
   const auto t_end = std::chrono::steady_clock::now();
   timings_.host_ms = std::chrono::duration<float, std::milli>(t_end - t_host0).count();
@@ -2060,9 +2112,11 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
       return std::chrono::duration<double, std::milli>(b - a).count();
     };
-    fprintf(stderr, "[rj host] validate %.3f dedupe %.3f layout %.3f lanes+blob-A %.3f sort/rows+blob-B %.3f ms\n",
+    fprintf(stderr,
+            "[rj host] validate %.3f dedupe %.3f layout %.3f lanes+blob-A %.3f | after K0: sort %.3f split %.3f "
+            "blob-B %.3f ms\n",
             ms(t_host0, t_dedupe), ms(t_dedupe, t_layout), ms(t_layout, t_lanes), ms(t_lanes, t_k0),
-            ms(t_k0, t_end));
+            ms(t_k0, t_sorted), ms(t_sorted, t_five), ms(t_five, t_end));
   }
   bool live = false;
   RjLive lv{};
@@ -2176,7 +2230,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   for (const RouteCopy &rc : routes_)  // to the caller's device / host memory
     RJ_HIP(hipMemcpy2DAsync(rc.user, rc.pitch, d_route_.as<uint8_t>() + rc.off, rc.pitch, rc.row_bytes, rc.rows,
                             hipMemcpyDefault, stream_));
-  RJ_HIP(hipStreamSynchronize(stream_));
+  RJ_HIP(WaitCall());
   if (live && *reinterpret_cast<volatile uint32_t *>(h_wide_flag_ + 1)) {
     // a live K2 workgroup gave up on its row (never expected; rj_fused.hip live_claim): decode
     // every row again in stream order, then redo the output stage -- all idempotent

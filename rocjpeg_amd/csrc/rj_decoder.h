@@ -92,6 +92,7 @@ class Decoder {
   // env RJ_SPLIT_HOST=0 turns it off; never while profiling (the timings are per handle).
   int DecodeSplit(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
   std::atomic<bool> split_host_{true};
+  std::vector<Stream *> lock_order_;  // DecodeOne's stream lock order (under mu_)
   std::unique_ptr<Decoder> helper_;
   static constexpr int kSplitHostMin = 1024;  // staged (non-resident) images a call needs to split
   hipEvent_t split_ev_ = nullptr;                // the first half's uploads are done (recorded on stream_)
@@ -186,6 +187,13 @@ class Decoder {
   hipEvent_t live_ev_[2] = {};  // fork (descriptors uploaded), join (the live K2 done)
   hipEvent_t live_t_[4] = {};   // profiling: live K2 span (its stream), rest + split span (after K1)
   DeviceBuffer d_live_;          // published-row slots
+  // upload B (K1 lane order, K2 row lists) on its own stream while K0 runs; K1 waits for it by an
+  // event instead of behind K0 in the call's stream (env RJ_UPLOAD_B_SIDE=0: in stream order)
+  bool side_b_ = true;
+  bool spin_sync_ = false;  // env RJ_SYNC_SPIN=1: WaitCall polls the stream instead of sleeping
+  hipError_t WaitCall();
+  hipStream_t bstream_ = nullptr;
+  hipEvent_t bev_ = nullptr;
 
   // a run of non-resident streams whose parse-time pinned copies are adjacent (one DMA)
   struct PinRun {
@@ -202,9 +210,10 @@ class Decoder {
     std::vector<uint64_t> stage_off, ecs_off;
     std::vector<uint32_t> chunk_img;
     std::vector<uint32_t> tab_of, row_prefix, grow_prefix, seg_lane0, lane_seg, bucket_pos, seg_pos, lane_split;
-    std::vector<uint2> seg_len;  // per interval: destuffed bytes, blocks (outlier split planning)
-    std::vector<uint16_t> seg_bkt;  // per interval: 32-B length bucket (outlier split planning)
-    std::vector<uint8_t> is_fused, row_group, routed, split_mark;
+    std::vector<uint32_t> bucket_cnt;  // the lane sort's 32-B length histogram (its bucket order)
+    std::vector<uint64_t> lane_len;    // per lane (sorted order): the interval's seg_lenblk
+    std::vector<uint64_t> split_bits;  // per interval: split by the five-wave layout
+    std::vector<uint8_t> is_fused, row_group, routed;
     std::vector<uint2> row_list;
     std::vector<uint32_t> prow_prefix, pgrow_prefix, prog_lanes, prog_bucket;  // progressive images
     std::vector<RjFoldJob> fold_jobs;
