@@ -197,6 +197,7 @@ int Decoder::Initialize() {
   RJ_HIP(hipEventCreateWithFlags(&split_ev_, hipEventDisableTiming));
   RJ_HIP(hipEventCreateWithFlags(&bev_, hipEventDisableTiming));
   if (const char *sp = getenv("RJ_SYNC_SPIN")) spin_sync_ = atoi(sp) != 0;
+  if (const char *kl = getenv("RJ_K0_LDS")) k0_lds_ = atoi(kl) != 0;
   if (const char *ub = getenv("RJ_UPLOAD_B_SIDE")) side_b_ = atoi(ub) != 0;
   if (const char *lk = getenv("RJ_K2_LIVE")) {  // 0 off; 2 (test): the live launch always gives up
     live_k2_ = atoi(lk) != 0;  // 1: on
@@ -1668,7 +1669,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (cbuf.count) RJ_HIP(hipMemsetAsync(cbuf.count, 0, sizeof(unsigned long long), stream_));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
   RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>(),
-                      reinterpret_cast<const uint32_t *>(dbase + off_dsmap)));
+                      reinterpret_cast<const uint32_t *>(dbase + off_dsmap), k0_lds_));
   const uint8_t *k1_src = d_destuff_.as<uint8_t>();
   if (prog_images) {  // progressive images: K1p level by level, then their K2 rows (dense)
     const uint32_t *d_plane = reinterpret_cast<const uint32_t *>(dbase + off_plane);

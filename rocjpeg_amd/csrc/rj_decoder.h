@@ -190,6 +190,7 @@ class Decoder {
   // upload B (K1 lane order, K2 row lists) on its own stream while K0 runs; K1 waits for it by an
   // event instead of behind K0 in the call's stream (env RJ_UPLOAD_B_SIDE=0: in stream order)
   bool side_b_ = true;
+  bool k0_lds_ = true;      // env RJ_K0_LDS=0: K0 stores a compacted chunk's bytes one by one (A/B)
   bool spin_sync_ = false;  // env RJ_SYNC_SPIN=1: WaitCall polls the stream instead of sleeping
   hipError_t WaitCall();
   hipStream_t bstream_ = nullptr;

@@ -9,8 +9,9 @@ namespace rj {
 
 // K0: byte-unstuffing of the entropy-coded data (one wavefront per RjDsBlock).
 // ds_map (may be null): the image holding K0 block 64 k, for k <= nblocks / 64, + a sentinel
+// lds: the block's output assembled in LDS, aligned dword stores (false: the byte-store form)
 hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nblocks, uint8_t *destuffed,
-                         const uint32_t *ds_map = nullptr);
+                         const uint32_t *ds_map = nullptr, bool lds = true);
 
 // K1 (rj_entropy.hip): Huffman entropy decode -> sparse entry streams + pieces.  stage 0: one
 // lane per interval chunk; 1: sync resolution; 2: serial re-decode of the flagged intervals.

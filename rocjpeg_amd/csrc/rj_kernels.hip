@@ -35,11 +35,20 @@ __device__ __forceinline__ uint32_t wave_exclusive_scan(uint32_t v, uint32_t &to
 // K0: destuff.  Within an interval's raw range the host guarantees only data bytes,
 // FF 00 pairs and FF fill runs in front of an FF 00 occur.  Byte i is dropped when
 // (b[i] == 00 && b[i-1] == FF) or (b[i] == FF && b[i+1] == FF).
+// kLds: the block's output is assembled in LDS (a chunk with an FF byte as LDS byte writes at
+// its compacted offsets) and leaves as aligned dword stores, bytes only at the two ends; without
+// it, such a chunk's bytes were four global byte stores per lane (~2/3 of 256-B chunks hold an
+// FF byte).
 // ---------------------------------------------------------------------------------------
+template <bool kLds>
 __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ imgs, int nimg,
                                                 uint8_t *__restrict__ destuffed, const uint32_t *__restrict__ ds_map) {
   static_assert(RJ_DS_BLOCK % 256u == 0 && RJ_DS_BLOCK <= 4096u, "256-B chunks, all loads issued up front");
   constexpr int kIt = RJ_DS_BLOCK / 256;
+  // LDS byte m + t holds output byte t (m: the output's misalignment, so LDS dword k is the
+  // output's aligned dword k)
+  __shared__ uint32_t s_out[kLds ? RJ_DS_BLOCK / 4 + 2 : 1];
+  uint8_t *const sb = reinterpret_cast<uint8_t *>(s_out);
   const uint32_t g = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   // the block's image: between the owners of blocks 64 (g / 64) and 64 (g / 64 + 1) (the host's
@@ -79,6 +88,7 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
   const uint32_t after = last ? 0x100u : uint32_t(src[len]);     // byte behind it (0x100: none)
   uint32_t out = 0;
   uint32_t prev_byte = before;  // byte in front of the current chunk
+  const uint32_t m0 = uint32_t(reinterpret_cast<uintptr_t>(dst)) & 3u;
 #pragma unroll
   for (int c = 0; c < kIt; c++) {
     const uint32_t base = uint32_t(c) * 256u;
@@ -90,6 +100,20 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
       const bool ff = ((t - 0x01010101u) & ~t & 0x80808080u) != 0;  // some byte == 0xFF
       if (base + 256u <= len && prev_byte != 0xFFu && __builtin_amdgcn_ballot_w64(ff) == 0) {
         const uint32_t wc = w[c];
+        if constexpr (kLds) {
+          const uint32_t pos = m0 + out, a = pos & 3u, k0 = pos >> 2;
+          if (a == 0) {
+            s_out[k0 + lane] = wc;
+          } else {
+            const uint32_t e = __builtin_amdgcn_alignbyte(wc, wave_prev(wc), 4u - a);
+            if (lane > 0) s_out[k0 + lane] = e;
+            else s_out[k0] = (s_out[k0] & ((1u << (8 * a)) - 1u)) | (wc << (8 * a));  // after the bytes before
+            if (lane == 63) s_out[k0 + 64] = wc >> (8 * (4 - a));
+          }
+          out += 256u;
+          prev_byte = __builtin_amdgcn_readlane(wc, 63) >> 24;
+          continue;
+        }
         const uint32_t m = uint32_t(reinterpret_cast<uintptr_t>(dst) + out) & 3u;  // wave-uniform
         uint8_t *D = dst + out - m;  // 4-B aligned
         if (m == 0) {
@@ -129,11 +153,29 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
     }
     uint32_t total;
     uint32_t o = wave_exclusive_scan(__popc(keep), total) + out;
+    if constexpr (kLds) {
+      o += m0;
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-      if (keep & (1u << k)) gp(dst)[o++] = uint8_t(b[k]);
+      for (int k = 0; k < 4; k++)
+        if (keep & (1u << k)) sb[o++] = uint8_t(b[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (keep & (1u << k)) gp(dst)[o++] = uint8_t(b[k]);
+    }
     out += total;
     prev_byte = __builtin_amdgcn_readlane(b[3], 63);
+  }
+  if constexpr (kLds) {
+    // LDS -> the output: aligned dwords [k_lo, k_hi), the bytes of a partial dword at either end
+    // (the head's bytes before m0 belong to the block in front)
+    __syncthreads();
+    const uint32_t end = m0 + out, k_lo = (m0 + 3u) >> 2, k_hi = end >> 2;
+    uint32_t *const D = reinterpret_cast<uint32_t *>(dst - m0);
+    for (uint32_t k = k_lo + lane; k < k_hi; k += 64) gp(D)[k] = s_out[k];
+    const uint32_t hb = lane, tb = 4u * max(k_hi, k_lo) + (lane - 4u);
+    if (lane < 4 && hb >= m0 && hb < min(4u * k_lo, end)) gp(dst - m0)[hb] = sb[hb];
+    if (lane >= 4 && lane < 8 && tb < end) gp(dst - m0)[tb] = sb[tb];
   }
   // last block: zero the interval's slack after the data (>= 16 B, rj_stream.cpp BuildPlan):
   // K1 reads whole 16-B chunks and must see zero bits past the end, as libjpeg inserts
@@ -144,9 +186,10 @@ __global__ __launch_bounds__(64) void k_destuff(const RjImageDev *__restrict__ i
 }
 
 hipError_t LaunchDestuff(hipStream_t st, const RjImageDev *imgs, int nimg, uint32_t nblocks, uint8_t *destuffed,
-                         const uint32_t *ds_map) {
+                         const uint32_t *ds_map, bool lds) {
   if (nblocks == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_destuff, dim3(nblocks), dim3(64), 0, st, imgs, nimg, destuffed, ds_map);
+  if (lds) hipLaunchKernelGGL(k_destuff<true>, dim3(nblocks), dim3(64), 0, st, imgs, nimg, destuffed, ds_map);
+  else hipLaunchKernelGGL(k_destuff<false>, dim3(nblocks), dim3(64), 0, st, imgs, nimg, destuffed, ds_map);
   return hipGetLastError();
 }
 
