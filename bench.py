@@ -889,6 +889,9 @@ def main():
             "live_rows": {"live": t["live"], "rows_beside_k1": t["live_rows"], "rows_after_k1": t["rest_rows"],
                           "gave_up": t["live_pad"], "live_span_ms": round(t["live_ms"], 4),
                           "after_k1_span_ms": round(t["rest_ms"], 4)},
+            # rj_decoder.h: the entry buffers the handle's first large calls tried (K1 + K2 ms each), the one kept
+            "entry_placement": {"k1_k2_ms": [round(x, 4) for x in t["place_ms"][:t["place_tried"]]],
+                                "picked": t["place_pick"]},
             "end_to_end_algorithmic_GBps": round(imgs_total * per_img / elapsed / 1e9, 2),
             "host_input_images_per_s_per_gpu": round(host_rate, 1) if host_rate else None,
             "parse_images_per_s": {"host_1_thread": round(parse_host_rate, 1),

@@ -123,6 +123,12 @@ typedef struct {
      after K1 (rows no ticket took, synced split rows), HIP events on each launch's stream */
   uint32_t live, live_rows, rest_rows, live_pad;
   float live_ms, rest_ms;
+  /* entry-buffer placement search: the K1 + K2 span (ms, HIP events) of each
+     entry buffer tried on this handle's first large lean calls, how many were tried, the one kept
+     (-1: the search is still running or was never started) */
+  float place_ms[4];
+  uint32_t place_tried;
+  int32_t place_pick;
 } RocJpegAmdTimings;
 
 RocJpegStatus rocJpegAmdSetProfiling(RocJpegHandle handle, int enable);
@@ -253,7 +259,7 @@ RocJpegStatus rocJpegAmdGetCoalesceStats(uint64_t *calls, uint64_t *combined, ui
  * 3: the resident sharded entry points; the work-table broadcast carries a status header.
  * 4: RocJpegAmdTimings.chunk_k1.  5: RocJpegAmdTimings.chunk_bytes (the call's chunk length).
  * 6: rocJpegAmdGetCoalesceStats, rocJpegAmdGetLastParseTimings, RocJpegAmdTimings.chunk_hyp. */
-#define ROCJPEG_AMD_ABI_VERSION 7
+#define ROCJPEG_AMD_ABI_VERSION 8
 RocJpegStatus rocJpegAmdGetAbiVersion(int *version);
 
 #if defined(__cplusplus)

@@ -26,7 +26,7 @@ EXT_SYMBOLS = (
     "rocJpegAmdShardCreate", "rocJpegAmdShardDecode", "rocJpegAmdShardGetImages", "rocJpegAmdShardDestroy",
     "rocJpegAmdGetAbiVersion", "rocJpegAmdStreamGetLeanTables",
 )
-ABI_VERSION = 7  # include/rocjpeg_amd.h ROCJPEG_AMD_ABI_VERSION
+ABI_VERSION = 8  # include/rocjpeg_amd.h ROCJPEG_AMD_ABI_VERSION
 
 
 class Status(enum.IntEnum):  # api/rocjpeg.h:53-67
@@ -110,7 +110,8 @@ class RocJpegAmdTimings(ctypes.Structure):
                 ("chunk_k1", ctypes.c_uint32), ("chunk_bytes", ctypes.c_uint32),
                 ("chunk_hyp", ctypes.c_uint32), ("lean_five", ctypes.c_uint32),
                 ("live", ctypes.c_uint32), ("live_rows", ctypes.c_uint32), ("rest_rows", ctypes.c_uint32),
-                ("live_pad", ctypes.c_uint32), ("live_ms", ctypes.c_float), ("rest_ms", ctypes.c_float)]
+                ("live_pad", ctypes.c_uint32), ("live_ms", ctypes.c_float), ("rest_ms", ctypes.c_float),
+                ("place_ms", ctypes.c_float * 4), ("place_tried", ctypes.c_uint32), ("place_pick", ctypes.c_int32)]
 
 
 class RocJpegAmdInterval(ctypes.Structure):  # include/rocjpeg_amd.h

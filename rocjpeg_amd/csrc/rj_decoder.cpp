@@ -134,6 +134,8 @@ Decoder::~Decoder() {
       if (e) (void)hipEventDestroy(e);
     if (split_ev_) (void)hipEventDestroy(split_ev_);
     if (bev_) (void)hipEventDestroy(bev_);
+    for (auto &e : place_ev_)
+      if (e) (void)hipEventDestroy(e);
     if (bstream_) (void)hipStreamDestroy(bstream_);
     if (lstream_) (void)hipStreamDestroy(lstream_);
     (void)hipStreamDestroy(stream_);
@@ -198,6 +200,9 @@ int Decoder::Initialize() {
   RJ_HIP(hipEventCreateWithFlags(&bev_, hipEventDisableTiming));
   if (const char *sp = getenv("RJ_SYNC_SPIN")) spin_sync_ = atoi(sp) != 0;
   if (const char *kl = getenv("RJ_K0_LDS")) k0_lds_ = atoi(kl) != 0;
+  for (auto &e : place_ev_) RJ_HIP(hipEventCreate(&e));
+  if (const char *pt = getenv("RJ_PLACE_TUNE")) place_tune_ = atoi(pt) != 0;
+  if (const char *es = getenv("RJ_ENT_SHIFT_KB")) ent_shift_ = uint64_t(std::max(0, atoi(es))) << 10;
   if (const char *ub = getenv("RJ_UPLOAD_B_SIDE")) side_b_ = atoi(ub) != 0;
   if (const char *lk = getenv("RJ_K2_LIVE")) {  // 0 off; 2 (test): the live launch always gives up
     live_k2_ = atoi(lk) != 0;  // 1: on
@@ -633,6 +638,22 @@ int Decoder::DecodeSplit(Stream *const *streams, int n, const RocJpegDecodeParam
 
 // The end of a call: the calling thread polls the stream (yielding between polls) instead of
 // sleeping in hipStreamSynchronize when spin_sync_ is set (env RJ_SYNC_SPIN=1).
+void Decoder::PlaceStep(float ms) {
+  const int k = place_state_ - 1;  // the candidate this call ran with (in d_entries_)
+  place_ms_[k] = ms;
+  if (place_best_ < 0 || ms < place_ms_[place_best_] * 0.985f) place_best_ = k;  // (1.5 %: above the noise)
+  const size_t cap = d_entries_.capacity();
+  place_bufs_[k].Swap(d_entries_);  // stays allocated, so that the next candidate is other memory
+  if (k + 1 < kPlaceCands && d_entries_.Ensure(cap) == kOk) {
+    place_state_ = k + 2;
+    return;
+  }
+  d_entries_.Release();  // done (or out of memory for another candidate): keep the fastest
+  d_entries_.Swap(place_bufs_[place_best_]);
+  for (DeviceBuffer &b : place_bufs_) b.Release();
+  place_state_ = -1;
+}
+
 hipError_t Decoder::WaitCall() {
   if (spin_sync_) {
     hipError_t e;
@@ -1454,7 +1475,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   RJ_CHECK(d_rec_.Ensure(std::max<uint64_t>(uint64_t(lanes_all) * RJ_MAX_RECORDS * sizeof(RjRecord), 256)));
   RJ_CHECK(d_chunkres_.Ensure(std::max<uint64_t>(uint64_t(lanes_all) * sizeof(RjChunkRes), 256)));
   RJ_CHECK(d_fallback_.Ensure(std::max<uint64_t>(uint64_t(seg_total) * 4, 256)));
-  RJ_CHECK(d_entries_.Ensure((ent_total + RJ_ENT_SLACK) * 4));
+  RJ_CHECK(d_entries_.Ensure((ent_total + RJ_ENT_SLACK) * 4 + ent_shift_));
   if (prog_images) {
     RJ_CHECK(d_coef_.Ensure(coef_dw_total * 4));
     RJ_CHECK(d_nz_.Ensure(nz_total * 8));
@@ -1462,7 +1483,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_CHECK(d_pprog_.Ensure(std::max<uint64_t>(uint64_t(pival_total + 1) * 4, 256)));  // + error flag
   }
   RjCoefBuf cbuf;
-  cbuf.ent = d_entries_.as<uint32_t>();
+  cbuf.ent = d_entries_.as<uint32_t>() + ent_shift_ / 4;
   cbuf.piece = d_piece_.as<RjPiece>();
   cbuf.rec = d_rec_.as<RjRecord>();
   cbuf.res = d_chunkres_.as<RjChunkRes>();
@@ -1968,9 +1989,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       std::memcpy(l2.data() + uint64_t(wsplit) * 64, lane_seg.data() + nsplit, uint64_t(seg_total - nsplit) * 4);
       hsplit.ent = AlignUp(ent_total, RJ_ENT_GROUP);
       hsplit.cap = cap;
-      RJ_CHECK(d_entries_.Ensure((hsplit.ent + uint64_t(wsplit) * 32 * cap + RJ_ENT_SLACK) * 4));
+      RJ_CHECK(d_entries_.Ensure((hsplit.ent + uint64_t(wsplit) * 32 * cap + RJ_ENT_SLACK) * 4 + ent_shift_));
       RJ_CHECK(d_piece_.Ensure(2ull * seg_total * sizeof(RjPiece)));
-      cbuf.ent = d_entries_.as<uint32_t>();
+      cbuf.ent = d_entries_.as<uint32_t>() + ent_shift_ / 4;
       cbuf.piece = d_piece_.as<RjPiece>();
       cbuf.piece_shift = 1;  // interval s: pieces 2s (head) and 2s + 1 (tail)
     }
@@ -2061,9 +2082,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         }
         hsplit.ent = AlignUp(ent_total, RJ_ENT_GROUP);
         hsplit.cap = cap;
-        RJ_CHECK(d_entries_.Ensure((hsplit.ent + uint64_t(top) * 32 * cap + RJ_ENT_SLACK) * 4));
+        RJ_CHECK(d_entries_.Ensure((hsplit.ent + uint64_t(top) * 32 * cap + RJ_ENT_SLACK) * 4 + ent_shift_));
         RJ_CHECK(d_piece_.Ensure(2ull * seg_total * sizeof(RjPiece)));
-        cbuf.ent = d_entries_.as<uint32_t>();
+        cbuf.ent = d_entries_.as<uint32_t>() + ent_shift_ / 4;
         cbuf.piece = d_piece_.as<RjPiece>();
         cbuf.piece_shift = 1;  // interval s: pieces 2s (head) and 2s + 1 (tail)
         timings_.lean_split = ns;
@@ -2109,6 +2130,9 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
 
   const auto t_end = std::chrono::steady_clock::now();
   timings_.host_ms = std::chrono::duration<float, std::milli>(t_end - t_host0).count();
+  if (Dbg(kDebugHost))
+    fprintf(stderr, "[rj place] entries %p output %p\n", static_cast<void *>(cbuf.ent),
+            n ? static_cast<void *>(dst[0].channel[0]) : nullptr);
   if (Dbg(kDebugHost)) {  // development: where the host planning time goes
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
       return std::chrono::duration<double, std::milli>(b - a).count();
@@ -2120,6 +2144,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
             ms(t_k0, t_sorted), ms(t_sorted, t_five), ms(t_five, t_end));
   }
   bool live = false;
+  bool place_warm = false, place_timed = false;
   RjLive lv{};
   *reinterpret_cast<volatile uint32_t *>(h_wide_flag_ + 1) = 0;  // a lost live row (never expected)
   if (ngroups > 1) {
@@ -2184,6 +2209,10 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         RJ_HIP(hipEventRecord(live_ev_[0], stream_));  // descriptors and lane lists uploaded, K0 done
         RJ_HIP(hipStreamWaitEvent(lstream_, live_ev_[0], 0));
       }
+      // entry-buffer placement search (rj_decoder.h): a large call times K1 + K2 while it runs
+      place_warm = place_tune_ && place_state_ == 0 && !live && fused_rows >= kPlaceMinRows;
+      place_timed = place_tune_ && place_state_ >= 1 && !live && fused_rows >= kPlaceMinRows;
+      if (place_timed) RJ_HIP(hipEventRecord(place_ev_[0], stream_));
       RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, k1_lanes, k1_src, d_tabs, d_lean, cbuf, k1_solo_lds_,
                              (nsplit || nsplit5) ? &hsplit : nullptr, nl_five != 0, live ? &lv : nullptr));
       if (live) {
@@ -2220,6 +2249,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr, wcnt, wlist,
                         split_rows, nsplit_rows));
 #endif
+      if (place_timed) RJ_HIP(hipEventRecord(place_ev_[1], stream_));
     }
     wide(general_rows, wcnt, wlist, true, false);
     RJ_HIP(LaunchRows(stream_, true, d_imgs, n, d_grows, nullptr, general_rows, cbuf, d_tabs,
@@ -2263,6 +2293,16 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
                               hipMemcpyDefault, stream_));
     RJ_HIP(hipStreamSynchronize(stream_));
   }
+  // (after every launch that reads this call's entries: the search may free an entry buffer)
+  if (place_warm) place_state_ = 1;
+  if (place_timed) {
+    float ms = 0.f;
+    RJ_HIP(hipEventElapsedTime(&ms, place_ev_[0], place_ev_[1]));
+    PlaceStep(ms);
+  }
+  for (int k = 0; k < 4; k++) timings_.place_ms[k] = k < kPlaceCands ? place_ms_[k] : 0.f;
+  timings_.place_tried = place_state_ < 0 ? uint32_t(kPlaceCands) : uint32_t(std::max(0, place_state_ - 1));
+  timings_.place_pick = place_state_ < 0 ? place_best_ : -1;
   if (prog_images && prog_pipe) {  // a refinement wave that gave up waiting (never expected)
     uint32_t err = 0;
     RJ_HIP(hipMemcpy(&err, d_pprog_.as<uint32_t>() + pival_total, 4, hipMemcpyDeviceToHost));

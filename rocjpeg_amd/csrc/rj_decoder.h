@@ -13,6 +13,7 @@
 #include <memory>
 #include <mutex>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "../../include/rocjpeg.h"
@@ -30,6 +31,10 @@ class DeviceBuffer {
   void Release();
   template <typename T> T *as() const { return static_cast<T *>(ptr_); }
   size_t capacity() const { return cap_; }
+  void Swap(DeviceBuffer &o) {
+    std::swap(ptr_, o.ptr_);
+    std::swap(cap_, o.cap_);
+  }
 
  private:
   void *ptr_ = nullptr;
@@ -191,6 +196,22 @@ class Decoder {
   // event instead of behind K0 in the call's stream (env RJ_UPLOAD_B_SIDE=0: in stream order)
   bool side_b_ = true;
   bool k0_lds_ = true;      // env RJ_K0_LDS=0: K0 stores a compacted chunk's bytes one by one (A/B)
+  uint64_t ent_shift_ = 0;  // env RJ_ENT_SHIFT_KB (placement probe): the entry streams start this far into their buffer
+  // Entry-buffer placement search: K2's time depends on where its entry buffer lies in HBM
+  // relative to the output (one process, fixed buffers: 2.32-2.34 or 2.44-2.47 ms per C2 call,
+  // stable for a given pair, not predictable from virtual addresses -- DESIGN.md 4 K2).  The
+  // first large lean calls of a handle time K1 + K2 (two events) with the entry buffer they
+  // have, then with up to kPlaceCands - 1 freshly allocated ones (the earlier ones stay
+  // allocated meanwhile, so each is new memory), and keep the fastest.  env RJ_PLACE_TUNE=0: off.
+  static constexpr int kPlaceCands = 3;
+  static constexpr uint32_t kPlaceMinRows = 16384;  // MCU rows of a call worth timing (C2: 69,632)
+  bool place_tune_ = true;
+  int place_state_ = 0;  // 0: next large call warms up; 1..kPlaceCands: measuring candidate state-1; -1 done
+  int place_best_ = -1;
+  float place_ms_[4] = {};
+  DeviceBuffer place_bufs_[kPlaceCands];
+  hipEvent_t place_ev_[2] = {};
+  void PlaceStep(float ms);
   bool spin_sync_ = false;  // env RJ_SYNC_SPIN=1: WaitCall polls the stream instead of sleeping
   hipError_t WaitCall();
   hipStream_t bstream_ = nullptr;

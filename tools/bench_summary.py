@@ -11,6 +11,6 @@ for line in open(sys.argv[1]):
           f"frac {r['frac']}  kernels {r['per_kernel_launch_ms_sum']}")
     print("  host_input", d.get("host_input_images_per_s_per_gpu"), " stages", d.get("stages_ms_per_step"))
     if "live_rows" in d:
-        print("  live", d["live_rows"], " parity", d.get("parity_timed_output"))
+        print("  live", d["live_rows"], " placement", d.get("entry_placement"), " parity", d.get("parity_timed_output"))
     for k, v in d.get("extra_workloads", {}).items():
         print(f"  {k}: {v['value']:.0f} img/s  {v['ms_per_step']} ms  {v.get('per_kernel_launch_ms_sum')}  parity {v.get('parity_sample')}")
