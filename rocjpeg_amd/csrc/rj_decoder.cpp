@@ -202,6 +202,8 @@ int Decoder::Initialize() {
   if (const char *kl = getenv("RJ_K0_LDS")) k0_lds_ = atoi(kl) != 0;
   for (auto &e : place_ev_) RJ_HIP(hipEventCreate(&e));
   if (const char *pt = getenv("RJ_PLACE_TUNE")) place_tune_ = atoi(pt) != 0;
+  if (const char *pk = getenv("RJ_PLACE_KEEP")) place_keep_ = atoi(pk) != 0;
+  if (const char *pc = getenv("RJ_PLACE_CANDS")) place_cands_ = std::max(1, std::min(kPlaceCands, atoi(pc)));
   if (const char *es = getenv("RJ_ENT_SHIFT_KB")) ent_shift_ = uint64_t(std::max(0, atoi(es))) << 10;
   if (const char *ub = getenv("RJ_UPLOAD_B_SIDE")) side_b_ = atoi(ub) != 0;
   if (const char *lk = getenv("RJ_K2_LIVE")) {  // 0 off; 2 (test): the live launch always gives up
@@ -644,13 +646,14 @@ void Decoder::PlaceStep(float ms) {
   if (place_best_ < 0 || ms < place_ms_[place_best_] * 0.985f) place_best_ = k;  // (1.5 %: above the noise)
   const size_t cap = d_entries_.capacity();
   place_bufs_[k].Swap(d_entries_);  // stays allocated, so that the next candidate is other memory
-  if (k + 1 < kPlaceCands && d_entries_.Ensure(cap) == kOk) {
+  if (k + 1 < place_cands_ && d_entries_.Ensure(cap) == kOk) {
     place_state_ = k + 2;
     return;
   }
   d_entries_.Release();  // done (or out of memory for another candidate): keep the fastest
   d_entries_.Swap(place_bufs_[place_best_]);
-  for (DeviceBuffer &b : place_bufs_) b.Release();
+  if (!place_keep_)
+    for (DeviceBuffer &b : place_bufs_) b.Release();
   place_state_ = -1;
 }
 
@@ -2209,9 +2212,13 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         RJ_HIP(hipEventRecord(live_ev_[0], stream_));  // descriptors and lane lists uploaded, K0 done
         RJ_HIP(hipStreamWaitEvent(lstream_, live_ev_[0], 0));
       }
-      // entry-buffer placement search (rj_decoder.h): a large call times K1 + K2 while it runs
-      place_warm = place_tune_ && place_state_ == 0 && !live && fused_rows >= kPlaceMinRows;
-      place_timed = place_tune_ && place_state_ >= 1 && !live && fused_rows >= kPlaceMinRows;
+      // entry-buffer placement search (rj_decoder.h): a large call times K1 + K2 while it runs.
+      // Resident bitstreams only: a staged call's time is its upload's, and its allocations and
+      // frees (which wait for the device) would stall DecodeSplit's other half
+      const bool place_call = place_tune_ && !live && fused_rows >= kPlaceMinRows && stage_bytes == 0 &&
+                              ecs_stage_bytes == 0;
+      place_warm = place_call && place_state_ == 0;
+      place_timed = place_call && place_state_ >= 1;
       if (place_timed) RJ_HIP(hipEventRecord(place_ev_[0], stream_));
       RJ_HIP(LaunchHuffLanes(stream_, d_imgs, n, 0u, k1_lanes, k1_src, d_tabs, d_lean, cbuf, k1_solo_lds_,
                              (nsplit || nsplit5) ? &hsplit : nullptr, nl_five != 0, live ? &lv : nullptr));
@@ -2294,14 +2301,14 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(hipStreamSynchronize(stream_));
   }
   // (after every launch that reads this call's entries: the search may free an entry buffer)
-  if (place_warm) place_state_ = 1;
+  if (place_warm && ++place_warm_ >= 2) place_state_ = 1;
   if (place_timed) {
     float ms = 0.f;
     RJ_HIP(hipEventElapsedTime(&ms, place_ev_[0], place_ev_[1]));
     PlaceStep(ms);
   }
   for (int k = 0; k < 4; k++) timings_.place_ms[k] = k < kPlaceCands ? place_ms_[k] : 0.f;
-  timings_.place_tried = place_state_ < 0 ? uint32_t(kPlaceCands) : uint32_t(std::max(0, place_state_ - 1));
+  timings_.place_tried = place_state_ < 0 ? uint32_t(place_cands_) : uint32_t(std::max(0, place_state_ - 1));
   timings_.place_pick = place_state_ < 0 ? place_best_ : -1;
   if (prog_images && prog_pipe) {  // a refinement wave that gave up waiting (never expected)
     uint32_t err = 0;

@@ -206,7 +206,13 @@ class Decoder {
   static constexpr int kPlaceCands = 3;
   static constexpr uint32_t kPlaceMinRows = 16384;  // MCU rows of a call worth timing (C2: 69,632)
   bool place_tune_ = true;
-  int place_state_ = 0;  // 0: next large call warms up; 1..kPlaceCands: measuring candidate state-1; -1 done
+  int place_cands_ = kPlaceCands;  // env RJ_PLACE_CANDS (1..kPlaceCands): candidates tried
+  // the other candidates stay allocated until the handle is destroyed: freeing ~5 GB of VRAM made
+  // the host-input path's uploads run at half speed for a while afterwards (126k -> 98k images/s;
+  // profiles/r6_experiments/k2_placement_probe.txt); env RJ_PLACE_KEEP=0 frees them
+  bool place_keep_ = true;
+  int place_state_ = 0;  // 0: warming up; 1..kPlaceCands: measuring candidate state-1; -1 done
+  int place_warm_ = 0;   // large calls before the first measurement (2: the second call still ran slower)
   int place_best_ = -1;
   float place_ms_[4] = {};
   DeviceBuffer place_bufs_[kPlaceCands];

@@ -24,6 +24,8 @@ def main():
             print(f"{n:4d}  {idle:17.1f}  {(k1[0] - e) / 1e3:9.1f}  {(k2[0] - k1[1]) / 1e3:9.1f}  "
                   f"{(k2[1] - s) / 1e3:7.1f}  {' '.join(other)}")
             prev_end, i, n = k2[1], i + 3, n + 1
+            while i < len(ev) and "k_rows" in ev[i][2]:  # the call's other K2 launches (split-aware, fix-up)
+                prev_end, i = ev[i][1], i + 1
             continue
         i += 1
 
