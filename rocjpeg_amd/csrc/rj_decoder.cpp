@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <thread>
 
 #include "rj_common.h"
@@ -163,8 +164,6 @@ int Decoder::Initialize() {
     return -7;  // ROCJPEG_STATUS_ARCH_MISMATCH
   }
   RJ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  // (created next to stream_: streams take the process's hardware queues round-robin)
-  RJ_HIP(hipStreamCreateWithFlags(&bstream_, hipStreamNonBlocking));
   for (auto &e : ev_) RJ_HIP(hipEventCreate(&e));
   if (const char *g = getenv("RJ_PIPE_GROUPS")) {
     pipe_groups_ = std::max(1, std::min(kMaxPipe, atoi(g)));
@@ -188,12 +187,9 @@ int Decoder::Initialize() {
   RJ_HIP(hipHostMalloc(reinterpret_cast<void **>(&h_wide_flag_), 64, hipHostMallocMapped | hipHostMallocCoherent));
   RJ_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_wide_flag_), h_wide_flag_, 0));
   *reinterpret_cast<volatile uint32_t *>(h_wide_flag_) = 0;
-  for (auto &q : pstream_) RJ_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
-  {
-    int lo = 0, hi = 0;  // "least" is the numerically greatest
-    RJ_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    RJ_HIP(hipStreamCreateWithPriority(&lstream_, hipStreamNonBlocking, lo));
-  }
+  // (the side streams -- pstream_, lstream_, bstream_ -- are created on first use: streams take
+  // the process's hardware queues round-robin at creation, and DecodeSplit's part handles each
+  // need a queue of their own for their stream_; unused side streams would push them onto shared ones)
   for (auto &e : live_ev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : live_t_) RJ_HIP(hipEventCreate(&e));
   RJ_HIP(hipEventCreateWithFlags(&split_ev_, hipEventDisableTiming));
@@ -212,6 +208,7 @@ int Decoder::Initialize() {
   }
   if (const char *ll = getenv("RJ_K2_LIVE_LDS")) live_lds_ = uint32_t(std::max(0, atoi(ll)));
   if (const char *sh = getenv("RJ_SPLIT_HOST")) split_host_ = atoi(sh) != 0;
+  if (const char *sp = getenv("RJ_SPLIT_PARTS")) split_parts_ = std::max(2, std::min(4, atoi(sp)));
   for (auto &e : pev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : pk1_) RJ_HIP(hipEventCreate(&e));
   for (auto &e : kev_) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -577,69 +574,90 @@ int Decoder::DecodeSplit(Stream *const *streams, int n, const RocJpegDecodeParam
   if (cst != kOk) return cst;
   {
     std::lock_guard<std::mutex> lock(mu_);
-    if (!helper_) {
+    while (int(helpers_.size()) < split_parts_ - 1) {
       std::unique_ptr<Decoder> h(new Decoder(backend_, device_));
-      if (h->Initialize() != kOk) {
-        split_host_ = false;  // (no second handle on this device: every call decodes whole)
-      } else {
-        h->split_host_ = false;
-        helper_ = std::move(h);
-      }
+      if (h->Initialize() != kOk) break;  // (fewer parts: as many handles as this device gives)
+      h->split_host_ = false;
+      helpers_.push_back(std::move(h));
     }
   }
-  if (!helper_) return DecodeOne(streams, n, params, dst);
-  // the halves' uploads in order on the copy engine: the second starts when the first is done, so
-  // the first half's kernels run while the second half's bytes cross PCIe (both uploads at once
-  // would share the engine and leave the GPU idle until both land)
-  const int half = n / 2;
-  int st2 = kOk;
-  Decoder *helper = helper_.get();
+  const int P = std::min(split_parts_, int(helpers_.size()) + 1);
+  if (P < 2) {
+    split_host_ = false;  // no second handle on this device: every call decodes whole
+    return DecodeOne(streams, n, params, dst);
+  }
+  // Part k decodes on its own handle and thread; the parts' uploads run in order on the copy
+  // engine (part k's waits for part k - 1's, an event), so each part's kernels run while the
+  // later parts' bytes cross PCIe.  The shares shrink: what is left exposed after the last
+  // upload is the last part's decode (profiles/r6_experiments/host_input_parts_ab.txt).
+  static const double kShare[5][4] = {{1, 0, 0, 0}, {1, 0, 0, 0}, {0.5, 0.5, 0, 0}, {0.4, 0.35, 0.25, 0},
+                                      {0.3, 0.28, 0.24, 0.18}};
+  int cut[5] = {0, 0, 0, 0, 0};
+  double acc = 0;
+  for (int k = 0; k < P; k++) {
+    acc += kShare[P][k];
+    cut[k + 1] = k + 1 == P ? n : std::max(cut[k] + 1, std::min(n - (P - 1 - k), int(acc * n + 0.5)));
+  }
+  Decoder *owner[4] = {this, nullptr, nullptr, nullptr};
+  for (int k = 1; k < P; k++) owner[k] = helpers_[size_t(k - 1)].get();
   std::mutex m;
   std::condition_variable cv;
-  bool signalled = false;
-  auto signal = [&] {
+  bool go[5] = {true, false, false, false, false};
+  auto signal = [&](int k) {  // part k may start: part k - 1's uploads are enqueued (or it failed)
     std::lock_guard<std::mutex> l(m);
-    if (!signalled) {
-      signalled = true;
+    if (!go[k]) {
+      go[k] = true;
       cv.notify_all();
     }
   };
-  std::thread t([&] {
+  for (int k = 0; k + 1 < P; k++) {
+    Decoder *next = owner[k + 1];
+    Decoder *self = owner[k];
+    next->upload_after_ = self->split_ev_;
+    self->uploaded_ = [&, k, self, next] {
+      if (hipEventRecord(self->split_ev_, self->stream_) != hipSuccess) next->upload_after_ = nullptr;
+      signal(k + 1);
+    };
+  }
+  int st[4] = {kOk, kOk, kOk, kOk};
+  std::exception_ptr err;
+  auto run = [&](int k) {
     {
       std::unique_lock<std::mutex> l(m);
-      cv.wait(l, [&] { return signalled; });
+      cv.wait(l, [&] { return go[k]; });
     }
     try {
-      st2 = helper->DecodeOne(streams + half, n - half, params, dst + half);
+      st[k] = owner[k]->DecodeOne(streams + cut[k], cut[k + 1] - cut[k], params, dst + cut[k]);
     } catch (...) {
-      st2 = kRuntimeError;
+      st[k] = kRuntimeError;
+      if (k == 0) err = std::current_exception();
     }
-    helper->upload_after_ = nullptr;
-  });
-  int st1;
-  helper->upload_after_ = split_ev_;
-  uploaded_ = [&] {
-    if (hipEventRecord(split_ev_, stream_) != hipSuccess) helper->upload_after_ = nullptr;
-    signal();
+    if (k + 1 < P) {  // a part that never uploaded leaves nothing to wait for
+      bool up;
+      {
+        std::lock_guard<std::mutex> l(m);
+        up = go[k + 1];
+      }
+      if (!up) owner[k + 1]->upload_after_ = nullptr;
+      signal(k + 1);
+    }
   };
-  try {
-    st1 = DecodeOne(streams, half, params, dst);
-  } catch (...) {
-    uploaded_ = nullptr;
-    helper->upload_after_ = nullptr;
-    signal();
-    t.join();
-    throw;
+  for (int k = 0; k < P; k++) owner[k]->split_part_ = true;
+  std::vector<std::thread> threads;
+  for (int k = 1; k < P; k++) threads.emplace_back(run, k);
+  run(0);
+  for (std::thread &t : threads) t.join();
+  for (int k = 0; k < P; k++) {
+    owner[k]->uploaded_ = nullptr;
+    owner[k]->upload_after_ = nullptr;
+    owner[k]->split_part_ = false;
   }
-  uploaded_ = nullptr;
-  if (!signalled) helper->upload_after_ = nullptr;  // (the first half never uploaded: nothing to wait for)
-  signal();
-  t.join();
-  return st1 != kOk ? st1 : st2;
+  if (err) std::rethrow_exception(err);
+  for (int k = 0; k < P; k++)
+    if (st[k] != kOk) return st[k];
+  return kOk;
 }
 
-// The end of a call: the calling thread polls the stream (yielding between polls) instead of
-// sleeping in hipStreamSynchronize when spin_sync_ is set (env RJ_SYNC_SPIN=1).
 void Decoder::PlaceStep(float ms) {
   const int k = place_state_ - 1;  // the candidate this call ran with (in d_entries_)
   place_ms_[k] = ms;
@@ -655,6 +673,16 @@ void Decoder::PlaceStep(float ms) {
   if (!place_keep_)
     for (DeviceBuffer &b : place_bufs_) b.Release();
   place_state_ = -1;
+}
+
+// The end of a call: the calling thread polls the stream (yielding between polls) instead of
+// sleeping in hipStreamSynchronize when spin_sync_ is set (env RJ_SYNC_SPIN=1).
+hipError_t Decoder::SideStream(hipStream_t &s, bool lowest_priority) {
+  if (s != nullptr) return hipSuccess;
+  if (!lowest_priority) return hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  int lo = 0, hi = 0;  // "least" is the numerically greatest
+  const hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  return e != hipSuccess ? e : hipStreamCreateWithPriority(&s, hipStreamNonBlocking, lo);
 }
 
 hipError_t Decoder::WaitCall() {
@@ -689,7 +717,7 @@ int Decoder::DecodeOne(Stream *const *streams, int n, const RocJpegDecodeParams 
   // re-parse or destroy cannot recycle memory a DMA is still reading
   if (r != kOk) {
     (void)hipStreamSynchronize(stream_);
-    (void)hipStreamSynchronize(bstream_);
+    if (bstream_) (void)hipStreamSynchronize(bstream_);
   }
   return r;
 }
@@ -1246,7 +1274,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   // K1 with its outlier split)
   const uint64_t round_lanes = uint64_t(cu_count_) * RJ_K1_WG;
   uint64_t cb_fill = std::max<uint64_t>(chunk_min_, (src_total + round_lanes - 1) / round_lanes);
-  if (2ull * seg_total >= round_lanes) {
+  if (2ull * seg_total >= round_lanes || split_part_) {
+    // (a DecodeSplit part keeps its intervals whole too: the other parts' kernels share the chip)
     cb_fill = std::max<uint64_t>(cb_fill, RJ_SPLIT_BYTES / 2);
   } else {
     // the lanes pack into workgroups with padding (an interval's chunks never straddle one):
@@ -1574,7 +1603,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     }
   }
   if (profiling_) RJ_HIP(hipEventRecord(ev_[0], stream_));
-  if (upload_after_ != nullptr) RJ_HIP(hipStreamWaitEvent(stream_, upload_after_, 0));  // DecodeSplit's second half
+  if (upload_after_ != nullptr) RJ_HIP(hipStreamWaitEvent(stream_, upload_after_, 0));  // DecodeSplit: after the previous part's uploads
   for (const PinRun &r : pin_runs)  // parse-time pinned bitstreams: straight to the device
     RJ_HIP(hipMemcpyAsync(decs + r.dev, r.host, r.len, hipMemcpyHostToDevice, stream_));
   if (stage_bytes || ecs_copy_bytes) {
@@ -1689,7 +1718,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
 
   const auto t_k0 = std::chrono::steady_clock::now();
   RJ_HIP(hipMemcpyAsync(dbase, h, blob_a, hipMemcpyHostToDevice, stream_));
-  if (uploaded_) uploaded_();  // DecodeSplit's first half: its uploads are enqueued
+  if (uploaded_) uploaded_();  // DecodeSplit: this part's uploads are enqueued
   if (cbuf.count) RJ_HIP(hipMemsetAsync(cbuf.count, 0, sizeof(unsigned long long), stream_));
   if (profiling_) RJ_HIP(hipEventRecord(ev_[1], stream_));
   RJ_HIP(LaunchDestuff(stream_, d_imgs, n, ds_total, d_destuff_.as<uint8_t>(),
@@ -1748,6 +1777,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       const bool side = prog_level_off[nlev] > prog_level_off[0];
       if (side) {
         RJ_HIP(hipEventRecord(prog_join_[0], stream_));
+        RJ_HIP(SideStream(pstream_[0]));
         RJ_HIP(hipStreamWaitEvent(pstream_[0], prog_join_[0], 0));
         for (uint32_t L = 0; L < nlev; L++) {
           RJ_HIP(pk_begin(pstream_[0]));
@@ -2123,6 +2153,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       // event (behind K0 in the call's stream the copy ran only once K0 was done: ~25 us before K1).
       // Only calls with nothing staged: beside staged bitstreams (DecodeSplit's two halves) the
       // small copy queued behind the other half's upload (host input 126k -> 98-108k images/s)
+      RJ_HIP(SideStream(bstream_));
       RJ_HIP(hipMemcpyAsync(dbase + blob_a, h + blob_a, blob_b - blob_a, hipMemcpyHostToDevice, bstream_));
       RJ_HIP(hipEventRecord(bev_, bstream_));
       RJ_HIP(hipStreamWaitEvent(stream_, bev_, 0));
@@ -2153,6 +2184,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   if (ngroups > 1) {
     RJ_HIP(hipEventRecord(pev_[kMaxPipe - 1], stream_));  // K0 and upload B done
     for (int g = 0; g < ngroups; g++) {
+      if (g < ngroups - 1) RJ_HIP(SideStream(pstream_[g]));
       hipStream_t st = g == ngroups - 1 ? stream_ : pstream_[g];
       if (st != stream_) RJ_HIP(hipStreamWaitEvent(st, pev_[kMaxPipe - 1], 0));
       if (profiling_) RJ_HIP(hipEventRecord(k1s_[g], st));
@@ -2210,6 +2242,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         lv.k1_waves = k1_groups * (k1_dec / 64u);
         lv.rows = fused_rows;
         RJ_HIP(hipEventRecord(live_ev_[0], stream_));  // descriptors and lane lists uploaded, K0 done
+        RJ_HIP(SideStream(lstream_, true));
         RJ_HIP(hipStreamWaitEvent(lstream_, live_ev_[0], 0));
       }
       // entry-buffer placement search (rj_decoder.h): a large call times K1 + K2 while it runs.

@@ -91,18 +91,20 @@ class Decoder {
   int DecodeLocked(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
   int DecodeOne(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
   // A large call whose bitstreams are in host memory (every call stages them over PCIe): its
-  // second half is decoded by a helper handle (same device, its own stream and buffers) on a
-  // second host thread, so one half's upload overlaps the other's kernels -- what two caller
-  // threads with a handle each get (tools/host_input_threads.py: 105k -> 135k images/s).
+  // images are cut into parts, each decoded by its own handle (helpers: same device, their own
+  // streams and buffers) on its own host thread, so one part's upload overlaps the earlier
+  // parts' kernels -- what caller threads with a handle each get (tools/host_input_threads.py).
   // env RJ_SPLIT_HOST=0 turns it off; never while profiling (the timings are per handle).
   int DecodeSplit(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
   std::atomic<bool> split_host_{true};
   std::vector<Stream *> lock_order_;  // DecodeOne's stream lock order (under mu_)
-  std::unique_ptr<Decoder> helper_;
+  std::vector<std::unique_ptr<Decoder>> helpers_;  // parts 1 .. split_parts_ - 1
+  int split_parts_ = 3;                             // env RJ_SPLIT_PARTS (2..4)
+  bool split_part_ = false;                         // this handle decodes a DecodeSplit part
   static constexpr int kSplitHostMin = 1024;  // staged (non-resident) images a call needs to split
-  hipEvent_t split_ev_ = nullptr;                // the first half's uploads are done (recorded on stream_)
-  hipEvent_t upload_after_ = nullptr;            // helper: wait for this before uploading
-  std::function<void()> uploaded_;               // first half: called once its uploads are enqueued
+  hipEvent_t split_ev_ = nullptr;                // DecodeSplit: this part's uploads are done (recorded on stream_)
+  hipEvent_t upload_after_ = nullptr;            // DecodeSplit part > 0: wait for this before uploading
+  std::function<void()> uploaded_;               // DecodeSplit part < last: called once its uploads are enqueued
   int ParseOnDeviceImpl(Stream *const *streams, const uint8_t *const *data, const size_t *len, int n);
   // Device of the allocation holding p (hipPointerGetAttributes, cached per call by address
   // range); -1: host memory (pinned or pageable).
@@ -220,6 +222,7 @@ class Decoder {
   void PlaceStep(float ms);
   bool spin_sync_ = false;  // env RJ_SYNC_SPIN=1: WaitCall polls the stream instead of sleeping
   hipError_t WaitCall();
+  hipError_t SideStream(hipStream_t &s, bool lowest_priority = false);  // created on first use
   hipStream_t bstream_ = nullptr;
   hipEvent_t bev_ = nullptr;
 

@@ -246,12 +246,16 @@ def test_c2_1024_live_rows_damaged(live_dec):
     assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
 
 
-def test_c2_1024_host_streams_two_handles(dec):
+@pytest.mark.parametrize("parts", ["2", "3", "4"])
+def test_c2_1024_host_streams_split_handles(parts, monkeypatch):
     """The drop-in input path: 1024 C2 streams in host memory (each call stages them over PCIe), on
-    a handle with profiling off -- the call decodes its second half on a helper handle on a second
-    host thread (rj_decoder.h DecodeSplit), so one half's upload overlaps the other's kernels.
-    Every image equal to the oracle; a bad stream in the second half fails the call with its status."""
+    a handle with profiling off -- the call is cut into `parts` parts (RJ_SPLIT_PARTS), each decoded
+    on its own handle and host thread (rj_decoder.h DecodeSplit), the uploads in order, so a part's
+    upload overlaps the earlier parts' kernels.  Every image equal to the oracle; a bad stream in a
+    later part fails the call with its status."""
     t = torch()
+    monkeypatch.setenv("RJ_SPLIT_PARTS", parts)
+    dec = R.JpegDecoder(R.Backend.HARDWARE, 0)
     distinct, copies = 64, 16
     datas = _c2_images(distinct, seed0=6060)
     with ThreadPoolExecutor(16) as ex:
@@ -268,6 +272,9 @@ def test_c2_1024_host_streams_two_handles(dec):
     s411 = R.JpegStream(O.fixture_bytes(by["c411_q90_128x64"]))
     st = dec.decode_batched(streams[:900] + [s411] + streams[901:], R.decode_params(R.OutputFormat.RGB), imgs)
     assert st == R.Status.JPEG_NOT_SUPPORTED, R.error_name(st)
+    st = dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs)  # and the handle goes on
+    assert st == 0, R.error_name(st)
+    dec.close()
 
 
 def test_c2_1024_default_pipelined_layout(dec):
