@@ -556,16 +556,11 @@ int Decoder::Decode(Stream *const *streams, int n, const RocJpegDecodeParams *pa
   if (streams == nullptr || params == nullptr || dst == nullptr || n < 0) return kInvalidParameter;
   for (int i = 0; i < n; i++)
     if (streams[i] == nullptr) return kInvalidParameter;
-  if (split_host_ && n >= kSplitHostMin && !profiling_ && path_policy_ == 0) {
-    int staged = 0;
-    for (int i = 0; i < n; i++) {
-      std::lock_guard<std::mutex> sl(streams[i]->mutex());
-      const Stream *s = streams[i];
-      staged += (s->resident.device == device_ && s->resident.generation == s->generation()) ? 0 : 1;
-    }
-    if (staged >= kSplitHostMin) return DecodeSplit(streams, n, params, dst);
-  }
-  return DecodeOne(streams, n, params, dst);
+  // (DecodeOne counts the staged streams under the stream locks it takes anyway, and hands a
+  // large staged call back for DecodeSplit before any work)
+  const bool may_split = split_host_ && n >= kSplitHostMin && !profiling_ && path_policy_ == 0;
+  const int r = DecodeOne(streams, n, params, dst, may_split);
+  return r == kWantSplit ? DecodeSplit(streams, n, params, dst) : r;
 }
 
 int Decoder::DecodeSplit(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
@@ -694,7 +689,8 @@ hipError_t Decoder::WaitCall() {
   return hipStreamSynchronize(stream_);
 }
 
-int Decoder::DecodeOne(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst) {
+int Decoder::DecodeOne(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst,
+                       bool may_split) {
   std::lock_guard<std::mutex> lock(mu_);
   // Hold every stream's lock for the call: a concurrent re-parse must not move its bytes.  Locks
   // are taken in address order (no deadlock between calls sharing streams); a batch already in
@@ -711,6 +707,14 @@ int Decoder::DecodeOne(Stream *const *streams, int n, const RocJpegDecodeParams 
   }
   locks.reserve(uniq.size());
   for (Stream *s : uniq) locks.emplace_back(s->mutex());
+  if (may_split) {
+    int staged = 0;
+    for (int i = 0; i < n; i++) {
+      const Stream *s = streams[i];
+      staged += (s->resident.device == device_ && s->resident.generation == s->generation()) ? 0 : 1;
+    }
+    if (staged >= kSplitHostMin) return kWantSplit;  // (nothing done yet; the locks are released)
+  }
   const int r = DecodeLocked(streams, n, params, dst);
   // an error return may leave copies in flight on the stream (from the parse-time pinned arena
   // or the staging buffers): they finish before the streams' locks are released, so a

@@ -89,7 +89,9 @@ class Decoder {
 
  private:
   int DecodeLocked(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
-  int DecodeOne(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst);
+  int DecodeOne(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst,
+                bool may_split = false);
+  static constexpr int kWantSplit = -1000;  // DecodeOne(may_split): a staged call for DecodeSplit
   // A large call whose bitstreams are in host memory (every call stages them over PCIe): its
   // images are cut into parts, each decoded by its own handle (helpers: same device, their own
   // streams and buffers) on its own host thread, so one part's upload overlaps the earlier
