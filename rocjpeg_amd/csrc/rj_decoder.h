@@ -101,7 +101,7 @@ class Decoder {
   std::atomic<bool> split_host_{true};
   std::vector<Stream *> lock_order_;  // DecodeOne's stream lock order (under mu_)
   std::vector<std::unique_ptr<Decoder>> helpers_;  // parts 1 .. split_parts_ - 1
-  int split_parts_ = 2;                             // env RJ_SPLIT_PARTS (2..4; 3 measured slower inside bench.py, below)
+  int split_parts_ = 2;                             // env RJ_SPLIT_PARTS (2..4; 3 measured slower inside bench.py: host_input_parts_ab.txt)
   bool split_part_ = false;                         // this handle decodes a DecodeSplit part
   static constexpr int kSplitHostMin = 1024;  // staged (non-resident) images a call needs to split
   hipEvent_t split_ev_ = nullptr;                // DecodeSplit: this part's uploads are done (recorded on stream_)
