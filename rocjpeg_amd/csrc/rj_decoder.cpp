@@ -691,6 +691,7 @@ hipError_t Decoder::WaitCall() {
 
 int Decoder::DecodeOne(Stream *const *streams, int n, const RocJpegDecodeParams *params, RocJpegImage *dst,
                        bool may_split) {
+  const auto t_call = std::chrono::steady_clock::now();
   std::lock_guard<std::mutex> lock(mu_);
   // Hold every stream's lock for the call: a concurrent re-parse must not move its bytes.  Locks
   // are taken in address order (no deadlock between calls sharing streams); a batch already in
@@ -715,6 +716,7 @@ int Decoder::DecodeOne(Stream *const *streams, int n, const RocJpegDecodeParams 
     }
     if (staged >= kSplitHostMin) return kWantSplit;  // (nothing done yet; the locks are released)
   }
+  const auto t_locked = std::chrono::steady_clock::now();
   const int r = DecodeLocked(streams, n, params, dst);
   // an error return may leave copies in flight on the stream (from the parse-time pinned arena
   // or the staging buffers): they finish before the streams' locks are released, so a
@@ -722,6 +724,18 @@ int Decoder::DecodeOne(Stream *const *streams, int n, const RocJpegDecodeParams 
   if (r != kOk) {
     (void)hipStreamSynchronize(stream_);
     if (bstream_) (void)hipStreamSynchronize(bstream_);
+  }
+  if (Dbg(kDebugHost)) {  // development: the call's host time outside DecodeLocked's planning
+    const auto t_ret = std::chrono::steady_clock::now();
+    locks.clear();
+    const auto t_unlocked = std::chrono::steady_clock::now();
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    fprintf(stderr, "[rj call] caller since the last return %.3f | locks %.3f | after the sync %.3f | unlock %.3f ms\n",
+            dbg_returned_.time_since_epoch().count() ? ms(dbg_returned_, t_call) : 0.0, ms(t_call, t_locked),
+            ms(dbg_synced_, t_ret), ms(t_ret, t_unlocked));
+    dbg_returned_ = std::chrono::steady_clock::now();
   }
   return r;
 }
@@ -2306,6 +2320,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     RJ_HIP(hipMemcpy2DAsync(rc.user, rc.pitch, d_route_.as<uint8_t>() + rc.off, rc.pitch, rc.row_bytes, rc.rows,
                             hipMemcpyDefault, stream_));
   RJ_HIP(WaitCall());
+  dbg_synced_ = std::chrono::steady_clock::now();
   if (live && *reinterpret_cast<volatile uint32_t *>(h_wide_flag_ + 1)) {
     // a live K2 workgroup gave up on its row (never expected; rj_fused.hip live_claim): decode
     // every row again in stream order, then redo the output stage -- all idempotent

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -145,6 +146,8 @@ class Decoder {
     kDebugStamps = 1u << 4, kDebugK1 = 1u << 5, kDebugK1Pieces = 1u << 6, kTestProgGiveUp = 1u << 7
   };
   uint32_t dbg_ = 0;
+  std::chrono::steady_clock::time_point dbg_synced_;  // RJ_DEBUG_HOST: the call's stream sync returned
+  std::chrono::steady_clock::time_point dbg_returned_;  // RJ_DEBUG_HOST: the last call returned
   bool Dbg(uint32_t f) const { return (dbg_ & f) != 0; }
   static constexpr int kMaxPipe = 4;  // = HIP's default hardware queues per process
   static constexpr int kWideSites = 4 + 2 * kMaxPipe;  // K2 launches per call, bound (fix-up counters)

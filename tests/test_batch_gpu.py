@@ -307,6 +307,41 @@ def test_c2_1024_default_pipelined_layout(dec):
     assert not bad, f"{len(bad)} images differ, first {bad[:8]}"
 
 
+@pytest.mark.parametrize("tune", ["1", "0"])
+def test_c2_1024_entry_placement_search(tune, monkeypatch):
+    """The entry-buffer placement search (rj_decoder.h PlaceStep): a fresh handle's first large
+    resident calls time K1 + K2 with three entry buffers and keep the fastest; every call's output
+    (each with another entry buffer) equals the oracle, the timings report the search, and
+    RJ_PLACE_TUNE=0 leaves it off.  Reference path: src/rocjpeg_decoder.cpp:196-292."""
+    t = torch()
+    monkeypatch.setenv("RJ_PLACE_TUNE", tune)
+    dec = R.JpegDecoder(R.Backend.HARDWARE, 0)
+    distinct, copies = 64, 16
+    datas = _c2_images(distinct, seed0=4242)
+    with ThreadPoolExecutor(16) as ex:
+        want = list(ex.map(lambda d: O.oracle_decode(d, int(R.OutputFormat.RGB), [(1080, 5760)]), datas))
+    streams = [R.JpegStream(datas[i % distinct]) for i in range(distinct * copies)]
+    dec.streams_to_device(streams)
+    out = t.empty((len(streams), 1080, 5760), dtype=t.uint8, device="cuda")
+    imgs = [R.make_image([out[i].data_ptr()], [5760]) for i in range(len(streams))]
+    ref = t.from_numpy(np.stack([w[0] for _, w in want])).to("cuda")
+    tms = []
+    for call in range(6):  # 2 warm calls, 3 measured candidates, then the kept one
+        out.fill_(0xA5)
+        st = dec.decode_batched(streams, R.decode_params(R.OutputFormat.RGB), imgs)
+        assert st == 0, R.error_name(st)
+        tms.append(dec.last_timings())
+        bad = [i for i in range(len(streams)) if not t.equal(out[i], ref[i % distinct])]
+        assert not bad, f"call {call}: {len(bad)} images differ, first {bad[:8]}"
+    if tune == "1":
+        assert [tm["place_tried"] for tm in tms] == [0, 0, 1, 2, 3, 3]
+        assert [tm["place_pick"] for tm in tms[:4]] == [-1] * 4 and 0 <= tms[-1]["place_pick"] <= 2
+        assert all(x > 0 for x in tms[-1]["place_ms"][:3]) and tms[-1]["place_ms"][3] == 0
+    else:
+        assert all(tm["place_tried"] == 0 and tm["place_pick"] == -1 for tm in tms)
+    dec.close()
+
+
 def test_c4_1024_default_outlier_split(dec):
     """BASELINE config C4 on one GPU (the per-rank shard of the 8-GPU config): 1024 mixed-resolution
     4:2:0 images (640x480 ... 3840x2160, RI = one MCU row; 256 distinct x 4) in one
