@@ -656,7 +656,7 @@ int Decoder::DecodeSplit(Stream *const *streams, int n, const RocJpegDecodeParam
 void Decoder::PlaceStep(float ms) {
   const int k = place_state_ - 1;  // the candidate this call ran with (in d_entries_)
   place_ms_[k] = ms;
-  if (place_best_ < 0 || ms < place_ms_[place_best_] * 0.985f) place_best_ = k;  // (1.5 %: above the noise)
+  if (place_best_ < 0 || ms < place_ms_[place_best_] * 0.995f) place_best_ = k;  // (0.5 %: the calls' noise)
   const size_t cap = d_entries_.capacity();
   place_bufs_[k].Swap(d_entries_);  // stays allocated, so that the next candidate is other memory
   if (k + 1 < place_cands_ && d_entries_.Ensure(cap) == kOk) {
