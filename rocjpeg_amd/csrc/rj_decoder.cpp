@@ -135,6 +135,8 @@ Decoder::~Decoder() {
       if (e) (void)hipEventDestroy(e);
     if (split_ev_) (void)hipEventDestroy(split_ev_);
     if (bev_) (void)hipEventDestroy(bev_);
+    if (kfork_ev_) (void)hipEventDestroy(kfork_ev_);
+    if (kjoin_ev_) (void)hipEventDestroy(kjoin_ev_);
     for (auto &e : place_ev_)
       if (e) (void)hipEventDestroy(e);
     if (bstream_) (void)hipStreamDestroy(bstream_);
@@ -196,6 +198,9 @@ int Decoder::Initialize() {
   RJ_HIP(hipEventCreateWithFlags(&bev_, hipEventDisableTiming));
   if (const char *sp = getenv("RJ_SYNC_SPIN")) spin_sync_ = atoi(sp) != 0;
   if (const char *kl = getenv("RJ_K0_LDS")) k0_lds_ = atoi(kl) != 0;
+  if (const char *ks = getenv("RJ_K2_SPLIT_SIDE")) k2_split_side_ = atoi(ks) != 0;
+  RJ_HIP(hipEventCreateWithFlags(&kfork_ev_, hipEventDisableTiming));
+  RJ_HIP(hipEventCreateWithFlags(&kjoin_ev_, hipEventDisableTiming));
   for (auto &e : place_ev_) RJ_HIP(hipEventCreate(&e));
   if (const char *pt = getenv("RJ_PLACE_TUNE")) place_tune_ = atoi(pt) != 0;
   if (const char *pk = getenv("RJ_PLACE_KEEP")) place_keep_ = atoi(pk) != 0;
@@ -2303,10 +2308,23 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       RJ_HIP(hipStreamWaitEvent(stream_, live_ev_[1], 0));
     } else {
       wide(fused_rows, wcnt, wlist, false, false);
+      // the split rows' launch beside the plain one, on the side stream (both after K1; one fix-up
+      // list, appended atomically): each fills the other's tail (env RJ_K2_SPLIT_SIDE=1; off by default,
+      // profiles/r6_experiments/k2_split_side_ab.txt)
+      const bool split_side = k2_split_side_ && nsplit_rows > 0 && cbuf.piece_shift != 0;
+      if (split_side) {
+        RJ_HIP(SideStream(bstream_));
+        RJ_HIP(hipEventRecord(kfork_ev_, stream_));
+        RJ_HIP(hipStreamWaitEvent(bstream_, kfork_ev_, 0));
+      }
 #ifndef RJ_EXP_SKIP_K2  // timing build: K0 + K1 only (the output is not written)
       RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr, wcnt, wlist,
-                        split_rows, nsplit_rows));
+                        split_rows, nsplit_rows, split_side ? bstream_ : nullptr));
 #endif
+      if (split_side) {
+        RJ_HIP(hipEventRecord(kjoin_ev_, bstream_));
+        RJ_HIP(hipStreamWaitEvent(stream_, kjoin_ev_, 0));
+      }
       if (place_timed) RJ_HIP(hipEventRecord(place_ev_[1], stream_));
     }
     wide(general_rows, wcnt, wlist, true, false);

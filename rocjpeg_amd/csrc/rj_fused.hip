@@ -1185,21 +1185,22 @@ hipError_t LaunchRowsFix(hipStream_t st, bool to_planes, bool dense, const RjIma
 hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
                       const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
                       uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list, const uint2 *split_rows,
-                      uint32_t nsplit_rows) {
+                      uint32_t nsplit_rows, hipStream_t split_st) {
   if (nrows == 0) return hipSuccess;
   if (coefs.piece_shift != 0 && split_rows != nullptr) {  // plain rows, then the split intervals' rows
     const uint32_t *no_prefix = nullptr;
+    hipStream_t sst = split_st != nullptr ? split_st : st;
     if (to_planes) {
       hipLaunchKernelGGL(k_rows<true>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs, tabsets,
                          planes, wide_cnt, wide_list);
       if (nsplit_rows)
-        hipLaunchKernelGGL(k_rows_split<true>, dim3(nsplit_rows), dim3(64), 0, st, imgs, nimg, no_prefix,
+        hipLaunchKernelGGL(k_rows_split<true>, dim3(nsplit_rows), dim3(64), 0, sst, imgs, nimg, no_prefix,
                            split_rows, coefs, tabsets, planes, wide_cnt, wide_list, 1u);
     } else {
       hipLaunchKernelGGL(k_rows<false>, dim3(nrows), dim3(64), 0, st, imgs, nimg, row_prefix, row_list, coefs, tabsets,
                          planes, wide_cnt, wide_list);
       if (nsplit_rows)
-        hipLaunchKernelGGL(k_rows_split<false>, dim3(nsplit_rows), dim3(64), 0, st, imgs, nimg, no_prefix,
+        hipLaunchKernelGGL(k_rows_split<false>, dim3(nsplit_rows), dim3(64), 0, sst, imgs, nimg, no_prefix,
                            split_rows, coefs, tabsets, planes, wide_cnt, wide_list, 1u);
     }
   } else if (coefs.piece_shift != 0) {  // lean split launch: pieces with skips / early terminators

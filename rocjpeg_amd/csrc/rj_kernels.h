@@ -62,7 +62,8 @@ hipError_t LaunchOutputJobs(hipStream_t st, const RjImageDev *imgs, const RjJobD
 hipError_t LaunchRows(hipStream_t st, bool to_planes, const RjImageDev *imgs, int nimg, const uint32_t *row_prefix,
                       const uint2 *row_list, uint32_t nrows, RjCoefBuf coefs, const RjTableSet *tabsets,
                       uint8_t *planes, uint32_t *wide_cnt, uint2 *wide_list, const uint2 *split_rows = nullptr,
-                      uint32_t nsplit_rows = 0);
+                      uint32_t nsplit_rows = 0, hipStream_t split_st = nullptr);
+// (split_st: the split rows' launch goes there, beside the plain launch; the caller forks and joins)
 // Live rows (rj_device.h RjLive): K2 beside K1 (second stream; grid = lv.rows, one workgroup per
 // ticket), and the stream-ordered K2 after K1 over the published rows no ticket took.
 hipError_t LaunchRowsLive(hipStream_t st, const RjImageDev *imgs, int nimg, const RjLive &lv, RjCoefBuf coefs,

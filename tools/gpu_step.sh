@@ -1,8 +1,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/r6s
-timeout -k 10 400 python3 -u -m pytest tests/test_batch_gpu.py -m gpu -x -q -k "placement or host_streams" --timeout 200 --timeout-method thread > gpurun_out/r6s/tests.log 2>&1 || { tail -30 gpurun_out/r6s/tests.log; exit 1; }
-tail -2 gpurun_out/r6s/tests.log
-RJ_DEBUG_HOST=1 timeout -k 10 240 python3 bench.py --steps 10 --warmup 2 --runs 1 --no-cpu-baseline --no-extras > gpurun_out/r6s/bench_host.log 2>&1 || { tail -20 gpurun_out/r6s/bench_host.log; exit 1; }
-grep "rj host\|rj call" gpurun_out/r6s/bench_host.log | sed -n 10,24p
-bash tools/gpu_evidence.sh r6c pmc
+mkdir -p gpurun_out/r6t
+timeout -k 10 400 python3 -u -m pytest tests/test_batch_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r6t/tests.log 2>&1 || { tail -30 gpurun_out/r6t/tests.log; exit 1; }
+tail -1 gpurun_out/r6t/tests.log
+STEPS=10 bash tools/gpu_ab_env.sh k2side:- k2seq:RJ_K2_SPLIT_SIDE=0
+for f in k2side_1 k2seq_1 k2side_2 k2seq_2; do grep -o '"entry_placement": {[^}]*}' gpurun_out/ab/$f.log; done
