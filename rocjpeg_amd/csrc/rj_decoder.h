@@ -212,10 +212,10 @@ class Decoder {
   // first large lean calls of a handle time K1 + K2 (two events) with the entry buffer they
   // have, then with up to kPlaceCands - 1 freshly allocated ones (the earlier ones stay
   // allocated meanwhile, so each is new memory), and keep the fastest.  env RJ_PLACE_TUNE=0: off.
-  static constexpr int kPlaceCands = 3;
+  static constexpr int kPlaceCands = 4;  // (the most RJ_PLACE_CANDS allows; 3 by default)
   static constexpr uint32_t kPlaceMinRows = 16384;  // MCU rows of a call worth timing (C2: 69,632)
   bool place_tune_ = true;
-  int place_cands_ = kPlaceCands;  // env RJ_PLACE_CANDS (1..kPlaceCands): candidates tried
+  int place_cands_ = 3;            // env RJ_PLACE_CANDS (1..kPlaceCands): candidates tried
   // the other candidates stay allocated until the handle is destroyed: freeing ~5 GB of VRAM made
   // the host-input path's uploads run at half speed for a while afterwards (126k -> 98k images/s;
   // profiles/r6_experiments/k2_placement_probe.txt); env RJ_PLACE_KEEP=0 frees them
