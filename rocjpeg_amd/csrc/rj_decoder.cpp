@@ -198,6 +198,7 @@ int Decoder::Initialize() {
   RJ_HIP(hipEventCreateWithFlags(&bev_, hipEventDisableTiming));
   if (const char *sp = getenv("RJ_SYNC_SPIN")) spin_sync_ = atoi(sp) != 0;
   if (const char *kl = getenv("RJ_K0_LDS")) k0_lds_ = atoi(kl) != 0;
+  if (const char *kl2 = getenv("RJ_K2_LPT")) k2_lpt_ = atoi(kl2) != 0;
   if (const char *ks = getenv("RJ_K2_SPLIT_SIDE")) k2_split_side_ = atoi(ks) != 0;
   RJ_HIP(hipEventCreateWithFlags(&kfork_ev_, hipEventDisableTiming));
   RJ_HIP(hipEventCreateWithFlags(&kjoin_ev_, hipEventDisableTiming));
@@ -1521,7 +1522,12 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   const uint64_t off_seg_lane0 = AlignUp(off_lane_seg + n_lane_seg * 4, 256);
   const uint64_t off_seg_ent = AlignUp(off_seg_lane0 + uint64_t(seg_lane0.size()) * 4, 256);
   const uint64_t off_row_list = AlignUp(off_seg_ent + uint64_t(seg_ent.size()) * 8, 256);
-  const uint64_t n_row_list = ngroups > 1 ? uint64_t(fused_rows) + general_rows : 0;  // upper bound
+  // K2's plain launch over the rows in lane order -- longest interval first, the order K1 ran
+  // them -- from an explicit (image, row) list (env RJ_K2_LPT=1): every interval one MCU row
+  bool k2_lpt = k2_lpt_ && lean && sorted && lpt_ && ngroups == 1 && prog_images == 0 && general_rows == 0 &&
+                fused_images == uint32_t(n);
+  for (int i = 0; i < n && k2_lpt; i++) k2_lpt = streams[i]->plan().rows_aligned;
+  const uint64_t n_row_list = ngroups > 1 ? uint64_t(fused_rows) + general_rows : (k2_lpt ? seg_total : 0);  // upper bound
   const uint64_t blob = AlignUp(off_row_list + n_row_list * sizeof(uint2), 256);
   RJ_CHECK(h_stage_.Ensure(blob));
   RJ_CHECK(d_desc_.Ensure(blob));
@@ -1907,8 +1913,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     // (image, row) in lane order -- K2 then starts each row from its record and the interval's
     // own piece, with no search over the images (rj_fused.hip row_body)
     std::vector<uint2> &row_list = sc_.row_list;
-    if (rows_from_lanes) row_list.resize(seg_total);
-    uint2 *rl = rows_from_lanes ? row_list.data() : nullptr;
+    if (rows_from_lanes || k2_lpt) row_list.resize(seg_total);
+    uint2 *rl = (rows_from_lanes || k2_lpt) ? row_list.data() : nullptr;
     uint32_t gs = 0;
     const bool want_pos = ngroups > 1;
     // the lean splits below (longest lanes first) read the intervals' exact lengths in lane order
@@ -1922,6 +1928,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
           const uint32_t l = pos[bucket(p.seg_bucket[q])]++;
           ls[l] = gs++;
           lane_len[l] = p.seg_lenblk[q];
+          if (rl) rl[l] = uint2{uint32_t(i), uint32_t(q)};
         }
       } else if (rl != nullptr || want_pos) {
         uint32_t r = 0;
@@ -2167,7 +2174,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     cbuf.seg_lane0 = nullptr;
   }
   // part B: everything up to the row lists, or only the lane list actually used
-  const uint64_t blob_b = (!any_split && sorted && ngroups == 1)
+  const uint64_t blob_b = (!any_split && sorted && ngroups == 1 && !k2_lpt)
                               ? std::min<uint64_t>(blob, AlignUp(off_lane_seg + uint64_t(nsplit ? nl_split : (nl_five ? nl_five + 2 * nsplit_rows : seg_total)) * 4, 256))
                               : blob;
   if (blob_b > blob_a) {
@@ -2318,8 +2325,8 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
         RJ_HIP(hipStreamWaitEvent(bstream_, kfork_ev_, 0));
       }
 #ifndef RJ_EXP_SKIP_K2  // timing build: K0 + K1 only (the output is not written)
-      RJ_HIP(LaunchRows(stream_, false, d_imgs, n, d_rows, nullptr, fused_rows, cbuf, d_tabs, nullptr, wcnt, wlist,
-                        split_rows, nsplit_rows, split_side ? bstream_ : nullptr));
+      RJ_HIP(LaunchRows(stream_, false, d_imgs, n, k2_lpt ? nullptr : d_rows, k2_lpt ? d_row_list : nullptr, fused_rows,
+                        cbuf, d_tabs, nullptr, wcnt, wlist, split_rows, nsplit_rows, split_side ? bstream_ : nullptr));
 #endif
       if (split_side) {
         RJ_HIP(hipEventRecord(kjoin_ev_, bstream_));

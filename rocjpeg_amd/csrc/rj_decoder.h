@@ -202,6 +202,7 @@ class Decoder {
   // upload B (K1 lane order, K2 row lists) on its own stream while K0 runs; K1 waits for it by an
   // event instead of behind K0 in the call's stream (env RJ_UPLOAD_B_SIDE=0: in stream order)
   bool side_b_ = true;
+  bool k2_lpt_ = false;         // env RJ_K2_LPT=1: a lean call's K2 rows in K1's lane order (longest first)
   bool k2_split_side_ = false;  // env RJ_K2_SPLIT_SIDE=1: the split rows' K2 launch beside the plain one (one process in two ran 11 % slower: off)
   hipEvent_t kfork_ev_ = nullptr, kjoin_ev_ = nullptr;  // K2's plain / split launches: fork, join
   bool k0_lds_ = true;      // env RJ_K0_LDS=0: K0 stores a compacted chunk's bytes one by one (A/B)
