@@ -1882,6 +1882,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
   uint32_t lane_off[kMaxPipe + 1] = {}, frow_off[kMaxPipe + 1] = {}, grow_off[kMaxPipe + 1] = {};
   uint32_t class_max[kMaxPipe] = {};  // longest interval (bytes) of each class
   bool rows_from_lanes = false;
+  uint32_t len_lanes = 0;  // lanes [0, len_lanes) have their exact length in sc_.lane_len
   bool lanes_desc = false;  // lane order: longest interval first
   if (sorted) {
     constexpr uint32_t kBuckets = 4096;  // 32-B length buckets up to 128 KB
@@ -1921,13 +1922,18 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     const bool want_len = lean && desc && ngroups == 1 && (outlier_split_ || (five_waves_ && split5_t_ > 0.0));
     std::vector<uint64_t> &lane_len = sc_.lane_len;
     if (want_len) lane_len.resize(seg_total);
+    // only the lanes a split may take (the longest; the splits' own lane budgets below) need theirs
+    const int64_t cu = cu_count_;
+    len_lanes = uint32_t(std::min<int64_t>(
+        seg_total, std::max<int64_t>({int64_t(0), 64 * cu * 2 * (RJ_HL_SPLIT_DEC / 64) - int64_t(seg_total),
+                                      64 * 5 * cu - int64_t(seg_total)}) + 128));
     for (int i = 0; i < n; i++) {
       const DecodePlan &p = streams[i]->plan();
       if (want_len) {
         for (size_t q = 0; q < p.segs.size(); q++) {
           const uint32_t l = pos[bucket(p.seg_bucket[q])]++;
           ls[l] = gs++;
-          lane_len[l] = p.seg_lenblk[q];
+          if (l < len_lanes) lane_len[l] = p.seg_lenblk[q];
           if (rl) rl[l] = uint2{uint32_t(i), uint32_t(q)};
         }
       } else if (rl != nullptr || want_pos) {
@@ -2078,7 +2084,7 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
       uint64_t cap = 0;
       if (split5_t_ > 0.0) {
         const double lim = double(lane_len(0).x) * split5_t_;
-        while (ns < seg_total) {
+        while (ns < len_lanes) {
           const uint32_t len = lane_len(ns).x;
           if (len < RJ_SPLIT_MIN_BYTES || double(len) <= lim) break;
           ns++;

@@ -1,6 +1,8 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/r6v
-RJ_K2_LPT=1 timeout -k 10 400 python3 -u -m pytest tests/test_batch_gpu.py tests/test_decode_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r6v/tests.log 2>&1 || { tail -30 gpurun_out/r6v/tests.log; exit 1; }
-tail -1 gpurun_out/r6v/tests.log
-STEPS=10 bash tools/gpu_ab_env.sh lpt:RJ_K2_LPT=1 img:-
+mkdir -p gpurun_out/r6w
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r6w/suite.log 2>&1 || { tail -30 gpurun_out/r6w/suite.log; exit 1; }
+tail -1 gpurun_out/r6w/suite.log
+RJ_DEBUG_HOST=1 timeout -k 10 240 python3 bench.py --steps 10 --warmup 2 --runs 1 --no-cpu-baseline --no-extras > gpurun_out/r6w/bench_host.log 2>&1 || { tail -20 gpurun_out/r6w/bench_host.log; exit 1; }
+grep "rj host" gpurun_out/r6w/bench_host.log | sed -n 8,12p
+python3 tools/bench_summary.py gpurun_out/r6w/bench_host.log | head -3
