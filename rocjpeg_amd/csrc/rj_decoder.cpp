@@ -199,6 +199,7 @@ int Decoder::Initialize() {
   if (const char *sp = getenv("RJ_SYNC_SPIN")) spin_sync_ = atoi(sp) != 0;
   if (const char *kl = getenv("RJ_K0_LDS")) k0_lds_ = atoi(kl) != 0;
   if (const char *kl2 = getenv("RJ_K2_LPT")) k2_lpt_ = atoi(kl2) != 0;
+  if (const char *sp2 = getenv("RJ_SORT_PAR")) sort_par_ = atoi(sp2) != 0;
   if (const char *ks = getenv("RJ_K2_SPLIT_SIDE")) k2_split_side_ = atoi(ks) != 0;
   RJ_HIP(hipEventCreateWithFlags(&kfork_ev_, hipEventDisableTiming));
   RJ_HIP(hipEventCreateWithFlags(&kjoin_ev_, hipEventDisableTiming));
@@ -1893,11 +1894,37 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     std::vector<uint32_t> &pos = sc_.bucket_pos;
     pos.assign(kBuckets, 0);
     bool aligned = fused_images == uint32_t(n - int(prog_images)) || fused_images == 0;
-    for (int i = 0; i < n; i++) {
-      const DecodePlan &p = streams[i]->plan();
-      if (p.progressive) continue;  // no K1 intervals, no rows in these launches
-      aligned = aligned && p.rows_aligned;
-      for (const uint16_t b : p.seg_bucket) pos[bucket(b)]++;
+    for (int i = 0; i < n && aligned; i++) aligned = streams[i]->plan().progressive || streams[i]->plan().rows_aligned;
+    const bool want_pos = ngroups > 1;
+    rows_from_lanes = ngroups > 1 && aligned;
+    // the lean splits below (longest lanes first) read the intervals' exact lengths in lane order
+    const bool want_len = lean && desc && ngroups == 1 && (outlier_split_ || (five_waves_ && split5_t_ > 0.0));
+    // a large lean call sorts on the pool: each part of the images counts its buckets, then places
+    // its intervals after the earlier parts' (the order is the sequential one)
+    // (env RJ_SORT_PAR=1; off by default: the workers' wake-ups made some calls' sort 0.27-0.55 ms
+    // against 0.09-0.12 ms, profiles/r6_experiments/sort_par.txt)
+    const bool par = sort_par_ && want_len && !want_pos && !rows_from_lanes && !k2_lpt && pool_.threads() > 1 &&
+                     seg_total >= 16384;
+    const int nparts = par ? std::min(4, pool_.threads()) : 1;
+    std::vector<uint32_t> &phist = sc_.part_hist;
+    if (par) {
+      phist.assign(size_t(nparts) * kBuckets, 0);
+      pool_.Run(nparts, [&](int t) {
+        uint32_t *H = phist.data() + size_t(t) * kBuckets;
+        for (int i = n * t / nparts; i < n * (t + 1) / nparts; i++) {
+          const DecodePlan &p = streams[i]->plan();
+          if (p.progressive) continue;
+          for (const uint16_t b : p.seg_bucket) H[bucket(b)]++;
+        }
+      }, nullptr);
+      for (int t = 0; t < nparts; t++)
+        for (uint32_t b = 0; b < kBuckets; b++) pos[b] += phist[size_t(t) * kBuckets + b];
+    } else {
+      for (int i = 0; i < n; i++) {
+        const DecodePlan &p = streams[i]->plan();
+        if (p.progressive) continue;  // no K1 intervals, no rows in these launches
+        for (const uint16_t b : p.seg_bucket) pos[bucket(b)]++;
+      }
     }
     sc_.bucket_cnt.assign(pos.begin(), pos.end());  // (the outlier split counts on it)
     for (uint32_t b = 0, cum = 0; b < kBuckets; b++) {
@@ -1909,7 +1936,6 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     uint32_t *ls = lane_seg.data();
     std::vector<uint32_t> &seg_pos = sc_.seg_pos;  // pipelined launch: each interval's lane
     if (ngroups > 1) seg_pos.resize(seg_total);
-    rows_from_lanes = ngroups > 1 && aligned;
     // rows from lanes: K2 row w of class g is lane lane_off[g] + w's interval, listed as
     // (image, row) in lane order -- K2 then starts each row from its record and the interval's
     // own piece, with no search over the images (rj_fused.hip row_body)
@@ -1917,9 +1943,6 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     if (rows_from_lanes || k2_lpt) row_list.resize(seg_total);
     uint2 *rl = (rows_from_lanes || k2_lpt) ? row_list.data() : nullptr;
     uint32_t gs = 0;
-    const bool want_pos = ngroups > 1;
-    // the lean splits below (longest lanes first) read the intervals' exact lengths in lane order
-    const bool want_len = lean && desc && ngroups == 1 && (outlier_split_ || (five_waves_ && split5_t_ > 0.0));
     std::vector<uint64_t> &lane_len = sc_.lane_len;
     if (want_len) lane_len.resize(seg_total);
     // only the lanes a split may take (the longest; the splits' own lane budgets below) need theirs
@@ -1927,7 +1950,31 @@ int Decoder::DecodeLocked(Stream *const *streams, int n, const RocJpegDecodePara
     len_lanes = uint32_t(std::min<int64_t>(
         seg_total, std::max<int64_t>({int64_t(0), 64 * cu * 2 * (RJ_HL_SPLIT_DEC / 64) - int64_t(seg_total),
                                       64 * 5 * cu - int64_t(seg_total)}) + 128));
-    for (int i = 0; i < n; i++) {
+    if (par) {
+      // part t's intervals of bucket b start after the earlier parts' ones of that bucket
+      for (uint32_t b = 0; b < kBuckets; b++) {
+        uint32_t at = pos[b];
+        for (int t = 0; t < nparts; t++) {
+          uint32_t &c = phist[size_t(t) * kBuckets + b];
+          const uint32_t cnt = c;
+          c = at;
+          at += cnt;
+        }
+      }
+      pool_.Run(nparts, [&](int t) {
+        uint32_t *P = phist.data() + size_t(t) * kBuckets;
+        for (int i = n * t / nparts; i < n * (t + 1) / nparts; i++) {
+          const DecodePlan &p = streams[i]->plan();
+          uint32_t g = imgs[i].seg_prefix;
+          for (size_t q = 0; q < p.segs.size(); q++) {
+            const uint32_t l = P[bucket(p.seg_bucket[q])]++;
+            ls[l] = g++;
+            if (l < len_lanes) lane_len[l] = p.seg_lenblk[q];
+          }
+        }
+      }, nullptr);
+    }
+    for (int i = 0; i < n && !par; i++) {
       const DecodePlan &p = streams[i]->plan();
       if (want_len) {
         for (size_t q = 0; q < p.segs.size(); q++) {

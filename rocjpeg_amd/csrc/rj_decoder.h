@@ -202,6 +202,7 @@ class Decoder {
   // upload B (K1 lane order, K2 row lists) on its own stream while K0 runs; K1 waits for it by an
   // event instead of behind K0 in the call's stream (env RJ_UPLOAD_B_SIDE=0: in stream order)
   bool side_b_ = true;
+  bool sort_par_ = false;       // env RJ_SORT_PAR=1: a large lean call's lane sort on the host pool
   bool k2_lpt_ = false;         // env RJ_K2_LPT=1: a lean call's K2 rows in K1's lane order (longest first)
   bool k2_split_side_ = false;  // env RJ_K2_SPLIT_SIDE=1: the split rows' K2 launch beside the plain one (one process in two ran 11 % slower: off)
   hipEvent_t kfork_ev_ = nullptr, kjoin_ev_ = nullptr;  // K2's plain / split launches: fork, join
@@ -251,6 +252,7 @@ class Decoder {
     std::vector<uint32_t> tab_of, row_prefix, grow_prefix, seg_lane0, lane_seg, bucket_pos, seg_pos, lane_split;
     std::vector<uint32_t> bucket_cnt;  // the lane sort's 32-B length histogram (its bucket order)
     std::vector<uint64_t> lane_len;    // per lane (sorted order): the interval's seg_lenblk
+    std::vector<uint32_t> part_hist;   // the lane sort on the pool: per part, bucket counts / next slots
     std::vector<uint64_t> split_bits;  // per interval: split by the five-wave layout
     std::vector<uint8_t> is_fused, row_group, routed;
     std::vector<uint2> row_list;
